@@ -1,0 +1,191 @@
+"""bench.py — LM iterations/s and ms/solve of the MI355X BA solver.
+
+A "step" is one complete Backend::Optimize solve (problem.solve(10),
+src/backend_lego.cpp:161) of a device-resident sliding window: restart from the
+uploaded initial state, run every LM trial to the reference stop rule.
+value = LM iterations completed per second, summed over ranks.
+
+Workload (BASELINE.json metric window, configs[2]): 20 keyframes, 50 000
+landmarks, 400 000 observations per GPU, fp64 throughout (>= the reference's
+double).  With N GPUs the window grows to N x 50 000 landmarks (landmark
+shards, poses replicated, one RCCL all-reduce of the reduced pose system per
+LM trial) -> "scaling": "weak"; value counts shard-iterations (iterations x N).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lego-slam_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import lego_ba  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6       # MI355X FP64 vector = matrix (spec)
+
+
+def lin_algorithmic_bytes(n_obs, n_lm, n_chunks_slab_bytes):
+    """Compulsory HBM bytes of one k_lin launch (DESIGN.md "k_lin roofline"):
+    per observation uv (16 B) + meta (4 B) + rho0 write (8 B); per landmark
+    X read/write (48 B) + H_ll cache read/write (192 B) + CSR (4 B); plus the
+    chunk slabs written."""
+    return 28 * n_obs + 244 * n_lm + n_chunks_slab_bytes
+
+
+def lin_algorithmic_flops(n_obs, k):
+    """fp64 flops of one k_lin TRIAL launch on a window with k observations per
+    landmark: back-substitution ~150/obs, evaluation + linearisation ~330/obs,
+    per-landmark Cholesky / solves ~60/k per obs, Schur pair blocks
+    108 * k(k+1)/2 MAC per landmark."""
+    per_obs = 150 + 330 + 60.0 / k
+    schur = 2 * 108 * k * (k + 1) / 2 / k
+    return n_obs * (per_obs + schur)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--landmarks", type=int, default=50000, help="landmarks per GPU")
+    ap.add_argument("--poses", type=int, default=20)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--family", default="stable", choices=["stable", "default"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--trials-per-sync", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world != 1:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+
+    from windows import STABLE
+    params = dict(STABLE) if args.family == "stable" else {}
+    L = args.landmarks
+    w = lego_ba.generate_window(P=args.poses, L=L * world, k=args.k, seed=args.seed,
+                                lm_begin=rank * L, lm_end=(rank + 1) * L, **params)
+    if args.family == "stable":
+        f = np.zeros(args.poses, np.uint8)
+        f[0] = 1
+        w["pose_fixed"] = f
+
+    comm_id = bytes(128)
+    if world > 1:
+        obj = [lego_ba.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    solver = lego_ba.Solver(device=local, world_size=world, rank=rank, comm_id=comm_id,
+                            trials_per_sync=args.trials_per_sync)
+    solver.upload(w)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        solver.solve_resident()
+    # ---- timed region (HIP events around every kernel, on the solver's stream) ----
+    solver.set_profiling(True)
+    solver.kernel_stats_reset()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = trials = 0
+    last = None
+    for _ in range(args.steps):
+        last = solver.solve_resident()
+        iters += last["iterations"]
+        trials += last["trials"]
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ks = solver.kernel_stats()
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    value = world * iters / dt
+    n_obs, n_lm = len(w["obs_pose"]), len(w["lm_xyz"])
+    lin_n, lin_ms = ks.get("k_lin", (0, 0.0))
+    lin_avg_ms = lin_ms / max(lin_n, 1)
+    n_chunks_est = max(1, (n_lm + 103) // 104)
+    slab_bytes = n_chunks_est * (6 * 256 + 8 * 33 + 4) * 8
+    bytes_per = lin_algorithmic_bytes(n_obs, n_lm, slab_bytes)
+    flops_per = lin_algorithmic_flops(n_obs, args.k)
+    achieved_gbs = bytes_per / (lin_avg_ms * 1e-3) / 1e9 if lin_avg_ms > 0 else 0.0
+    achieved_tfs = flops_per / (lin_avg_ms * 1e-3) / 1e12 if lin_avg_ms > 0 else 0.0
+
+    out = {
+        "metric": "LM iterations/sec + ms/solve, 20KF/50k-pts/400k-obs window; final chi2 vs ref",
+        "value": round(value, 3),
+        "unit": "LM iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic (tools/window_gen.c, family={args.family}, seed={args.seed})",
+        "config": {"workload": f"sliding-window BA solve(10): {args.poses} KF / {L * world} landmarks / "
+                               f"{n_obs * world} obs ({L} landmarks per GPU)",
+                   "keyframes": args.poses, "landmarks_per_gpu": L, "obs_per_gpu": n_obs,
+                   "parallelism": f"landmark-shard x{world}"},
+        "iterations_per_solve": iters / args.steps,
+        "trials_per_solve": trials / args.steps,
+        "chi2_final": last["chi2_final"],
+        "kernels_ms_per_solve": {k: round(v[1] / args.steps, 4) for k, v in ks.items()},
+        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_lin", "avg_launch_ms": round(lin_avg_ms, 5), "bytes_per_launch": bytes_per},
+        "roofline_fp64": {"achieved": round(achieved_tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": round(achieved_tfs / FP64_PEAK_TFS, 4), "flops_per_launch": flops_per},
+    }
+    if world == 1 and not args.no_cpu:
+        import oracle_bind
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        t = time.perf_counter()
+        o = oracle_bind.solve(w, n_threads=threads)
+        ct = time.perf_counter() - t
+        out["cpu_baseline"] = {"value": round(o["iterations"] / ct, 4), "unit": "LM iterations/s",
+                               "cores": threads, "kind": "port",
+                               "sample": "one full solve(10) of the same window by the block-sparse oracle "
+                                         f"(oracle/lego_oracle.c ref_sparse), {ct:.2f} s, {o['iterations']} iterations"}
+        out["chi2_rel_vs_oracle"] = abs(last["chi2_final"] - o["chi2_final"]) / o["chi2_final"]
+        out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+    print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+/*
+ * lego_ba.h — C ABI of the MI355X sliding-window bundle-adjustment solver.
+ *
+ * Drop-in boundary for LEGO-SLAM's backend optimisation.
+ * The reference builds a `lego::Problem` inside `Backend::Optimize`
+ * (src/backend_lego.cpp:57-158), calls `problem.solve(10)` (:161) and then reads
+ * each edge's robust chi2 and the vertex estimates back (:163-217).  This ABI
+ * replaces exactly that block with one call:
+ *
+ *     reference                                   this ABI
+ *     ---------------------------------------     ----------------------------
+ *     lego::Problem problem(SLAM)  problem.h:53   lh_create
+ *     addVertex / addEdge          problem.h:65,69 lh_window (flat arrays)
+ *     setInitialLambda             problem.h:99   lh_options.lambda_init
+ *     setVerbose                   problem.h:104  lh_options.verbose
+ *     setStrategyType              problem.h:62   lh_options.strategy
+ *     solve(iterations)            problem.cpp:156 lh_solve
+ *     edge->getRobustChi2()        base_edge.cpp:33 lh_result.edge_robust_chi2
+ *     vertex->getEstimate()        base_vertex.h:34 lh_result.pose_Tcw / lm_xyz
+ *     outlier threshold loop       backend_lego.cpp:163-194 lh_classify_outliers
+ *     ~Problem                     problem.cpp:32 lh_destroy
+ *
+ * Plain C types only (no torch, Eigen or Sophus in any signature).  No C++
+ * exception crosses the ABI; every entry point returns an lh_status.
+ * A handle is single-threaded; use one handle per calling thread (the
+ * reference runs one Problem on the backend thread and one on the frontend
+ * thread).  Handles share no global state (the reference's global_vertex_id /
+ * global_edge_id counters, base_vertex.cpp:5 / base_edge.cpp:6, have no analogue).
+ */
+#ifndef LEGO_BA_H
+#define LEGO_BA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LH_ABI_VERSION 1
+
+typedef enum lh_status {
+    LH_OK = 0,
+    LH_E_EMPTY = 1,       /* no vertices or no edges: Problem::solve returns false (problem.cpp:157-161) */
+    LH_E_BADARG = 2,      /* null pointer, index out of range, bad option                              */
+    LH_E_HIP = 3,         /* HIP runtime error (device missing, OOM, launch failure)                    */
+    LH_E_RCCL = 4,        /* RCCL communicator / collective error                                       */
+    LH_E_UNSUPPORTED = 5, /* window outside the supported envelope (see DESIGN.md "Limits")            */
+    LH_E_STATE = 6        /* call out of order (e.g. lh_solve_resident before lh_upload)               */
+} lh_status;
+
+/* Problem::StrategyType (problem.h:45-50) */
+typedef enum lh_strategy { LH_STRATEGY_DEFAULT = 0, LH_STRATEGY_1 = 1 } lh_strategy;
+
+/* Reduced pose-system solver: the reference uses Eigen LDLT (problem.cpp:420);
+   PCG is the correct Jacobi-PCG the reference left commented out (:422). */
+typedef enum lh_linear_solver { LH_SOLVER_LDLT = 0, LH_SOLVER_PCG = 1 } lh_linear_solver;
+
+typedef struct lh_options {
+    int32_t abi_version;      /* must be LH_ABI_VERSION                                      */
+    int32_t max_iters;        /* outer LM iterations, solve(10)          backend_lego.cpp:161 */
+    int32_t max_trials;       /* false_cnt_threshold = 10                problem.cpp:178      */
+    int32_t strategy;         /* lh_strategy                             problem.h:45         */
+    double huber_delta;       /* HuberCost(5.991); <= 0: no robust kernel backend_lego.cpp:92-94 */
+    double stop_dchi2;        /* diffChiThreshold_ = 1e-5 (absolute)     problem.h:165        */
+    double tau;               /* 1e-5                                    problem.cpp:495      */
+    double lambda_cap;        /* 5e10                                    problem.cpp:494      */
+    double lambda_init;       /* < 0: computed; >= 0: setInitialLambda   problem.h:99-102     */
+    int32_t linear_solver;    /* lh_linear_solver                                             */
+    int32_t verbose;          /* print the reference's per-iteration line problem.cpp:180-184 */
+    int32_t device;           /* HIP device ordinal, -1 = current device                      */
+    int32_t world_size;       /* landmark shards (one process per GPU); 1 = single GPU        */
+    int32_t rank;             /* this process's shard                                         */
+    int32_t degenerate_guard; /* 0: reference semantics (rank-deficient H_ll poisons the step,
+                                 problem.cpp:396-400); 1: skip such landmarks' Schur terms    */
+    int32_t trials_per_sync;  /* LM trials enqueued per host poll of the stop flag (0: auto)  */
+    int32_t profile;          /* 1: time every kernel with HIP events (lh_kernel_stats)       */
+    uint8_t comm_id[128];     /* ncclUniqueId from lh_comm_unique_id on rank 0 (world_size>1) */
+} lh_options;
+
+/*
+ * One sliding window.  Caller-owned, read-only during the call.
+ * Order contract: poses in ascending keyframe id and landmarks in ascending
+ * landmark id, i.e. the reference's ordering (Problem::setOrdering,
+ * problem.cpp:234-255: std::map by vertex id, poses first).  Observation order
+ * is free (the reference's is unordered_map hash order).
+ */
+typedef struct lh_window {
+    int32_t n_poses;
+    const double *pose_Tcw;    /* [n_poses][12] row-major [R | t], T_cw (VertexPose estimate, lego_types.h:37,57) */
+    const uint8_t *pose_fixed; /* [n_poses] or NULL; nonzero = BaseVertex::setFixed (base_vertex.h:50)              */
+    int32_t n_landmarks;
+    const double *lm_xyz;      /* [n_landmarks][3] world position (VertexXYZ, lego_types.h:97-115) */
+    int64_t n_obs;
+    const uint32_t *obs_pose;  /* [n_obs] pose index                                                */
+    const uint32_t *obs_lm;    /* [n_obs] landmark index                                            */
+    const uint8_t *obs_cam;    /* [n_obs] camera index or NULL (all camera 0)                       */
+    const double *obs_uv;      /* [n_obs][2] pixel measurement (toVec2 of cv::KeyPoint, algorithm.h:37) */
+    double K[4];               /* fx, fy, cx, cy (Camera::K, camera.h:36-41)                         */
+    int32_t n_cams;            /* number of extrinsics in cam_ext (0 with cam_ext NULL = identity)   */
+    const double *cam_ext;     /* [n_cams][12] row-major [R | t] camera extrinsic (Camera::pose_)    */
+} lh_window;
+
+typedef struct lh_result {
+    /* caller-owned outputs; any pointer may be NULL */
+    double *pose_Tcw;          /* [n_poses][12]                                                   */
+    double *lm_xyz;            /* [n_landmarks][3]                                                */
+    double *edge_robust_chi2;  /* [n_obs] rho0 of the residuals as last evaluated, window order
+                                  (stale after an all-rejected exit, as backend_lego.cpp:171 sees) */
+    double *trace_chi2;        /* [trace_cap] currentChi_ at the top of each outer iteration       */
+    double *trace_lambda;      /* [trace_cap] currentLambda_ at the same point                     */
+    int32_t trace_cap;
+    /* scalar outputs */
+    int32_t trace_len;
+    int32_t iterations;        /* outer LM iterations completed (problem.cpp:207)                  */
+    int32_t trials;            /* solveLinearEquation calls                                        */
+    int32_t accepted;          /* accepted trials                                                  */
+    double chi2_initial;       /* 0.5 * sum rho0 at the input state (problem.cpp:475-479)          */
+    double chi2_final;         /* currentChi_ at exit                                              */
+    double lambda_final;
+    double time_ms;            /* wall time of the LM solve on the device (excludes upload)        */
+} lh_result;
+
+typedef struct lh_kernel_stats {
+    int64_t launches[8];       /* per kernel class, see lh_kernel_name                             */
+    double total_ms[8];
+} lh_kernel_stats;
+
+typedef struct lh_handle lh_handle;
+
+const char *lh_strerror(int status);
+void lh_default_options(lh_options *opt);
+const char *lh_kernel_name(int kernel_class);
+
+/* RCCL: rank 0 creates the id and ships it to the other ranks (any transport). */
+int lh_comm_unique_id(uint8_t out[128]);
+
+int lh_create(lh_handle **h, const lh_options *opt);
+void lh_destroy(lh_handle *h);
+
+/* Host-buffer path: upload, solve, download.  The drop-in for problem.solve(). */
+int lh_solve(lh_handle *h, const lh_window *in, lh_result *out);
+
+/* Device-resident path (bench): lh_upload preprocesses and copies the window
+   once; every lh_solve_resident restarts from the uploaded initial state. */
+int lh_upload(lh_handle *h, const lh_window *in);
+int lh_solve_resident(lh_handle *h, lh_result *out);
+
+int lh_kernel_stats_get(lh_handle *h, lh_kernel_stats *out);
+int lh_set_profiling(lh_handle *h, int on);   /* toggle lh_options.profile on a live handle */
+void lh_kernel_stats_reset(lh_handle *h);
+
+/*
+ * Backend::Optimize outlier pass (backend_lego.cpp:163-194): starting from
+ * chi2_th, double the threshold (at most 5 times) while the inlier ratio is
+ * <= 0.5, then flag edges with robust chi2 > threshold.  is_outlier may be NULL.
+ */
+int lh_classify_outliers(const double *edge_robust_chi2, int64_t n_obs, double chi2_th,
+                         uint8_t *is_outlier, double *th_out, int64_t *n_inlier, int64_t *n_outlier);
+
+/* ---- test hooks (not part of the reference interface) ---- */
+/* f64 MFMA accumulator-layout probe: D(16x16) = A(16x4) * B(4x16), device pointers, row-major */
+int lh_debug_mfma_probe(const double *A, const double *B, double *D);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,87 @@
+// lh_common.h — data layout shared by the HIP kernels and the host side of
+// liblego_ba.so.  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#define LH_HD __host__ __device__
+#else
+#define LH_HD
+#endif
+
+// ---- envelope ---------------------------------------------------------------
+#define LH_PMAX 21            // poses per window (reduced system n = 6P <= 126 fits LDS)
+#define LH_UMAX 10            // distinct poses in one chunk window (6U <= 64 rows)
+#define LH_TMAX 4             // 16-row MFMA tiles per window side
+#define LH_SB_LM 8            // landmarks per sub-batch (one wave)
+#define LH_SB_OBS 64          // observations per sub-batch (one per lane)
+#define LH_WAVES 4            // waves per k_lin workgroup
+#define LH_TASKS 33           // per-pose values a sub-batch emits: Hpp(21) bp(6) bsd(6)
+#define LH_MAX_CAMS 4
+#define LH_TRACE 64
+#define LH_NPAD 128           // reduced system padded size (LDS LDLT)
+
+#define LH_SLAB_TILES (LH_TMAX * (LH_TMAX + 1) / 2)
+#define LH_SLAB_TASK_OFF (LH_SLAB_TILES * 256)
+#define LH_SLAB_SC_OFF (LH_SLAB_TASK_OFF + LH_UMAX * LH_TASKS)
+#define LH_SLAB_STRIDE (LH_SLAB_SC_OFF + 8)
+
+// slab scalars
+#define LH_SC_CHI2 0          // sum rho0 (not halved)
+#define LH_SC_SCALE 1         // landmark part of dx^T(lambda dx + b)
+#define LH_SC_NDEG 2          // rank-deficient H_ll landmarks
+#define LH_SC_MAXD 3          // max |H_ll diag| (a max, not a sum)
+
+// per-landmark cache: Cholesky of H_ll (6), b_l (3), diag H_ll (3)
+#define LH_CACHE 12
+
+// per (pose, cam) table: R_T(9) t_T(3) R_ct(9) t_ct(3); per cam ext R_e(9) t_e(3)
+#define LH_PT 24
+
+// obs meta packing
+#define LH_META(pose, cam, slot, lms) ((uint32_t)(pose) | ((uint32_t)(cam) << 12) | ((uint32_t)(slot) << 16) | ((uint32_t)(lms) << 20))
+#define LH_META_POSE(m) ((m) & 0xFFFu)
+#define LH_META_CAM(m) (((m) >> 12) & 0xFu)
+#define LH_META_SLOT(m) (((m) >> 16) & 0xFu)
+#define LH_META_LMS(m) (((m) >> 20) & 0x7u)
+
+struct lh_chunk {
+    uint32_t sb_begin, sb_end;   // sub-batch range
+    uint8_t U, T, pad0, pad1;
+    uint16_t pose[LH_UMAX];      // window slot -> pose
+};
+
+struct lh_subbatch {
+    uint32_t lm_begin, obs_begin;
+    uint16_t n_lm, n_obs;
+};
+
+// reduced-system buffer layout (one per state buffer)
+struct lh_rs_layout {
+    int npairs, off_S, off_bs, off_bp, off_hd, off_sc, total;
+};
+
+LH_HD static inline lh_rs_layout lh_rs_make(int P) {
+    lh_rs_layout L;
+    L.npairs = P * (P + 1) / 2;
+    L.off_S = 0;
+    L.off_bs = L.npairs * 36;
+    L.off_bp = L.off_bs + 6 * P;
+    L.off_hd = L.off_bp + 6 * P;
+    L.off_sc = L.off_hd + 6 * P;
+    L.total = L.off_sc + 8;
+    return L;
+}
+
+// LM controller state (device resident, mirrors Problem's members problem.h:157-165)
+struct lh_ctrl {
+    double chi, lambda, ni, last_chi, spose, chi2_initial;
+    int32_t iter, false_cnt, trials, accepted, done, cur, trace_len, nonpd;
+    double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
+};
+
+struct lh_params {
+    int32_t P, n, ncam, max_iters, max_trials, strategy, guard, lambda_given;
+    double huber_delta, stop_dchi2, tau, lambda_cap, lambda_init;
+    double K[4];
+};

@@ -1,0 +1,809 @@
+// lh_host.cpp — C ABI (include/lego_ba.h) of the MI355X BA solver: window
+// preprocessing, device buffers, the LM launch loop and the RCCL exchange.
+//
+// Host-side work per window (once, at lh_upload):
+//   * landmark-major CSR of the observations, each landmark's observations in
+//     ascending pose order (the reference visits edges in hash order; any order
+//     is the same problem);
+//   * landmarks sorted by observation span and packed into chunks whose union
+//     of observing poses fits one MFMA window (<= LH_UMAX poses), chunks split
+//     into wave sub-batches (<= 8 landmarks, <= 64 observations);
+//   * the reduce plan: for every pose pair, the chunks that touch it.
+// Per solve nothing but kernel launches (and, with >1 rank, one RCCL all-reduce
+// per LM trial) happens on the host; it polls the device stop flag every few
+// trials.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <numeric>
+#include <vector>
+
+#include "../../include/lego_ba.h"
+#include "lh_common.h"
+
+extern "C" {
+hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
+                         const lh_subbatch* sbs, const uint32_t* lm_ptr, const double* obs_uv, const uint32_t* obs_meta,
+                         double* Xbuf, double* cache, const double* ptab, const double* ext, const lh_ctrl* ctrl,
+                         const double* dxp, double* edge_rho, double* slabs, lh_params prm, int L, uint32_t fixed_mask);
+hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double* slabs, const uint32_t* pair_ptr,
+                            const uint32_t* items, const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage,
+                            double* maxd, lh_params prm, int n_chunks);
+hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
+                          double* pose_qt, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
+                          int* host_done);
+hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
+}
+
+namespace {
+
+enum { KC_LIN = 0, KC_REDUCE = 1, KC_CTRL = 2, KC_ALLREDUCE = 3, KC_INIT = 4, KC_N = 8 };
+const char* kKernelNames[KC_N] = {"k_lin", "k_reduce", "k_ctrl", "allreduce", "k_lin_init", "", "", ""};
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) n = std::max<size_t>(count, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+// ---- Eigen quaternion <-> matrix (host copies of the formulas the kernels use) ----
+void q_from_R(const double* R, double q[4]) {
+#define M(i, j) R[3 * (i) + (j)]
+    double t = M(0, 0) + M(1, 1) + M(2, 2);
+    if (t > 0.0) {
+        t = std::sqrt(t + 1.0);
+        q[0] = 0.5 * t;
+        t = 0.5 / t;
+        q[1] = (M(2, 1) - M(1, 2)) * t;
+        q[2] = (M(0, 2) - M(2, 0)) * t;
+        q[3] = (M(1, 0) - M(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = std::sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (M(k, j) - M(j, k)) * t;
+        c[j] = (M(j, i) + M(i, j)) * t;
+        c[k] = (M(k, i) + M(i, k)) * t;
+        q[1] = c[0]; q[2] = c[1]; q[3] = c[2];
+    }
+#undef M
+}
+
+void R_from_q(const double q[4], double R[9]) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;          R[2] = txz + twy;
+    R[3] = txy + twz;          R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;          R[7] = tyz + twx;          R[8] = 1.0 - (txx + tyy);
+}
+
+void pose_table(const double q[4], const double t[3], const double* e, double* pt) {
+    double R[9];
+    R_from_q(q, R);
+    for (int i = 0; i < 9; ++i) pt[i] = R[i];
+    for (int i = 0; i < 3; ++i) pt[9 + i] = t[i];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) pt[12 + 3 * i + j] = e[3 * i] * R[j] + e[3 * i + 1] * R[3 + j] + e[3 * i + 2] * R[6 + j];
+    for (int i = 0; i < 3; ++i) pt[21 + i] = e[3 * i] * t[0] + e[3 * i + 1] * t[1] + e[3 * i + 2] * t[2] + e[9 + i];
+}
+
+}  // namespace
+
+struct lh_handle {
+    lh_options opt;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    bool uploaded = false;
+
+    // window (host copies needed to answer a solve)
+    int P = 0, L = 0, L_act = 0, ncam = 1;
+    int64_t O = 0;
+    uint32_t fixed_mask = 0;
+    lh_params prm{};
+    std::vector<int32_t> lm_perm;      // chunked landmark -> window landmark
+    std::vector<int64_t> obs_perm;     // chunked obs -> window obs
+    std::vector<double> lm_in;         // window input positions (landmarks with no edge keep them)
+    int n_chunks = 0;
+    int tgroup_begin[LH_TMAX + 2] = {0};
+    lh_rs_layout LY{};
+
+    // device buffers
+    DevBuf<lh_chunk> d_chunks;
+    DevBuf<lh_subbatch> d_sbs;
+    DevBuf<uint32_t> d_lm_ptr, d_meta, d_pair_ptr, d_items;
+    DevBuf<uint16_t> d_pair_pq;
+    DevBuf<double> d_uv, d_X, d_Xinit, d_cache, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs,
+        d_rs_stage, d_rs_commit, d_maxd, d_dxp;
+    DevBuf<lh_ctrl> d_ctrl;
+    lh_ctrl* h_ctrl = nullptr;   // pinned
+    int* h_done = nullptr;       // pinned
+
+    // profiling
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> event_pool;
+    size_t event_next = 0;
+    int64_t launches[KC_N] = {0};
+    double total_ms[KC_N] = {0};
+};
+
+namespace {
+
+#define HIPCHK(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) {                                                                          \
+            if (getenv("LH_DEBUG")) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return LH_E_HIP;                                                                             \
+        }                                                                                                \
+    } while (0)
+
+#define NCCLCHK(x)                                                                                       \
+    do {                                                                                                 \
+        ncclResult_t r_ = (x);                                                                           \
+        if (r_ != ncclSuccess) {                                                                         \
+            if (getenv("LH_DEBUG")) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, ncclGetErrorString(r_)); \
+            return LH_E_RCCL;                                                                            \
+        }                                                                                                \
+    } while (0)
+
+hipEvent_t next_event(lh_handle* h) {
+    if (h->event_next == h->event_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        h->event_pool.push_back(e);
+    }
+    return h->event_pool[h->event_next++];
+}
+
+struct Prof {
+    lh_handle* h;
+    int kc;
+    hipEvent_t a = nullptr, b = nullptr;
+    Prof(lh_handle* hh, int k) : h(hh), kc(k) {
+        if (h->opt.profile) {
+            a = next_event(h);
+            b = next_event(h);
+            if (a) (void)hipEventRecord(a, h->stream);
+        }
+    }
+    ~Prof() {
+        if (a && b) {
+            (void)hipEventRecord(b, h->stream);
+            h->pending.push_back({kc, {a, b}});
+        }
+    }
+};
+
+void collect_profile(lh_handle* h) {
+    for (auto& pe : h->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pe.second.first, pe.second.second) == hipSuccess) {
+            h->launches[pe.first] += 1;
+            h->total_ms[pe.first] += ms;
+        }
+    }
+    h->pending.clear();
+    h->event_next = 0;
+}
+
+int validate(const lh_window* w) {
+    if (!w) return LH_E_BADARG;
+    if (w->n_poses < 0 || w->n_landmarks < 0 || w->n_obs < 0) return LH_E_BADARG;
+    if (w->n_poses > 0 && !w->pose_Tcw) return LH_E_BADARG;
+    if (w->n_landmarks > 0 && !w->lm_xyz) return LH_E_BADARG;
+    if (w->n_obs > 0 && (!w->obs_pose || !w->obs_lm || !w->obs_uv)) return LH_E_BADARG;
+    if (w->n_cams < 0 || w->n_cams > LH_MAX_CAMS || (w->n_cams > 0 && !w->cam_ext)) return LH_E_BADARG;
+    const int ncam = w->n_cams > 0 ? w->n_cams : 1;
+    for (int64_t o = 0; o < w->n_obs; ++o) {
+        if (w->obs_pose[o] >= (uint32_t)w->n_poses || w->obs_lm[o] >= (uint32_t)w->n_landmarks) return LH_E_BADARG;
+        if (w->obs_cam && w->obs_cam[o] >= ncam) return LH_E_BADARG;
+    }
+    return LH_OK;
+}
+
+int upload_impl(lh_handle* h, const lh_window* w) {
+    int st = validate(w);
+    if (st != LH_OK) return st;
+    h->uploaded = false;
+    const int P = w->n_poses, L = w->n_landmarks;
+    const int64_t O = w->n_obs;
+    if (h->opt.world_size <= 1 && (O == 0 || (P + L) == 0)) return LH_E_EMPTY;   // problem.cpp:157-161
+    if (P > LH_PMAX) return LH_E_UNSUPPORTED;
+    const int ncam = w->n_cams > 0 ? w->n_cams : 1;
+    h->P = P; h->L = L; h->O = O; h->ncam = ncam;
+    h->fixed_mask = 0;
+    if (w->pose_fixed)
+        for (int p = 0; p < P; ++p)
+            if (w->pose_fixed[p]) h->fixed_mask |= 1u << p;
+
+    // ---- landmark-major CSR, observations in ascending pose order ----
+    std::vector<int64_t> cnt(L + 1, 0);
+    for (int64_t o = 0; o < O; ++o) cnt[w->obs_lm[o] + 1]++;
+    for (int l = 0; l < L; ++l) cnt[l + 1] += cnt[l];
+    std::vector<int64_t> csr(O);
+    {
+        std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+        for (int64_t o = 0; o < O; ++o) csr[pos[w->obs_lm[o]]++] = o;
+    }
+    std::vector<uint32_t> lm_mask(L, 0);
+    std::vector<int> lm_first(L, 0), lm_last(L, 0);
+    for (int l = 0; l < L; ++l) {
+        auto b = csr.begin() + cnt[l], e = csr.begin() + cnt[l + 1];
+        std::sort(b, e, [&](int64_t x, int64_t y) {
+            if (w->obs_pose[x] != w->obs_pose[y]) return w->obs_pose[x] < w->obs_pose[y];
+            return x < y;
+        });
+        uint32_t m = 0;
+        for (auto it = b; it != e; ++it) {
+            const uint32_t bit = 1u << w->obs_pose[*it];
+            if (m & bit) return LH_E_UNSUPPORTED;   // two edges landmark->same pose (DESIGN.md "Limits")
+            m |= bit;
+        }
+        if (e - b > LH_SB_OBS) return LH_E_UNSUPPORTED;
+        if (__builtin_popcount(m) > LH_UMAX) return LH_E_UNSUPPORTED;
+        lm_mask[l] = m;
+        if (m) { lm_first[l] = __builtin_ctz(m); lm_last[l] = 31 - __builtin_clz(m); }
+    }
+
+    // ---- landmark order: by observation span, so chunks share small windows ----
+    std::vector<int32_t> order;
+    order.reserve(L);
+    for (int l = 0; l < L; ++l)
+        if (lm_mask[l]) order.push_back(l);   // landmarks without edges are not vertices (backend_lego.cpp:126)
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        if (lm_first[a] != lm_first[b]) return lm_first[a] < lm_first[b];
+        if (lm_last[a] != lm_last[b]) return lm_last[a] < lm_last[b];
+        return lm_mask[a] < lm_mask[b];
+    });
+    const int Lact = (int)order.size();
+    int chunk_lm = (int)((Lact + 511) / 512);
+    chunk_lm = ((chunk_lm + LH_SB_LM - 1) / LH_SB_LM) * LH_SB_LM;
+    chunk_lm = std::max(32, std::min(256, chunk_lm));
+
+    struct ChunkTmp { std::vector<int32_t> lms; uint32_t mask; };
+    std::vector<ChunkTmp> ctmp;
+    for (int32_t l : order) {
+        const uint32_t m = lm_mask[l];
+        if (ctmp.empty() || (int)ctmp.back().lms.size() >= chunk_lm ||
+            __builtin_popcount(ctmp.back().mask | m) > LH_UMAX) {
+            ctmp.push_back(ChunkTmp{{}, 0u});
+        }
+        ctmp.back().lms.push_back(l);
+        ctmp.back().mask |= m;
+    }
+    // group chunks by MFMA tile count T (one launch per T)
+    auto chunkT = [](uint32_t mask) { return (6 * __builtin_popcount(mask) + 15) / 16; };
+    std::vector<int> corder(ctmp.size());
+    std::iota(corder.begin(), corder.end(), 0);
+    std::stable_sort(corder.begin(), corder.end(), [&](int a, int b) { return chunkT(ctmp[a].mask) < chunkT(ctmp[b].mask); });
+
+    std::vector<lh_chunk> chunks;
+    std::vector<lh_subbatch> sbs;
+    std::vector<uint32_t> lm_ptr;
+    std::vector<uint32_t> meta;
+    std::vector<double> uv, Xinit;
+    h->lm_perm.clear();
+    h->obs_perm.clear();
+    lm_ptr.reserve(Lact + 1);
+    meta.reserve(O);
+    uv.reserve(2 * O);
+    Xinit.reserve(3 * (size_t)Lact);
+    h->obs_perm.reserve(O);
+    h->lm_perm.reserve(Lact);
+    for (int T = 0; T <= LH_TMAX + 1; ++T) h->tgroup_begin[T] = 0;
+    int slot_of[32];
+    for (int ci : corder) {
+        const ChunkTmp& c = ctmp[ci];
+        lh_chunk ck{};
+        const int U = __builtin_popcount(c.mask);
+        ck.U = (uint8_t)U;
+        ck.T = (uint8_t)chunkT(c.mask);
+        {
+            int s = 0;
+            for (int p = 0; p < 32; ++p) {
+                if (c.mask & (1u << p)) { ck.pose[s] = (uint16_t)p; slot_of[p] = s; ++s; }
+            }
+        }
+        ck.sb_begin = (uint32_t)sbs.size();
+        lh_subbatch sb{};
+        bool open = false;
+        for (int32_t l : c.lms) {
+            const int k = (int)(cnt[l + 1] - cnt[l]);
+            if (!open || sb.n_lm >= LH_SB_LM || sb.n_obs + k > LH_SB_OBS) {
+                if (open) sbs.push_back(sb);
+                sb = lh_subbatch{};
+                sb.lm_begin = (uint32_t)h->lm_perm.size();
+                sb.obs_begin = (uint32_t)h->obs_perm.size();
+                open = true;
+            }
+            const int lms = sb.n_lm;
+            lm_ptr.push_back((uint32_t)h->obs_perm.size());
+            h->lm_perm.push_back(l);
+            for (int a = 0; a < 3; ++a) Xinit.push_back(w->lm_xyz[3 * (size_t)l + a]);
+            for (int64_t q = cnt[l]; q < cnt[l + 1]; ++q) {
+                const int64_t o = csr[q];
+                const uint32_t p = w->obs_pose[o];
+                const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
+                meta.push_back(LH_META(p, cam, slot_of[p], lms));
+                uv.push_back(w->obs_uv[2 * o]);
+                uv.push_back(w->obs_uv[2 * o + 1]);
+                h->obs_perm.push_back(o);
+            }
+            sb.n_lm++;
+            sb.n_obs = (uint16_t)(sb.n_obs + k);
+        }
+        if (open) sbs.push_back(sb);
+        ck.sb_end = (uint32_t)sbs.size();
+        chunks.push_back(ck);
+    }
+    lm_ptr.push_back((uint32_t)h->obs_perm.size());
+    h->n_chunks = (int)chunks.size();
+    // T group boundaries
+    {
+        int c = 0;
+        for (int T = 1; T <= LH_TMAX + 1; ++T) {
+            h->tgroup_begin[T] = c;
+            while (c < h->n_chunks && chunks[c].T == T) ++c;
+        }
+        h->tgroup_begin[LH_TMAX + 1] = h->n_chunks;
+    }
+
+    // ---- reduce plan: for every pose pair (p <= q) the chunks touching it ----
+    const int npairs = P * (P + 1) / 2;
+    std::vector<uint16_t> pair_pq(2 * (size_t)std::max(npairs, 1));
+    std::vector<std::vector<uint32_t>> plist(npairs);
+    {
+        int b = 0;
+        for (int p = 0; p < P; ++p)
+            for (int q = p; q < P; ++q, ++b) { pair_pq[2 * b] = (uint16_t)p; pair_pq[2 * b + 1] = (uint16_t)q; }
+    }
+    for (int ci = 0; ci < h->n_chunks; ++ci) {
+        const lh_chunk& ck = chunks[ci];
+        for (int s = 0; s < ck.U; ++s)
+            for (int t = s; t < ck.U; ++t) {
+                const int p = ck.pose[s], q = ck.pose[t];
+                const int b = p * P - (p * (p - 1)) / 2 + (q - p);
+                plist[b].push_back(((uint32_t)ci << 8) | ((uint32_t)s << 4) | (uint32_t)t);
+            }
+    }
+    std::vector<uint32_t> pair_ptr(npairs + 1, 0), items;
+    for (int b = 0; b < npairs; ++b) {
+        pair_ptr[b + 1] = pair_ptr[b] + (uint32_t)plist[b].size();
+        items.insert(items.end(), plist[b].begin(), plist[b].end());
+    }
+
+    // ---- camera extrinsics and initial pose tables ----
+    std::vector<double> ext(12 * (size_t)ncam);
+    for (int c = 0; c < ncam; ++c) {
+        if (w->n_cams > 0) {
+            // SE3(estimate) round trip: R_e = R(q(R_in)) as Sophus stores it
+            const double* E = w->cam_ext + 12 * c;
+            double R[9] = {E[0], E[1], E[2], E[4], E[5], E[6], E[8], E[9], E[10]}, q[4], Rq[9];
+            q_from_R(R, q);
+            R_from_q(q, Rq);
+            for (int i = 0; i < 9; ++i) ext[12 * c + i] = Rq[i];
+            ext[12 * c + 9] = E[3]; ext[12 * c + 10] = E[7]; ext[12 * c + 11] = E[11];
+        } else {
+            const double I[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+            std::memcpy(&ext[12 * c], I, sizeof(I));
+        }
+    }
+    std::vector<double> qt(8 * (size_t)P * 2, 0.0), ptab(2 * (size_t)P * ncam * LH_PT);
+    for (int p = 0; p < P; ++p) {
+        const double* T = w->pose_Tcw + 12 * p;
+        double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]}, q[4];
+        q_from_R(R, q);
+        double t[3] = {T[3], T[7], T[11]};
+        for (int s = 0; s < 2; ++s) {
+            double* o = &qt[8 * ((size_t)s * P + p)];
+            for (int i = 0; i < 4; ++i) o[i] = q[i];
+            for (int i = 0; i < 3; ++i) o[4 + i] = t[i];
+            for (int c = 0; c < ncam; ++c) pose_table(q, t, &ext[12 * c], &ptab[((size_t)s * P * ncam + (size_t)p * ncam + c) * LH_PT]);
+        }
+    }
+
+    // ---- params ----
+    lh_params& prm = h->prm;
+    prm.P = P;
+    prm.n = 6 * P;
+    prm.ncam = ncam;
+    prm.max_iters = h->opt.max_iters;
+    prm.max_trials = h->opt.max_trials;
+    prm.strategy = h->opt.strategy;
+    prm.guard = h->opt.degenerate_guard;
+    prm.lambda_given = h->opt.lambda_init >= 0.0;
+    prm.huber_delta = h->opt.huber_delta;
+    prm.stop_dchi2 = h->opt.stop_dchi2;
+    prm.tau = h->opt.tau;
+    prm.lambda_cap = h->opt.lambda_cap;
+    prm.lambda_init = h->opt.lambda_init;
+    for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
+    h->LY = lh_rs_make(P);
+    h->L_act = Lact;
+    h->lm_in.assign(w->lm_xyz, w->lm_xyz + 3 * (size_t)L);
+
+    // ---- device buffers ----
+    const size_t PT = (size_t)P * ncam * LH_PT;
+    HIPCHK(h->d_chunks.ensure(chunks.size()));
+    HIPCHK(h->d_sbs.ensure(sbs.size()));
+    HIPCHK(h->d_lm_ptr.ensure(lm_ptr.size()));
+    HIPCHK(h->d_meta.ensure(meta.size()));
+    HIPCHK(h->d_uv.ensure(uv.size()));
+    HIPCHK(h->d_pair_ptr.ensure(pair_ptr.size()));
+    HIPCHK(h->d_items.ensure(items.size()));
+    HIPCHK(h->d_pair_pq.ensure(pair_pq.size()));
+    HIPCHK(h->d_Xinit.ensure(Xinit.size()));
+    HIPCHK(h->d_X.ensure(2 * Xinit.size()));
+    HIPCHK(h->d_cache.ensure(2 * (size_t)Lact * LH_CACHE));
+    HIPCHK(h->d_ptab.ensure(2 * PT));
+    HIPCHK(h->d_ptab_init.ensure(2 * PT));
+    HIPCHK(h->d_qt.ensure(qt.size()));
+    HIPCHK(h->d_qt_init.ensure(qt.size()));
+    HIPCHK(h->d_ext.ensure(ext.size()));
+    HIPCHK(h->d_rho.ensure((size_t)O));
+    HIPCHK(h->d_slabs.ensure((size_t)h->n_chunks * LH_SLAB_STRIDE));
+    HIPCHK(h->d_rs_stage.ensure(h->LY.total));
+    HIPCHK(h->d_rs_commit.ensure(h->LY.total));
+    HIPCHK(h->d_maxd.ensure(1));
+    HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
+    HIPCHK(h->d_ctrl.ensure(1));
+    hipStream_t s = h->stream;
+    auto up = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+    };
+    HIPCHK(up(h->d_chunks.p, chunks.data(), chunks.size() * sizeof(lh_chunk)));
+    HIPCHK(up(h->d_sbs.p, sbs.data(), sbs.size() * sizeof(lh_subbatch)));
+    HIPCHK(up(h->d_lm_ptr.p, lm_ptr.data(), lm_ptr.size() * sizeof(uint32_t)));
+    HIPCHK(up(h->d_meta.p, meta.data(), meta.size() * sizeof(uint32_t)));
+    HIPCHK(up(h->d_uv.p, uv.data(), uv.size() * sizeof(double)));
+    HIPCHK(up(h->d_pair_ptr.p, pair_ptr.data(), pair_ptr.size() * sizeof(uint32_t)));
+    HIPCHK(up(h->d_items.p, items.data(), items.size() * sizeof(uint32_t)));
+    HIPCHK(up(h->d_pair_pq.p, pair_pq.data(), pair_pq.size() * sizeof(uint16_t)));
+    HIPCHK(up(h->d_Xinit.p, Xinit.data(), Xinit.size() * sizeof(double)));
+    HIPCHK(up(h->d_ptab_init.p, ptab.data(), ptab.size() * sizeof(double)));
+    HIPCHK(up(h->d_qt_init.p, qt.data(), qt.size() * sizeof(double)));
+    HIPCHK(up(h->d_ext.p, ext.data(), ext.size() * sizeof(double)));
+    HIPCHK(hipStreamSynchronize(s));   // host vectors die at return
+    h->uploaded = true;
+    return LH_OK;
+}
+
+int enqueue_trial(lh_handle* h, int mode) {
+    hipStream_t s = h->stream;
+    {
+        Prof pr(h, mode == 0 ? KC_INIT : KC_LIN);
+        for (int T = 1; T <= LH_TMAX; ++T) {
+            const int c0 = h->tgroup_begin[T], c1 = h->tgroup_begin[T + 1];
+            HIPCHK(lh_launch_lin(T, mode, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_lm_ptr.p, h->d_uv.p,
+                                 h->d_meta.p, h->d_X.p, h->d_cache.p, h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p,
+                                 h->d_rho.p, h->d_slabs.p, h->prm, h->L_act, h->fixed_mask));
+        }
+    }
+    {
+        Prof pr(h, KC_REDUCE);
+        HIPCHK(lh_launch_reduce(s, h->d_chunks.p, h->d_slabs.p, h->d_pair_ptr.p, h->d_items.p, h->d_pair_pq.p,
+                                h->d_ctrl.p, h->d_rs_stage.p, h->d_maxd.p, h->prm, h->n_chunks));
+    }
+    if (h->comm) {
+        Prof pr(h, KC_ALLREDUCE);
+        if (mode == 0) NCCLCHK(ncclAllReduce(h->d_maxd.p, h->d_maxd.p, 1, ncclFloat64, ncclMax, h->comm, s));
+        NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
+    }
+    {
+        Prof pr(h, KC_CTRL);
+        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_qt.p, h->d_ptab.p,
+                              h->d_ext.p, h->d_dxp.p, h->prm, mode, nullptr));
+    }
+    return LH_OK;
+}
+
+int solve_resident_impl(lh_handle* h, lh_result* out) {
+    if (!h->uploaded) return LH_E_STATE;
+    hipStream_t s = h->stream;
+    const int P = h->P;
+    const size_t PT = (size_t)P * h->ncam * LH_PT;
+    // restart from the uploaded initial state
+    HIPCHK(hipMemcpyAsync(h->d_X.p, h->d_Xinit.p, 3 * (size_t)h->L_act * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_qt.p, h->d_qt_init.p, 16 * (size_t)P * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_ptab.p, h->d_ptab_init.p, 2 * PT * sizeof(double), hipMemcpyDeviceToDevice, s));
+    std::memset(h->h_ctrl, 0, sizeof(lh_ctrl));
+    h->h_ctrl->cur = 0;
+    HIPCHK(hipMemcpyAsync(h->d_ctrl.p, h->h_ctrl, sizeof(lh_ctrl), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(h->d_dxp.p, 0, 6 * (size_t)std::max(P, 1) * sizeof(double), s));
+
+    hipEvent_t e0 = next_event(h), e1 = next_event(h);
+    if (!e0 || !e1) return LH_E_HIP;
+    HIPCHK(hipEventRecord(e0, s));
+    int st = enqueue_trial(h, 0);
+    if (st != LH_OK) return st;
+    const int max_total = std::max(0, h->opt.max_iters) * std::max(1, h->opt.max_trials);
+    int batch = h->opt.trials_per_sync > 0 ? h->opt.trials_per_sync : 4;
+    int enq = 0;
+    while (enq < max_total) {
+        const int nb = std::min(batch, max_total - enq);
+        for (int i = 0; i < nb; ++i) {
+            st = enqueue_trial(h, 1);
+            if (st != LH_OK) return st;
+        }
+        enq += nb;
+        HIPCHK(hipMemcpyAsync(h->h_done, &h->d_ctrl.p->done, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (*h->h_done) break;
+    }
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipMemcpyAsync(h->h_ctrl, h->d_ctrl.p, sizeof(lh_ctrl), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    const lh_ctrl& c = *h->h_ctrl;
+    const int cur = c.cur;
+
+    if (out) {
+        out->iterations = c.iter;
+        out->trials = c.trials;
+        out->accepted = c.accepted;
+        out->chi2_initial = c.chi2_initial;
+        out->chi2_final = c.chi;
+        out->lambda_final = c.lambda;
+        out->time_ms = ms;
+        out->trace_len = std::min(c.trace_len, std::min(out->trace_cap, LH_TRACE));
+        for (int i = 0; i < out->trace_len; ++i) {
+            if (out->trace_chi2) out->trace_chi2[i] = c.trace_chi[i];
+            if (out->trace_lambda) out->trace_lambda[i] = c.trace_lambda[i];
+        }
+        if (out->pose_Tcw) {
+            std::vector<double> qt(8 * (size_t)P);
+            if (P) HIPCHK(hipMemcpy(qt.data(), h->d_qt.p + 8 * (size_t)cur * P, qt.size() * sizeof(double), hipMemcpyDeviceToHost));
+            for (int p = 0; p < P; ++p) {
+                double R[9];
+                R_from_q(&qt[8 * p], R);   // SE3::matrix() (lego_types.h:90)
+                double* T = out->pose_Tcw + 12 * p;
+                for (int i = 0; i < 3; ++i) {
+                    T[4 * i] = R[3 * i]; T[4 * i + 1] = R[3 * i + 1]; T[4 * i + 2] = R[3 * i + 2];
+                    T[4 * i + 3] = qt[8 * p + 4 + i];
+                }
+            }
+        }
+        if (out->lm_xyz) {
+            std::memcpy(out->lm_xyz, h->lm_in.data(), h->lm_in.size() * sizeof(double));
+            std::vector<double> X(3 * (size_t)h->L_act);
+            if (h->L_act) HIPCHK(hipMemcpy(X.data(), h->d_X.p + 3 * (size_t)cur * h->L_act, X.size() * sizeof(double), hipMemcpyDeviceToHost));
+            for (int i = 0; i < h->L_act; ++i)
+                for (int a = 0; a < 3; ++a) out->lm_xyz[3 * (size_t)h->lm_perm[i] + a] = X[3 * (size_t)i + a];
+        }
+        if (out->edge_robust_chi2) {
+            std::vector<double> r((size_t)h->O);
+            if (h->O) HIPCHK(hipMemcpy(r.data(), h->d_rho.p, r.size() * sizeof(double), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < h->O; ++i) out->edge_robust_chi2[h->obs_perm[i]] = r[i];
+        }
+    }
+    if (h->opt.verbose) {
+        printf("==========LEGO OPTIMIZER (MI355X)==========\n");
+        for (int i = 0; i < std::min(c.trace_len, LH_TRACE); ++i)
+            printf("Iteration = %d,\tChi = %g,\tLambda = %g\n", i, c.trace_chi[i], c.trace_lambda[i]);
+        printf("\nInfo: \nTimeCost(SolveProblem) = %g ms\n", (double)ms);
+    }
+    if (h->opt.profile) collect_profile(h);
+    else h->event_next = 0;
+    return LH_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+const char* lh_strerror(int status) {
+    switch (status) {
+        case LH_OK: return "ok";
+        case LH_E_EMPTY: return "empty problem: no vertices or no edges";
+        case LH_E_BADARG: return "bad argument";
+        case LH_E_HIP: return "HIP runtime error";
+        case LH_E_RCCL: return "RCCL error";
+        case LH_E_UNSUPPORTED: return "window outside the supported envelope";
+        case LH_E_STATE: return "call out of order";
+        default: return "unknown status";
+    }
+}
+
+const char* lh_kernel_name(int kc) { return (kc >= 0 && kc < KC_N) ? kKernelNames[kc] : ""; }
+
+void lh_default_options(lh_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->abi_version = LH_ABI_VERSION;
+    o->max_iters = 10;
+    o->max_trials = 10;
+    o->strategy = LH_STRATEGY_DEFAULT;
+    o->huber_delta = 5.991;
+    o->stop_dchi2 = 1e-5;
+    o->tau = 1e-5;
+    o->lambda_cap = 5e10;
+    o->lambda_init = -1.0;
+    o->linear_solver = LH_SOLVER_LDLT;
+    o->verbose = 0;
+    o->device = -1;
+    o->world_size = 1;
+    o->rank = 0;
+    o->degenerate_guard = 0;
+    o->trials_per_sync = 0;
+    o->profile = 0;
+}
+
+int lh_comm_unique_id(uint8_t out[128]) {
+    if (!out) return LH_E_BADARG;
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(out, &id, 128);
+    return LH_OK;
+}
+
+int lh_create(lh_handle** hp, const lh_options* opt) {
+    if (!hp || !opt) return LH_E_BADARG;
+    *hp = nullptr;
+    if (opt->abi_version != LH_ABI_VERSION) return LH_E_BADARG;
+    if (opt->max_iters < 0 || opt->max_trials < 0 || opt->world_size < 1 || opt->rank < 0 ||
+        opt->rank >= opt->world_size || (opt->strategy != 0 && opt->strategy != 1))
+        return LH_E_BADARG;
+    if (opt->linear_solver != LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
+    lh_handle* h = new (std::nothrow) lh_handle();
+    if (!h) return LH_E_HIP;
+    h->opt = *opt;
+    int dev = opt->device;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) { delete h; return LH_E_HIP; }
+    }
+    if (hipSetDevice(dev) != hipSuccess) { delete h; return LH_E_HIP; }
+    h->device = dev;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return LH_E_HIP; }
+    if (hipHostMalloc((void**)&h->h_ctrl, sizeof(lh_ctrl), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_done, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        lh_destroy(h);
+        return LH_E_HIP;
+    }
+    if (opt->world_size > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, opt->comm_id, sizeof(id));
+        if (ncclCommInitRank(&h->comm, opt->world_size, id, opt->rank) != ncclSuccess) {
+            h->comm = nullptr;
+            lh_destroy(h);
+            return LH_E_RCCL;
+        }
+    }
+    *hp = h;
+    return LH_OK;
+}
+
+void lh_destroy(lh_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->comm) ncclCommDestroy(h->comm);
+    for (auto e : h->event_pool) (void)hipEventDestroy(e);
+    h->d_chunks.release(); h->d_sbs.release(); h->d_lm_ptr.release(); h->d_meta.release();
+    h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release();
+    h->d_uv.release(); h->d_X.release(); h->d_Xinit.release(); h->d_cache.release(); h->d_ptab.release();
+    h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
+    h->d_slabs.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_maxd.release(); h->d_dxp.release();
+    h->d_ctrl.release();
+    if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
+    if (h->h_done) (void)hipHostFree(h->h_done);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int lh_upload(lh_handle* h, const lh_window* in) {
+    if (!h) return LH_E_BADARG;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    try {
+        return upload_impl(h, in);
+    } catch (const std::bad_alloc&) {
+        return LH_E_HIP;
+    } catch (...) {
+        return LH_E_BADARG;
+    }
+}
+
+int lh_solve_resident(lh_handle* h, lh_result* out) {
+    if (!h) return LH_E_BADARG;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    try {
+        return solve_resident_impl(h, out);
+    } catch (...) {
+        return LH_E_HIP;
+    }
+}
+
+int lh_solve(lh_handle* h, const lh_window* in, lh_result* out) {
+    int st = lh_upload(h, in);
+    if (st != LH_OK) return st;
+    return lh_solve_resident(h, out);
+}
+
+int lh_kernel_stats_get(lh_handle* h, lh_kernel_stats* out) {
+    if (!h || !out) return LH_E_BADARG;
+    for (int i = 0; i < KC_N; ++i) { out->launches[i] = h->launches[i]; out->total_ms[i] = h->total_ms[i]; }
+    return LH_OK;
+}
+
+int lh_set_profiling(lh_handle* h, int on) {
+    if (!h) return LH_E_BADARG;
+    h->opt.profile = on ? 1 : 0;
+    return LH_OK;
+}
+
+void lh_kernel_stats_reset(lh_handle* h) {
+    if (!h) return;
+    for (int i = 0; i < KC_N; ++i) { h->launches[i] = 0; h->total_ms[i] = 0.0; }
+}
+
+int lh_classify_outliers(const double* rchi2, int64_t n_obs, double chi2_th, uint8_t* is_outlier, double* th_out,
+                         int64_t* n_inlier, int64_t* n_outlier) {
+    if (n_obs < 0 || (n_obs > 0 && !rchi2)) return LH_E_BADARG;
+    // backend_lego.cpp:164-184
+    int64_t cin = 0, cout = 0;
+    int iteration = 0;
+    while (iteration < 5) {
+        cout = 0;
+        cin = 0;
+        for (int64_t i = 0; i < n_obs; ++i) {
+            if (rchi2[i] > chi2_th) cout++;
+            else cin++;
+        }
+        double ratio = cin / double(cin + cout);
+        if (ratio > 0.5) break;
+        chi2_th *= 2;
+        iteration++;
+    }
+    // :186-194
+    if (is_outlier)
+        for (int64_t i = 0; i < n_obs; ++i) is_outlier[i] = rchi2[i] > chi2_th ? 1 : 0;
+    if (th_out) *th_out = chi2_th;
+    if (n_inlier) *n_inlier = cin;
+    if (n_outlier) *n_outlier = cout;
+    return LH_OK;
+}
+
+// test hook: f64 MFMA accumulator layout probe (A 16x4 row-major, B 4x16, D 16x16), device pointers
+int lh_debug_mfma_probe(const double* A, const double* B, double* D) {
+    if (lh_launch_mfma_probe(A, B, D) != hipSuccess) return LH_E_HIP;
+    if (hipDeviceSynchronize() != hipSuccess) return LH_E_HIP;
+    return LH_OK;
+}
+
+}  // extern "C"

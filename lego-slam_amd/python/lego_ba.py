@@ -1,0 +1,336 @@
+"""
+lego_ba — ctypes bindings for the MI355X BA solver C ABI (include/lego_ba.h)
+and for the synthetic window generator (lego-slam_amd/tools/lh_window.h).
+
+This is plumbing for tests/bench: the product is liblego_ba.so (HIP kernels +
+C ABI); this module only marshals numpy arrays across that boundary.  It never
+falls back to a CPU path: if liblego_ba.so is missing, Solver() raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # lego-slam_amd/
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+BA_LIB = os.path.join(LIB_DIR, "liblego_ba.so")
+WIN_LIB = os.path.join(LIB_DIR, "liblego_window.so")
+
+# --------------------------------------------------------------------------
+# window generator
+# --------------------------------------------------------------------------
+
+
+class LhwParams(C.Structure):
+    _fields_ = [
+        ("n_poses", C.c_int32), ("n_landmarks", C.c_int32),
+        ("k_min", C.c_int32), ("k_max", C.c_int32),
+        ("pose_mode", C.c_int32), ("seed", C.c_uint64),
+        ("noise_px", C.c_double), ("outlier_frac", C.c_double),
+        ("right_frac", C.c_double), ("baseline", C.c_double),
+        ("step_m", C.c_double), ("yaw_sigma", C.c_double),
+        ("depth_min", C.c_double), ("depth_max", C.c_double),
+        ("pose_rot_sigma", C.c_double), ("pose_trans_sigma", C.c_double),
+        ("lm_sigma", C.c_double), ("K", C.c_double * 4),
+        ("width", C.c_double), ("height", C.c_double),
+    ]
+
+
+_winlib = None
+
+
+def _wl():
+    global _winlib
+    if _winlib is None:
+        if not os.path.exists(WIN_LIB):
+            raise RuntimeError(f"{WIN_LIB} not built (run __graft_entry__.build())")
+        lib = C.CDLL(WIN_LIB)
+        lib.lhw_default_params.argtypes = [C.POINTER(LhwParams)]
+        lib.lhw_count_obs.argtypes = [C.POINTER(LhwParams), C.c_int32, C.c_int32]
+        lib.lhw_count_obs.restype = C.c_int64
+        lib.lhw_poses.argtypes = [C.POINTER(LhwParams), C.c_void_p, C.c_void_p]
+        lib.lhw_cameras.argtypes = [C.POINTER(LhwParams), C.c_void_p]
+        lib.lhw_landmarks.argtypes = [C.POINTER(LhwParams), C.c_int32, C.c_int32] + [C.c_void_p] * 6
+        lib.lhw_landmarks.restype = C.c_int64
+        _winlib = lib
+    return _winlib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# Named configurations (BASELINE.json "configs").
+CONFIGS = {
+    "C1": dict(P=5, L=200, k=5),        # CPU plumbing window
+    "mini": dict(P=10, L=500, k=8),
+    "C2": dict(P=10, L=5000, k=8),
+    "C3": dict(P=20, L=50000, k=8),     # bench workload (metric window)
+    "C4": dict(P=20, L=500000, k=8),    # 8-GPU window
+}
+
+
+def window_params(P=20, L=50000, k=8, k_max=None, seed=0, **kw):
+    p = LhwParams()
+    _wl().lhw_default_params(C.byref(p))
+    p.n_poses, p.n_landmarks, p.k_min = P, L, k
+    p.k_max = k if k_max is None else k_max
+    p.seed = seed
+    for name, v in kw.items():
+        if name == "K":
+            for i in range(4):
+                p.K[i] = v[i]
+        else:
+            setattr(p, name, v)
+    return p
+
+
+def generate_window(P=20, L=50000, k=8, seed=0, lm_begin=0, lm_end=None, **kw):
+    """Generate landmarks [lm_begin, lm_end) of a synthetic window (all poses)."""
+    p = window_params(P=P, L=L, k=k, seed=seed, **kw)
+    lib = _wl()
+    lm_end = L if lm_end is None else lm_end
+    n_lm = lm_end - lm_begin
+    n_obs = lib.lhw_count_obs(C.byref(p), lm_begin, lm_end)
+    w = dict(
+        n_poses=P,
+        pose_true=np.zeros((P, 12)), pose_Tcw=np.zeros((P, 12)),
+        lm_true=np.zeros((n_lm, 3)), lm_xyz=np.zeros((n_lm, 3)),
+        obs_pose=np.zeros(n_obs, np.uint32), obs_lm=np.zeros(n_obs, np.uint32),
+        obs_cam=np.zeros(n_obs, np.uint8), obs_uv=np.zeros((n_obs, 2)),
+        cam_ext=np.zeros((2, 12)), K=np.array(list(p.K)),
+    )
+    lib.lhw_poses(C.byref(p), _ptr(w["pose_true"]), _ptr(w["pose_Tcw"]))
+    lib.lhw_cameras(C.byref(p), _ptr(w["cam_ext"]))
+    got = lib.lhw_landmarks(C.byref(p), lm_begin, lm_end, _ptr(w["lm_true"]), _ptr(w["lm_xyz"]),
+                            _ptr(w["obs_pose"]), _ptr(w["obs_lm"]), _ptr(w["obs_cam"]), _ptr(w["obs_uv"]))
+    assert got == n_obs, (got, n_obs)
+    return w
+
+
+def config_window(name, seed=0, **kw):
+    c = dict(CONFIGS[name])
+    c.update(kw)
+    return generate_window(seed=seed, **c)
+
+
+# --------------------------------------------------------------------------
+# solver C ABI (include/lego_ba.h)
+# --------------------------------------------------------------------------
+
+LH_OK, LH_E_EMPTY, LH_E_BADARG, LH_E_HIP, LH_E_RCCL, LH_E_UNSUPPORTED, LH_E_STATE = range(7)
+
+
+class LhOptions(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("max_iters", C.c_int32), ("max_trials", C.c_int32),
+        ("strategy", C.c_int32), ("huber_delta", C.c_double), ("stop_dchi2", C.c_double),
+        ("tau", C.c_double), ("lambda_cap", C.c_double), ("lambda_init", C.c_double),
+        ("linear_solver", C.c_int32), ("verbose", C.c_int32), ("device", C.c_int32),
+        ("world_size", C.c_int32), ("rank", C.c_int32), ("degenerate_guard", C.c_int32),
+        ("trials_per_sync", C.c_int32), ("profile", C.c_int32), ("comm_id", C.c_uint8 * 128),
+    ]
+
+
+class LhWindow(C.Structure):
+    _fields_ = [
+        ("n_poses", C.c_int32), ("pose_Tcw", C.c_void_p), ("pose_fixed", C.c_void_p),
+        ("n_landmarks", C.c_int32), ("lm_xyz", C.c_void_p),
+        ("n_obs", C.c_int64), ("obs_pose", C.c_void_p), ("obs_lm", C.c_void_p),
+        ("obs_cam", C.c_void_p), ("obs_uv", C.c_void_p),
+        ("K", C.c_double * 4), ("n_cams", C.c_int32), ("cam_ext", C.c_void_p),
+    ]
+
+
+class LhResult(C.Structure):
+    _fields_ = [
+        ("pose_Tcw", C.c_void_p), ("lm_xyz", C.c_void_p), ("edge_robust_chi2", C.c_void_p),
+        ("trace_chi2", C.c_void_p), ("trace_lambda", C.c_void_p), ("trace_cap", C.c_int32),
+        ("trace_len", C.c_int32), ("iterations", C.c_int32), ("trials", C.c_int32),
+        ("accepted", C.c_int32), ("chi2_initial", C.c_double), ("chi2_final", C.c_double),
+        ("lambda_final", C.c_double), ("time_ms", C.c_double),
+    ]
+
+
+class LhKernelStats(C.Structure):
+    _fields_ = [("launches", C.c_int64 * 8), ("total_ms", C.c_double * 8)]
+
+
+# every symbol include/lego_ba.h declares (tests check the .so exports them all)
+ABI_SYMBOLS = [
+    "lh_strerror", "lh_default_options", "lh_kernel_name", "lh_comm_unique_id",
+    "lh_create", "lh_destroy", "lh_solve", "lh_upload", "lh_solve_resident",
+    "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
+]
+
+_balib = None
+
+
+def ba_lib():
+    """Load liblego_ba.so.  Raises if it is missing: there is no fallback."""
+    global _balib
+    if _balib is None:
+        if not os.path.exists(BA_LIB):
+            raise RuntimeError(f"{BA_LIB} not built: the HIP extension is required (no CPU fallback)")
+        lib = C.CDLL(BA_LIB)
+        lib.lh_strerror.restype = C.c_char_p
+        lib.lh_strerror.argtypes = [C.c_int]
+        lib.lh_default_options.argtypes = [C.POINTER(LhOptions)]
+        lib.lh_kernel_name.restype = C.c_char_p
+        lib.lh_kernel_name.argtypes = [C.c_int]
+        lib.lh_comm_unique_id.argtypes = [C.c_void_p]
+        lib.lh_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(LhOptions)]
+        lib.lh_destroy.argtypes = [C.c_void_p]
+        lib.lh_solve.argtypes = [C.c_void_p, C.POINTER(LhWindow), C.POINTER(LhResult)]
+        lib.lh_upload.argtypes = [C.c_void_p, C.POINTER(LhWindow)]
+        lib.lh_solve_resident.argtypes = [C.c_void_p, C.POINTER(LhResult)]
+        lib.lh_kernel_stats_get.argtypes = [C.c_void_p, C.POINTER(LhKernelStats)]
+        lib.lh_kernel_stats_reset.argtypes = [C.c_void_p]
+        lib.lh_set_profiling.argtypes = [C.c_void_p, C.c_int]
+        lib.lh_classify_outliers.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]
+        _balib = lib
+    return _balib
+
+
+def default_options(**kw):
+    o = LhOptions()
+    ba_lib().lh_default_options(C.byref(o))
+    for k, v in kw.items():
+        if k == "comm_id":
+            for i in range(128):
+                o.comm_id[i] = v[i]
+        else:
+            setattr(o, k, v)
+    return o
+
+
+class LhError(RuntimeError):
+    def __init__(self, status, where):
+        self.status = status
+        msg = ba_lib().lh_strerror(status).decode()
+        super().__init__(f"{where}: {msg} ({status})")
+
+
+def _check(st, where):
+    if st != LH_OK:
+        raise LhError(st, where)
+
+
+def _as(a, dt):
+    return None if a is None else np.ascontiguousarray(a, dtype=dt)
+
+
+class _WindowRef:
+    """Keeps the numpy arrays an LhWindow points to alive."""
+
+    def __init__(self, w):
+        self.arrays = dict(
+            pose=_as(w["pose_Tcw"], np.float64), fixed=_as(w.get("pose_fixed"), np.uint8),
+            lm=_as(w["lm_xyz"], np.float64), op=_as(w["obs_pose"], np.uint32),
+            ol=_as(w["obs_lm"], np.uint32), oc=_as(w.get("obs_cam"), np.uint8),
+            uv=_as(w["obs_uv"], np.float64), ext=_as(w.get("cam_ext"), np.float64),
+        )
+        a = self.arrays
+        s = LhWindow()
+        s.n_poses = a["pose"].shape[0]
+        s.pose_Tcw = _ptr(a["pose"])
+        s.pose_fixed = _ptr(a["fixed"])
+        s.n_landmarks = a["lm"].shape[0]
+        s.lm_xyz = _ptr(a["lm"])
+        s.n_obs = a["op"].shape[0]
+        s.obs_pose, s.obs_lm, s.obs_cam, s.obs_uv = _ptr(a["op"]), _ptr(a["ol"]), _ptr(a["oc"]), _ptr(a["uv"])
+        for i in range(4):
+            s.K[i] = float(w["K"][i])
+        s.n_cams = 0 if a["ext"] is None else a["ext"].shape[0]
+        s.cam_ext = _ptr(a["ext"])
+        self.s = s
+
+
+class Solver:
+    """One lh_handle (one GPU / one landmark shard)."""
+
+    def __init__(self, **opts):
+        lib = ba_lib()
+        self.opts = default_options(**opts)
+        h = C.c_void_p()
+        _check(lib.lh_create(C.byref(h), C.byref(self.opts)), "lh_create")
+        self.h = h
+        self._win = None
+
+    def close(self):
+        if self.h:
+            ba_lib().lh_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _result(self, n_poses, n_lm, n_obs, trace_cap=64, want_states=True, want_edges=True):
+        out = dict(
+            pose_Tcw=np.zeros((n_poses, 12)) if want_states else None,
+            lm_xyz=np.zeros((n_lm, 3)) if want_states else None,
+            edge_robust_chi2=np.zeros(n_obs) if want_edges else None,
+            trace_chi2=np.zeros(trace_cap), trace_lambda=np.zeros(trace_cap),
+        )
+        r = LhResult()
+        r.pose_Tcw, r.lm_xyz = _ptr(out["pose_Tcw"]), _ptr(out["lm_xyz"])
+        r.edge_robust_chi2 = _ptr(out["edge_robust_chi2"])
+        r.trace_chi2, r.trace_lambda = _ptr(out["trace_chi2"]), _ptr(out["trace_lambda"])
+        r.trace_cap = trace_cap
+        return r, out
+
+    @staticmethod
+    def _finish(r, out):
+        n = r.trace_len
+        out["trace_chi2"] = out["trace_chi2"][:n]
+        out["trace_lambda"] = out["trace_lambda"][:n]
+        for f in ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "time_ms"):
+            out[f] = getattr(r, f)
+        return out
+
+    def solve(self, w, trace_cap=64):
+        ref = _WindowRef(w)
+        r, out = self._result(ref.s.n_poses, ref.s.n_landmarks, ref.s.n_obs, trace_cap)
+        _check(ba_lib().lh_solve(self.h, C.byref(ref.s), C.byref(r)), "lh_solve")
+        return self._finish(r, out)
+
+    def upload(self, w):
+        self._win = _WindowRef(w)
+        _check(ba_lib().lh_upload(self.h, C.byref(self._win.s)), "lh_upload")
+
+    def solve_resident(self, want_states=False, want_edges=False, trace_cap=64):
+        s = self._win.s
+        r, out = self._result(s.n_poses, s.n_landmarks, s.n_obs, trace_cap, want_states, want_edges)
+        _check(ba_lib().lh_solve_resident(self.h, C.byref(r)), "lh_solve_resident")
+        return self._finish(r, out)
+
+    def kernel_stats(self):
+        st = LhKernelStats()
+        _check(ba_lib().lh_kernel_stats_get(self.h, C.byref(st)), "lh_kernel_stats_get")
+        names = [ba_lib().lh_kernel_name(i).decode() for i in range(8)]
+        return {names[i]: (st.launches[i], st.total_ms[i]) for i in range(8) if st.launches[i] > 0}
+
+    def kernel_stats_reset(self):
+        ba_lib().lh_kernel_stats_reset(self.h)
+
+    def set_profiling(self, on):
+        _check(ba_lib().lh_set_profiling(self.h, int(on)), "lh_set_profiling")
+
+
+def comm_unique_id():
+    buf = (C.c_uint8 * 128)()
+    _check(ba_lib().lh_comm_unique_id(buf), "lh_comm_unique_id")
+    return bytes(buf)
+
+
+def classify_outliers(edge_rchi2, chi2_th=5.991):
+    e = np.ascontiguousarray(edge_rchi2, np.float64)
+    flags = np.zeros(e.shape[0], np.uint8)
+    th, ni, no = C.c_double(), C.c_int64(), C.c_int64()
+    _check(ba_lib().lh_classify_outliers(_ptr(e), e.shape[0], chi2_th, _ptr(flags), C.byref(th),
+                                         C.byref(ni), C.byref(no)), "lh_classify_outliers")
+    return flags.astype(bool), th.value, ni.value, no.value

@@ -1,0 +1,972 @@
+/*
+ * lego_oracle.c — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference
+ * LEGO-SLAM backend solve (lego::Problem in SLAM mode driven by
+ * Backend::Optimize).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this file; the product never links it.
+ *
+ * PARITY UNPINNED: the reference cannot be compiled here (Eigen3, Sophus,
+ * OpenCV, glog are absent) and its only test
+ * (test/legoslam_test_triangulation.cpp) is off this path, so no reference
+ * output pins this restatement.  It is cross-checked against an independent
+ * NumPy twin (oracle/lego_oracle_np.py) and against known-answer tests.
+ *
+ * Two variants with identical per-edge arithmetic and LM logic:
+ *   variant 0  "ref_dense":  literal — dense n x n H, dense Hmm_inv, dense
+ *              tempH = Hpm * Hmm_inv, LDLT of the reduced system.
+ *              (problem.cpp:273-358, :380-430).  Small windows only.
+ *   variant 1  "ref_sparse": block-sparse — per-landmark H_ll, per-pose H_pp,
+ *              per-(landmark,pose) H_pl, per-landmark Schur; OpenMP over
+ *              landmarks with a fixed-order reduction.  The CPU baseline.
+ *
+ * Third-party arithmetic restated (versions unpinned in the reference):
+ *   Eigen  Quaternion(Matrix3), toRotationMatrix, _transformVector, quaternion
+ *          product; PartialPivLU inverse (problem.cpp:399); LDLT with
+ *          diagonal pivoting and its pseudo-inverse solve (problem.cpp:420).
+ *   Sophus SE3(Matrix4), SE3::exp, SE3 * SE3, SO3 renormalisation (Sophus 1.0).
+ * Evaluation order follows the reference expressions; compile with
+ * -ffp-contract=off (the reference's x86-64 build has no FMA).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef struct orc_options {
+    int32_t max_iters;     /* solve(10)              backend_lego.cpp:161 */
+    int32_t max_trials;    /* false_cnt_threshold    problem.cpp:178      */
+    int32_t strategy;      /* 0 DEFAULT, 1 STRATEGY1 problem.h:45-50      */
+    int32_t verbose;
+    int32_t n_threads;     /* ref_sparse OpenMP threads (0 = runtime default) */
+    int32_t gate_mode;     /* 0: reference Huber gate (rho1 + 2 rho2 e2 > 0.0, base_edge.cpp:55);
+                              1: diagnostic only - treat the analytically-zero residue as 0 */
+    double huber_delta;    /* 5.991; <= 0: no cost function */
+    double stop_dchi2;     /* 1e-5 */
+    double tau;            /* 1e-5 */
+    double lambda_cap;     /* 5e10 */
+    double lambda_init;    /* < 0 computed */
+} orc_options;
+
+typedef struct orc_stats {
+    double chi2_initial, chi2_final, lambda_final, time_ms;
+    int32_t iterations, trials, accepted, trace_len;
+} orc_stats;
+
+/* ======================= Eigen / Sophus restatements ======================= */
+
+/* Eigen::Quaternion from rotation matrix (quaternionbase_assign_impl<.,3,3>).
+   q = {w, x, y, z}; R row-major. */
+static void q_from_R(const double *R, double q[4]) {
+#define M(i, j) R[3 * (i) + (j)]
+    double t = M(0, 0) + M(1, 1) + M(2, 2);
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[0] = 0.5 * t;
+        t = 0.5 / t;
+        q[1] = (M(2, 1) - M(1, 2)) * t;
+        q[2] = (M(0, 2) - M(2, 0)) * t;
+        q[3] = (M(1, 0) - M(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (M(k, j) - M(j, k)) * t;
+        c[j] = (M(j, i) + M(i, j)) * t;
+        c[k] = (M(k, i) + M(i, k)) * t;
+        q[1] = c[0]; q[2] = c[1]; q[3] = c[2];
+    }
+#undef M
+}
+
+/* Eigen QuaternionBase::toRotationMatrix */
+static void R_from_q(const double q[4], double *R) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;          R[2] = txz + twy;
+    R[3] = txy + twz;          R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;          R[7] = tyz + twx;          R[8] = 1.0 - (txx + tyy);
+}
+
+static void cross3(const double a[3], const double b[3], double c[3]) {
+    double c0 = a[1] * b[2] - a[2] * b[1];
+    double c1 = a[2] * b[0] - a[0] * b[2];
+    double c2 = a[0] * b[1] - a[1] * b[0];
+    c[0] = c0; c[1] = c1; c[2] = c2;
+}
+
+/* Eigen QuaternionBase::_transformVector */
+static void q_rotate(const double q[4], const double v[3], double out[3]) {
+    double uv[3], uv2[3];
+    cross3(q + 1, v, uv);
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    cross3(q + 1, uv, uv2);
+    for (int i = 0; i < 3; ++i) out[i] = v[i] + q[0] * uv[i] + uv2[i];
+}
+
+/* Eigen quaternion product + Sophus SO3Base::operator*= renormalisation */
+static void q_mul(const double a[4], const double b[4], double o[4]) {
+    double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
+    double z = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
+    double sq = w * w + x * x + y * y + z * z;
+    if (sq != 1.0) {
+        double s = 2.0 / (1.0 + sq);
+        w *= s; x *= s; y *= s; z *= s;
+    }
+    o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+
+typedef struct { double q[4]; double t[3]; } se3_t;
+
+/* Sophus SE3(Matrix4): estimate_ is the 4x4 (here row-major [R|t], 12 doubles) */
+static void se3_from_mat(const double *T12, se3_t *T) {
+    double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
+    q_from_R(R, T->q);
+    T->t[0] = T12[3]; T->t[1] = T12[7]; T->t[2] = T12[11];
+}
+/* SE3::matrix() */
+static void se3_to_mat(const se3_t *T, double *T12) {
+    double R[9];
+    R_from_q(T->q, R);
+    for (int i = 0; i < 3; ++i) {
+        T12[4 * i] = R[3 * i]; T12[4 * i + 1] = R[3 * i + 1]; T12[4 * i + 2] = R[3 * i + 2];
+        T12[4 * i + 3] = T->t[i];
+    }
+}
+/* SE3 * SE3: (so3*so3, t + so3*t') */
+static void se3_mul(const se3_t *A, const se3_t *B, se3_t *C) {
+    se3_t r;
+    double rt[3];
+    q_mul(A->q, B->q, r.q);
+    q_rotate(A->q, B->t, rt);
+    for (int i = 0; i < 3; ++i) r.t[i] = A->t[i] + rt[i];
+    *C = r;
+}
+/* SE3 * point */
+static void se3_apply(const se3_t *T, const double X[3], double Y[3]) {
+    double r[3];
+    q_rotate(T->q, X, r);
+    for (int i = 0; i < 3; ++i) Y[i] = r[i] + T->t[i];
+}
+
+/* Sophus SE3::exp, twist a = (upsilon[3] translation, omega[3] rotation) */
+static void se3_exp(const double a[6], se3_t *T) {
+    const double eps = 1e-10; /* Sophus Constants<double>::epsilon() */
+    const double *w = a + 3;
+    double theta_sq = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double theta = sqrt(theta_sq);
+    double half_theta = 0.5 * theta;
+    double imag, real;
+    if (theta < eps) {
+        double theta_po4 = theta_sq * theta_sq;
+        imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
+        real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * theta_po4;
+    } else {
+        double s = sin(half_theta);
+        imag = s / theta;
+        real = cos(half_theta);
+    }
+    T->q[0] = real; T->q[1] = imag * w[0]; T->q[2] = imag * w[1]; T->q[3] = imag * w[2];
+    double V[9];
+    if (theta < eps) {
+        R_from_q(T->q, V);
+    } else {
+        double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+        double Om2[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                Om2[3 * i + j] = Om[3 * i] * Om[j] + Om[3 * i + 1] * Om[3 + j] + Om[3 * i + 2] * Om[6 + j];
+        double c1 = (1.0 - cos(theta)) / theta_sq;
+        double c2 = (theta - sin(theta)) / (theta_sq * theta);
+        for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * Om[i] + c2 * Om2[i];
+    }
+    for (int i = 0; i < 3; ++i) T->t[i] = V[3 * i] * a[0] + V[3 * i + 1] * a[1] + V[3 * i + 2] * a[2];
+}
+
+/* Eigen PartialPivLU(3x3).inverse() (dynamic-size block inverse, problem.cpp:399).
+   A, Ainv row-major 3x3. */
+static void lu_inverse3(const double *A, double *Ainv) {
+    double lu[9];
+    int tr[3];
+    memcpy(lu, A, sizeof(lu));
+    for (int k = 0; k < 3; ++k) {
+        int piv = k;
+        double big = fabs(lu[3 * k + k]);
+        for (int i = k + 1; i < 3; ++i)
+            if (fabs(lu[3 * i + k]) > big) { big = fabs(lu[3 * i + k]); piv = i; }
+        tr[k] = piv;
+        if (big != 0.0) {
+            if (piv != k)
+                for (int j = 0; j < 3; ++j) { double t = lu[3 * k + j]; lu[3 * k + j] = lu[3 * piv + j]; lu[3 * piv + j] = t; }
+            for (int i = k + 1; i < 3; ++i) lu[3 * i + k] /= lu[3 * k + k];
+        }
+        for (int i = k + 1; i < 3; ++i)
+            for (int j = k + 1; j < 3; ++j) lu[3 * i + j] -= lu[3 * i + k] * lu[3 * k + j];
+    }
+    /* dst = P * I */
+    double X[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int k = 0; k < 3; ++k)
+        if (tr[k] != k)
+            for (int j = 0; j < 3; ++j) { double t = X[3 * k + j]; X[3 * k + j] = X[3 * tr[k] + j]; X[3 * tr[k] + j] = t; }
+    /* unit-lower forward substitution, column-oriented */
+    for (int k = 0; k < 3; ++k)
+        for (int i = k + 1; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) X[3 * i + j] -= lu[3 * i + k] * X[3 * k + j];
+    /* upper back substitution */
+    for (int k = 2; k >= 0; --k) {
+        for (int j = 0; j < 3; ++j) X[3 * k + j] /= lu[3 * k + k];
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < 3; ++j) X[3 * i + j] -= lu[3 * i + k] * X[3 * k + j];
+    }
+    memcpy(Ainv, X, sizeof(X));
+}
+
+/* Eigen LDLT<Lower> (ldlt_inplace::unblocked, diagonal pivoting) followed by
+   LDLT::_solve_impl.  A is n x n row-major (lower triangle used), destroyed. */
+static void ldlt_solve(double *A, int n, const double *b, double *x) {
+    int *tr = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+    double *temp = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+#define A_(i, j) A[(size_t)(i) * (size_t)n + (size_t)(j)]
+    int all_zero = 0;
+    for (int k = 0; k < n; ++k) {
+        int idx = k;
+        double big = fabs(A_(k, k));
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(A_(i, i)) > big) { big = fabs(A_(i, i)); idx = i; }
+        tr[k] = idx;
+        if (k != idx) {
+            for (int j = 0; j < k; ++j) { double t = A_(k, j); A_(k, j) = A_(idx, j); A_(idx, j) = t; }
+            for (int i = idx + 1; i < n; ++i) { double t = A_(i, k); A_(i, k) = A_(i, idx); A_(i, idx) = t; }
+            { double t = A_(k, k); A_(k, k) = A_(idx, idx); A_(idx, idx) = t; }
+            for (int i = k + 1; i < idx; ++i) { double t = A_(i, k); A_(i, k) = A_(idx, i); A_(idx, i) = t; }
+        }
+        int rs = n - k - 1;
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = A_(j, j) * A_(k, j);
+            double s = 0.0;
+            for (int j = 0; j < k; ++j) s += A_(k, j) * temp[j];
+            A_(k, k) -= s;
+            for (int i = k + 1; i < n; ++i) {
+                double si = 0.0;
+                for (int j = 0; j < k; ++j) si += A_(i, j) * temp[j];
+                A_(i, k) -= si;
+            }
+        }
+        double akk = A_(k, k);
+        int valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            for (int j = 0; j < n; ++j) tr[j] = j;
+            all_zero = 1;
+            break;
+        }
+        if (rs > 0 && valid)
+            for (int i = k + 1; i < n; ++i) A_(i, k) /= akk;
+    }
+    /* solve */
+    for (int i = 0; i < n; ++i) x[i] = b[i];
+    for (int k = 0; k < n; ++k) { int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
+    if (!all_zero) {
+        for (int k = 0; k < n; ++k)
+            for (int i = k + 1; i < n; ++i) x[i] -= A_(i, k) * x[k];
+    }
+    const double tol = 2.2250738585072014e-308; /* numeric_limits<double>::min() */
+    for (int i = 0; i < n; ++i) {
+        double d = A_(i, i);
+        if (fabs(d) > tol) x[i] /= d; else x[i] = 0.0;
+    }
+    if (!all_zero) {
+        for (int k = n - 1; k >= 0; --k)
+            for (int i = 0; i < k; ++i) x[i] -= A_(k, i) * x[k];
+    }
+    for (int k = n - 1; k >= 0; --k) { int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
+#undef A_
+    free(tr);
+    free(temp);
+}
+
+/* ============================ problem state ============================== */
+
+typedef struct {
+    /* inputs */
+    int32_t P, L, ncam, variant;
+    int64_t O;
+    const uint8_t *fixed;
+    const uint32_t *op, *ol;
+    const uint8_t *oc;
+    const double *uv;
+    double K[4];
+    se3_t *ext;
+    orc_options opt;
+    /* state: estimate_ and estimate_backup_ */
+    double *pose, *pose_bak; /* P x 12 */
+    double *lm, *lm_bak;     /* L x 3  */
+    /* per edge (residual_ as last computed, Jacobians, robust weights) */
+    double *res;             /* O x 2 */
+    /* linearisation */
+    double *H, *b;           /* dense: n x n, n */
+    double *Hpp, *bp;        /* sparse: P x 36, P x 6 */
+    double *Hll, *bl;        /* L x 9, L x 3 */
+    double *Hpl;             /* per edge 6x3 (row-major) */
+    double *dx;              /* n */
+    double *hdiag;           /* n: diag of Hessian_ (lambda init, STRATEGY1) */
+    /* landmark-major edge order */
+    int64_t *lm_ptr, *lm_edges;
+    int64_t n;
+    double chi, lambda, ni;
+} prob_t;
+
+/* ---- EdgeProjection arithmetic (include/legoslam/lego_types.h:200-254) ---- */
+
+static void edge_residual(const prob_t *pb, int64_t e, double r[2]) {
+    se3_t T;
+    se3_from_mat(pb->pose + 12 * (size_t)pb->op[e], &T);
+    const double *X = pb->lm + 3 * (size_t)pb->ol[e];
+    int c = pb->oc ? pb->oc[e] : 0;
+    double Pb[3], Pc[3];
+    se3_apply(&T, X, Pb);             /* T * X                 */
+    se3_apply(&pb->ext[c], Pb, Pc);   /* _cam_ext * (T * X)    */
+    const double fx = pb->K[0], fy = pb->K[1], cx = pb->K[2], cy = pb->K[3];
+    double p0 = fx * Pc[0] + 0.0 * Pc[1] + cx * Pc[2]; /* _K * Pc, row by row */
+    double p1 = 0.0 * Pc[0] + fy * Pc[1] + cy * Pc[2];
+    double p2 = 0.0 * Pc[0] + 0.0 * Pc[1] + 1.0 * Pc[2];
+    double den = p2 + 1e-18;                          /* pos_pixel /= (z + 1e-18) */
+    p0 /= den; p1 /= den;
+    r[0] = pb->uv[2 * e] - p0;                        /* measurement_ - pos_pixel */
+    r[1] = pb->uv[2 * e + 1] - p1;
+}
+
+static void edge_jacobians(const prob_t *pb, int64_t e, double Jp[12], double Jl[6]) {
+    se3_t T, ET;
+    se3_from_mat(pb->pose + 12 * (size_t)pb->op[e], &T);
+    int c = pb->oc ? pb->oc[e] : 0;
+    const double *X = pb->lm + 3 * (size_t)pb->ol[e];
+    se3_mul(&pb->ext[c], &T, &ET);    /* _cam_ext * T * pw: (ext*T)*pw */
+    double Pc[3];
+    se3_apply(&ET, X, Pc);
+    const double fx = pb->K[0], fy = pb->K[1];
+    const double x = Pc[0], y = Pc[1], z = Pc[2];
+    const double zi = 1.0 / (z + 1e-18);
+    const double zi2 = zi * zi;
+    Jp[0] = -fx * zi;             Jp[1] = 0.0;              Jp[2] = fx * x * zi2;
+    Jp[3] = fx * x * y * zi2;     Jp[4] = -fx - fx * x * x * zi2; Jp[5] = fx * y * zi;
+    Jp[6] = 0.0;                  Jp[7] = -fy * zi;         Jp[8] = fy * y * zi2;
+    Jp[9] = fy + fy * y * y * zi2; Jp[10] = -fy * x * y * zi2; Jp[11] = -fy * x * zi;
+    /* j_j = j_i(:, 0:3) * ext.rotationMatrix() * T.rotationMatrix() */
+    double Re[9], Rt[9], A[6];
+    R_from_q(pb->ext[c].q, Re);
+    R_from_q(T.q, Rt);
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j)
+            A[3 * i + j] = Jp[6 * i] * Re[j] + Jp[6 * i + 1] * Re[3 + j] + Jp[6 * i + 2] * Re[6 + j];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j)
+            Jl[3 * i + j] = A[3 * i] * Rt[j] + A[3 * i + 1] * Rt[3 + j] + A[3 * i + 2] * Rt[6 + j];
+}
+
+/* HuberCost::compute (cost_function.cpp:5-17) */
+static void huber(double delta, double e2, double rho[3]) {
+    double d2 = delta * delta;
+    if (e2 <= d2) { rho[0] = e2; rho[1] = 1.0; rho[2] = 0.0; }
+    else {
+        double s = sqrt(e2);
+        rho[0] = 2 * s * delta - d2;
+        rho[1] = delta / s;
+        rho[2] = -0.5 * rho[1] / e2;
+    }
+}
+
+/* BaseEdge::getRobustChi2 (base_edge.cpp:33-42) */
+static double robust_chi2(const prob_t *pb, const double r[2]) {
+    double e2 = r[0] * r[0] + r[1] * r[1]; /* r^T * I * r */
+    if (pb->opt.huber_delta > 0) { double rho[3]; huber(pb->opt.huber_delta, e2, rho); return rho[0]; }
+    return e2;
+}
+
+/* BaseEdge::computeRobustInformation (base_edge.cpp:44-64); W row-major 2x2 */
+static void robust_info(const prob_t *pb, const double r[2], double W[4], double *drho) {
+    if (pb->opt.huber_delta > 0) {
+        double e2 = r[0] * r[0] + r[1] * r[1];
+        double rho[3];
+        huber(pb->opt.huber_delta, e2, rho);
+        W[0] = rho[1]; W[1] = 0.0; W[2] = 0.0; W[3] = rho[1];
+        if (rho[1] + 2 * rho[2] * e2 > 0.0 && !(pb->opt.gate_mode == 1 && e2 > pb->opt.huber_delta * pb->opt.huber_delta)) {
+            double s = 2 * rho[2];
+            W[0] += s * r[0] * r[0]; W[1] += s * r[0] * r[1];
+            W[2] += s * r[1] * r[0]; W[3] += s * r[1] * r[1];
+        }
+        *drho = rho[1];
+    } else {
+        W[0] = 1.0; W[1] = 0.0; W[2] = 0.0; W[3] = 1.0;
+        *drho = 1.0;
+    }
+}
+
+/* hessian = (J_i^T W) J_j for J_i (2 x di), J_j (2 x dj); out di x dj row-major */
+static void jtwj(const double *Ji, int di, const double W[4], const double *Jj, int dj, double *out) {
+    double JtW[12];
+    for (int a = 0; a < di; ++a)
+        for (int m = 0; m < 2; ++m) JtW[2 * a + m] = Ji[a] * W[m] + Ji[di + a] * W[2 + m];
+    for (int a = 0; a < di; ++a)
+        for (int c = 0; c < dj; ++c) out[dj * a + c] = JtW[2 * a] * Jj[c] + JtW[2 * a + 1] * Jj[dj + c];
+}
+
+/* per-edge linearisation pieces shared by both variants */
+typedef struct { double Hpp[36], Hpl[18], Hll[9], bp[6], bl[3]; } edge_lin_t;
+
+static void edge_linearize(prob_t *pb, int64_t e, edge_lin_t *E) {
+    double r[2], Jp[12], Jl[6], W[4], drho;
+    edge_residual(pb, e, r);
+    pb->res[2 * e] = r[0];
+    pb->res[2 * e + 1] = r[1];
+    edge_jacobians(pb, e, Jp, Jl);
+    robust_info(pb, r, W, &drho);
+    int pf = pb->fixed && pb->fixed[pb->op[e]];
+    memset(E, 0, sizeof(*E));
+    if (!pf) {
+        jtwj(Jp, 6, W, Jp, 6, E->Hpp);
+        jtwj(Jp, 6, W, Jl, 3, E->Hpl);
+        for (int a = 0; a < 6; ++a) E->bp[a] = -((drho * Jp[a]) * r[0] + (drho * Jp[6 + a]) * r[1]);
+    }
+    jtwj(Jl, 3, W, Jl, 3, E->Hll);
+    for (int a = 0; a < 3; ++a) E->bl[a] = -((drho * Jl[a]) * r[0] + (drho * Jl[3 + a]) * r[1]);
+}
+
+/* ================================ dense ================================== */
+
+static void build_dense(prob_t *pb) {
+    const int64_t n = pb->n;
+    const int64_t np = 6 * (int64_t)pb->P;
+    memset(pb->H, 0, sizeof(double) * (size_t)(n * n));
+    memset(pb->b, 0, sizeof(double) * (size_t)n);
+    for (int64_t e = 0; e < pb->O; ++e) {
+        edge_lin_t E;
+        edge_linearize(pb, e, &E);
+        int64_t ip = 6 * (int64_t)pb->op[e], il = np + 3 * (int64_t)pb->ol[e];
+        for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 6; ++c) pb->H[(ip + a) * n + ip + c] += E.Hpp[6 * a + c];
+        for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 3; ++c) {
+                pb->H[(ip + a) * n + il + c] += E.Hpl[3 * a + c];
+                pb->H[(il + c) * n + ip + a] += E.Hpl[3 * a + c];
+            }
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) pb->H[(il + a) * n + il + c] += E.Hll[3 * a + c];
+        for (int a = 0; a < 6; ++a) pb->b[ip + a] += E.bp[a];
+        for (int a = 0; a < 3; ++a) pb->b[il + a] += E.bl[a];
+    }
+    for (int64_t i = 0; i < n; ++i) pb->hdiag[i] = pb->H[i * n + i];
+}
+
+static void solve_dense(prob_t *pb) {
+    const int64_t n = pb->n, np = 6 * (int64_t)pb->P, nm = n - np;
+    double *Hmm_inv = (double *)calloc((size_t)(nm * nm), sizeof(double));
+    for (int32_t l = 0; l < pb->L; ++l) {
+        double blk[9], inv[9];
+        int64_t o = np + 3 * (int64_t)l;
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) blk[3 * a + c] = pb->H[(o + a) * n + o + c];
+        lu_inverse3(blk, inv);
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) Hmm_inv[(3 * l + a) * nm + 3 * l + c] = inv[3 * a + c];
+    }
+    /* tempH = Hpm * Hmm_inv */
+    double *tempH = (double *)calloc((size_t)(np * nm), sizeof(double));
+    for (int64_t i = 0; i < np; ++i)
+        for (int64_t k = 0; k < nm; ++k) {
+            double h = pb->H[i * n + np + k];
+            for (int64_t j = 0; j < nm; ++j) tempH[i * nm + j] += h * Hmm_inv[k * nm + j];
+        }
+    /* S = Hpp - tempH * Hmp; bs = bpp - tempH * bmm */
+    double *S = (double *)malloc(sizeof(double) * (size_t)(np * np));
+    double *bs = (double *)malloc(sizeof(double) * (size_t)np);
+    for (int64_t i = 0; i < np; ++i) {
+        for (int64_t j = 0; j < np; ++j) {
+            double s = 0.0;
+            for (int64_t k = 0; k < nm; ++k) s += tempH[i * nm + k] * pb->H[(np + k) * n + j];
+            S[i * np + j] = pb->H[i * n + j] - s;
+        }
+        double s = 0.0;
+        for (int64_t k = 0; k < nm; ++k) s += tempH[i * nm + k] * pb->b[np + k];
+        bs[i] = pb->b[i] - s;
+    }
+    for (int64_t i = 0; i < np; ++i) {
+        if (pb->opt.strategy == 0) S[i * np + i] += pb->lambda;
+        else S[i * np + i] += pb->lambda * S[i * np + i];
+    }
+    ldlt_solve(S, (int)np, bs, pb->dx);
+    /* dxl = Hmm_inv * (bmm - Hmp * dxp) */
+    double *tmp = (double *)malloc(sizeof(double) * (size_t)(nm > 0 ? nm : 1));
+    for (int64_t k = 0; k < nm; ++k) {
+        double s = 0.0;
+        for (int64_t j = 0; j < np; ++j) s += pb->H[(np + k) * n + j] * pb->dx[j];
+        tmp[k] = pb->b[np + k] - s;
+    }
+    for (int64_t k = 0; k < nm; ++k) {
+        double s = 0.0;
+        for (int64_t j = 0; j < nm; ++j) s += Hmm_inv[k * nm + j] * tmp[j];
+        pb->dx[np + k] = s;
+    }
+    free(tmp); free(S); free(bs); free(tempH); free(Hmm_inv);
+}
+
+/* ================================ sparse ================================= */
+
+static int nthreads(const prob_t *pb) {
+#ifdef _OPENMP
+    return pb->opt.n_threads > 0 ? pb->opt.n_threads : omp_get_max_threads();
+#else
+    (void)pb;
+    return 1;
+#endif
+}
+
+static void build_sparse(prob_t *pb) {
+    const int32_t P = pb->P;
+    const int nt = nthreads(pb);
+    double *part = (double *)calloc((size_t)nt * (size_t)P * 42, sizeof(double));
+#pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+        int tid = omp_get_thread_num();
+#else
+        int tid = 0;
+#endif
+        double *myHpp = part + (size_t)tid * (size_t)P * 42;
+        double *mybp = myHpp + (size_t)P * 36;
+#pragma omp for schedule(static)
+        for (int32_t l = 0; l < pb->L; ++l) {
+            double Hll[9] = {0}, bl[3] = {0};
+            for (int64_t q = pb->lm_ptr[l]; q < pb->lm_ptr[l + 1]; ++q) {
+                int64_t e = pb->lm_edges[q];
+                edge_lin_t E;
+                edge_linearize(pb, e, &E);
+                uint32_t p = pb->op[e];
+                for (int a = 0; a < 36; ++a) myHpp[36 * (size_t)p + a] += E.Hpp[a];
+                for (int a = 0; a < 6; ++a) mybp[6 * (size_t)p + a] += E.bp[a];
+                for (int a = 0; a < 9; ++a) Hll[a] += E.Hll[a];
+                for (int a = 0; a < 3; ++a) bl[a] += E.bl[a];
+                memcpy(pb->Hpl + 18 * (size_t)e, E.Hpl, sizeof(E.Hpl));
+            }
+            memcpy(pb->Hll + 9 * (size_t)l, Hll, sizeof(Hll));
+            memcpy(pb->bl + 3 * (size_t)l, bl, sizeof(bl));
+        }
+    }
+    memset(pb->Hpp, 0, sizeof(double) * (size_t)P * 36);
+    memset(pb->bp, 0, sizeof(double) * (size_t)P * 6);
+    for (int t = 0; t < nt; ++t) {
+        const double *h = part + (size_t)t * (size_t)P * 42;
+        for (size_t a = 0; a < (size_t)P * 36; ++a) pb->Hpp[a] += h[a];
+        for (size_t a = 0; a < (size_t)P * 6; ++a) pb->bp[a] += h[(size_t)P * 36 + a];
+    }
+    free(part);
+    for (int32_t p = 0; p < P; ++p)
+        for (int a = 0; a < 6; ++a) {
+            pb->hdiag[6 * p + a] = pb->Hpp[36 * p + 7 * a];
+            pb->b[6 * p + a] = pb->bp[6 * p + a];
+        }
+    for (int32_t l = 0; l < pb->L; ++l)
+        for (int a = 0; a < 3; ++a) {
+            pb->hdiag[6 * (int64_t)P + 3 * l + a] = pb->Hll[9 * (size_t)l + 4 * a];
+            pb->b[6 * (int64_t)P + 3 * l + a] = pb->bl[3 * (size_t)l + a];
+        }
+}
+
+static void solve_sparse(prob_t *pb) {
+    const int32_t P = pb->P;
+    const int64_t np = 6 * (int64_t)P;
+    const int nt = nthreads(pb);
+    double *part = (double *)calloc((size_t)nt * (size_t)(np * np + np), sizeof(double));
+    double *Hinv = (double *)malloc(sizeof(double) * 9 * (size_t)(pb->L > 0 ? pb->L : 1));
+#pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+        int tid = omp_get_thread_num();
+#else
+        int tid = 0;
+#endif
+        double *myS = part + (size_t)tid * (size_t)(np * np + np);
+        double *mybs = myS + np * np;
+        double Hpl[64 * 18];
+        int32_t pose_of[64];
+#pragma omp for schedule(static)
+        for (int32_t l = 0; l < pb->L; ++l) {
+            double *inv = Hinv + 9 * (size_t)l;
+            lu_inverse3(pb->Hll + 9 * (size_t)l, inv);
+            /* merge the landmark's edges per pose: H_pl block of the dense H */
+            int nb = 0;
+            for (int64_t q = pb->lm_ptr[l]; q < pb->lm_ptr[l + 1]; ++q) {
+                int64_t e = pb->lm_edges[q];
+                int32_t p = (int32_t)pb->op[e];
+                if (nb > 0 && pose_of[nb - 1] == p) {
+                    for (int a = 0; a < 18; ++a) Hpl[18 * (nb - 1) + a] += pb->Hpl[18 * (size_t)e + a];
+                } else if (nb < 64) {
+                    pose_of[nb] = p;
+                    memcpy(Hpl + 18 * nb, pb->Hpl + 18 * (size_t)e, 18 * sizeof(double));
+                    ++nb;
+                }
+            }
+            const double *bl = pb->bl + 3 * (size_t)l;
+            for (int i = 0; i < nb; ++i) {
+                double tH[18]; /* tempH block: Hpl_i * Hll^-1 */
+                for (int a = 0; a < 6; ++a)
+                    for (int c = 0; c < 3; ++c)
+                        tH[3 * a + c] = Hpl[18 * i + 3 * a] * inv[c] + Hpl[18 * i + 3 * a + 1] * inv[3 + c] +
+                                        Hpl[18 * i + 3 * a + 2] * inv[6 + c];
+                int64_t pi = 6 * (int64_t)pose_of[i];
+                for (int j = 0; j < nb; ++j) {
+                    int64_t pj = 6 * (int64_t)pose_of[j];
+                    for (int a = 0; a < 6; ++a)
+                        for (int c = 0; c < 6; ++c)
+                            myS[(pi + a) * np + pj + c] += tH[3 * a] * Hpl[18 * j + 3 * c] +
+                                                           tH[3 * a + 1] * Hpl[18 * j + 3 * c + 1] +
+                                                           tH[3 * a + 2] * Hpl[18 * j + 3 * c + 2];
+                }
+                for (int a = 0; a < 6; ++a) mybs[pi + a] += tH[3 * a] * bl[0] + tH[3 * a + 1] * bl[1] + tH[3 * a + 2] * bl[2];
+            }
+        }
+    }
+    double *S = (double *)malloc(sizeof(double) * (size_t)(np * np));
+    double *bs = (double *)malloc(sizeof(double) * (size_t)np);
+    for (int64_t i = 0; i < np * np; ++i) S[i] = 0.0;
+    for (int64_t i = 0; i < np; ++i) bs[i] = 0.0;
+    for (int t = 0; t < nt; ++t) {
+        const double *s = part + (size_t)t * (size_t)(np * np + np);
+        for (int64_t i = 0; i < np * np; ++i) S[i] += s[i];
+        for (int64_t i = 0; i < np; ++i) bs[i] += s[np * np + i];
+    }
+    free(part);
+    for (int32_t p = 0; p < P; ++p)
+        for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 6; ++c) S[(6 * p + a) * np + 6 * p + c] = pb->Hpp[36 * p + 6 * a + c] - S[(6 * p + a) * np + 6 * p + c];
+    for (int64_t i = 0; i < np; ++i)
+        for (int64_t j = 0; j < np; ++j)
+            if (i / 6 != j / 6) S[i * np + j] = -S[i * np + j];
+    for (int64_t i = 0; i < np; ++i) bs[i] = pb->bp[i] - bs[i];
+    for (int64_t i = 0; i < np; ++i) {
+        if (pb->opt.strategy == 0) S[i * np + i] += pb->lambda;
+        else S[i * np + i] += pb->lambda * S[i * np + i];
+    }
+    ldlt_solve(S, (int)np, bs, pb->dx);
+    free(S); free(bs);
+    /* back substitution: dxl = Hll^-1 (bl - Hlp * dxp) */
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t l = 0; l < pb->L; ++l) {
+        double t[3];
+        for (int a = 0; a < 3; ++a) {
+            double s = 0.0;
+            for (int64_t q = pb->lm_ptr[l]; q < pb->lm_ptr[l + 1]; ++q) {
+                int64_t e = pb->lm_edges[q];
+                const double *h = pb->Hpl + 18 * (size_t)e;
+                const double *d = pb->dx + 6 * (size_t)pb->op[e];
+                for (int c = 0; c < 6; ++c) s += h[3 * c + a] * d[c];
+            }
+            t[a] = pb->bl[3 * (size_t)l + a] - s;
+        }
+        const double *inv = Hinv + 9 * (size_t)l;
+        for (int a = 0; a < 3; ++a)
+            pb->dx[np + 3 * (int64_t)l + a] = inv[3 * a] * t[0] + inv[3 * a + 1] * t[1] + inv[3 * a + 2] * t[2];
+    }
+    free(Hinv);
+}
+
+/* =============================== LM driver =============================== */
+
+static void build_hessian(prob_t *pb) {
+    if (pb->variant == 0) build_dense(pb); else build_sparse(pb);
+    memset(pb->dx, 0, sizeof(double) * (size_t)pb->n); /* delta_x_ = 0 (problem.cpp:357) */
+}
+
+static void solve_linear(prob_t *pb) {
+    if (pb->variant == 0) solve_dense(pb); else solve_sparse(pb);
+}
+
+/* Problem::updateStates (problem.cpp:433-455) with VertexPose::add / VertexXYZ::add */
+static void update_states(prob_t *pb) {
+    memcpy(pb->pose_bak, pb->pose, sizeof(double) * 12 * (size_t)pb->P);
+    memcpy(pb->lm_bak, pb->lm, sizeof(double) * 3 * (size_t)pb->L);
+    for (int32_t p = 0; p < pb->P; ++p) {
+        const double *d = pb->dx + 6 * (size_t)p;
+        double u[6];
+        int bad = 0;
+        for (int a = 0; a < 6; ++a) if (isnan(d[a]) || isinf(d[a])) bad = 1;
+        for (int a = 0; a < 6; ++a) u[a] = bad ? 0.0 : d[a];
+        se3_t E, T, R;
+        se3_exp(u, &E);
+        se3_from_mat(pb->pose + 12 * (size_t)p, &T);
+        se3_mul(&E, &T, &R);
+        se3_to_mat(&R, pb->pose + 12 * (size_t)p);
+    }
+    const int64_t np = 6 * (int64_t)pb->P;
+#pragma omp parallel for schedule(static) num_threads(nthreads(pb))
+    for (int32_t l = 0; l < pb->L; ++l) {
+        const double *d = pb->dx + np + 3 * (int64_t)l;
+        if (!isnan(d[0]) && !isnan(d[1]) && !isnan(d[2]) && !isinf(d[0]) && !isinf(d[1]) && !isinf(d[2])) {
+            pb->lm[3 * (size_t)l] += d[0];
+            pb->lm[3 * (size_t)l + 1] += d[1];
+            pb->lm[3 * (size_t)l + 2] += d[2];
+        }
+    }
+}
+
+static void rollback_states(prob_t *pb) {
+    memcpy(pb->pose, pb->pose_bak, sizeof(double) * 12 * (size_t)pb->P);
+    memcpy(pb->lm, pb->lm_bak, sizeof(double) * 3 * (size_t)pb->L);
+}
+
+/* sum of robust chi2 over the current residuals, fixed order */
+static double sum_rchi2(prob_t *pb, int recompute) {
+    const int nt = pb->variant == 0 ? 1 : nthreads(pb);
+    double *part = (double *)calloc((size_t)nt, sizeof(double));
+#pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+        int tid = omp_get_thread_num();
+#else
+        int tid = 0;
+#endif
+        double s = 0.0;
+#pragma omp for schedule(static)
+        for (int64_t e = 0; e < pb->O; ++e) {
+            if (recompute) edge_residual(pb, e, pb->res + 2 * e);
+            s += robust_chi2(pb, pb->res + 2 * e);
+        }
+        part[tid] = s;
+    }
+    double s = 0.0;
+    for (int t = 0; t < nt; ++t) s += part[t];
+    free(part);
+    return s;
+}
+
+static void lambda_init(prob_t *pb) {
+    pb->ni = 2.0;
+    pb->lambda = -1.0;
+    pb->chi = 0.5 * sum_rchi2(pb, 0);
+    if (pb->opt.strategy == 0) {
+        if (pb->opt.lambda_init < 0) {
+            double m = 0.0;
+            for (int64_t i = 0; i < pb->n; ++i) m = fmax(fabs(pb->hdiag[i]), m);
+            m = fmin(pb->opt.lambda_cap, m);
+            pb->lambda = pb->opt.tau * m;
+        } else {
+            pb->lambda = pb->opt.lambda_init;
+        }
+    } else {
+        pb->lambda = 1e-5;
+    }
+}
+
+static int good_step(prob_t *pb) {
+    double temp_chi = 0.5 * sum_rchi2(pb, 1);
+    if (pb->opt.strategy == 0) {
+        double scale = 0.0;
+        for (int64_t i = 0; i < pb->n; ++i) scale += pb->dx[i] * (pb->lambda * pb->dx[i] + pb->b[i]);
+        scale = 0.5 * scale;
+        scale += 1e-10;
+        double rho = (pb->chi - temp_chi) / scale;
+        if (rho > 0 && isfinite(temp_chi)) {
+            double alpha = 1.0 - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2.0 / 3.0);
+            double f = fmax(1.0 / 3.0, alpha);
+            pb->lambda *= f;
+            pb->ni = 2;
+            pb->chi = temp_chi;
+            return 1;
+        }
+        pb->lambda *= pb->ni;
+        pb->ni *= 2;
+        return 0;
+    } else {
+        double scale = 0.0;
+        for (int64_t i = 0; i < pb->n; ++i) scale += pb->dx[i] * (pb->lambda * pb->hdiag[i] * pb->dx[i] + pb->b[i]);
+        scale = 0.5 * scale;
+        scale += 1e-10;
+        double rho = (pb->chi - temp_chi) / scale;
+        if (rho > 0 && isfinite(temp_chi)) {
+            pb->lambda = fmax(pb->lambda / 9.0, 1e-7);
+            pb->chi = temp_chi;
+            return 1;
+        }
+        pb->lambda = fmin(pb->lambda * 11.0, 1e7);
+        return 0;
+    }
+}
+
+typedef struct { const uint32_t *ol, *op; } sort_ctx_t;
+static const sort_ctx_t *g_sort_ctx;
+static int cmp_edge_q(const void *a, const void *b) {
+    int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    const sort_ctx_t *c = g_sort_ctx;
+    if (c->ol[x] != c->ol[y]) return c->ol[x] < c->ol[y] ? -1 : 1;
+    if (c->op[x] != c->op[y]) return c->op[x] < c->op[y] ? -1 : 1;
+    return x < y ? -1 : (x > y);
+}
+
+double orc_now_ms(void);
+
+/*
+ * orc_solve — Backend::Optimize's problem.solve(max_iters) on one window.
+ * Returns 0 on success, 1 for an empty problem (problem.cpp:157-161),
+ * 2 for bad arguments.
+ */
+int orc_solve(int variant, int32_t P, const double *pose_in, const uint8_t *fixed,
+              int32_t L, const double *lm_in, int64_t O, const uint32_t *op, const uint32_t *ol,
+              const uint8_t *oc, const double *uv, const double *K, int32_t ncam, const double *cam_ext,
+              const orc_options *opt, double *pose_out, double *lm_out, double *edge_rchi2,
+              double *trace_chi, double *trace_lambda, int32_t trace_cap, orc_stats *st) {
+    memset(st, 0, sizeof(*st));
+    if (P < 0 || L < 0 || O < 0) return 2;
+    if (O == 0 || (P + L) == 0) return 1;
+    for (int64_t e = 0; e < O; ++e) {
+        if (op[e] >= (uint32_t)P || ol[e] >= (uint32_t)L) return 2;
+        if (oc && oc[e] >= (uint8_t)(ncam > 0 ? ncam : 1)) return 2;
+    }
+    double t0 = orc_now_ms();
+    prob_t pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.P = P; pb.L = L; pb.O = O; pb.variant = variant;
+    pb.fixed = fixed; pb.op = op; pb.ol = ol; pb.oc = oc; pb.uv = uv;
+    memcpy(pb.K, K, sizeof(pb.K));
+    pb.opt = *opt;
+    int nc = ncam > 0 ? ncam : 1;
+    pb.ext = (se3_t *)malloc(sizeof(se3_t) * (size_t)nc);
+    for (int c = 0; c < nc; ++c) {
+        if (cam_ext && ncam > 0) se3_from_mat(cam_ext + 12 * c, &pb.ext[c]);
+        else { double I12[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}; se3_from_mat(I12, &pb.ext[c]); }
+    }
+    pb.n = 6 * (int64_t)P + 3 * (int64_t)L;
+    pb.pose = (double *)malloc(sizeof(double) * 12 * (size_t)P);
+    pb.pose_bak = (double *)malloc(sizeof(double) * 12 * (size_t)P);
+    pb.lm = (double *)malloc(sizeof(double) * 3 * (size_t)(L > 0 ? L : 1));
+    pb.lm_bak = (double *)malloc(sizeof(double) * 3 * (size_t)(L > 0 ? L : 1));
+    memcpy(pb.pose, pose_in, sizeof(double) * 12 * (size_t)P);
+    memcpy(pb.lm, lm_in, sizeof(double) * 3 * (size_t)L);
+    pb.res = (double *)calloc(2 * (size_t)O, sizeof(double));
+    pb.dx = (double *)calloc((size_t)pb.n, sizeof(double));
+    pb.b = (double *)calloc((size_t)pb.n, sizeof(double));
+    pb.hdiag = (double *)calloc((size_t)pb.n, sizeof(double));
+    if (variant == 0) {
+        pb.H = (double *)malloc(sizeof(double) * (size_t)(pb.n * pb.n));
+    } else {
+        pb.Hpp = (double *)malloc(sizeof(double) * 36 * (size_t)P);
+        pb.bp = (double *)malloc(sizeof(double) * 6 * (size_t)P);
+        pb.Hll = (double *)malloc(sizeof(double) * 9 * (size_t)(L > 0 ? L : 1));
+        pb.bl = (double *)malloc(sizeof(double) * 3 * (size_t)(L > 0 ? L : 1));
+        pb.Hpl = (double *)malloc(sizeof(double) * 18 * (size_t)O);
+        pb.lm_ptr = (int64_t *)calloc((size_t)L + 1, sizeof(int64_t));
+        pb.lm_edges = (int64_t *)malloc(sizeof(int64_t) * (size_t)O);
+        for (int64_t e = 0; e < O; ++e) pb.lm_edges[e] = e;
+        sort_ctx_t sc = {ol, op};
+        g_sort_ctx = &sc;
+        qsort(pb.lm_edges, (size_t)O, sizeof(int64_t), cmp_edge_q);
+        for (int64_t e = 0; e < O; ++e) pb.lm_ptr[ol[e] + 1]++;
+        for (int32_t l = 0; l < L; ++l) pb.lm_ptr[l + 1] += pb.lm_ptr[l];
+    }
+
+    /* ---- Problem::solve (problem.cpp:156-230) ---- */
+    if (pb.opt.verbose) printf("==========LEGO OPTIMIZER==========\n");
+    build_hessian(&pb);
+    lambda_init(&pb);
+    st->chi2_initial = pb.chi;
+    int stop = 0, iter = 0;
+    double last_chi = 1e20;
+    while (!stop && iter < pb.opt.max_iters) {
+        if (pb.opt.verbose) printf("Iteration = %d,\tChi = %g,\tLambda = %g\n", iter, pb.chi, pb.lambda);
+        if (st->trace_len < trace_cap) {
+            if (trace_chi) trace_chi[st->trace_len] = pb.chi;
+            if (trace_lambda) trace_lambda[st->trace_len] = pb.lambda;
+        }
+        st->trace_len++;
+        int ok = 0, false_cnt = 0;
+        while (!ok && false_cnt < pb.opt.max_trials) {
+            solve_linear(&pb);
+            update_states(&pb);
+            ok = good_step(&pb);
+            st->trials++;
+            if (ok) { build_hessian(&pb); false_cnt = 0; st->accepted++; }
+            else { false_cnt++; rollback_states(&pb); }
+        }
+        ++iter;
+        if (last_chi - pb.chi < pb.opt.stop_dchi2) {
+            if (pb.opt.verbose) printf("\nStop the optimization: [last_chi_(%g) - currentChi_(%g) = %g] < %g\n",
+                                        last_chi, pb.chi, last_chi - pb.chi, pb.opt.stop_dchi2);
+            stop = 1;
+        }
+        last_chi = pb.chi;
+    }
+    st->iterations = iter;
+    st->chi2_final = pb.chi;
+    st->lambda_final = pb.lambda;
+    if (st->trace_len > trace_cap) st->trace_len = trace_cap;
+
+    if (pose_out) memcpy(pose_out, pb.pose, sizeof(double) * 12 * (size_t)P);
+    if (lm_out) memcpy(lm_out, pb.lm, sizeof(double) * 3 * (size_t)L);
+    if (edge_rchi2)
+        for (int64_t e = 0; e < O; ++e) edge_rchi2[e] = robust_chi2(&pb, pb.res + 2 * e);
+    st->time_ms = orc_now_ms() - t0;
+
+    free(pb.ext); free(pb.pose); free(pb.pose_bak); free(pb.lm); free(pb.lm_bak);
+    free(pb.res); free(pb.dx); free(pb.b); free(pb.hdiag);
+    free(pb.H); free(pb.Hpp); free(pb.bp); free(pb.Hll); free(pb.bl); free(pb.Hpl);
+    free(pb.lm_ptr); free(pb.lm_edges);
+    return 0;
+}
+
+#include <time.h>
+double orc_now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
+/* ---- small exports for known-answer tests ---- */
+void orc_se3_exp(const double a[6], double T12[12]) { se3_t T; se3_exp(a, &T); se3_to_mat(&T, T12); }
+void orc_se3_left_update(const double a[6], const double T12[12], double out12[12]) {
+    se3_t E, T, R;
+    se3_exp(a, &E);
+    se3_from_mat(T12, &T);
+    se3_mul(&E, &T, &R);
+    se3_to_mat(&R, out12);
+}
+void orc_huber(double delta, double e2, double rho[3]) { huber(delta, e2, rho); }
+void orc_lu_inverse3(const double A[9], double Ainv[9]) { lu_inverse3(A, Ainv); }
+void orc_ldlt_solve(const double *A, int n, const double *b, double *x) {
+    double *M = (double *)malloc(sizeof(double) * (size_t)n * (size_t)n);
+    memcpy(M, A, sizeof(double) * (size_t)n * (size_t)n);
+    ldlt_solve(M, n, b, x);
+    free(M);
+}
+/* residual / Jacobians / robust weight of one edge, for finite-difference tests */
+void orc_edge_eval(const double T12[12], const double X[3], const double uv[2], const double K[4],
+                   const double ext12[12], double huber_delta, double r[2], double Jp[12], double Jl[6],
+                   double W[4], double *drho, double *rchi2) {
+    prob_t pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.P = 1; pb.L = 1; pb.O = 1;
+    double pose[12], lm[3];
+    memcpy(pose, T12, sizeof(pose));
+    memcpy(lm, X, sizeof(lm));
+    uint32_t z = 0;
+    pb.pose = pose; pb.lm = lm; pb.op = &z; pb.ol = &z; pb.uv = uv;
+    memcpy(pb.K, K, sizeof(pb.K));
+    se3_t ext;
+    se3_from_mat(ext12, &ext);
+    pb.ext = &ext;
+    pb.opt.huber_delta = huber_delta;
+    edge_residual(&pb, 0, r);
+    edge_jacobians(&pb, 0, Jp, Jl);
+    robust_info(&pb, r, W, drho);
+    *rchi2 = robust_chi2(&pb, r);
+}

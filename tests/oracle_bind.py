@@ -1,0 +1,132 @@
+"""
+oracle_bind — ctypes binding to oracle/liblego_oracle.so (TEST INFRASTRUCTURE).
+
+The oracle is the checker: a CPU restatement of the reference solve
+(oracle/lego_oracle.c).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg use it.  Parity is unpinned (see oracle/lego_oracle.c header).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_LIB = os.path.join(ROOT, "oracle", "liblego_oracle.so")
+
+
+class OrcOptions(C.Structure):
+    _fields_ = [
+        ("max_iters", C.c_int32), ("max_trials", C.c_int32), ("strategy", C.c_int32),
+        ("verbose", C.c_int32), ("n_threads", C.c_int32), ("gate_mode", C.c_int32),
+        ("huber_delta", C.c_double), ("stop_dchi2", C.c_double), ("tau", C.c_double),
+        ("lambda_cap", C.c_double), ("lambda_init", C.c_double),
+    ]
+
+
+class OrcStats(C.Structure):
+    _fields_ = [
+        ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("lambda_final", C.c_double),
+        ("time_ms", C.c_double), ("iterations", C.c_int32), ("trials", C.c_int32),
+        ("accepted", C.c_int32), ("trace_len", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(ORACLE_LIB)
+        vp = C.c_void_p
+        L.orc_solve.argtypes = [C.c_int, C.c_int32, vp, vp, C.c_int32, vp, C.c_int64, vp, vp, vp, vp, vp,
+                                C.c_int32, vp, C.POINTER(OrcOptions), vp, vp, vp, vp, vp, C.c_int32,
+                                C.POINTER(OrcStats)]
+        L.orc_solve.restype = C.c_int
+        L.orc_se3_exp.argtypes = [vp, vp]
+        L.orc_se3_left_update.argtypes = [vp, vp, vp]
+        L.orc_huber.argtypes = [C.c_double, C.c_double, vp]
+        L.orc_lu_inverse3.argtypes = [vp, vp]
+        L.orc_ldlt_solve.argtypes = [vp, C.c_int, vp, vp]
+        L.orc_edge_eval.argtypes = [vp] * 5 + [C.c_double] + [vp] * 6
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def options(max_iters=10, max_trials=10, strategy=0, huber_delta=5.991, stop_dchi2=1e-5, tau=1e-5,
+            lambda_cap=5e10, lambda_init=-1.0, verbose=0, n_threads=0, gate_mode=0):
+    return OrcOptions(max_iters, max_trials, strategy, verbose, n_threads, gate_mode, huber_delta, stop_dchi2,
+                      tau, lambda_cap, lambda_init)
+
+
+def solve(w, variant=1, trace_cap=64, **opt):
+    """Run the oracle on window dict `w` (lego_ba.generate_window layout)."""
+    a = lambda k, dt: None if w.get(k) is None else np.ascontiguousarray(w[k], dtype=dt)
+    pose, lm = a("pose_Tcw", np.float64), a("lm_xyz", np.float64)
+    op, ol, oc, uv = a("obs_pose", np.uint32), a("obs_lm", np.uint32), a("obs_cam", np.uint8), a("obs_uv", np.float64)
+    fixed, ext = a("pose_fixed", np.uint8), a("cam_ext", np.float64)
+    K = np.ascontiguousarray(w["K"], np.float64)
+    P, L, O = pose.shape[0], lm.shape[0], op.shape[0]
+    out = dict(pose_Tcw=np.zeros((P, 12)), lm_xyz=np.zeros((L, 3)), edge_robust_chi2=np.zeros(O),
+               trace_chi2=np.zeros(trace_cap), trace_lambda=np.zeros(trace_cap))
+    st = OrcStats()
+    o = options(**opt)
+    rc = lib().orc_solve(variant, P, _p(pose), _p(fixed), L, _p(lm), O, _p(op), _p(ol), _p(oc), _p(uv), _p(K),
+                         0 if ext is None else ext.shape[0], _p(ext), C.byref(o), _p(out["pose_Tcw"]),
+                         _p(out["lm_xyz"]), _p(out["edge_robust_chi2"]), _p(out["trace_chi2"]),
+                         _p(out["trace_lambda"]), trace_cap, C.byref(st))
+    out["status"] = rc
+    out["trace_chi2"] = out["trace_chi2"][:st.trace_len]
+    out["trace_lambda"] = out["trace_lambda"][:st.trace_len]
+    for f in ("chi2_initial", "chi2_final", "lambda_final", "time_ms", "iterations", "trials", "accepted"):
+        out[f] = getattr(st, f)
+    return out
+
+
+def se3_exp(a):
+    T = np.zeros(12)
+    lib().orc_se3_exp(_p(np.ascontiguousarray(a, np.float64)), _p(T))
+    return T
+
+
+def se3_left_update(a, T12):
+    out = np.zeros(12)
+    lib().orc_se3_left_update(_p(np.ascontiguousarray(a, np.float64)), _p(np.ascontiguousarray(T12, np.float64)), _p(out))
+    return out
+
+
+def huber(delta, e2):
+    rho = np.zeros(3)
+    lib().orc_huber(delta, e2, _p(rho))
+    return rho
+
+
+def lu_inverse3(A):
+    out = np.zeros(9)
+    lib().orc_lu_inverse3(_p(np.ascontiguousarray(A, np.float64).reshape(9)), _p(out))
+    return out.reshape(3, 3)
+
+
+def ldlt_solve(A, b):
+    A = np.ascontiguousarray(A, np.float64)
+    x = np.zeros(A.shape[0])
+    lib().orc_ldlt_solve(_p(A), A.shape[0], _p(np.ascontiguousarray(b, np.float64)), _p(x))
+    return x
+
+
+def edge_eval(T12, X, uv, K, ext12=None, huber_delta=5.991):
+    if ext12 is None:
+        ext12 = np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0], np.float64)
+    r, Jp, Jl, W = np.zeros(2), np.zeros(12), np.zeros(6), np.zeros(4)
+    drho, rc = C.c_double(), C.c_double()
+    f = lambda v: _p(np.ascontiguousarray(v, np.float64))
+    lib().orc_edge_eval(f(T12), f(X), f(uv), f(K), f(ext12), huber_delta, _p(r), _p(Jp), _p(Jl), _p(W),
+                        C.byref(drho), C.byref(rc))
+    return dict(r=r, Jp=Jp.reshape(2, 6), Jl=Jl.reshape(2, 3), W=W.reshape(2, 2), drho=drho.value, rchi2=rc.value)
