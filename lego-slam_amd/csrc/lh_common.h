@@ -35,8 +35,19 @@
 // per-landmark cache: Cholesky of H_ll (6), b_l (3), diag H_ll (3)
 #define LH_CACHE 12
 
-// per (pose, cam) table: R_T(9) t_T(3) R_ct(9) t_ct(3); per cam ext R_e(9) t_e(3)
+// Pose state is estimate_ itself: a row-major [R | t] matrix per pose (12 doubles,
+// VertexPose stores the 4x4, lego_types.h:37,57).  Every use converts it to
+// Sophus' (quaternion, t) as SE3(estimate_) does (lego_types.h:211,229); the
+// per-trial pose table caches those conversions:
+//   per (pose, cam), LH_PT doubles:  q_T[4] t_T[3] | q_et[4] t_et[3] (ext*T) | R_T[9] | pad
+//   per cam, LH_EXT doubles:         q_e[4] t_e[3] | R_e[9]
 #define LH_PT 24
+#define LH_PT_QT 0
+#define LH_PT_TT 4
+#define LH_PT_QET 7
+#define LH_PT_TET 11
+#define LH_PT_RT 14
+#define LH_EXT 16
 
 // obs meta packing
 #define LH_META(pose, cam, slot, lms) ((uint32_t)(pose) | ((uint32_t)(cam) << 12) | ((uint32_t)(slot) << 16) | ((uint32_t)(lms) << 20))
@@ -82,6 +93,8 @@ struct lh_ctrl {
 
 struct lh_params {
     int32_t P, n, ncam, max_iters, max_trials, strategy, guard, lambda_given;
+    int32_t ext_identity;   // bit c: camera c's extrinsic is exactly the identity
+    int32_t pad_;
     double huber_delta, stop_dchi2, tau, lambda_cap, lambda_init;
     double K[4];
 };

@@ -40,6 +40,7 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           double* pose_qt, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
                           int* host_done);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
+hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
 }
 
 namespace {
@@ -107,14 +108,49 @@ void R_from_q(const double q[4], double R[9]) {
     R[6] = txz - twy;          R[7] = tyz + twx;          R[8] = 1.0 - (txx + tyy);
 }
 
-void pose_table(const double q[4], const double t[3], const double* e, double* pt) {
-    double R[9];
-    R_from_q(q, R);
-    for (int i = 0; i < 9; ++i) pt[i] = R[i];
-    for (int i = 0; i < 3; ++i) pt[9 + i] = t[i];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) pt[12 + 3 * i + j] = e[3 * i] * R[j] + e[3 * i + 1] * R[3 + j] + e[3 * i + 2] * R[6 + j];
-    for (int i = 0; i < 3; ++i) pt[21 + i] = e[3 * i] * t[0] + e[3 * i + 1] * t[1] + e[3 * i + 2] * t[2] + e[9 + i];
+void cross3(const double a[3], const double b[3], double c[3]) {
+    const double c0 = a[1] * b[2] - a[2] * b[1], c1 = a[2] * b[0] - a[0] * b[2], c2 = a[0] * b[1] - a[1] * b[0];
+    c[0] = c0; c[1] = c1; c[2] = c2;
+}
+
+void q_rotate(const double* q, const double v[3], double o[3]) {
+    double uv[3], uv2[3];
+    cross3(q + 1, v, uv);
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    cross3(q + 1, uv, uv2);
+    for (int i = 0; i < 3; ++i) o[i] = v[i] + q[0] * uv[i] + uv2[i];
+}
+
+void q_mul(const double* a, const double* b, double o[4]) {
+    double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
+    double z = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
+    const double sq = w * w + x * x + y * y + z * z;
+    if (sq != 1.0) {
+        const double sc = 2.0 / (1.0 + sq);
+        w *= sc; x *= sc; y *= sc; z *= sc;
+    }
+    o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+
+// host mirror of d_pose_table (lh_kernels.hip): estimate_ -> (q_T, t_T, ext*T, R_T)
+void pose_table(const double* T12, const double* e, double* pt) {
+    const double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
+    double q[4];
+    q_from_R(R, q);
+    const double t[3] = {T12[3], T12[7], T12[11]};
+    for (int i = 0; i < 4; ++i) pt[LH_PT_QT + i] = q[i];
+    for (int i = 0; i < 3; ++i) pt[LH_PT_TT + i] = t[i];
+    double qet[4], rt[3];
+    q_mul(e, q, qet);
+    q_rotate(e, t, rt);
+    for (int i = 0; i < 4; ++i) pt[LH_PT_QET + i] = qet[i];
+    for (int i = 0; i < 3; ++i) pt[LH_PT_TET + i] = e[4 + i] + rt[i];
+    double Rt[9];
+    R_from_q(q, Rt);
+    for (int i = 0; i < 9; ++i) pt[LH_PT_RT + i] = Rt[i];
+    pt[23] = 0.0;
 }
 
 }  // namespace
@@ -159,11 +195,13 @@ struct lh_handle {
 
 namespace {
 
+bool g_debug = getenv("LH_DEBUG") != nullptr;
+
 #define HIPCHK(x)                                                                                        \
     do {                                                                                                 \
         hipError_t e_ = (x);                                                                             \
         if (e_ != hipSuccess) {                                                                          \
-            if (getenv("LH_DEBUG")) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            if (g_debug) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, hipGetErrorString(e_)); \
             return LH_E_HIP;                                                                             \
         }                                                                                                \
     } while (0)
@@ -172,7 +210,7 @@ namespace {
     do {                                                                                                 \
         ncclResult_t r_ = (x);                                                                           \
         if (r_ != ncclSuccess) {                                                                         \
-            if (getenv("LH_DEBUG")) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, ncclGetErrorString(r_)); \
+            if (g_debug) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, ncclGetErrorString(r_)); \
             return LH_E_RCCL;                                                                            \
         }                                                                                                \
     } while (0)
@@ -394,7 +432,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
             for (int t = s; t < ck.U; ++t) {
                 const int p = ck.pose[s], q = ck.pose[t];
                 const int b = p * P - (p * (p - 1)) / 2 + (q - p);
-                plist[b].push_back(((uint32_t)ci << 8) | ((uint32_t)s << 4) | (uint32_t)t);
+                plist[b].push_back(((uint32_t)ci << 11) | ((uint32_t)ck.T << 8) | ((uint32_t)s << 4) | (uint32_t)t);
             }
     }
     std::vector<uint32_t> pair_ptr(npairs + 1, 0), items;
@@ -403,33 +441,30 @@ int upload_impl(lh_handle* h, const lh_window* w) {
         items.insert(items.end(), plist[b].begin(), plist[b].end());
     }
 
-    // ---- camera extrinsics and initial pose tables ----
-    std::vector<double> ext(12 * (size_t)ncam);
+    // ---- camera extrinsics (Sophus SE3 of Camera::pose_) and initial pose tables ----
+    std::vector<double> ext(LH_EXT * (size_t)ncam);
+    int ext_identity = 0;
     for (int c = 0; c < ncam; ++c) {
-        if (w->n_cams > 0) {
-            // SE3(estimate) round trip: R_e = R(q(R_in)) as Sophus stores it
-            const double* E = w->cam_ext + 12 * c;
-            double R[9] = {E[0], E[1], E[2], E[4], E[5], E[6], E[8], E[9], E[10]}, q[4], Rq[9];
-            q_from_R(R, q);
-            R_from_q(q, Rq);
-            for (int i = 0; i < 9; ++i) ext[12 * c + i] = Rq[i];
-            ext[12 * c + 9] = E[3]; ext[12 * c + 10] = E[7]; ext[12 * c + 11] = E[11];
-        } else {
-            const double I[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
-            std::memcpy(&ext[12 * c], I, sizeof(I));
-        }
+        static const double I12[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        const double* E = (w->n_cams > 0) ? w->cam_ext + 12 * c : I12;
+        const double R[9] = {E[0], E[1], E[2], E[4], E[5], E[6], E[8], E[9], E[10]};
+        double q[4], Rq[9];
+        q_from_R(R, q);
+        R_from_q(q, Rq);
+        double* e = &ext[LH_EXT * (size_t)c];
+        for (int i = 0; i < 4; ++i) e[i] = q[i];
+        e[4] = E[3]; e[5] = E[7]; e[6] = E[11];
+        for (int i = 0; i < 9; ++i) e[7 + i] = Rq[i];
+        if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0 && e[4] == 0.0 && e[5] == 0.0 && e[6] == 0.0)
+            ext_identity |= 1 << c;
     }
-    std::vector<double> qt(8 * (size_t)P * 2, 0.0), ptab(2 * (size_t)P * ncam * LH_PT);
+    std::vector<double> pose(24 * (size_t)P), ptab(2 * (size_t)P * ncam * LH_PT);
     for (int p = 0; p < P; ++p) {
         const double* T = w->pose_Tcw + 12 * p;
-        double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]}, q[4];
-        q_from_R(R, q);
-        double t[3] = {T[3], T[7], T[11]};
         for (int s = 0; s < 2; ++s) {
-            double* o = &qt[8 * ((size_t)s * P + p)];
-            for (int i = 0; i < 4; ++i) o[i] = q[i];
-            for (int i = 0; i < 3; ++i) o[4 + i] = t[i];
-            for (int c = 0; c < ncam; ++c) pose_table(q, t, &ext[12 * c], &ptab[((size_t)s * P * ncam + (size_t)p * ncam + c) * LH_PT]);
+            std::memcpy(&pose[12 * ((size_t)s * P + p)], T, 12 * sizeof(double));
+            for (int c = 0; c < ncam; ++c)
+                pose_table(T, &ext[LH_EXT * (size_t)c], &ptab[((size_t)s * P * ncam + (size_t)p * ncam + c) * LH_PT]);
         }
     }
 
@@ -443,6 +478,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     prm.strategy = h->opt.strategy;
     prm.guard = h->opt.degenerate_guard;
     prm.lambda_given = h->opt.lambda_init >= 0.0;
+    prm.ext_identity = ext_identity;
     prm.huber_delta = h->opt.huber_delta;
     prm.stop_dchi2 = h->opt.stop_dchi2;
     prm.tau = h->opt.tau;
@@ -468,8 +504,8 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->d_cache.ensure(2 * (size_t)Lact * LH_CACHE));
     HIPCHK(h->d_ptab.ensure(2 * PT));
     HIPCHK(h->d_ptab_init.ensure(2 * PT));
-    HIPCHK(h->d_qt.ensure(qt.size()));
-    HIPCHK(h->d_qt_init.ensure(qt.size()));
+    HIPCHK(h->d_qt.ensure(pose.size()));
+    HIPCHK(h->d_qt_init.ensure(pose.size()));
     HIPCHK(h->d_ext.ensure(ext.size()));
     HIPCHK(h->d_rho.ensure((size_t)O));
     HIPCHK(h->d_slabs.ensure((size_t)h->n_chunks * LH_SLAB_STRIDE));
@@ -493,12 +529,24 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(up(h->d_pair_pq.p, pair_pq.data(), pair_pq.size() * sizeof(uint16_t)));
     HIPCHK(up(h->d_Xinit.p, Xinit.data(), Xinit.size() * sizeof(double)));
     HIPCHK(up(h->d_ptab_init.p, ptab.data(), ptab.size() * sizeof(double)));
-    HIPCHK(up(h->d_qt_init.p, qt.data(), qt.size() * sizeof(double)));
+    HIPCHK(up(h->d_qt_init.p, pose.data(), pose.size() * sizeof(double)));
     HIPCHK(up(h->d_ext.p, ext.data(), ext.size() * sizeof(double)));
     HIPCHK(hipStreamSynchronize(s));   // host vectors die at return
     h->uploaded = true;
     return LH_OK;
 }
+
+#define DBGSYNC(name)                                                                                   \
+    do {                                                                                                \
+        if (g_debug) {                                                                                  \
+            hipError_t e_ = hipStreamSynchronize(s);                                                    \
+            if (e_ == hipSuccess) e_ = hipGetLastError();                                               \
+            if (e_ != hipSuccess) {                                                                     \
+                fprintf(stderr, "lego_ba: %s failed: %s\n", name, hipGetErrorString(e_));               \
+                return LH_E_HIP;                                                                        \
+            }                                                                                           \
+        }                                                                                               \
+    } while (0)
 
 int enqueue_trial(lh_handle* h, int mode) {
     hipStream_t s = h->stream;
@@ -509,12 +557,14 @@ int enqueue_trial(lh_handle* h, int mode) {
             HIPCHK(lh_launch_lin(T, mode, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_lm_ptr.p, h->d_uv.p,
                                  h->d_meta.p, h->d_X.p, h->d_cache.p, h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p,
                                  h->d_rho.p, h->d_slabs.p, h->prm, h->L_act, h->fixed_mask));
+            DBGSYNC("k_lin");
         }
     }
     {
         Prof pr(h, KC_REDUCE);
         HIPCHK(lh_launch_reduce(s, h->d_chunks.p, h->d_slabs.p, h->d_pair_ptr.p, h->d_items.p, h->d_pair_pq.p,
                                 h->d_ctrl.p, h->d_rs_stage.p, h->d_maxd.p, h->prm, h->n_chunks));
+        DBGSYNC("k_reduce");
     }
     if (h->comm) {
         Prof pr(h, KC_ALLREDUCE);
@@ -525,6 +575,7 @@ int enqueue_trial(lh_handle* h, int mode) {
         Prof pr(h, KC_CTRL);
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_qt.p, h->d_ptab.p,
                               h->d_ext.p, h->d_dxp.p, h->prm, mode, nullptr));
+        DBGSYNC("k_ctrl");
     }
     return LH_OK;
 }
@@ -536,7 +587,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     const size_t PT = (size_t)P * h->ncam * LH_PT;
     // restart from the uploaded initial state
     HIPCHK(hipMemcpyAsync(h->d_X.p, h->d_Xinit.p, 3 * (size_t)h->L_act * sizeof(double), hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->d_qt.p, h->d_qt_init.p, 16 * (size_t)P * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_qt.p, h->d_qt_init.p, 24 * (size_t)P * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(h->d_ptab.p, h->d_ptab_init.p, 2 * PT * sizeof(double), hipMemcpyDeviceToDevice, s));
     std::memset(h->h_ctrl, 0, sizeof(lh_ctrl));
     h->h_ctrl->cur = 0;
@@ -583,19 +634,9 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
             if (out->trace_chi2) out->trace_chi2[i] = c.trace_chi[i];
             if (out->trace_lambda) out->trace_lambda[i] = c.trace_lambda[i];
         }
-        if (out->pose_Tcw) {
-            std::vector<double> qt(8 * (size_t)P);
-            if (P) HIPCHK(hipMemcpy(qt.data(), h->d_qt.p + 8 * (size_t)cur * P, qt.size() * sizeof(double), hipMemcpyDeviceToHost));
-            for (int p = 0; p < P; ++p) {
-                double R[9];
-                R_from_q(&qt[8 * p], R);   // SE3::matrix() (lego_types.h:90)
-                double* T = out->pose_Tcw + 12 * p;
-                for (int i = 0; i < 3; ++i) {
-                    T[4 * i] = R[3 * i]; T[4 * i + 1] = R[3 * i + 1]; T[4 * i + 2] = R[3 * i + 2];
-                    T[4 * i + 3] = qt[8 * p + 4 + i];
-                }
-            }
-        }
+        if (out->pose_Tcw && P)   // estimate_ of every VertexPose (backend_lego.cpp:198-213)
+            HIPCHK(hipMemcpy(out->pose_Tcw, h->d_qt.p + 12 * (size_t)cur * P, 12 * (size_t)P * sizeof(double),
+                             hipMemcpyDeviceToHost));
         if (out->lm_xyz) {
             std::memcpy(out->lm_xyz, h->lm_in.data(), h->lm_in.size() * sizeof(double));
             std::vector<double> X(3 * (size_t)h->L_act);
@@ -797,6 +838,12 @@ int lh_classify_outliers(const double* rchi2, int64_t n_obs, double chi2_th, uin
     if (n_inlier) *n_inlier = cin;
     if (n_outlier) *n_outlier = cout;
     return LH_OK;
+}
+
+// diagnostic hook: per-phase wave-cycle totals of the -DLH_STAMPS build (zeros otherwise)
+int lh_debug_stamps(unsigned long long* out, int n, int reset) {
+    if (!out || n < 0) return LH_E_BADARG;
+    return lh_read_stamps(out, n, reset) == hipSuccess ? LH_OK : LH_E_HIP;
 }
 
 // test hook: f64 MFMA accumulator layout probe (A 16x4 row-major, B 4x16, D 16x16), device pointers

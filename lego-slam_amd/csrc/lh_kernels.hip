@@ -24,6 +24,32 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 #define LMR_SZ 16                    // per-landmark slots in the per-wave landmark region
 #define K_LIN_SMEM (LH_WAVES * SCR_SZ + LH_WAVES * LH_SB_LM * LMR_SZ + LH_WAVES * 16)
 
+// Diagnostic build (-DLH_STAMPS): per-phase wave-cycle totals via s_memtime,
+// summed over all waves into lh_stamps[] (cdna_hip_programming.md §7 "In-kernel
+// stamps").  The product build compiles these to nothing.
+#ifdef LH_STAMPS
+__device__ unsigned long long lh_stamps[64];
+#define STAMP_DECL unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_;
+#define STAMP(i)                                                                   \
+    do {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+        st1_ = __builtin_amdgcn_s_memtime();                                       \
+        if ((threadIdx.x & 63) == 0) atomicAdd(&lh_stamps[(i)], st1_ - st0_);      \
+        st0_ = st1_;                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#endif
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)x, l);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -31,10 +57,132 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // ============================================================================
-// Per-edge arithmetic, in the reference's expression order with contraction
-// off: the Huber gate (base_edge.cpp:55) tests the sign of a rounding residue.
+// Eigen / Sophus arithmetic and the per-edge path, in the reference's
+// expression order with contraction off.  This is a bitwise mirror of the
+// oracle's restatement (oracle/lego_oracle.c): the Huber gate
+// (base_edge.cpp:55) tests the sign of a rounding residue, so the residual
+// must be computed exactly as the reference computes it.
 // ============================================================================
 #pragma clang fp contract(off)
+
+// Eigen Quaternion(Matrix3): q = {w, x, y, z}, R row-major
+__device__ inline void d_q_from_R(const double* R, double q[4]) {
+    double t = R[0] + R[4] + R[8];
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[0] = 0.5 * t;
+        t = 0.5 / t;
+        q[1] = (R[7] - R[5]) * t;
+        q[2] = (R[2] - R[6]) * t;
+        q[3] = (R[3] - R[1]) * t;
+    } else {
+        int i = 0;
+        if (R[4] > R[0]) i = 1;
+        if (R[8] > R[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (R[3 * k + j] - R[3 * j + k]) * t;
+        c[j] = (R[3 * j + i] + R[3 * i + j]) * t;
+        c[k] = (R[3 * k + i] + R[3 * i + k]) * t;
+        q[1] = c[0]; q[2] = c[1]; q[3] = c[2];
+    }
+}
+
+// Eigen QuaternionBase::toRotationMatrix
+__device__ inline void d_R_from_q(const double q[4], double R[9]) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;          R[2] = txz + twy;
+    R[3] = txy + twz;          R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;          R[7] = tyz + twx;          R[8] = 1.0 - (txx + tyy);
+}
+
+__device__ __forceinline__ void d_cross(const double a[3], const double b[3], double c[3]) {
+    const double c0 = a[1] * b[2] - a[2] * b[1], c1 = a[2] * b[0] - a[0] * b[2], c2 = a[0] * b[1] - a[1] * b[0];
+    c[0] = c0; c[1] = c1; c[2] = c2;
+}
+
+// Eigen QuaternionBase::_transformVector (Sophus SO3 * point)
+__device__ __forceinline__ void d_q_rotate(const double* q, const double v[3], double o[3]) {
+    double uv[3], uv2[3];
+    d_cross(q + 1, v, uv);
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    d_cross(q + 1, uv, uv2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[i] = v[i] + q[0] * uv[i] + uv2[i];
+}
+
+// Eigen quaternion product + Sophus SO3Base::operator*= renormalisation
+__device__ inline void d_q_mul(const double* a, const double* b, double o[4]) {
+    double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
+    double z = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
+    const double sq = w * w + x * x + y * y + z * z;
+    if (sq != 1.0) {
+        const double sc = 2.0 / (1.0 + sq);
+        w *= sc; x *= sc; y *= sc; z *= sc;
+    }
+    o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+
+// Sophus SE3::exp, twist (upsilon, omega) -> (q, t)   (Sophus 1.0 se3.hpp)
+__device__ inline void d_se3_exp(const double a[6], double q[4], double t[3]) {
+    const double eps = 1e-10;
+    const double* w = a + 3;
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const double th = sqrt(th2);
+    const double half = 0.5 * th;
+    double im, re;
+    if (th < eps) {
+        const double th4 = th2 * th2;
+        im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
+        re = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
+    } else {
+        im = sin(half) / th;
+        re = cos(half);
+    }
+    q[0] = re; q[1] = im * w[0]; q[2] = im * w[1]; q[3] = im * w[2];
+    double V[9];
+    if (th < eps) {
+        d_R_from_q(q, V);
+    } else {
+        const double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+        double Om2[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                Om2[3 * i + j] = Om[3 * i] * Om[j] + Om[3 * i + 1] * Om[3 + j] + Om[3 * i + 2] * Om[6 + j];
+        const double c1 = (1.0 - cos(th)) / th2;
+        const double c2 = (th - sin(th)) / (th2 * th);
+        for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * Om[i] + c2 * Om2[i];
+    }
+    for (int i = 0; i < 3; ++i) t[i] = V[3 * i] * a[0] + V[3 * i + 1] * a[1] + V[3 * i + 2] * a[2];
+}
+
+// estimate_ (row-major [R|t]) -> pose table entry for camera extrinsic e (LH_EXT layout)
+__device__ inline void d_pose_table(const double* T12, const double* __restrict__ e, double* pt) {
+    const double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
+    double q[4];
+    d_q_from_R(R, q);                                   // SE3(estimate_)
+    const double t[3] = {T12[3], T12[7], T12[11]};
+    for (int i = 0; i < 4; ++i) pt[LH_PT_QT + i] = q[i];
+    for (int i = 0; i < 3; ++i) pt[LH_PT_TT + i] = t[i];
+    double qet[4], rt[3];
+    d_q_mul(e, q, qet);                                 // _cam_ext * T
+    d_q_rotate(e, t, rt);
+    for (int i = 0; i < 4; ++i) pt[LH_PT_QET + i] = qet[i];
+    for (int i = 0; i < 3; ++i) pt[LH_PT_TET + i] = e[4 + i] + rt[i];
+    double Rt[9];
+    d_R_from_q(q, Rt);                                  // T.rotationMatrix()
+    for (int i = 0; i < 9; ++i) pt[LH_PT_RT + i] = Rt[i];
+    pt[23] = 0.0;
+}
 
 struct EdgeEval {
     double r0, r1, e2, rho0, rho1, rho2;
@@ -43,22 +191,30 @@ struct EdgeEval {
     double Jl[6];    // 2 x 3
 };
 
-// residual_ = z - pi(K (ext (T X))) with pi(q) = q / (q_z + 1e-18)   (lego_types.h:200-216)
-// pt: R_T(9) t_T(3) R_ct(9) t_ct(3); e: R_e(9) t_e(3)
-__device__ __forceinline__ void edge_residual(const double* __restrict__ pt, const double* __restrict__ e,
+// residual_ = z - pi(K (ext (T X))), pi(q) = q / (q_z + 1e-18)   (lego_types.h:200-216)
+__device__ __forceinline__ void edge_residual(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
                                               const double X[3], double u, double v, const lh_params& prm,
                                               double& r0, double& r1) {
     double Pb[3], Pc[3];
+    d_q_rotate(pt + LH_PT_QT, X, Pb);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) Pb[i] = pt[3 * i] * X[0] + pt[3 * i + 1] * X[1] + pt[3 * i + 2] * X[2] + pt[9 + i];
+    for (int i = 0; i < 3; ++i) Pb[i] = Pb[i] + pt[LH_PT_TT + i];
+    if (ext_id) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) Pc[i] = e[3 * i] * Pb[0] + e[3 * i + 1] * Pb[1] + e[3 * i + 2] * Pb[2] + e[9 + i];
+        for (int i = 0; i < 3; ++i) Pc[i] = Pb[i];       // identity quaternion and zero t: exact
+    } else {
+        d_q_rotate(e, Pb, Pc);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pc[i] = Pc[i] + e[4 + i];
+    }
     const double fx = prm.K[0], fy = prm.K[1], cx = prm.K[2], cy = prm.K[3];
-    double p0 = fx * Pc[0] + cx * Pc[2];
+    double p0 = fx * Pc[0] + cx * Pc[2];                  // + 0 * Pc[1]: exact
     double p1 = fy * Pc[1] + cy * Pc[2];
-    double den = Pc[2] + 1e-18;
-    r0 = u - p0 / den;
-    r1 = v - p1 / den;
+    const double den = Pc[2] + 1e-18;
+    p0 /= den;
+    p1 /= den;
+    r0 = u - p0;
+    r1 = v - p1;
 }
 
 // HuberCost::compute (cost_function.cpp:5-17) + computeRobustInformation (base_edge.cpp:44-64)
@@ -70,14 +226,14 @@ __device__ __forceinline__ void edge_robust(EdgeEval& E, const lh_params& prm) {
         if (E.e2 <= d2) {
             E.rho0 = E.e2; E.rho1 = 1.0; E.rho2 = 0.0;
         } else {
-            double s = sqrt(E.e2);
+            const double s = sqrt(E.e2);
             E.rho0 = 2 * s * delta - d2;
             E.rho1 = delta / s;
             E.rho2 = -0.5 * E.rho1 / E.e2;
         }
         E.W00 = E.rho1; E.W01 = 0.0; E.W10 = 0.0; E.W11 = E.rho1;
         if (E.rho1 + 2 * E.rho2 * E.e2 > 0.0) {
-            double s2 = 2 * E.rho2;
+            const double s2 = 2 * E.rho2;
             E.W00 += s2 * E.r0 * E.r0;
             E.W01 += s2 * E.r0 * E.r1;
             E.W10 += s2 * E.r1 * E.r0;
@@ -90,12 +246,12 @@ __device__ __forceinline__ void edge_robust(EdgeEval& E, const lh_params& prm) {
 }
 
 // EdgeProjection::computeJacobians (lego_types.h:218-254) at Pc = (ext T) X
-__device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, const double X[3], const lh_params& prm,
-                                               double Jp[12], double Jl[6]) {
+__device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
+                                               const double X[3], const lh_params& prm, double Jp[12], double Jl[6]) {
     double Pc[3];
-    const double* R = pt + 12;
+    d_q_rotate(pt + LH_PT_QET, X, Pc);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) Pc[i] = R[3 * i] * X[0] + R[3 * i + 1] * X[1] + R[3 * i + 2] * X[2] + pt[21 + i];
+    for (int i = 0; i < 3; ++i) Pc[i] = Pc[i] + pt[LH_PT_TET + i];
     const double fx = prm.K[0], fy = prm.K[1];
     const double x = Pc[0], y = Pc[1], z = Pc[2];
     const double zi = 1.0 / (z + 1e-18);
@@ -104,98 +260,30 @@ __device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, co
     Jp[3] = fx * x * y * zi2;      Jp[4] = -fx - fx * x * x * zi2; Jp[5] = fx * y * zi;
     Jp[6] = 0.0;                   Jp[7] = -fy * zi;             Jp[8] = fy * y * zi2;
     Jp[9] = fy + fy * y * y * zi2; Jp[10] = -fy * x * y * zi2;   Jp[11] = -fy * x * zi;
-    // j_j = j_i(:, 0:3) * R_ext * R_T  (R_ct = R_ext R_T)
+    // j_j = (j_i(:, 0:3) * ext.rotationMatrix()) * T.rotationMatrix()
+    double A[6];
+    if (ext_id) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) A[3 * i + j] = Jp[6 * i + j];   // J * I: exact
+    } else {
+        const double* Re = e + 7;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                A[3 * i + j] = Jp[6 * i] * Re[j] + Jp[6 * i + 1] * Re[3 + j] + Jp[6 * i + 2] * Re[6 + j];
+    }
+    const double* Rt = pt + LH_PT_RT;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-            Jl[3 * i + j] = Jp[6 * i] * R[j] + Jp[6 * i + 1] * R[3 + j] + Jp[6 * i + 2] * R[6 + j];
+            Jl[3 * i + j] = A[3 * i] * Rt[j] + A[3 * i + 1] * Rt[3 + j] + A[3 * i + 2] * Rt[6 + j];
 }
 
 #pragma clang fp contract(fast)
-
-// ============================================================================
-// small SE(3) helpers (Eigen / Sophus formulas) used by k_ctrl
-// ============================================================================
-__device__ inline void d_R_from_q(const double q[4], double R[9]) {
-    const double w = q[0], x = q[1], y = q[2], z = q[3];
-    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
-    const double twx = tx * w, twy = ty * w, twz = tz * w;
-    const double txx = tx * x, txy = ty * x, txz = tz * x;
-    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
-    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;          R[2] = txz + twy;
-    R[3] = txy + twz;          R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
-    R[6] = txz - twy;          R[7] = tyz + twx;          R[8] = 1.0 - (txx + tyy);
-}
-
-__device__ inline void d_cross(const double a[3], const double b[3], double c[3]) {
-    double c0 = a[1] * b[2] - a[2] * b[1], c1 = a[2] * b[0] - a[0] * b[2], c2 = a[0] * b[1] - a[1] * b[0];
-    c[0] = c0; c[1] = c1; c[2] = c2;
-}
-
-__device__ inline void d_q_rotate(const double q[4], const double v[3], double o[3]) {
-    double uv[3], uv2[3];
-    d_cross(q + 1, v, uv);
-    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
-    d_cross(q + 1, uv, uv2);
-    for (int i = 0; i < 3; ++i) o[i] = v[i] + q[0] * uv[i] + uv2[i];
-}
-
-// Sophus SE3::exp(upsilon, omega) -> (q, t)
-__device__ inline void d_se3_exp(const double a[6], double q[4], double t[3]) {
-    const double eps = 1e-10;
-    const double* w = a + 3;
-    double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    double th = sqrt(th2);
-    double im, re;
-    if (th < eps) {
-        double th4 = th2 * th2;
-        im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
-        re = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
-    } else {
-        im = sin(0.5 * th) / th;
-        re = cos(0.5 * th);
-    }
-    q[0] = re; q[1] = im * w[0]; q[2] = im * w[1]; q[3] = im * w[2];
-    double V[9];
-    if (th < eps) {
-        d_R_from_q(q, V);
-    } else {
-        double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-        double c1 = (1.0 - cos(th)) / th2, c2 = (th - sin(th)) / (th2 * th);
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) {
-                double o2 = Om[3 * i] * Om[j] + Om[3 * i + 1] * Om[3 + j] + Om[3 * i + 2] * Om[6 + j];
-                V[3 * i + j] = ((i == j) ? 1.0 : 0.0) + c1 * Om[3 * i + j] + c2 * o2;
-            }
-    }
-    for (int i = 0; i < 3; ++i) t[i] = V[3 * i] * a[0] + V[3 * i + 1] * a[1] + V[3 * i + 2] * a[2];
-}
-
-// Eigen quaternion product + Sophus renormalisation (SO3Base::operator*=)
-__device__ inline void d_q_mul(const double a[4], const double b[4], double o[4]) {
-    double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
-    double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
-    double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
-    double z = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
-    double sq = w * w + x * x + y * y + z * z;
-    if (sq != 1.0) {
-        double s = 2.0 / (1.0 + sq);
-        w *= s; x *= s; y *= s; z *= s;
-    }
-    o[0] = w; o[1] = x; o[2] = y; o[3] = z;
-}
-
-// pose table entry for (q, t) and camera extrinsic e = (R_e, t_e)
-__device__ inline void d_pose_table(const double q[4], const double t[3], const double* __restrict__ e, double* pt) {
-    double R[9];
-    d_R_from_q(q, R);
-    for (int i = 0; i < 9; ++i) pt[i] = R[i];
-    for (int i = 0; i < 3; ++i) pt[9 + i] = t[i];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) pt[12 + 3 * i + j] = e[3 * i] * R[j] + e[3 * i + 1] * R[3 + j] + e[3 * i + 2] * R[6 + j];
-    for (int i = 0; i < 3; ++i) pt[21 + i] = e[3 * i] * t[0] + e[3 * i + 1] * t[1] + e[3 * i + 2] * t[2] + e[9 + i];
-}
 
 // ============================================================================
 // k_lin: one workgroup (4 waves) per landmark chunk; one sub-batch (<= 8
@@ -247,6 +335,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
     for (int m = 0; m < Cfg::NTASK; ++m) task[m] = 0.0;
     double chi_acc = 0.0, scale_acc = 0.0, maxd = 0.0, ndeg = 0.0;
     const int U = ck.U;
+    STAMP_DECL
 
     for (int sb = ck.sb_begin + wave; sb < (int)ck.sb_end; sb += LH_WAVES) {
         const lh_subbatch S = sbs[sb];
@@ -264,7 +353,8 @@ __global__ __launch_bounds__(256, 2) void k_lin(
             v = obs_uv[2 * (size_t)o + 1];
             X[0] = Xc[3 * (size_t)lm]; X[1] = Xc[3 * (size_t)lm + 1]; X[2] = Xc[3 * (size_t)lm + 2];
         }
-        const double* e = ext + cam * 12;
+        const double* e = ext + cam * LH_EXT;
+        const bool ext_id = (prm.ext_identity >> cam) & 1;
 
         // ---- back-substitution of the pending pose step (problem.cpp:426-429) ----
         if (TRIAL) {
@@ -272,9 +362,9 @@ __global__ __launch_bounds__(256, 2) void k_lin(
             if (has && !pfixed) {
                 const double* pt = ptc + (p * prm.ncam + cam) * LH_PT;
                 EdgeEval E;
-                edge_residual(pt, e, X, u, v, prm, E.r0, E.r1);
+                edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
                 edge_robust(E, prm);
-                edge_jacobians(pt, X, prm, E.Jp, E.Jl);
+                edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
                 const double* d = dxp + 6 * p;
                 double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
@@ -318,6 +408,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
             }
         }
 
+        STAMP(0);
         // ---- evaluate and linearise at the candidate (problem.cpp:285-331, :523-526) ----
         double hll[6] = {0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
         double hpp[21], bp[6], hpl[18];
@@ -330,9 +421,9 @@ __global__ __launch_bounds__(256, 2) void k_lin(
         if (has) {
             const double* pt = ptn + (p * prm.ncam + cam) * LH_PT;
             EdgeEval E;
-            edge_residual(pt, e, X, u, v, prm, E.r0, E.r1);
+            edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
             edge_robust(E, prm);
-            edge_jacobians(pt, X, prm, E.Jp, E.Jl);
+            edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
             edge_rho[o] = E.rho0;
             chi_acc += E.rho0;
             const double dr = (prm.huber_delta > 0.0) ? E.rho1 : 1.0;
@@ -370,6 +461,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
             }
         }
 
+        STAMP(1);
         // ---- per-landmark H_ll, b_l; Cholesky; cache for the next back-substitution ----
         wave_sync();
 #pragma unroll
@@ -409,6 +501,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
         }
         wave_sync();
 
+        STAMP(2);
         // ---- per observation: G = H_pl L^-T and bsd = G w = H_pl H_ll^-1 b_l ----
         double G[18], bsd[6];
 #pragma unroll
@@ -432,6 +525,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
             }
         }
 
+        STAMP(3);
         // ---- per-pose sums (H_pp, b_p, bsd) in ascending lane order ----
 #pragma unroll
         for (int i = 0; i < 21; ++i) scr[LH_TASKS * lane + i] = hpp[i];
@@ -461,6 +555,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
         }
         wave_sync();
 
+        STAMP(4);
         // ---- G rows into the window image [k][16T], then the MFMA SYRK ----
         {
             double2* z = reinterpret_cast<double2*>(scr);
@@ -475,6 +570,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
                 for (int j = 0; j < 3; ++j) scr[(3 * ls + j) * Cfg::GS + 6 * slot + a] = G[3 * a + j];
         }
         wave_sync();
+        STAMP(5);
         const int nk = (3 * nlm + 3) >> 2;
         for (int s = 0; s < nk; ++s) {
             double f[T];
@@ -491,6 +587,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
                 }
         }
         wave_sync();
+        STAMP(6);
     }
 
     // ---- combine the 4 waves in fixed order and write the chunk slab ----
@@ -531,6 +628,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
     for (int i = tid; i < ntile; i += 256) gs[i] = sl[i];
     for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = sl[LH_SLAB_TASK_OFF + i];
     if (tid < 4) gs[LH_SLAB_SC_OFF + tid] = sl[LH_SLAB_SC_OFF + tid];
+    STAMP(7);
 }
 
 // ============================================================================
@@ -541,17 +639,21 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
     return a * 6 - (a * (a - 1)) / 2 + (b - a);
 }
 
-__global__ __launch_bounds__(64) void k_reduce(const lh_chunk* __restrict__ chunks, const double* __restrict__ slabs,
-                                               const uint32_t* __restrict__ pair_ptr, const uint32_t* __restrict__ items,
-                                               const uint16_t* __restrict__ pair_pq, const lh_ctrl* __restrict__ ctrl,
-                                               double* __restrict__ rs, double* __restrict__ maxd_out, lh_params prm,
-                                               int n_chunks) {
+#define RT 1024
+#define RW (RT / 64)
+
+__global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs, const uint32_t* __restrict__ pair_ptr,
+                                               const uint32_t* __restrict__ items, const uint16_t* __restrict__ pair_pq,
+                                               const lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
+                                               double* __restrict__ maxd_out, lh_params prm, int n_chunks) {
     if (__builtin_amdgcn_readfirstlane(ctrl->done)) return;
+    STAMP_DECL
+    __shared__ double part[3][RW][64];
     const lh_rs_layout LY = lh_rs_make(prm.P);
-    const int b = blockIdx.x, lane = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (b == LY.npairs) {
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
-        for (int c = lane; c < n_chunks; c += 64) {
+        for (int c = tid; c < n_chunks; c += RT) {
             const double* sc = slabs + (size_t)c * LH_SLAB_STRIDE + LH_SLAB_SC_OFF;
             s0 += sc[0]; s1 += sc[1]; s2 += sc[2]; mx = fmax(mx, sc[3]);
         }
@@ -559,43 +661,61 @@ __global__ __launch_bounds__(64) void k_reduce(const lh_chunk* __restrict__ chun
             s0 += __shfl_xor(s0, off); s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off);
             mx = fmax(mx, __shfl_xor(mx, off));
         }
-        if (lane == 0) {
-            rs[LY.off_sc + LH_SC_CHI2] = s0;
-            rs[LY.off_sc + LH_SC_SCALE] = s1;
-            rs[LY.off_sc + LH_SC_NDEG] = s2;
-            rs[LY.off_sc + LH_SC_MAXD] = mx;
-            *maxd_out = mx;
+        if (lane == 0) { part[0][wave][0] = s0; part[1][wave][0] = s1; part[2][wave][0] = s2; part[0][wave][1] = mx; }
+        __syncthreads();
+        if (tid == 0) {
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, m = 0.0;
+            for (int w = 0; w < RW; ++w) { a0 += part[0][w][0]; a1 += part[1][w][0]; a2 += part[2][w][0]; m = fmax(m, part[0][w][1]); }
+            rs[LY.off_sc + LH_SC_CHI2] = a0;
+            rs[LY.off_sc + LH_SC_SCALE] = a1;
+            rs[LY.off_sc + LH_SC_NDEG] = a2;
+            rs[LY.off_sc + LH_SC_MAXD] = m;
+            *maxd_out = m;
         }
         return;
     }
     const int p = pair_pq[2 * b], q = pair_pq[2 * b + 1];
+    const bool diag = p == q;
     const int a = lane / 6, bb = lane - 6 * (lane / 6);
-    double sch = 0.0, hp = 0.0, bpv = 0.0, bsv = 0.0;
+    // lanes 0..35: S entry (a, bb) [+ H_pp entry on the diagonal]; 36..41: b_p; 42..47: bsd
+    int off_s = 0, off_h = 0;
+    if (lane < 36) off_h = LH_SLAB_TASK_OFF + (diag ? ((a < bb ? a : bb) * 6 - ((a < bb ? a : bb) * ((a < bb ? a : bb) - 1)) / 2 + ((a < bb ? bb : a) - (a < bb ? a : bb))) : 0);
+    else if (lane < 42) off_h = LH_SLAB_TASK_OFF + 21 + (lane - 36);
+    else if (lane < 48) off_h = LH_SLAB_TASK_OFF + 27 + (lane - 42);
+    const bool act_s = lane < 36, act_h = (lane < 36 && diag) || (lane >= 36 && lane < 48 && diag);
+    double vs = 0.0, vh = 0.0;
     const int it0 = pair_ptr[b], it1 = pair_ptr[b + 1];
-    for (int it = it0; it < it1; ++it) {
+    for (int it = it0 + wave; it < it1; it += RW) {
         const uint32_t item = items[it];
-        const int ch = item >> 8, sp = (item >> 4) & 15, sq = item & 15;
-        const int T = chunks[ch].T;
+        const int ch = item >> 11, T = (item >> 8) & 7, sp = (item >> 4) & 15, sq = item & 15;
         const double* sl = slabs + (size_t)ch * LH_SLAB_STRIDE;
+        if (act_s) {
+            int ra = 6 * sp + a, rc = 6 * sq + bb;
+            if ((ra >> 4) > (rc >> 4)) { const int t = ra; ra = rc; rc = t; }
+            const int R = ra >> 4, Cc = rc >> 4;
+            off_s = (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15);
+            vs += sl[off_s];
+        }
+        if (act_h) vh += sl[off_h + sp * LH_TASKS];
+    }
+    part[0][wave][lane] = vs;
+    part[1][wave][lane] = vh;
+    __syncthreads();
+    if (wave == 0) {
+        double s = 0.0, h = 0.0;
+        for (int w = 0; w < RW; ++w) { s += part[0][w][lane]; h += part[1][w][lane]; }
         if (lane < 36) {
-            int ra = 6 * sp + a, rb = 6 * sq + bb;
-            if ((ra >> 4) > (rb >> 4)) { int t = ra; ra = rb; rb = t; }
-            const int R = ra >> 4, Cc = rb >> 4;
-            const int ti = R * T - (R * (R - 1)) / 2 + (Cc - R);
-            sch += sl[ti * 256 + (ra & 15) * 16 + (rb & 15)];
-            if (p == q) hp += sl[LH_SLAB_TASK_OFF + sp * LH_TASKS + hpp_index(a < bb ? a : bb, a < bb ? bb : a)];
-        } else if (p == q && lane < 42) {
-            bpv += sl[LH_SLAB_TASK_OFF + sp * LH_TASKS + 21 + (lane - 36)];
-            bsv += sl[LH_SLAB_TASK_OFF + sp * LH_TASKS + 27 + (lane - 36)];
+            rs[LY.off_S + b * 36 + lane] = (diag ? h : 0.0) - s;
+            if (diag && a == bb) rs[LY.off_hd + 6 * p + a] = h;
+        }
+        // b_p (lanes 36..41) and bs = b_p - bsd (needs lane + 6)
+        const double bsd = __shfl_down(h, 6);
+        if (diag && lane >= 36 && lane < 42) {
+            rs[LY.off_bp + 6 * p + (lane - 36)] = h;
+            rs[LY.off_bs + 6 * p + (lane - 36)] = h - bsd;
         }
     }
-    if (lane < 36) {
-        rs[LY.off_S + b * 36 + lane] = (p == q ? hp : 0.0) - sch;
-        if (p == q && a == bb) rs[LY.off_hd + 6 * p + a] = hp;
-    } else if (p == q && lane < 42) {
-        rs[LY.off_bp + 6 * p + (lane - 36)] = bpv;
-        rs[LY.off_bs + 6 * p + (lane - 36)] = bpv - bsv;
-    }
+    STAMP(20);
 }
 
 // ============================================================================
@@ -613,7 +733,7 @@ __device__ inline double rs_S(const double* __restrict__ rs, const lh_rs_layout&
 
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
-                                             double* __restrict__ pose_qt, double* __restrict__ ptab,
+                                             double* __restrict__ pose_mat, double* __restrict__ ptab,
                                              const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
     __shared__ double A[LH_NPAD * AS];
@@ -626,6 +746,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P;
     const lh_rs_layout LY = lh_rs_make(P);
+    STAMP_DECL
 
     // ---------------- LM bookkeeping (one thread) ----------------
     if (tid == 0) {
@@ -724,6 +845,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         __syncthreads();
     }
     if (done) return;
+    STAMP(10);
     const double lambda = ctrl->lambda;
     const double* rs = rs_commit;
 
@@ -737,10 +859,13 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     __syncthreads();
     for (int i = tid; i < n; i += CT) {
-        const double di = fabs(dg[i]);
+        // total order (NaN last, ties by index) so perm is a permutation even for a poisoned S
+        double di = fabs(dg[i]);
+        if (!(di == di)) di = -1.0;
         int r = 0;
         for (int j = 0; j < n; ++j) {
-            const double dj = fabs(dg[j]);
+            double dj = fabs(dg[j]);
+            if (!(dj == dj)) dj = -1.0;
             r += (dj > di) || (dj == di && j < i);
         }
         perm[r] = i;
@@ -755,6 +880,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     for (int i = tid; i < n; i += CT) yv[i] = rs[LY.off_bs + perm[i]];
     __syncthreads();
 
+    STAMP(11);
     // ---------------- blocked right-looking LDL^T, panel width 8 ----------------
     for (int k0 = 0; k0 < n; k0 += 8) {
         const int kb = min(8, n - k0);
@@ -770,7 +896,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 if (c < kb) {
-                    const double d = __shfl(p0[c], c);
+                    const double d = readlane_d(p0[c], c);
                     const double inv = (d != 0.0) ? 1.0 / d : 0.0;
                     const double x0 = p0[c], x1 = p1[c];
                     if (lane == 0) Dv[k0 + c] = d;
@@ -782,7 +908,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #pragma unroll
                     for (int c2 = c + 1; c2 < 8; ++c2) {
                         if (c2 < kb) {
-                            const double xj = __shfl(p0[c], c2);   // unscaled column c at row k0 + c2
+                            const double xj = readlane_d(p0[c], c2);   // unscaled column c at row k0 + c2
                             if (below0 && lane >= c2) p0[c2] -= l0 * xj;
                             if (below1) p1[c2] -= l1 * xj;
                         }
@@ -835,11 +961,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         __syncthreads();
     }
 
+    STAMP(12);
     // ---------------- solve: L z = y, z /= D, L^T w = z (LDLT::_solve_impl) ----------------
     if (wave == 0) {
         double z0 = (lane < n) ? yv[lane] : 0.0, z1 = (lane + 64 < n) ? yv[lane + 64] : 0.0;
         for (int k = 0; k < n; ++k) {
-            const double zk = (k < 64) ? __shfl(z0, k) : __shfl(z1, k - 64);
+            const double zk = (k < 64) ? readlane_d(z0, k) : readlane_d(z1, k - 64);
             if (lane > k && lane < n) z0 -= A[lane * AS + k] * zk;
             if (lane + 64 > k && lane + 64 < n) z1 -= A[(lane + 64) * AS + k] * zk;
         }
@@ -847,7 +974,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         if (lane < n) { const double d = Dv[lane]; z0 = fabs(d) > tol ? z0 / d : 0.0; }
         if (lane + 64 < n) { const double d = Dv[lane + 64]; z1 = fabs(d) > tol ? z1 / d : 0.0; }
         for (int k = n - 1; k >= 0; --k) {
-            const double zk = (k < 64) ? __shfl(z0, k) : __shfl(z1, k - 64);
+            const double zk = (k < 64) ? readlane_d(z0, k) : readlane_d(z1, k - 64);
             if (lane < k) z0 -= A[k * AS + lane] * zk;
             if (lane + 64 < k) z1 -= A[k * AS + lane + 64] * zk;
         }
@@ -856,6 +983,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     __syncthreads();
 
+    STAMP(13);
     // ---------------- pose part of the gain denominator; candidate poses ----------------
     double sp = 0.0;
     for (int i = tid; i < n; i += CT) {
@@ -872,16 +1000,23 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         bool bad = false;
         for (int a = 0; a < 6; ++a) { up[a] = dxp[6 * pidx + a]; bad |= !isfinite(up[a]); }
         if (bad) for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
-        double qe[4], te[3], qn[4], tr[3];
+        // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix()
+        double qe[4], te[3], qT[4], qn[4], tr[3], Rn[9];
         d_se3_exp(up, qe, te);
-        const double* qc = pose_qt + ((size_t)cur * P + pidx) * 8;
-        d_q_mul(qe, qc, qn);
-        d_q_rotate(qe, qc + 4, tr);
-        double* qo = pose_qt + ((size_t)cand * P + pidx) * 8;
-        for (int i = 0; i < 4; ++i) qo[i] = qn[i];
-        for (int i = 0; i < 3; ++i) qo[4 + i] = te[i] + tr[i];
+        const double* Tc = pose_mat + ((size_t)cur * P + pidx) * 12;
+        const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
+        const double tc[3] = {Tc[3], Tc[7], Tc[11]};
+        d_q_from_R(Rc, qT);
+        d_q_mul(qe, qT, qn);
+        d_q_rotate(qe, tc, tr);
+        d_R_from_q(qn, Rn);
+        double* To = pose_mat + ((size_t)cand * P + pidx) * 12;
+        for (int i = 0; i < 3; ++i) {
+            To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
+            To[4 * i + 3] = te[i] + tr[i];
+        }
         for (int cam = 0; cam < prm.ncam; ++cam)
-            d_pose_table(qo, qo + 4, ext + 12 * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
+            d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
     }
     __syncthreads();
     if (tid == 0) {
@@ -889,6 +1024,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         for (int w = 0; w < CT / 64; ++w) s += s_red[w];
         ctrl->spose = s;
     }
+    STAMP(14);
 }
 
 // ============================================================================
@@ -921,16 +1057,17 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double* slabs, const uint32_t* pair_ptr,
                             const uint32_t* items, const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage,
                             double* maxd, lh_params prm, int n_chunks) {
+    (void)chunks;
     const int npairs = prm.P * (prm.P + 1) / 2;
-    hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(64), 0, st, chunks, slabs, pair_ptr, items, pair_pq, ctrl,
+    hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, slabs, pair_ptr, items, pair_pq, ctrl,
                        rs_stage, maxd, prm, n_chunks);
     return hipGetLastError();
 }
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          double* pose_qt, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
+                          double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
                           int* host_done) {
-    hipLaunchKernelGGL(k_ctrl, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pose_qt, ptab, ext, dxp, prm,
+    hipLaunchKernelGGL(k_ctrl, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pose_mat, ptab, ext, dxp, prm,
                        mode, (volatile int*)host_done);
     return hipGetLastError();
 }
@@ -941,6 +1078,22 @@ __global__ void k_mfma_probe(const double* A, const double* B, double* D) {
     v4d acc = {0.0, 0.0, 0.0, 0.0};
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(l & 15) * 4 + (l >> 4)], B[(l >> 4) * 16 + (l & 15)], acc, 0, 0, 0);
     for (int i = 0; i < 4; ++i) D[((l >> 4) + 4 * i) * 16 + (l & 15)] = acc[i];
+}
+
+hipError_t lh_read_stamps(unsigned long long* out, int n, int reset) {
+#ifdef LH_STAMPS
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lh_stamps), sizeof(unsigned long long) * (n < 64 ? n : 64));
+    if (e != hipSuccess) return e;
+    if (reset) {
+        unsigned long long z[64] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(lh_stamps), z, sizeof(z));
+    }
+    return e;
+#else
+    for (int i = 0; i < n; ++i) out[i] = 0;
+    (void)reset;
+    return hipSuccess;
+#endif
 }
 
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D) {

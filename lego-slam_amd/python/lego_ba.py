@@ -13,7 +13,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # lego-slam_amd/
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-BA_LIB = os.path.join(LIB_DIR, "liblego_ba.so")
+BA_LIB = os.environ.get("LH_LIB") or os.path.join(LIB_DIR, "liblego_ba.so")
 WIN_LIB = os.path.join(LIB_DIR, "liblego_window.so")
 
 # --------------------------------------------------------------------------
@@ -319,6 +319,15 @@ class Solver:
 
     def set_profiling(self, on):
         _check(ba_lib().lh_set_profiling(self.h, int(on)), "lh_set_profiling")
+
+
+def debug_stamps(reset=True):
+    """Per-phase wave-cycle totals from the LH_STAMPS diagnostic build (zeros otherwise)."""
+    lib = ba_lib()
+    lib.lh_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    out = (C.c_ulonglong * 64)()
+    _check(lib.lh_debug_stamps(out, 64, int(reset)), "lh_debug_stamps")
+    return np.array(out[:], dtype=np.uint64)
 
 
 def comm_unique_id():
