@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--poses", type=int, default=20)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--family", default="stable", choices=["stable", "default"])
+    ap.add_argument("--family", default="stable_noout", choices=["stable_noout", "stable", "default"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--trials-per-sync", type=int, default=0)
@@ -79,11 +79,13 @@ def main():
     torch.cuda.set_device(local)
 
     from windows import STABLE
-    params = dict(STABLE) if args.family == "stable" else {}
+    params = dict(STABLE) if args.family.startswith("stable") else {}
+    if args.family == "stable_noout":
+        params["outlier_frac"] = 0.0
     L = args.landmarks
     w = lego_ba.generate_window(P=args.poses, L=L * world, k=args.k, seed=args.seed,
                                 lm_begin=rank * L, lm_end=(rank + 1) * L, **params)
-    if args.family == "stable":
+    if args.family.startswith("stable"):
         f = np.zeros(args.poses, np.uint8)
         f[0] = 1
         w["pose_fixed"] = f

@@ -50,7 +50,8 @@
 #define LH_EXT 16
 
 // obs meta packing
-#define LH_META(pose, cam, slot, lms) ((uint32_t)(pose) | ((uint32_t)(cam) << 12) | ((uint32_t)(slot) << 16) | ((uint32_t)(lms) << 20))
+#define LH_META(pose, cam, slot, lms) ((uint32_t)(pose) | ((uint32_t)(cam) << 12) | ((uint32_t)(slot) << 16) | ((uint32_t)(lms) << 20) | LH_META_VALID)
+#define LH_META_VALID (1u << 23)
 #define LH_META_POSE(m) ((m) & 0xFFFu)
 #define LH_META_CAM(m) (((m) >> 12) & 0xFu)
 #define LH_META_SLOT(m) (((m) >> 16) & 0xFu)
@@ -62,9 +63,13 @@ struct lh_chunk {
     uint16_t pose[LH_UMAX];      // window slot -> pose
 };
 
+// A sub-batch is one wave's unit of work: n_lm landmarks, landmark l owning the
+// aligned lane group [l*G, l*G + k_l) of the sub-batch's 64 observation slots
+// (slots sb*64 .. sb*64+63; unused slots carry a meta word without LH_META_VALID).
 struct lh_subbatch {
-    uint32_t lm_begin, obs_begin;
-    uint16_t n_lm, n_obs;
+    uint32_t lm_begin;
+    uint8_t n_lm, lg;      // landmarks, log2(G) lanes per landmark
+    uint16_t pad;
 };
 
 // reduced-system buffer layout (one per state buffer)

@@ -30,7 +30,7 @@
 
 extern "C" {
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
-                         const lh_subbatch* sbs, const uint32_t* lm_ptr, const double* obs_uv, const uint32_t* obs_meta,
+                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta,
                          double* Xbuf, double* cache, const double* ptab, const double* ext, const lh_ctrl* ctrl,
                          const double* dxp, double* edge_rho, double* slabs, lh_params prm, int L, uint32_t fixed_mask);
 hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double* slabs, const uint32_t* pair_ptr,
@@ -177,7 +177,7 @@ struct lh_handle {
     // device buffers
     DevBuf<lh_chunk> d_chunks;
     DevBuf<lh_subbatch> d_sbs;
-    DevBuf<uint32_t> d_lm_ptr, d_meta, d_pair_ptr, d_items;
+    DevBuf<uint32_t> d_meta, d_pair_ptr, d_items;
     DevBuf<uint16_t> d_pair_pq;
     DevBuf<double> d_uv, d_X, d_Xinit, d_cache, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs,
         d_rs_stage, d_rs_commit, d_maxd, d_dxp;
@@ -325,8 +325,9 @@ int upload_impl(lh_handle* h, const lh_window* w) {
         return lm_mask[a] < lm_mask[b];
     });
     const int Lact = (int)order.size();
+    // ~512 chunks (2 workgroups per CU), 4*8-landmark multiples so the 4 waves get equal work
     int chunk_lm = (int)((Lact + 511) / 512);
-    chunk_lm = ((chunk_lm + LH_SB_LM - 1) / LH_SB_LM) * LH_SB_LM;
+    chunk_lm = ((chunk_lm + 4 * LH_SB_LM - 1) / (4 * LH_SB_LM)) * (4 * LH_SB_LM);
     chunk_lm = std::max(32, std::min(256, chunk_lm));
 
     struct ChunkTmp { std::vector<int32_t> lms; uint32_t mask; };
@@ -348,19 +349,15 @@ int upload_impl(lh_handle* h, const lh_window* w) {
 
     std::vector<lh_chunk> chunks;
     std::vector<lh_subbatch> sbs;
-    std::vector<uint32_t> lm_ptr;
     std::vector<uint32_t> meta;
     std::vector<double> uv, Xinit;
     h->lm_perm.clear();
     h->obs_perm.clear();
-    lm_ptr.reserve(Lact + 1);
-    meta.reserve(O);
-    uv.reserve(2 * O);
     Xinit.reserve(3 * (size_t)Lact);
-    h->obs_perm.reserve(O);
     h->lm_perm.reserve(Lact);
     for (int T = 0; T <= LH_TMAX + 1; ++T) h->tgroup_begin[T] = 0;
     int slot_of[32];
+    auto pow2ceil = [](int k) { int g = 1, lg = 0; while (g < k) { g <<= 1; ++lg; } return lg; };
     for (int ci : corder) {
         const ChunkTmp& c = ctmp[ci];
         lh_chunk ck{};
@@ -374,38 +371,47 @@ int upload_impl(lh_handle* h, const lh_window* w) {
             }
         }
         ck.sb_begin = (uint32_t)sbs.size();
-        lh_subbatch sb{};
-        bool open = false;
-        for (int32_t l : c.lms) {
-            const int k = (int)(cnt[l + 1] - cnt[l]);
-            if (!open || sb.n_lm >= LH_SB_LM || sb.n_obs + k > LH_SB_OBS) {
-                if (open) sbs.push_back(sb);
-                sb = lh_subbatch{};
-                sb.lm_begin = (uint32_t)h->lm_perm.size();
-                sb.obs_begin = (uint32_t)h->obs_perm.size();
-                open = true;
+        // sub-batches: landmark l owns the aligned lane group [l*G, l*G + k_l) of 64 slots
+        size_t i = 0;
+        while (i < c.lms.size()) {
+            int lg = 0, n = 0;
+            while (i + n < c.lms.size() && n < LH_SB_LM) {
+                const int32_t l = c.lms[i + n];
+                const int lgn = std::max(lg, pow2ceil((int)(cnt[l + 1] - cnt[l])));
+                if ((n + 1) << lgn > LH_SB_OBS) break;
+                lg = lgn;
+                ++n;
             }
-            const int lms = sb.n_lm;
-            lm_ptr.push_back((uint32_t)h->obs_perm.size());
-            h->lm_perm.push_back(l);
-            for (int a = 0; a < 3; ++a) Xinit.push_back(w->lm_xyz[3 * (size_t)l + a]);
-            for (int64_t q = cnt[l]; q < cnt[l + 1]; ++q) {
-                const int64_t o = csr[q];
-                const uint32_t p = w->obs_pose[o];
-                const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
-                meta.push_back(LH_META(p, cam, slot_of[p], lms));
-                uv.push_back(w->obs_uv[2 * o]);
-                uv.push_back(w->obs_uv[2 * o + 1]);
-                h->obs_perm.push_back(o);
+            lh_subbatch sb{};
+            sb.lm_begin = (uint32_t)h->lm_perm.size();
+            sb.n_lm = (uint8_t)n;
+            sb.lg = (uint8_t)lg;
+            const size_t base = meta.size();
+            meta.resize(base + LH_SB_OBS, 0u);
+            uv.resize(2 * (base + LH_SB_OBS), 0.0);
+            h->obs_perm.resize(base + LH_SB_OBS, -1);
+            for (int q = 0; q < n; ++q) {
+                const int32_t l = c.lms[i + q];
+                h->lm_perm.push_back(l);
+                for (int a = 0; a < 3; ++a) Xinit.push_back(w->lm_xyz[3 * (size_t)l + a]);
+                int j = 0;
+                for (int64_t r = cnt[l]; r < cnt[l + 1]; ++r, ++j) {
+                    const int64_t o = csr[r];
+                    const uint32_t p = w->obs_pose[o];
+                    const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
+                    const size_t slot = base + ((size_t)q << lg) + (size_t)j;
+                    meta[slot] = LH_META(p, cam, slot_of[p], q);
+                    uv[2 * slot] = w->obs_uv[2 * o];
+                    uv[2 * slot + 1] = w->obs_uv[2 * o + 1];
+                    h->obs_perm[slot] = o;
+                }
             }
-            sb.n_lm++;
-            sb.n_obs = (uint16_t)(sb.n_obs + k);
+            sbs.push_back(sb);
+            i += n;
         }
-        if (open) sbs.push_back(sb);
         ck.sb_end = (uint32_t)sbs.size();
         chunks.push_back(ck);
     }
-    lm_ptr.push_back((uint32_t)h->obs_perm.size());
     h->n_chunks = (int)chunks.size();
     // T group boundaries
     {
@@ -493,7 +499,6 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     const size_t PT = (size_t)P * ncam * LH_PT;
     HIPCHK(h->d_chunks.ensure(chunks.size()));
     HIPCHK(h->d_sbs.ensure(sbs.size()));
-    HIPCHK(h->d_lm_ptr.ensure(lm_ptr.size()));
     HIPCHK(h->d_meta.ensure(meta.size()));
     HIPCHK(h->d_uv.ensure(uv.size()));
     HIPCHK(h->d_pair_ptr.ensure(pair_ptr.size()));
@@ -507,7 +512,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->d_qt.ensure(pose.size()));
     HIPCHK(h->d_qt_init.ensure(pose.size()));
     HIPCHK(h->d_ext.ensure(ext.size()));
-    HIPCHK(h->d_rho.ensure((size_t)O));
+    HIPCHK(h->d_rho.ensure(meta.size()));
     HIPCHK(h->d_slabs.ensure((size_t)h->n_chunks * LH_SLAB_STRIDE));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
@@ -521,7 +526,6 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     };
     HIPCHK(up(h->d_chunks.p, chunks.data(), chunks.size() * sizeof(lh_chunk)));
     HIPCHK(up(h->d_sbs.p, sbs.data(), sbs.size() * sizeof(lh_subbatch)));
-    HIPCHK(up(h->d_lm_ptr.p, lm_ptr.data(), lm_ptr.size() * sizeof(uint32_t)));
     HIPCHK(up(h->d_meta.p, meta.data(), meta.size() * sizeof(uint32_t)));
     HIPCHK(up(h->d_uv.p, uv.data(), uv.size() * sizeof(double)));
     HIPCHK(up(h->d_pair_ptr.p, pair_ptr.data(), pair_ptr.size() * sizeof(uint32_t)));
@@ -554,7 +558,7 @@ int enqueue_trial(lh_handle* h, int mode) {
         Prof pr(h, mode == 0 ? KC_INIT : KC_LIN);
         for (int T = 1; T <= LH_TMAX; ++T) {
             const int c0 = h->tgroup_begin[T], c1 = h->tgroup_begin[T + 1];
-            HIPCHK(lh_launch_lin(T, mode, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_lm_ptr.p, h->d_uv.p,
+            HIPCHK(lh_launch_lin(T, mode, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p,
                                  h->d_meta.p, h->d_X.p, h->d_cache.p, h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p,
                                  h->d_rho.p, h->d_slabs.p, h->prm, h->L_act, h->fixed_mask));
             DBGSYNC("k_lin");
@@ -645,9 +649,10 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
                 for (int a = 0; a < 3; ++a) out->lm_xyz[3 * (size_t)h->lm_perm[i] + a] = X[3 * (size_t)i + a];
         }
         if (out->edge_robust_chi2) {
-            std::vector<double> r((size_t)h->O);
-            if (h->O) HIPCHK(hipMemcpy(r.data(), h->d_rho.p, r.size() * sizeof(double), hipMemcpyDeviceToHost));
-            for (int64_t i = 0; i < h->O; ++i) out->edge_robust_chi2[h->obs_perm[i]] = r[i];
+            std::vector<double> r(h->obs_perm.size());
+            if (!r.empty()) HIPCHK(hipMemcpy(r.data(), h->d_rho.p, r.size() * sizeof(double), hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < r.size(); ++i)
+                if (h->obs_perm[i] >= 0) out->edge_robust_chi2[h->obs_perm[i]] = r[i];
         }
     }
     if (h->opt.verbose) {
@@ -756,7 +761,7 @@ void lh_destroy(lh_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm) ncclCommDestroy(h->comm);
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
-    h->d_chunks.release(); h->d_sbs.release(); h->d_lm_ptr.release(); h->d_meta.release();
+    h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release();
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release();
     h->d_uv.release(); h->d_X.release(); h->d_Xinit.release(); h->d_cache.release(); h->d_ptab.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();

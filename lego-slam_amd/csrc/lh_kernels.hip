@@ -21,26 +21,32 @@
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define SCR_SZ 2112                  // per-wave scratch: max(64*33, 24*80) doubles
-#define LMR_SZ 16                    // per-landmark slots in the per-wave landmark region
-#define K_LIN_SMEM (LH_WAVES * SCR_SZ + LH_WAVES * LH_SB_LM * LMR_SZ + LH_WAVES * 16)
+#define K_LIN_SMEM (LH_WAVES * SCR_SZ)
 
 // Diagnostic build (-DLH_STAMPS): per-phase wave-cycle totals via s_memtime,
 // summed over all waves into lh_stamps[] (cdna_hip_programming.md §7 "In-kernel
 // stamps").  The product build compiles these to nothing.
 #ifdef LH_STAMPS
 __device__ unsigned long long lh_stamps[64];
-#define STAMP_DECL unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_;
+#define STAMP_DECL unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_, sacc_[24] = {0};
 #define STAMP(i)                                                                   \
     do {                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                         \
         st1_ = __builtin_amdgcn_s_memtime();                                       \
-        if ((threadIdx.x & 63) == 0) atomicAdd(&lh_stamps[(i)], st1_ - st0_);      \
+        sacc_[(i) % 24] += st1_ - st0_;                                            \
         st0_ = st1_;                                                               \
         __builtin_amdgcn_sched_barrier(0);                                         \
+    } while (0)
+#define STAMP_FLUSH(base, cnt)                                                     \
+    do {                                                                           \
+        if ((threadIdx.x & 63) == 0)                                               \
+            for (int i_ = 0; i_ < (cnt); ++i_)                                     \
+                if (sacc_[((base) + i_) % 24]) atomicAdd(&lh_stamps[(base) + i_], sacc_[((base) + i_) % 24]); \
     } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(i)
+#define STAMP_FLUSH(base, cnt)
 #endif
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -68,27 +74,40 @@ __device__ __forceinline__ void wave_sync() {
 // Eigen Quaternion(Matrix3): q = {w, x, y, z}, R row-major
 __device__ inline void d_q_from_R(const double* R, double q[4]) {
     double t = R[0] + R[4] + R[8];
+    double w, x, y, z;     // scalars, not an indexed array: keeps the pose code out of scratch
     if (t > 0.0) {
         t = sqrt(t + 1.0);
-        q[0] = 0.5 * t;
+        w = 0.5 * t;
         t = 0.5 / t;
-        q[1] = (R[7] - R[5]) * t;
-        q[2] = (R[2] - R[6]) * t;
-        q[3] = (R[3] - R[1]) * t;
+        x = (R[7] - R[5]) * t;
+        y = (R[2] - R[6]) * t;
+        z = (R[3] - R[1]) * t;
     } else {
         int i = 0;
         if (R[4] > R[0]) i = 1;
-        if (R[8] > R[4 * i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        q[0] = (R[3 * k + j] - R[3 * j + k]) * t;
-        c[j] = (R[3 * j + i] + R[3 * i + j]) * t;
-        c[k] = (R[3 * k + i] + R[3 * i + k]) * t;
-        q[1] = c[0]; q[2] = c[1]; q[3] = c[2];
+        if (R[8] > (i ? R[4] : R[0])) i = 2;
+        // Eigen's c[i], c[j], c[k] with j = (i+1)%3, k = (j+1)%3, written out per case
+        if (i == 0) {
+            t = sqrt(R[0] - R[4] - R[8] + 1.0);
+            x = 0.5 * t; t = 0.5 / t;
+            w = (R[7] - R[5]) * t;
+            y = (R[3] + R[1]) * t;
+            z = (R[6] + R[2]) * t;
+        } else if (i == 1) {
+            t = sqrt(R[4] - R[8] - R[0] + 1.0);
+            y = 0.5 * t; t = 0.5 / t;
+            w = (R[2] - R[6]) * t;
+            z = (R[7] + R[5]) * t;
+            x = (R[1] + R[3]) * t;
+        } else {
+            t = sqrt(R[8] - R[0] - R[4] + 1.0);
+            z = 0.5 * t; t = 0.5 / t;
+            w = (R[3] - R[1]) * t;
+            x = (R[2] + R[6]) * t;
+            y = (R[5] + R[7]) * t;
+        }
     }
+    q[0] = w; q[1] = x; q[2] = y; q[3] = z;
 }
 
 // Eigen QuaternionBase::toRotationMatrix
@@ -294,16 +313,21 @@ struct LinCfg {
     static constexpr int NT = T * (T + 1) / 2;          // upper MFMA tiles of the window
     static constexpr int GS = (T == 1) ? 16 : (T == 4 ? 80 : 48);  // G row stride: 16T + pad, conflict-free b64 frag loads
     static constexpr int UMAX = (16 * T) / 6;           // window poses that fit 16T rows
-    static constexpr int NTASK = (UMAX * LH_TASKS + 63) / 64;
 };
+
+// butterfly sum over the aligned lane group of G = 1 << lg lanes (every lane gets the total)
+__device__ __forceinline__ double group_sum(double v, int lg) {
+    for (int off = 1; off < (1 << lg); off <<= 1) v += __shfl_xor(v, off);
+    return v;
+}
 
 template <int T, bool TRIAL>
 __global__ __launch_bounds__(256, 2) void k_lin(
-    const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const uint32_t* __restrict__ lm_ptr,
-    const double* __restrict__ obs_uv, const uint32_t* __restrict__ obs_meta, double* __restrict__ Xbuf,
-    double* __restrict__ cache, const double* __restrict__ ptab, const double* __restrict__ ext,
-    const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp, double* __restrict__ edge_rho,
-    double* __restrict__ slabs, lh_params prm, int L, uint32_t fixed_mask, int chunk_base) {
+    const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
+    const uint32_t* __restrict__ obs_meta, double* __restrict__ Xbuf, double* __restrict__ cache,
+    const double* __restrict__ ptab, const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl,
+    const double* __restrict__ dxp, double* __restrict__ edge_rho, double* __restrict__ slabs, lh_params prm, int L,
+    uint32_t fixed_mask, int chunk_base) {
     using Cfg = LinCfg<T>;
     __shared__ __attribute__((aligned(16))) double smem[K_LIN_SMEM];
 
@@ -317,8 +341,6 @@ __global__ __launch_bounds__(256, 2) void k_lin(
     const int PT = prm.P * prm.ncam * LH_PT;
 
     double* scr = smem + wave * SCR_SZ;
-    double* lmr = smem + LH_WAVES * SCR_SZ + wave * (LH_SB_LM * LMR_SZ);
-    uint64_t* masks = reinterpret_cast<uint64_t*>(smem + LH_WAVES * SCR_SZ + LH_WAVES * LH_SB_LM * LMR_SZ) + wave * 16;
 
     const double* Xc = Xbuf + (size_t)cur * L * 3;
     double* Xn = Xbuf + (size_t)cand * L * 3;
@@ -330,28 +352,55 @@ __global__ __launch_bounds__(256, 2) void k_lin(
     v4d acc[Cfg::NT];
 #pragma unroll
     for (int t = 0; t < Cfg::NT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
-    double task[Cfg::NTASK];
+    double task[Cfg::UMAX];
 #pragma unroll
-    for (int m = 0; m < Cfg::NTASK; ++m) task[m] = 0.0;
+    for (int u = 0; u < Cfg::UMAX; ++u) task[u] = 0.0;
     double chi_acc = 0.0, scale_acc = 0.0, maxd = 0.0, ndeg = 0.0;
     const int U = ck.U;
     STAMP_DECL
 
-    for (int sb = ck.sb_begin + wave; sb < (int)ck.sb_end; sb += LH_WAVES) {
+    // prefetch of the first sub-batch's observation words
+    int sb = ck.sb_begin + wave;
+    uint32_t meta_n = 0u;
+    double u_n = 0.0, v_n = 0.0;
+    if (sb < (int)ck.sb_end) {
+        const int o = sb * 64 + lane;
+        meta_n = obs_meta[o];
+        u_n = obs_uv[2 * (size_t)o];
+        v_n = obs_uv[2 * (size_t)o + 1];
+    }
+
+    for (; sb < (int)ck.sb_end; sb += LH_WAVES) {
         const lh_subbatch S = sbs[sb];
-        const int nobs = S.n_obs, nlm = S.n_lm;
-        const bool has = lane < nobs;
-        const int o = S.obs_begin + lane;
-        const uint32_t meta = has ? obs_meta[o] : 0u;
-        const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta), ls = LH_META_LMS(meta);
+        const int lg = S.lg, nlm = S.n_lm;
+        const int ls = lane >> lg, gj = lane & ((1 << lg) - 1);
+        const bool lead = gj == 0 && ls < nlm;       // one lane per landmark writes its results
+        const uint32_t meta = meta_n;
+        const double u = u_n, v = v_n;
+        const int o = sb * 64 + lane;
+        // prefetch the next sub-batch of this wave
+        {
+            const int sbn = sb + LH_WAVES;
+            if (sbn < (int)ck.sb_end) {
+                const int on = sbn * 64 + lane;
+                meta_n = obs_meta[on];
+                u_n = obs_uv[2 * (size_t)on];
+                v_n = obs_uv[2 * (size_t)on + 1];
+            }
+        }
+        const bool has = (meta & LH_META_VALID) != 0u;
+        const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta);
         const bool pfixed = (fixed_mask >> p) & 1u;
-        const int lm = S.lm_begin + ls;
+        const bool lmok = ls < nlm;
+        const int lm = S.lm_begin + (lmok ? ls : 0);
         double X[3] = {0.0, 0.0, 0.0};
-        double u = 0.0, v = 0.0;
-        if (has) {
-            u = obs_uv[2 * (size_t)o];
-            v = obs_uv[2 * (size_t)o + 1];
+        double cl[LH_CACHE];
+        if (lmok) {
             X[0] = Xc[3 * (size_t)lm]; X[1] = Xc[3 * (size_t)lm + 1]; X[2] = Xc[3 * (size_t)lm + 2];
+        }
+        if (TRIAL && lmok) {
+#pragma unroll
+            for (int i = 0; i < LH_CACHE; ++i) cl[i] = cc[(size_t)lm * LH_CACHE + i];
         }
         const double* e = ext + cam * LH_EXT;
         const bool ext_id = (prm.ext_identity >> cam) & 1;
@@ -369,46 +418,35 @@ __global__ __launch_bounds__(256, 2) void k_lin(
                 double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
                 for (int a = 0; a < 6; ++a) { jd0 += E.Jp[a] * d[a]; jd1 += E.Jp[6 + a] * d[a]; }
-                double y0 = E.W00 * jd0 + E.W01 * jd1, y1 = E.W10 * jd0 + E.W11 * jd1;
+                const double y0 = E.W00 * jd0 + E.W01 * jd1, y1 = E.W10 * jd0 + E.W11 * jd1;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) v3[c] = E.Jl[c] * y0 + E.Jl[3 + c] * y1;
             }
-            scr[3 * lane] = v3[0]; scr[3 * lane + 1] = v3[1]; scr[3 * lane + 2] = v3[2];
-            wave_sync();
-            if (lane < nlm) {
-                const int lmj = S.lm_begin + lane;
-                const int i0 = (int)(lm_ptr[lmj] - S.obs_begin), i1 = (int)(lm_ptr[lmj + 1] - S.obs_begin);
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-                for (int i = i0; i < i1; ++i) { s0 += scr[3 * i]; s1 += scr[3 * i + 1]; s2 += scr[3 * i + 2]; }
-                const double* cl = cc + (size_t)lmj * LH_CACHE;
+            const double s0 = group_sum(v3[0], lg), s1 = group_sum(v3[1], lg), s2 = group_sum(v3[2], lg);
+            if (lmok) {
                 const double l00 = cl[0], l10 = cl[1], l11 = cl[2], l20 = cl[3], l21 = cl[4], l22 = cl[5];
                 const double b0 = cl[6], b1 = cl[7], b2 = cl[8];
-                double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
-                double y0 = t0 / l00, y1 = (t1 - l10 * y0) / l11, y2 = (t2 - l20 * y0 - l21 * y1) / l22;
-                double d2 = y2 / l22, d1 = (y1 - l21 * d2) / l11, d0 = (y0 - l10 * d1 - l20 * d2) / l00;
+                const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+                const double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
+                const double y0 = t0 * i00, y1 = (t1 - l10 * y0) * i11, y2 = (t2 - l20 * y0 - l21 * y1) * i22;
+                double d2 = y2 * i22, d1 = (y1 - l21 * d2) * i11, d0 = (y0 - l10 * d1 - l20 * d2) * i00;
                 if (prm.guard && !(l00 == l00)) { d0 = d1 = d2 = 0.0; }   // skipped degenerate landmark
-                double sc;
-                if (prm.strategy == 0) sc = d0 * (lambda * d0 + b0) + d1 * (lambda * d1 + b1) + d2 * (lambda * d2 + b2);
-                else sc = d0 * (lambda * cl[9] * d0 + b0) + d1 * (lambda * cl[10] * d1 + b1) + d2 * (lambda * cl[11] * d2 + b2);
-                scale_acc += sc;
-                const double x0 = Xc[3 * (size_t)lmj], x1 = Xc[3 * (size_t)lmj + 1], x2 = Xc[3 * (size_t)lmj + 2];
-                double n0 = x0, n1 = x1, n2 = x2;
-                if (isfinite(d0) && isfinite(d1) && isfinite(d2)) { n0 = x0 + d0; n1 = x1 + d1; n2 = x2 + d2; }   // VertexXYZ::add
-                Xn[3 * (size_t)lmj] = n0; Xn[3 * (size_t)lmj + 1] = n1; Xn[3 * (size_t)lmj + 2] = n2;
-                lmr[LMR_SZ * lane] = n0; lmr[LMR_SZ * lane + 1] = n1; lmr[LMR_SZ * lane + 2] = n2;
+                double x0 = X[0], x1 = X[1], x2 = X[2];
+                if (isfinite(d0) && isfinite(d1) && isfinite(d2)) { x0 += d0; x1 += d1; x2 += d2; }   // VertexXYZ::add
+                if (lead) {
+                    double sc;
+                    if (prm.strategy == 0) sc = d0 * (lambda * d0 + b0) + d1 * (lambda * d1 + b1) + d2 * (lambda * d2 + b2);
+                    else sc = d0 * (lambda * cl[9] * d0 + b0) + d1 * (lambda * cl[10] * d1 + b1) + d2 * (lambda * cl[11] * d2 + b2);
+                    scale_acc += sc;
+                    Xn[3 * (size_t)lm] = x0; Xn[3 * (size_t)lm + 1] = x1; Xn[3 * (size_t)lm + 2] = x2;
+                }
+                X[0] = x0; X[1] = x1; X[2] = x2;
             }
-            wave_sync();
-            if (has) { X[0] = lmr[LMR_SZ * ls]; X[1] = lmr[LMR_SZ * ls + 1]; X[2] = lmr[LMR_SZ * ls + 2]; }
-        } else {
-            if (lane < nlm) {
-                const int lmj = S.lm_begin + lane;
-                Xn[3 * (size_t)lmj] = Xc[3 * (size_t)lmj];
-                Xn[3 * (size_t)lmj + 1] = Xc[3 * (size_t)lmj + 1];
-                Xn[3 * (size_t)lmj + 2] = Xc[3 * (size_t)lmj + 2];
-            }
+        } else if (lead) {
+            Xn[3 * (size_t)lm] = X[0]; Xn[3 * (size_t)lm + 1] = X[1]; Xn[3 * (size_t)lm + 2] = X[2];
         }
-
         STAMP(0);
+
         // ---- evaluate and linearise at the candidate (problem.cpp:285-331, :523-526) ----
         double hll[6] = {0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
         double hpp[21], bp[6], hpl[18];
@@ -460,102 +498,87 @@ __global__ __launch_bounds__(256, 2) void k_lin(
                 }
             }
         }
-
         STAMP(1);
-        // ---- per-landmark H_ll, b_l; Cholesky; cache for the next back-substitution ----
-        wave_sync();
-#pragma unroll
-        for (int i = 0; i < 6; ++i) scr[9 * lane + i] = hll[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) scr[9 * lane + 6 + i] = bl[i];
-        wave_sync();
-        if (lane < nlm) {
-            const int lmj = S.lm_begin + lane;
-            const int i0 = (int)(lm_ptr[lmj] - S.obs_begin), i1 = (int)(lm_ptr[lmj + 1] - S.obs_begin);
-            double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            for (int i = i0; i < i1; ++i)
-#pragma unroll
-                for (int j = 0; j < 9; ++j) h[j] += scr[9 * i + j];
-            maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
-            double l00 = sqrt(h[0]);
-            double l10 = h[1] / l00, l20 = h[2] / l00;
-            double a11 = h[3] - l10 * l10;
-            double l11 = sqrt(a11);
-            double l21 = (h[4] - l20 * l10) / l11;
-            double a22 = h[5] - l20 * l20 - l21 * l21;
-            double l22 = sqrt(a22);
-            const bool pd = (h[0] > 0.0) && (a11 > 0.0) && (a22 > 0.0) && isfinite(l22) && isfinite(l21);
-            if (!pd) {
-                ndeg += 1.0;
-                l00 = __builtin_nan("");   // poisons the Schur step, as a singular LU inverse does (problem.cpp:399)
-            }
-            double w0 = h[6] / l00, w1 = (h[7] - l10 * w0) / l11, w2 = (h[8] - l20 * w0 - l21 * w1) / l22;
-            double* cl = cn + (size_t)lmj * LH_CACHE;
-            cl[0] = l00; cl[1] = l10; cl[2] = l11; cl[3] = l20; cl[4] = l21; cl[5] = l22;
-            cl[6] = h[6]; cl[7] = h[7]; cl[8] = h[8];
-            cl[9] = h[0]; cl[10] = h[3]; cl[11] = h[5];
-            double* lr = lmr + LMR_SZ * lane;
-            lr[3] = l00; lr[4] = l10; lr[5] = l11; lr[6] = l20; lr[7] = l21; lr[8] = l22;
-            lr[9] = w0; lr[10] = w1; lr[11] = w2;
-            lr[12] = pd ? 1.0 : 0.0;
-        }
-        wave_sync();
 
+        // ---- per-landmark H_ll, b_l over the lane group; Cholesky (redundant per lane) ----
+        double h[9];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) h[i] = group_sum(hll[i], lg);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) h[6 + i] = group_sum(bl[i], lg);
+        double l00 = sqrt(h[0]);
+        double i00 = 1.0 / l00;
+        double l10 = h[1] * i00, l20 = h[2] * i00;
+        const double a11 = h[3] - l10 * l10;
+        const double l11 = sqrt(a11), i11 = 1.0 / l11;
+        const double l21 = (h[4] - l20 * l10) * i11;
+        const double a22 = h[5] - l20 * l20 - l21 * l21;
+        const double l22 = sqrt(a22), i22 = 1.0 / l22;
+        const bool pd = (h[0] > 0.0) && (a11 > 0.0) && (a22 > 0.0) && isfinite(l22) && isfinite(l21);
+        if (!pd) { l00 = __builtin_nan(""); i00 = __builtin_nan(""); }   // poisons the step, like a singular LU inverse (problem.cpp:399)
+        const double w0 = h[6] * i00, w1 = (h[7] - l10 * w0) * i11, w2 = (h[8] - l20 * w0 - l21 * w1) * i22;
+        if (lead) {
+            maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
+            if (!pd) ndeg += 1.0;
+            double* cw = cn + (size_t)lm * LH_CACHE;
+            cw[0] = l00; cw[1] = l10; cw[2] = l11; cw[3] = l20; cw[4] = l21; cw[5] = l22;
+            cw[6] = h[6]; cw[7] = h[7]; cw[8] = h[8];
+            cw[9] = h[0]; cw[10] = h[3]; cw[11] = h[5];
+        }
         STAMP(2);
+
         // ---- per observation: G = H_pl L^-T and bsd = G w = H_pl H_ll^-1 b_l ----
         double G[18], bsd[6];
 #pragma unroll
         for (int i = 0; i < 18; ++i) G[i] = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) bsd[i] = 0.0;
-        if (has && !pfixed) {
-            const double* lr = lmr + LMR_SZ * ls;
-            const double l00 = lr[3], l10 = lr[4], l11 = lr[5], l20 = lr[6], l21 = lr[7], l22 = lr[8];
-            const double w0 = lr[9], w1 = lr[10], w2 = lr[11];
-            const bool skip = prm.guard && lr[12] == 0.0;
-            if (!skip) {
+        if (has && !pfixed && !(prm.guard && !pd)) {
 #pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    double g0 = hpl[3 * a] / l00;
-                    double g1 = (hpl[3 * a + 1] - l10 * g0) / l11;
-                    double g2 = (hpl[3 * a + 2] - l20 * g0 - l21 * g1) / l22;
-                    G[3 * a] = g0; G[3 * a + 1] = g1; G[3 * a + 2] = g2;
-                    bsd[a] = g0 * w0 + g1 * w1 + g2 * w2;
-                }
+            for (int a = 0; a < 6; ++a) {
+                const double g0 = hpl[3 * a] * i00;
+                const double g1 = (hpl[3 * a + 1] - l10 * g0) * i11;
+                const double g2 = (hpl[3 * a + 2] - l20 * g0 - l21 * g1) * i22;
+                G[3 * a] = g0; G[3 * a + 1] = g1; G[3 * a + 2] = g2;
+                bsd[a] = g0 * w0 + g1 * w1 + g2 * w2;
             }
         }
-
         STAMP(3);
-        // ---- per-pose sums (H_pp, b_p, bsd) in ascending lane order ----
+
+        // ---- per-pose sums (H_pp, b_p, bsd): lanes 0..32 walk each pose's observations in lane order ----
 #pragma unroll
         for (int i = 0; i < 21; ++i) scr[LH_TASKS * lane + i] = hpp[i];
 #pragma unroll
         for (int i = 0; i < 6; ++i) scr[LH_TASKS * lane + 21 + i] = bp[i];
 #pragma unroll
         for (int i = 0; i < 6; ++i) scr[LH_TASKS * lane + 27 + i] = bsd[i];
-        for (int uu = 0; uu < U; ++uu) {
-            uint64_t mk = __ballot(has && slot == uu);
-            if (lane == 0) masks[uu] = mk;
-        }
         wave_sync();
 #pragma unroll
-        for (int m = 0; m < Cfg::NTASK; ++m) {
-            const int t = lane + 64 * m;
-            if (t < U * LH_TASKS) {
-                const int uu = t / LH_TASKS, ee = t - uu * LH_TASKS;
-                uint64_t mk = masks[uu];
-                double s = task[m];
-                while (mk) {
-                    const int i = __builtin_ctzll(mk);
-                    s += scr[LH_TASKS * i + ee];
-                    mk &= mk - 1;
+        for (int uu = 0; uu < Cfg::UMAX; ++uu) {
+            if (uu < U) {
+                uint64_t mk = __ballot(has && slot == uu);
+                if (lane < LH_TASKS) {
+                    double sacc = task[uu];
+                    while (mk) {
+                        const int i0 = __builtin_ctzll(mk);
+                        mk &= mk - 1;
+                        if (mk) {
+                            const int i1 = __builtin_ctzll(mk);
+                            mk &= mk - 1;
+                            const double a0 = scr[LH_TASKS * i0 + lane], a1 = scr[LH_TASKS * i1 + lane];
+                            sacc += a0;
+                            sacc += a1;
+                        } else {
+                            sacc += scr[LH_TASKS * i0 + lane];
+                        }
+                    }
+                    task[uu] = sacc;
                 }
-                task[m] = s;
             }
         }
         wave_sync();
-
         STAMP(4);
+
         // ---- G rows into the window image [k][16T], then the MFMA SYRK ----
         {
             double2* z = reinterpret_cast<double2*>(scr);
@@ -590,45 +613,53 @@ __global__ __launch_bounds__(256, 2) void k_lin(
         STAMP(6);
     }
 
-    // ---- combine the 4 waves in fixed order and write the chunk slab ----
-    __syncthreads();
-    double* sl = smem;   // reuses the scratch (SLAB_STRIDE <= 4 * SCR_SZ)
-    const int ntile = Cfg::NT * 256;
-    const int ntask = U * LH_TASKS;
-    // wave-level scalar reductions (fixed butterfly)
+    // ---- combine the 4 waves, (w0 + w2) + (w1 + w3), and write the chunk slab ----
     for (int off = 32; off > 0; off >>= 1) {
         chi_acc += __shfl_xor(chi_acc, off);
         scale_acc += __shfl_xor(scale_acc, off);
         ndeg += __shfl_xor(ndeg, off);
         maxd = fmax(maxd, __shfl_xor(maxd, off));
     }
-    for (int w = 0; w < LH_WAVES; ++w) {
-        if (wave == w) {
+    __syncthreads();
+    const int ntile = Cfg::NT * 256;
+    const int ntask = U * LH_TASKS;
+    for (int phase = 0; phase < 2; ++phase) {
+        if ((wave >> 1) == phase) {
+            double* sl = smem + (wave & 1) * LH_SLAB_STRIDE;
+            const bool first = phase == 0;
 #pragma unroll
             for (int t = 0; t < Cfg::NT; ++t)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int idx = t * 256 + ((lane >> 4) + 4 * i) * 16 + (lane & 15);
-                    sl[idx] = (w == 0 ? 0.0 : sl[idx]) + acc[t][i];
+                    sl[idx] = (first ? 0.0 : sl[idx]) + acc[t][i];
                 }
+            if (lane < LH_TASKS) {
 #pragma unroll
-            for (int m = 0; m < Cfg::NTASK; ++m) {
-                const int t = lane + 64 * m;
-                if (t < ntask) sl[LH_SLAB_TASK_OFF + t] = (w == 0 ? 0.0 : sl[LH_SLAB_TASK_OFF + t]) + task[m];
+                for (int uu = 0; uu < Cfg::UMAX; ++uu) {
+                    if (uu < U) {
+                        const int idx = LH_SLAB_TASK_OFF + uu * LH_TASKS + lane;
+                        sl[idx] = (first ? 0.0 : sl[idx]) + task[uu];
+                    }
+                }
             }
             if (lane == 0) {
                 double* sc = sl + LH_SLAB_SC_OFF;
-                if (w == 0) { sc[0] = chi_acc; sc[1] = scale_acc; sc[2] = ndeg; sc[3] = maxd; }
+                if (first) { sc[0] = chi_acc; sc[1] = scale_acc; sc[2] = ndeg; sc[3] = maxd; }
                 else { sc[0] += chi_acc; sc[1] += scale_acc; sc[2] += ndeg; sc[3] = fmax(sc[3], maxd); }
             }
         }
         __syncthreads();
     }
+    const double* s0 = smem;
+    const double* s1 = smem + LH_SLAB_STRIDE;
     double* gs = slabs + (size_t)chunk * LH_SLAB_STRIDE;
-    for (int i = tid; i < ntile; i += 256) gs[i] = sl[i];
-    for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = sl[LH_SLAB_TASK_OFF + i];
-    if (tid < 4) gs[LH_SLAB_SC_OFF + tid] = sl[LH_SLAB_SC_OFF + tid];
+    for (int i = tid; i < ntile; i += 256) gs[i] = s0[i] + s1[i];
+    for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = s0[LH_SLAB_TASK_OFF + i] + s1[LH_SLAB_TASK_OFF + i];
+    if (tid < 3) gs[LH_SLAB_SC_OFF + tid] = s0[LH_SLAB_SC_OFF + tid] + s1[LH_SLAB_SC_OFF + tid];
+    if (tid == 3) gs[LH_SLAB_SC_OFF + 3] = fmax(s0[LH_SLAB_SC_OFF + 3], s1[LH_SLAB_SC_OFF + 3]);
     STAMP(7);
+    STAMP_FLUSH(0, 8);
 }
 
 // ============================================================================
@@ -716,19 +747,39 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
         }
     }
     STAMP(20);
+    STAMP_FLUSH(20, 1);
 }
 
 // ============================================================================
 // k_ctrl: LM controller + reduced-system solve, one workgroup of 256 threads.
+//
+//  1. one global round trip: every thread prefetches its slice of BOTH reduced
+//     systems (staged candidate linearisation and committed one) plus the
+//     controller and pose matrices, while thread 0 runs isGoodStepInLM;
+//  2. the chosen system is scattered straight from registers into LDS in Eigen's
+//     LDLT pivot order (problem.cpp:420; left-looking Eigen LDLT pivots on the
+//     ORIGINAL |diag|, so the order is a static sort), committing it on accept;
+//  3. right-looking blocked LDL^T, panel 8: every panel thread factors the 8x8
+//     diagonal block redundantly in registers (no cross-lane chain), then its
+//     own row; the right-hand side rides along as an extra row (row NP), so the
+//     forward substitution is part of the factorisation;
+//  4. blocked back substitution in one wave; candidate poses (VertexPose::add).
+// The matrix is padded to NE = ceil8(n) with identity rows: no bounds tests in
+// the inner loops.
 // ============================================================================
 #define CT 256
-#define AS (LH_NPAD + 1)   // LDS row stride of the reduced matrix (odd: conflict-free column reads)
+#define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
+#define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
+#define XS 9                  // LDS row stride of the panel's unscaled columns
+#define RS_MAX (LH_PMAX * (LH_PMAX + 1) / 2 * 36 + 18 * LH_PMAX + 8)
+#define NLD ((RS_MAX + CT - 1) / CT)
 
-__device__ inline double rs_S(const double* __restrict__ rs, const lh_rs_layout& LY, int P, int i, int j) {
-    int pi = i / 6, pj = j / 6, a = i - 6 * pi, b = j - 6 * pj;
-    if (pi > pj) { int t = pi; pi = pj; pj = t; t = a; a = b; b = t; }
-    const int pair = pi * P - (pi * (pi - 1)) / 2 + (pj - pi);
-    return rs[LY.off_S + pair * 36 + a * 6 + b];
+// 1/d with one v_rcp_f64 and two Newton steps (the LDLT pivots are not a bitwise-mirrored path)
+__device__ __forceinline__ double fast_rcp(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return r;
 }
 
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
@@ -736,260 +787,366 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                                              double* __restrict__ pose_mat, double* __restrict__ ptab,
                                              const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
-    __shared__ double A[LH_NPAD * AS];
-    __shared__ double Xp[LH_NPAD * 8];     // unscaled panel column values
-    __shared__ double Dv[LH_NPAD], yv[LH_NPAD], dg[LH_NPAD];
-    __shared__ int perm[LH_NPAD];
+    __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
+    __shared__ double Xp[NP * XS];        // unscaled panel columns (W = L D) for the trailing update
+    __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP], tmp8[8];
+    __shared__ int perm[NP], iperm[NP];
+    __shared__ unsigned char pr_p[LH_PMAX * (LH_PMAX + 1) / 2], pr_q[LH_PMAX * (LH_PMAX + 1) / 2];
     __shared__ int s_flags[4];
-    __shared__ double s_red[CT / 64];
+    __shared__ double s_red[CT / 64], s_lam;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int P = prm.P, n = 6 * P;
+    const int P = prm.P, n = 6 * P, NE = (n + 7) & ~7;
     const lh_rs_layout LY = lh_rs_make(P);
     STAMP_DECL
 
-    // ---------------- LM bookkeeping (one thread) ----------------
+    // ---------------- 1. prefetch (one round trip) ----------------
+    double vs[NLD], vc[NLD];
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+        const int i = u * CT + tid;
+        const bool in = i < LY.total;
+        vs[u] = in ? rs_stage[i] : 0.0;
+        vc[u] = in ? rs_commit[i] : 0.0;
+    }
+    double pm0[12], pm1[12];
+    if (tid < P) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { pm0[i] = pose_mat[(size_t)tid * 12 + i]; pm1[i] = pose_mat[((size_t)P + tid) * 12 + i]; }
+    }
+    if (tid < P) {
+        const int base = tid * P - (tid * (tid - 1)) / 2;
+        for (int q = tid; q < P; ++q) { pr_p[base + q - tid] = (unsigned char)tid; pr_q[base + q - tid] = (unsigned char)q; }
+    }
+    if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
+        double mx = 0.0;
+#pragma unroll
+        for (int u = 0; u < NLD; ++u) {
+            const int i = u * CT + tid;
+            if (i >= LY.off_hd && i < LY.off_hd + n) mx = fmax(mx, fabs(vs[u]));
+        }
+        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+        if (lane == 0) s_red[wave] = mx;
+        __syncthreads();
+    }
+
+    // ---------------- LM bookkeeping (thread 0) ----------------
     if (tid == 0) {
-        lh_ctrl& c = *ctrl;
-        int accept_copy = 0;
-        if (!c.done) {
-            const double tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
+        double chi = ctrl->chi, lam = ctrl->lambda, ni = ctrl->ni, last = ctrl->last_chi, spose = ctrl->spose;
+        double chi0 = ctrl->chi2_initial;
+        int iter = ctrl->iter, fc = ctrl->false_cnt, trials = ctrl->trials, nacc = ctrl->accepted;
+        int done = ctrl->done, cur = ctrl->cur, tl = ctrl->trace_len;
+        const double tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
+        const double sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+        int accept = 0, trace = 0;
+        if (!done) {
             if (mode == 0) {
                 // computeLambdaInitLM (problem.cpp:470-504)
-                c.ni = 2.0;
-                c.chi = tchi;
-                c.chi2_initial = tchi;
+                ni = 2.0;
+                chi = tchi;
+                chi0 = tchi;
                 if (prm.strategy == 0) {
                     if (!prm.lambda_given) {
                         double m = 0.0;
-                        for (int i = 0; i < n; ++i) m = fmax(fabs(rs_stage[LY.off_hd + i]), m);
+                        for (int w = 0; w < CT / 64; ++w) m = fmax(m, s_red[w]);
                         m = fmax(*maxd_in, m);
                         m = fmin(prm.lambda_cap, m);
-                        c.lambda = prm.tau * m;
+                        lam = prm.tau * m;
                     } else {
-                        c.lambda = prm.lambda_init;
+                        lam = prm.lambda_init;
                     }
                 } else {
-                    c.lambda = 1e-5;
+                    lam = 1e-5;
                 }
-                c.last_chi = 1e20;
-                c.iter = 0; c.false_cnt = 0; c.trials = 0; c.accepted = 0; c.trace_len = 0;
-                c.cur = 1 - c.cur;     // the initial linearisation becomes the committed one
-                accept_copy = 1;
-                if (prm.max_iters <= 0) c.done = 1;
-                else { c.trace_chi[0] = c.chi; c.trace_lambda[0] = c.lambda; c.trace_len = 1; }
+                last = 1e20;
+                iter = 0; fc = 0; trials = 0; nacc = 0; tl = 0;
+                cur = 1 - cur;           // the initial linearisation becomes the committed one
+                accept = 1;
+                if (prm.max_iters <= 0) done = 1;
+                else trace = 1;
             } else {
                 // isGoodStepInLM (problem.cpp:520-581)
-                bool ok;
-                const double sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+                double scale = 0.5 * (spose + sl);
+                scale += 1e-10;
+                const double rho = (chi - tchi) / scale;
+                const bool ok = rho > 0 && isfinite(tchi);
                 if (prm.strategy == 0) {
-                    double scale = 0.5 * (c.spose + sl);
-                    scale += 1e-10;
-                    const double rho = (c.chi - tchi) / scale;
-                    ok = rho > 0 && isfinite(tchi);
                     if (ok) {
                         double alpha = 1.0 - pow((2 * rho - 1), 3);
                         alpha = fmin(alpha, 2.0 / 3.0);
-                        c.lambda *= fmax(1.0 / 3.0, alpha);
-                        c.ni = 2;
-                        c.chi = tchi;
+                        lam *= fmax(1.0 / 3.0, alpha);
+                        ni = 2;
+                        chi = tchi;
                     } else {
-                        c.lambda *= c.ni;
-                        c.ni *= 2;
+                        lam *= ni;
+                        ni *= 2;
                     }
                 } else {
-                    double scale = 0.5 * (c.spose + sl);
-                    scale += 1e-10;
-                    const double rho = (c.chi - tchi) / scale;
-                    ok = rho > 0 && isfinite(tchi);
-                    if (ok) { c.lambda = fmax(c.lambda / 9.0, 1e-7); c.chi = tchi; }
-                    else c.lambda = fmin(c.lambda * 11.0, 1e7);
+                    if (ok) { lam = fmax(lam / 9.0, 1e-7); chi = tchi; }
+                    else lam = fmin(lam * 11.0, 1e7);
                 }
-                c.trials += 1;
-                bool inner_end = false;
+                trials += 1;
+                bool inner_end;
                 if (ok) {
-                    c.accepted += 1;
-                    c.cur = 1 - c.cur;   // commit candidate landmarks, caches and poses
-                    accept_copy = 1;
-                    c.false_cnt = 0;
+                    nacc += 1;
+                    cur = 1 - cur;       // commit candidate landmarks, caches and poses
+                    accept = 1;
+                    fc = 0;
                     inner_end = true;
                 } else {
-                    c.false_cnt += 1;    // rollbackStates: the committed buffers are untouched
-                    inner_end = c.false_cnt >= prm.max_trials;
+                    fc += 1;             // rollbackStates: the committed buffers are untouched
+                    inner_end = fc >= prm.max_trials;
                 }
                 if (inner_end) {
-                    c.iter += 1;
-                    if (c.last_chi - c.chi < prm.stop_dchi2) c.done = 1;
-                    c.last_chi = c.chi;
-                    if (!c.done && c.iter >= prm.max_iters) c.done = 1;
-                    if (!c.done) {
-                        c.false_cnt = 0;
-                        if (c.trace_len < LH_TRACE) {
-                            c.trace_chi[c.trace_len] = c.chi;
-                            c.trace_lambda[c.trace_len] = c.lambda;
-                        }
-                        c.trace_len += 1;
-                    }
+                    iter += 1;
+                    if (last - chi < prm.stop_dchi2) done = 1;
+                    last = chi;
+                    if (!done && iter >= prm.max_iters) done = 1;
+                    if (!done) { fc = 0; trace = 1; }
                 }
             }
+            if (trace) {
+                if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
+                tl += 1;
+            }
+            ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
+            ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
+            ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+            if (done && host_done) *host_done = 1;
         }
-        s_flags[0] = c.done;
-        s_flags[1] = accept_copy;
-        s_flags[2] = c.cur;
-        if (c.done && host_done) *host_done = 1;
+        s_flags[0] = done;
+        s_flags[1] = accept;
+        s_flags[2] = cur;
+        s_lam = lam;
     }
     __syncthreads();
-    const int done = s_flags[0], cur = s_flags[2];
-    if (s_flags[1]) {
-        for (int i = tid; i < LY.total; i += CT) rs_commit[i] = rs_stage[i];
-        __syncthreads();
-    }
+    const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
     if (done) return;
-    STAMP(10);
-    const double lambda = ctrl->lambda;
-    const double* rs = rs_commit;
+    const double lambda = s_lam;
+    STAMP(17);
 
-    // ---------------- (S + lambda D) with Eigen's LDLT pivot order ----------------
-    // Eigen LDLT (left-looking) pivots on the largest remaining original
-    // diagonal: the order of |diag| descending (problem.cpp:420).
-    for (int i = tid; i < n; i += CT) {
-        double d = rs_S(rs, LY, P, i, i);
-        d = (prm.strategy == 0) ? d + lambda : d + lambda * d;
-        dg[i] = d;
+    // ---------------- 2. commit, diag + lambda, pivot order, scatter into LDS ----------------
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+        const int i = u * CT + tid;
+        const double v = accept ? vs[u] : vc[u];
+        vs[u] = v;
+        if (accept && i < LY.total) rs_commit[i] = v;
+        if (i < LY.off_bs) {
+            const int blk = i / 36, r = i - 36 * blk, a = r / 6, b = r - 6 * (r / 6);
+            if (a == b && pr_p[blk] == pr_q[blk]) {
+                const int g = 6 * pr_p[blk] + a;
+                dg[g] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
+            }
+        } else if (i < LY.off_bp) {
+            bsv[i - LY.off_bs] = v;
+        } else if (i < LY.off_hd) {
+            bpv[i - LY.off_bp] = v;
+        } else if (i < LY.off_hd + n) {
+            hdv[i - LY.off_hd] = v;
+        }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += CT) {
-        // total order (NaN last, ties by index) so perm is a permutation even for a poisoned S
-        double di = fabs(dg[i]);
+    if (tid < n) {
+        // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation
+        double di = fabs(dg[tid]);
         if (!(di == di)) di = -1.0;
         int r = 0;
         for (int j = 0; j < n; ++j) {
             double dj = fabs(dg[j]);
             if (!(dj == dj)) dj = -1.0;
-            r += (dj > di) || (dj == di && j < i);
+            r += (dj > di) || (dj == di && j < tid);
         }
-        perm[r] = i;
+        perm[r] = tid;
+        iperm[tid] = r;
+    } else if (tid < NP) {
+        perm[tid] = tid;
+        iperm[tid] = tid;
     }
     __syncthreads();
-    for (int idx = tid; idx < n * n; idx += CT) {
-        const int r = idx / n, s = idx - r * n;
-        if (s > r) continue;
-        const int i = perm[r], j = perm[s];
-        A[r * AS + s] = (r == s) ? dg[i] : rs_S(rs, LY, P, i, j);
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+        const int i = u * CT + tid;
+        if (i < LY.off_bs) {
+            const int blk = i / 36, r = i - 36 * blk, a = r / 6, b = r - 6 * (r / 6);
+            const int ri = iperm[6 * pr_p[blk] + a], rj = iperm[6 * pr_q[blk] + b];
+            if (pr_p[blk] != pr_q[blk]) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
+            else if (ri > rj) A[ri * AS + rj] = vs[u];
+        }
     }
-    for (int i = tid; i < n; i += CT) yv[i] = rs[LY.off_bs + perm[i]];
+    if (tid < NE) {
+        A[tid * AS + tid] = tid < n ? dg[perm[tid]] : 1.0;
+        A[NP * AS + tid] = tid < n ? bsv[perm[tid]] : 0.0;
+    }
+    for (int x = tid; x < (NE - n) * NE; x += CT) {   // identity padding rows
+        const int r = n + x / NE, c = x - NE * (x / NE);
+        if (c < r) A[r * AS + c] = 0.0;
+    }
     __syncthreads();
-
     STAMP(11);
-    // ---------------- blocked right-looking LDL^T, panel width 8 ----------------
-    for (int k0 = 0; k0 < n; k0 += 8) {
-        const int kb = min(8, n - k0);
-        if (wave == 0) {
-            // panel rows k0 + lane and k0 + 64 + lane, columns k0..k0+kb-1, in registers
-            double p0[8], p1[8];
-            const int i0 = k0 + lane, i1 = k0 + 64 + lane;
+
+    // ---------------- 3. blocked right-looking LDL^T (+ forward substitution in row NP) ----------------
+    for (int k0 = 0; k0 < NE; k0 += 8) {
+        const int nrow = NE - k0 + 1;                 // panel rows k0..NE-1 and the rhs row
+        if (tid < nrow) {
+            const int i = (tid == nrow - 1) ? NP : k0 + tid;
+            // 8x8 diagonal block, factored redundantly by every panel thread
+            double B[8][8], Wb[8][8], dv[8], inv[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int c = 0; c <= r; ++c) B[r][c] = A[(k0 + r) * AS + k0 + c];
+            double a[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) a[c] = A[i * AS + k0 + c];
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                p0[c] = (c < kb && i0 < n && c <= lane) ? A[i0 * AS + k0 + c] : 0.0;
-                p1[c] = (c < kb && i1 < n) ? A[i1 * AS + k0 + c] : 0.0;
+                dv[c] = B[c][c];
+                const bool valid = fabs(dv[c]) > 0.0;     // Eigen ldlt_inplace: pivot_is_valid
+                inv[c] = valid ? fast_rcp(dv[c]) : 1.0;
+#pragma unroll
+                for (int r = c + 1; r < 8; ++r) Wb[r][c] = B[r][c];
+#pragma unroll
+                for (int r = c + 1; r < 8; ++r) {
+                    const double l = Wb[r][c] * inv[c];
+                    B[r][c] = l;
+#pragma unroll
+                    for (int r2 = c + 1; r2 <= r; ++r2) B[r][r2] -= l * Wb[r2][c];
+                }
             }
+            const int ri = i - k0;
+            if (ri < 8) {
+                // the diagonal block: the thread of its first row writes L and D of all 8 rows
+                if (ri == 0) {
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                if (c < kb) {
-                    const double d = readlane_d(p0[c], c);
-                    const double inv = (d != 0.0) ? 1.0 / d : 0.0;
-                    const double x0 = p0[c], x1 = p1[c];
-                    if (lane == 0) Dv[k0 + c] = d;
-                    if (i0 < n) Xp[i0 * 8 + c] = x0;
-                    if (i1 < n) Xp[i1 * 8 + c] = x1;
-                    const bool below0 = lane > c, below1 = true;
-                    const double l0 = below0 ? (d != 0.0 ? x0 * inv : x0) : x0;
-                    const double l1 = (d != 0.0 ? x1 * inv : x1);
+                    for (int r = 0; r < 8; ++r) {
 #pragma unroll
-                    for (int c2 = c + 1; c2 < 8; ++c2) {
-                        if (c2 < kb) {
-                            const double xj = readlane_d(p0[c], c2);   // unscaled column c at row k0 + c2
-                            if (below0 && lane >= c2) p0[c2] -= l0 * xj;
-                            if (below1) p1[c2] -= l1 * xj;
-                        }
+                        for (int c = 0; c < r; ++c) A[(k0 + r) * AS + k0 + c] = B[r][c];
+                        A[(k0 + r) * AS + k0 + r] = dv[r];
                     }
-                    if (below0) p0[c] = l0;
-                    p1[c] = l1;
                 }
-            }
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                if (c < kb) {
-                    if (i0 < n && c <= lane) A[i0 * AS + k0 + c] = p0[c];
-                    if (i1 < n) A[i1 * AS + k0 + c] = p1[c];
-                }
-            }
-        }
-        __syncthreads();
-        // trailing update: A[i][j] -= sum_c L[i][c] X[j][c], k0+kb <= j <= i < n, in 4x4 micro-tiles
-        const int m0 = k0 + kb;
-        const int mt = (n - m0 + 3) >> 2;
-        const int ntile = mt * (mt + 1) / 2;
-        for (int x = tid; x < ntile; x += CT) {
-            int I = (int)((sqrt(8.0 * x + 1.0) - 1.0) * 0.5);
-            while ((I + 1) * (I + 2) / 2 <= x) ++I;
-            while (I * (I + 1) / 2 > x) --I;
-            const int J = x - I * (I + 1) / 2;
-            const int rb = m0 + 4 * I, cb = m0 + 4 * J;
-            double Lr[4][8], Xc8[4][8];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
+            } else {
+                double w[8];
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
-                    const int i = rb + r, j = cb + r;
-                    Lr[r][c] = (i < n && c < kb) ? A[i * AS + k0 + c] : 0.0;
-                    Xc8[r][c] = (j < n && c < kb) ? Xp[j * 8 + c] : 0.0;
+                    w[c] = a[c];
+                    const double l = a[c] * inv[c];
+                    a[c] = l;
+#pragma unroll
+                    for (int c2 = c + 1; c2 < 8; ++c2) a[c2] -= l * Wb[c2][c];
                 }
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 8; ++c) A[i * AS + k0 + c] = a[c];
+                if (i < NP) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const int i = rb + r, j = cb + s;
-                    if (i < n && j <= i) {
-                        double acc = 0.0;
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) acc += Lr[r][c] * Xc8[s][c];
-                        A[i * AS + j] -= acc;
-                    }
+                    for (int c = 0; c < 8; ++c) Xp[i * XS + c] = w[c];
                 }
+            }
         }
         __syncthreads();
+        STAMP(15);
+        // trailing update: A[i][j] -= sum_c L[i][c] W[j][c], k0+8 <= j <= i < NE, 4x4 micro-tiles;
+        // plus 1x4 tiles of the rhs row
+        const int m0 = k0 + 8;
+        const int mt = (NE - m0) >> 2;
+        const int ntile = mt * (mt + 1) / 2;
+        for (int x = tid; x < ntile + mt; x += CT) {
+            int rb, cb, nr;
+            if (x < ntile) {
+                int I = (int)((sqrtf(8.0f * (float)x + 1.0f) - 1.0f) * 0.5f);
+                while ((I + 1) * (I + 2) / 2 <= x) ++I;
+                while (I * (I + 1) / 2 > x) --I;
+                const int J = x - I * (I + 1) / 2;
+                rb = m0 + 4 * I; cb = m0 + 4 * J; nr = 4;
+            } else {
+                rb = NP; cb = m0 + 4 * (x - ntile); nr = 1;
+            }
+            double Xc[4][8];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) Xc[s2][c] = Xp[(cb + s2) * XS + c];
+            if (nr == 4) {
+                double Lr[4][8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) Lr[r][c] = A[(rb + r) * AS + k0 + c];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        double acc = 0.0;
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) acc += Lr[r][c] * Xc[s2][c];
+                        A[(rb + r) * AS + cb + s2] -= acc;
+                    }
+            } else {
+                double Lr[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) Lr[c] = A[NP * AS + k0 + c];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) acc += Lr[c] * Xc[s2][c];
+                    A[NP * AS + cb + s2] -= acc;
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(16);
     }
 
-    STAMP(12);
-    // ---------------- solve: L z = y, z /= D, L^T w = z (LDLT::_solve_impl) ----------------
+    // ---------------- 4. z /= D (Eigen tolerance), back substitution L^T x = z ----------------
     if (wave == 0) {
-        double z0 = (lane < n) ? yv[lane] : 0.0, z1 = (lane + 64 < n) ? yv[lane + 64] : 0.0;
-        for (int k = 0; k < n; ++k) {
-            const double zk = (k < 64) ? readlane_d(z0, k) : readlane_d(z1, k - 64);
-            if (lane > k && lane < n) z0 -= A[lane * AS + k] * zk;
-            if (lane + 64 > k && lane + 64 < n) z1 -= A[(lane + 64) * AS + k] * zk;
+        const double tol = 2.2250738585072014e-308;   // LDLT::_solve_impl: (numeric_limits::min)()
+        const int r0 = lane, r1 = lane + 64;
+        double t0 = 0.0, t1 = 0.0;
+        if (r0 < NE) { const double d = A[r0 * AS + r0]; t0 = fabs(d) > tol ? A[NP * AS + r0] : 0.0; }
+        if (r1 < NE) { const double d = A[r1 * AS + r1]; t1 = fabs(d) > tol ? A[NP * AS + r1] : 0.0; }
+        for (int kb = NE - 8; kb >= 0; kb -= 8) {
+            // L columns of the rows above this block (independent of the block's solution)
+            double c0[8], c1[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                c0[v] = A[(kb + v) * AS + r0];
+                c1[v] = A[(kb + v) * AS + (r1 & (NP - 1))];
+            }
+            if (r0 >= kb && r0 < kb + 8) tmp8[r0 - kb] = t0;
+            if (r1 >= kb && r1 < kb + 8) tmp8[r1 - kb] = t1;
+            wave_sync();
+            double x[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) x[v] = tmp8[v];
+#pragma unroll
+            for (int v = 7; v >= 0; --v) {
+#pragma unroll
+                for (int w2 = v + 1; w2 < 8; ++w2) x[v] -= A[(kb + w2) * AS + kb + v] * x[w2];
+            }
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                if (r0 == kb + v) t0 = x[v];
+                if (r1 == kb + v) t1 = x[v];
+            }
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) { s0 += c0[v] * x[v]; s1 += c1[v] * x[v]; }
+            if (r0 < kb) t0 -= s0;
+            if (r1 < kb) t1 -= s1;
+            wave_sync();
         }
-        const double tol = 2.2250738585072014e-308;
-        if (lane < n) { const double d = Dv[lane]; z0 = fabs(d) > tol ? z0 / d : 0.0; }
-        if (lane + 64 < n) { const double d = Dv[lane + 64]; z1 = fabs(d) > tol ? z1 / d : 0.0; }
-        for (int k = n - 1; k >= 0; --k) {
-            const double zk = (k < 64) ? readlane_d(z0, k) : readlane_d(z1, k - 64);
-            if (lane < k) z0 -= A[k * AS + lane] * zk;
-            if (lane + 64 < k) z1 -= A[k * AS + lane + 64] * zk;
-        }
-        if (lane < n) dxp[perm[lane]] = z0;
-        if (lane + 64 < n) dxp[perm[lane + 64]] = z1;
+        if (r0 < n) { xs[perm[r0]] = t0; dxp[perm[r0]] = t0; }
+        if (r1 < n) { xs[perm[r1]] = t1; dxp[perm[r1]] = t1; }
     }
     __syncthreads();
-
     STAMP(13);
+
     // ---------------- pose part of the gain denominator; candidate poses ----------------
     double sp = 0.0;
-    for (int i = tid; i < n; i += CT) {
-        const double d = dxp[i];
-        const double b = rs[LY.off_bp + i];
-        sp += (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * rs[LY.off_hd + i] * d + b);
+    if (tid < n) {
+        const double d = xs[tid], b = bpv[tid];
+        sp = (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[tid] * d + b);
     }
     for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
     if (lane == 0) s_red[wave] = sp;
@@ -998,33 +1155,44 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         const int pidx = tid;
         double up[6];
         bool bad = false;
-        for (int a = 0; a < 6; ++a) { up[a] = dxp[6 * pidx + a]; bad |= !isfinite(up[a]); }
-        if (bad) for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
+#pragma unroll
+        for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
+        if (bad) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
+        }
         // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix()
         double qe[4], te[3], qT[4], qn[4], tr[3], Rn[9];
         d_se3_exp(up, qe, te);
-        const double* Tc = pose_mat + ((size_t)cur * P + pidx) * 12;
+        double Tc[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) Tc[i] = cur ? pm1[i] : pm0[i];
         const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
         const double tc[3] = {Tc[3], Tc[7], Tc[11]};
         d_q_from_R(Rc, qT);
         d_q_mul(qe, qT, qn);
         d_q_rotate(qe, tc, tr);
         d_R_from_q(qn, Rn);
-        double* To = pose_mat + ((size_t)cand * P + pidx) * 12;
+        double To[12];
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
             To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
             To[4 * i + 3] = te[i] + tr[i];
         }
+        double* Tg = pose_mat + ((size_t)cand * P + pidx) * 12;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) Tg[i] = To[i];
         for (int cam = 0; cam < prm.ncam; ++cam)
             d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
     }
     __syncthreads();
     if (tid == 0) {
-        double s = 0.0;
-        for (int w = 0; w < CT / 64; ++w) s += s_red[w];
-        ctrl->spose = s;
+        double s2 = 0.0;
+        for (int w = 0; w < CT / 64; ++w) s2 += s_red[w];
+        ctrl->spose = s2;
     }
     STAMP(14);
+    STAMP_FLUSH(10, 8);
 }
 
 // ============================================================================
@@ -1033,12 +1201,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 extern "C" {
 
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
-                         const lh_subbatch* sbs, const uint32_t* lm_ptr, const double* obs_uv, const uint32_t* obs_meta,
+                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta,
                          double* Xbuf, double* cache, const double* ptab, const double* ext, const lh_ctrl* ctrl,
                          const double* dxp, double* edge_rho, double* slabs, lh_params prm, int L, uint32_t fixed_mask) {
     if (nchunks <= 0) return hipSuccess;
     dim3 g(nchunks), b(256);
-#define LH_LIN(TT, TR) hipLaunchKernelGGL((k_lin<TT, TR>), g, b, 0, st, chunks, sbs, lm_ptr, obs_uv, obs_meta, Xbuf, cache, ptab, ext, ctrl, dxp, edge_rho, slabs, prm, L, fixed_mask, chunk_base)
+#define LH_LIN(TT, TR) hipLaunchKernelGGL((k_lin<TT, TR>), g, b, 0, st, chunks, sbs, obs_uv, obs_meta, Xbuf, cache, ptab, ext, ctrl, dxp, edge_rho, slabs, prm, L, fixed_mask, chunk_base)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
         case 3: LH_LIN(1, true); break;

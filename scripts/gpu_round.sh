@@ -12,4 +12,3 @@ LH_LIB=lego-slam_amd/lib/liblego_ba_stamps.so timeout -k 10 300 python scripts/s
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1; rc=$?; echo "rc=$rc" >> gpurun_out/prof.log
 [ $rc -eq 0 ] || exit $rc
-rocprofv3 -L > gpurun_out/counters.txt 2>&1 || true

@@ -12,7 +12,7 @@ from windows import window  # noqa: E402
 
 NAMES = {0: "lin:backsub", 1: "lin:linearize", 2: "lin:Hll+chol", 3: "lin:G+bsd", 4: "lin:pose-tasks",
          5: "lin:G-image", 6: "lin:mfma", 7: "lin:combine+slab", 10: "ctrl:LM+copy", 11: "ctrl:S+perm+load",
-         12: "ctrl:LDLT", 13: "ctrl:solve", 14: "ctrl:poses", 20: "reduce"}
+         12: "ctrl:LDLT(rest)", 13: "ctrl:solve", 14: "ctrl:poses", 15: "ctrl:LDLT panel", 16: "ctrl:LDLT update", 17: "ctrl:LM logic", 20: "reduce"}
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 w = window(cfg, seed=0, family="stable_noout")
@@ -26,7 +26,7 @@ for _ in range(n):
     trials += s.solve_resident()["trials"] + 1
 st = lego_ba.debug_stamps(reset=True)
 lin = sum(int(st[i]) for i in range(8))
-ctrl = sum(int(st[i]) for i in range(10, 15))
+ctrl = sum(int(st[i]) for i in range(10, 18))
 print(f"{cfg}: {trials} k_lin launches; totals (wave-cycles/launch): lin {lin / trials:.3e} ctrl {ctrl / trials:.3e} reduce {int(st[20]) / trials:.3e}")
 for i, nm in NAMES.items():
     v = int(st[i])
