@@ -32,8 +32,14 @@
 #define LH_SC_NDEG 2          // rank-deficient H_ll landmarks
 #define LH_SC_MAXD 3          // max |H_ll diag| (a max, not a sum)
 
-// per-landmark cache: Cholesky of H_ll (6), b_l (3), diag H_ll (3)
-#define LH_CACHE 12
+// per-landmark record (one 128-B line, double-buffered committed/candidate):
+// X (3) | Cholesky of H_ll (6) | b_l (3) | diag H_ll (3) | pad.  A sub-batch owns 8
+// consecutive records, so one wave moves its landmarks with one 16-B access per lane.
+#define LH_REC 16
+#define LH_REC_X 0
+#define LH_REC_L 3
+#define LH_REC_B 9
+#define LH_REC_HD 12
 
 // Pose state is estimate_ itself: a row-major [R | t] matrix per pose (12 doubles,
 // VertexPose stores the 4x4, lego_types.h:37,57).  Every use converts it to

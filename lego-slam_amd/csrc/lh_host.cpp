@@ -30,15 +30,15 @@
 
 extern "C" {
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
-                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta,
-                         double* Xbuf, double* cache, const double* ptab, const double* ext, const lh_ctrl* ctrl,
-                         const double* dxp, double* edge_rho, double* slabs, lh_params prm, int L, uint32_t fixed_mask);
+                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
+                         const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
+                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint32_t fixed_mask);
 hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double* slabs, const uint32_t* pair_ptr,
                             const uint32_t* items, const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage,
                             double* maxd, lh_params prm, int n_chunks);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          double* pose_qt, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
-                          int* host_done);
+                          const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
+                          lh_params prm, int mode, int* host_done);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
 }
@@ -167,7 +167,7 @@ struct lh_handle {
     int64_t O = 0;
     uint32_t fixed_mask = 0;
     lh_params prm{};
-    std::vector<int32_t> lm_perm;      // chunked landmark -> window landmark
+    std::vector<int32_t> lm_perm;      // landmark record slot -> window landmark (-1: padding)
     std::vector<int64_t> obs_perm;     // chunked obs -> window obs
     std::vector<double> lm_in;         // window input positions (landmarks with no edge keep them)
     int n_chunks = 0;
@@ -177,9 +177,9 @@ struct lh_handle {
     // device buffers
     DevBuf<lh_chunk> d_chunks;
     DevBuf<lh_subbatch> d_sbs;
-    DevBuf<uint32_t> d_meta, d_pair_ptr, d_items;
+    DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
     DevBuf<uint16_t> d_pair_pq;
-    DevBuf<double> d_uv, d_X, d_Xinit, d_cache, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs,
+    DevBuf<double> d_uv, d_rec, d_rec_init, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs,
         d_rs_stage, d_rs_commit, d_maxd, d_dxp;
     DevBuf<lh_ctrl> d_ctrl;
     lh_ctrl* h_ctrl = nullptr;   // pinned
@@ -332,17 +332,20 @@ int upload_impl(lh_handle* h, const lh_window* w) {
 
     struct ChunkTmp { std::vector<int32_t> lms; uint32_t mask; };
     std::vector<ChunkTmp> ctmp;
+    // a chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new
+    // chunk rather than let the union grow past the larger of the two tile counts
+    auto chunkT = [](uint32_t mask) { return (6 * __builtin_popcount(mask) + 15) / 16; };
     for (int32_t l : order) {
         const uint32_t m = lm_mask[l];
         if (ctmp.empty() || (int)ctmp.back().lms.size() >= chunk_lm ||
-            __builtin_popcount(ctmp.back().mask | m) > LH_UMAX) {
+            __builtin_popcount(ctmp.back().mask | m) > LH_UMAX ||
+            chunkT(ctmp.back().mask | m) > std::max(chunkT(ctmp.back().mask), chunkT(m))) {
             ctmp.push_back(ChunkTmp{{}, 0u});
         }
         ctmp.back().lms.push_back(l);
         ctmp.back().mask |= m;
     }
     // group chunks by MFMA tile count T (one launch per T)
-    auto chunkT = [](uint32_t mask) { return (6 * __builtin_popcount(mask) + 15) / 16; };
     std::vector<int> corder(ctmp.size());
     std::iota(corder.begin(), corder.end(), 0);
     std::stable_sort(corder.begin(), corder.end(), [&](int a, int b) { return chunkT(ctmp[a].mask) < chunkT(ctmp[b].mask); });
@@ -350,11 +353,9 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     std::vector<lh_chunk> chunks;
     std::vector<lh_subbatch> sbs;
     std::vector<uint32_t> meta;
-    std::vector<double> uv, Xinit;
+    std::vector<double> uv, rec_init;
     h->lm_perm.clear();
     h->obs_perm.clear();
-    Xinit.reserve(3 * (size_t)Lact);
-    h->lm_perm.reserve(Lact);
     for (int T = 0; T <= LH_TMAX + 1; ++T) h->tgroup_begin[T] = 0;
     int slot_of[32];
     auto pow2ceil = [](int k) { int g = 1, lg = 0; while (g < k) { g <<= 1; ++lg; } return lg; };
@@ -383,7 +384,9 @@ int upload_impl(lh_handle* h, const lh_window* w) {
                 ++n;
             }
             lh_subbatch sb{};
-            sb.lm_begin = (uint32_t)h->lm_perm.size();
+            sb.lm_begin = (uint32_t)(sbs.size() * LH_SB_LM);   // records sb*8 .. sb*8+7
+            h->lm_perm.resize(sb.lm_begin + LH_SB_LM, -1);
+            rec_init.resize((size_t)(sb.lm_begin + LH_SB_LM) * LH_REC, 0.0);
             sb.n_lm = (uint8_t)n;
             sb.lg = (uint8_t)lg;
             const size_t base = meta.size();
@@ -392,8 +395,8 @@ int upload_impl(lh_handle* h, const lh_window* w) {
             h->obs_perm.resize(base + LH_SB_OBS, -1);
             for (int q = 0; q < n; ++q) {
                 const int32_t l = c.lms[i + q];
-                h->lm_perm.push_back(l);
-                for (int a = 0; a < 3; ++a) Xinit.push_back(w->lm_xyz[3 * (size_t)l + a]);
+                h->lm_perm[sb.lm_begin + q] = l;
+                for (int a = 0; a < 3; ++a) rec_init[(size_t)(sb.lm_begin + q) * LH_REC + LH_REC_X + a] = w->lm_xyz[3 * (size_t)l + a];
                 int j = 0;
                 for (int64_t r = cnt[l]; r < cnt[l + 1]; ++r, ++j) {
                     const int64_t o = csr[r];
@@ -492,7 +495,16 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     prm.lambda_init = h->opt.lambda_init;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     h->LY = lh_rs_make(P);
-    h->L_act = Lact;
+    h->L_act = (int)h->lm_perm.size();   // landmark records (padded to 8 per sub-batch)
+    // reduced-system element map for k_ctrl's register scatter: S element i of pose pair
+    // (pi, pj), pi <= pj, row a, col b  ->  global rows gi = 6 pi + a, gj = 6 pj + b
+    std::vector<uint32_t> rsmap((size_t)h->LY.npairs * 36);
+    for (int pi = 0, blk = 0; pi < P; ++pi)
+        for (int pj = pi; pj < P; ++pj, ++blk)
+            for (int a = 0; a < 6; ++a)
+                for (int b = 0; b < 6; ++b)
+                    rsmap[(size_t)blk * 36 + 6 * a + b] = (uint32_t)(6 * pi + a) | ((uint32_t)(6 * pj + b) << 8) |
+                                                        ((pi == pj ? 1u : 0u) << 16);
     h->lm_in.assign(w->lm_xyz, w->lm_xyz + 3 * (size_t)L);
 
     // ---- device buffers ----
@@ -504,9 +516,8 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->d_pair_ptr.ensure(pair_ptr.size()));
     HIPCHK(h->d_items.ensure(items.size()));
     HIPCHK(h->d_pair_pq.ensure(pair_pq.size()));
-    HIPCHK(h->d_Xinit.ensure(Xinit.size()));
-    HIPCHK(h->d_X.ensure(2 * Xinit.size()));
-    HIPCHK(h->d_cache.ensure(2 * (size_t)Lact * LH_CACHE));
+    HIPCHK(h->d_rec_init.ensure(rec_init.size()));
+    HIPCHK(h->d_rec.ensure(2 * rec_init.size()));
     HIPCHK(h->d_ptab.ensure(2 * PT));
     HIPCHK(h->d_ptab_init.ensure(2 * PT));
     HIPCHK(h->d_qt.ensure(pose.size()));
@@ -516,6 +527,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->d_slabs.ensure((size_t)h->n_chunks * LH_SLAB_STRIDE));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
+    HIPCHK(h->d_rsmap.ensure(rsmap.size()));
     HIPCHK(h->d_maxd.ensure(1));
     HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
     HIPCHK(h->d_ctrl.ensure(1));
@@ -531,10 +543,11 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(up(h->d_pair_ptr.p, pair_ptr.data(), pair_ptr.size() * sizeof(uint32_t)));
     HIPCHK(up(h->d_items.p, items.data(), items.size() * sizeof(uint32_t)));
     HIPCHK(up(h->d_pair_pq.p, pair_pq.data(), pair_pq.size() * sizeof(uint16_t)));
-    HIPCHK(up(h->d_Xinit.p, Xinit.data(), Xinit.size() * sizeof(double)));
+    HIPCHK(up(h->d_rec_init.p, rec_init.data(), rec_init.size() * sizeof(double)));
     HIPCHK(up(h->d_ptab_init.p, ptab.data(), ptab.size() * sizeof(double)));
     HIPCHK(up(h->d_qt_init.p, pose.data(), pose.size() * sizeof(double)));
     HIPCHK(up(h->d_ext.p, ext.data(), ext.size() * sizeof(double)));
+    HIPCHK(up(h->d_rsmap.p, rsmap.data(), rsmap.size() * sizeof(uint32_t)));
     HIPCHK(hipStreamSynchronize(s));   // host vectors die at return
     h->uploaded = true;
     return LH_OK;
@@ -559,7 +572,7 @@ int enqueue_trial(lh_handle* h, int mode) {
         for (int T = 1; T <= LH_TMAX; ++T) {
             const int c0 = h->tgroup_begin[T], c1 = h->tgroup_begin[T + 1];
             HIPCHK(lh_launch_lin(T, mode, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p,
-                                 h->d_meta.p, h->d_X.p, h->d_cache.p, h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p,
+                                 h->d_meta.p, h->d_rec.p, h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p,
                                  h->d_rho.p, h->d_slabs.p, h->prm, h->L_act, h->fixed_mask));
             DBGSYNC("k_lin");
         }
@@ -577,7 +590,7 @@ int enqueue_trial(lh_handle* h, int mode) {
     }
     {
         Prof pr(h, KC_CTRL);
-        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_qt.p, h->d_ptab.p,
+        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p, h->d_ptab.p,
                               h->d_ext.p, h->d_dxp.p, h->prm, mode, nullptr));
         DBGSYNC("k_ctrl");
     }
@@ -590,7 +603,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     const int P = h->P;
     const size_t PT = (size_t)P * h->ncam * LH_PT;
     // restart from the uploaded initial state
-    HIPCHK(hipMemcpyAsync(h->d_X.p, h->d_Xinit.p, 3 * (size_t)h->L_act * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_rec.p, h->d_rec_init.p, LH_REC * (size_t)h->L_act * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(h->d_qt.p, h->d_qt_init.p, 24 * (size_t)P * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(h->d_ptab.p, h->d_ptab_init.p, 2 * PT * sizeof(double), hipMemcpyDeviceToDevice, s));
     std::memset(h->h_ctrl, 0, sizeof(lh_ctrl));
@@ -643,10 +656,14 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
                              hipMemcpyDeviceToHost));
         if (out->lm_xyz) {
             std::memcpy(out->lm_xyz, h->lm_in.data(), h->lm_in.size() * sizeof(double));
-            std::vector<double> X(3 * (size_t)h->L_act);
-            if (h->L_act) HIPCHK(hipMemcpy(X.data(), h->d_X.p + 3 * (size_t)cur * h->L_act, X.size() * sizeof(double), hipMemcpyDeviceToHost));
+            std::vector<double> R(LH_REC * (size_t)h->L_act);
+            if (h->L_act)
+                HIPCHK(hipMemcpy(R.data(), h->d_rec.p + LH_REC * (size_t)cur * h->L_act, R.size() * sizeof(double),
+                                 hipMemcpyDeviceToHost));
             for (int i = 0; i < h->L_act; ++i)
-                for (int a = 0; a < 3; ++a) out->lm_xyz[3 * (size_t)h->lm_perm[i] + a] = X[3 * (size_t)i + a];
+                if (h->lm_perm[i] >= 0)
+                    for (int a = 0; a < 3; ++a)
+                        out->lm_xyz[3 * (size_t)h->lm_perm[i] + a] = R[LH_REC * (size_t)i + LH_REC_X + a];
         }
         if (out->edge_robust_chi2) {
             std::vector<double> r(h->obs_perm.size());
@@ -763,9 +780,9 @@ void lh_destroy(lh_handle* h) {
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release();
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release();
-    h->d_uv.release(); h->d_X.release(); h->d_Xinit.release(); h->d_cache.release(); h->d_ptab.release();
+    h->d_uv.release(); h->d_rec.release(); h->d_rec_init.release(); h->d_ptab.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
-    h->d_slabs.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_maxd.release(); h->d_dxp.release();
+    h->d_slabs.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release(); h->d_dxp.release();
     h->d_ctrl.release();
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);

@@ -21,7 +21,6 @@
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define SCR_SZ 2112                  // per-wave scratch: max(64*33, 24*80) doubles
-#define K_LIN_SMEM (LH_WAVES * SCR_SZ)
 
 // Diagnostic build (-DLH_STAMPS): per-phase wave-cycle totals via s_memtime,
 // summed over all waves into lh_stamps[] (cdna_hip_programming.md §7 "In-kernel
@@ -322,14 +321,14 @@ __device__ __forceinline__ double group_sum(double v, int lg) {
 }
 
 template <int T, bool TRIAL>
-__global__ __launch_bounds__(256, 2) void k_lin(
+__global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
-    const uint32_t* __restrict__ obs_meta, double* __restrict__ Xbuf, double* __restrict__ cache,
-    const double* __restrict__ ptab, const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl,
-    const double* __restrict__ dxp, double* __restrict__ edge_rho, double* __restrict__ slabs, lh_params prm, int L,
-    uint32_t fixed_mask, int chunk_base) {
+    const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
+    const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
+    double* __restrict__ edge_rho, double* __restrict__ slabs, lh_params prm, int nrec, uint32_t fixed_mask,
+    int chunk_base) {
     using Cfg = LinCfg<T>;
-    __shared__ __attribute__((aligned(16))) double smem[K_LIN_SMEM];
+    extern __shared__ __attribute__((aligned(16))) double dsm[];
 
     if (__builtin_amdgcn_readfirstlane(ctrl->done)) return;
     const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
@@ -337,17 +336,34 @@ __global__ __launch_bounds__(256, 2) void k_lin(
     const double lambda = ctrl->lambda;
     const int chunk = chunk_base + blockIdx.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const lh_chunk ck = chunks[chunk];
-    const int PT = prm.P * prm.ncam * LH_PT;
+    const int ncam = prm.ncam;
+    const int PT = prm.P * ncam * LH_PT;
+    const int U = chunks[chunk].U;
+    const uint32_t sb_begin = chunks[chunk].sb_begin, sb_end = chunks[chunk].sb_end;
+    const uint16_t* __restrict__ cpose = chunks[chunk].pose;
 
-    double* scr = smem + wave * SCR_SZ;
+    double* scr = dsm + wave * SCR_SZ;
+    // the chunk's window, LDS-resident: committed and candidate pose tables per (slot, camera),
+    // the pending pose step per slot, the camera extrinsics
+    double* wt_c = dsm + LH_WAVES * SCR_SZ;
+    double* wt_n = wt_c + LH_UMAX * ncam * LH_PT;
+    double* wdx = wt_n + LH_UMAX * ncam * LH_PT;
+    double* wext = wdx + LH_UMAX * 6;
+    {
+        const int per = ncam * LH_PT, ne = U * per;
+        for (int i = tid; i < ne; i += 256) {
+            const int sl = i / per;
+            const size_t g = (size_t)cpose[sl] * per + (i - sl * per);
+            wt_c[i] = pose_tab[(size_t)cur * PT + g];
+            wt_n[i] = pose_tab[(size_t)cand * PT + g];
+        }
+        if (TRIAL)
+            for (int i = tid; i < 6 * U; i += 256) wdx[i] = dxp[6 * cpose[i / 6] + (i - 6 * (i / 6))];
+        for (int i = tid; i < ncam * LH_EXT; i += 256) wext[i] = ext[i];
+    }
 
-    const double* Xc = Xbuf + (size_t)cur * L * 3;
-    double* Xn = Xbuf + (size_t)cand * L * 3;
-    const double* cc = cache + (size_t)cur * L * LH_CACHE;
-    double* cn = cache + (size_t)cand * L * LH_CACHE;
-    const double* ptc = ptab + (size_t)cur * PT;
-    const double* ptn = ptab + (size_t)cand * PT;
+    const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
+    double* __restrict__ rn = rec + (size_t)cand * nrec * LH_REC;
 
     v4d acc[Cfg::NT];
 #pragma unroll
@@ -356,65 +372,71 @@ __global__ __launch_bounds__(256, 2) void k_lin(
 #pragma unroll
     for (int u = 0; u < Cfg::UMAX; ++u) task[u] = 0.0;
     double chi_acc = 0.0, scale_acc = 0.0, maxd = 0.0, ndeg = 0.0;
-    const int U = ck.U;
     STAMP_DECL
 
-    // prefetch of the first sub-batch's observation words
-    int sb = ck.sb_begin + wave;
+    // prefetch of the first sub-batch: observation words and the 8 landmark records
+    int sb = (int)sb_begin + wave;
     uint32_t meta_n = 0u;
     double u_n = 0.0, v_n = 0.0;
-    if (sb < (int)ck.sb_end) {
+    double2 r_n = double2{0.0, 0.0};
+    if (sb < (int)sb_end) {
         const int o = sb * 64 + lane;
         meta_n = obs_meta[o];
         u_n = obs_uv[2 * (size_t)o];
         v_n = obs_uv[2 * (size_t)o + 1];
+        r_n = rc2[(size_t)sb * 64 + lane];
     }
+    __syncthreads();   // window tables
 
-    for (; sb < (int)ck.sb_end; sb += LH_WAVES) {
+    for (; sb < (int)sb_end; sb += LH_WAVES) {
         const lh_subbatch S = sbs[sb];
         const int lg = S.lg, nlm = S.n_lm;
         const int ls = lane >> lg, gj = lane & ((1 << lg) - 1);
-        const bool lead = gj == 0 && ls < nlm;       // one lane per landmark writes its results
+        const bool lmok = ls < nlm;
+        const bool lead = gj == 0 && lmok;           // one lane per landmark writes its record
         const uint32_t meta = meta_n;
         const double u = u_n, v = v_n;
+        const double2 rr = r_n;
         const int o = sb * 64 + lane;
-        // prefetch the next sub-batch of this wave
         {
             const int sbn = sb + LH_WAVES;
-            if (sbn < (int)ck.sb_end) {
+            if (sbn < (int)sb_end) {
                 const int on = sbn * 64 + lane;
                 meta_n = obs_meta[on];
                 u_n = obs_uv[2 * (size_t)on];
                 v_n = obs_uv[2 * (size_t)on + 1];
+                r_n = rc2[(size_t)sbn * 64 + lane];
             }
         }
+        // landmark records through LDS: lane -> its landmark's record
+        reinterpret_cast<double2*>(scr)[lane] = rr;
+        wave_sync();
+        const double* myrec = scr + (ls & 7) * LH_REC;
+        double X[3] = {myrec[LH_REC_X], myrec[LH_REC_X + 1], myrec[LH_REC_X + 2]};
+        double cl[12];
+        if (TRIAL) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) cl[i] = myrec[LH_REC_L + i];
+        }
+        wave_sync();
+
         const bool has = (meta & LH_META_VALID) != 0u;
         const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta);
         const bool pfixed = (fixed_mask >> p) & 1u;
-        const bool lmok = ls < nlm;
-        const int lm = S.lm_begin + (lmok ? ls : 0);
-        double X[3] = {0.0, 0.0, 0.0};
-        double cl[LH_CACHE];
-        if (lmok) {
-            X[0] = Xc[3 * (size_t)lm]; X[1] = Xc[3 * (size_t)lm + 1]; X[2] = Xc[3 * (size_t)lm + 2];
-        }
-        if (TRIAL && lmok) {
-#pragma unroll
-            for (int i = 0; i < LH_CACHE; ++i) cl[i] = cc[(size_t)lm * LH_CACHE + i];
-        }
-        const double* e = ext + cam * LH_EXT;
+        const bool live = has && !pfixed;
+        const double* e = wext + cam * LH_EXT;
         const bool ext_id = (prm.ext_identity >> cam) & 1;
 
         // ---- back-substitution of the pending pose step (problem.cpp:426-429) ----
         if (TRIAL) {
             double v3[3] = {0.0, 0.0, 0.0};
-            if (has && !pfixed) {
-                const double* pt = ptc + (p * prm.ncam + cam) * LH_PT;
+            if (live) {
+                const double* pt = wt_c + (slot * ncam + cam) * LH_PT;
                 EdgeEval E;
                 edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
                 edge_robust(E, prm);
                 edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
-                const double* d = dxp + 6 * p;
+                const double* d = wdx + 6 * slot;
                 double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
                 for (int a = 0; a < 6; ++a) { jd0 += E.Jp[a] * d[a]; jd1 += E.Jp[6 + a] * d[a]; }
@@ -438,26 +460,21 @@ __global__ __launch_bounds__(256, 2) void k_lin(
                     if (prm.strategy == 0) sc = d0 * (lambda * d0 + b0) + d1 * (lambda * d1 + b1) + d2 * (lambda * d2 + b2);
                     else sc = d0 * (lambda * cl[9] * d0 + b0) + d1 * (lambda * cl[10] * d1 + b1) + d2 * (lambda * cl[11] * d2 + b2);
                     scale_acc += sc;
-                    Xn[3 * (size_t)lm] = x0; Xn[3 * (size_t)lm + 1] = x1; Xn[3 * (size_t)lm + 2] = x2;
                 }
                 X[0] = x0; X[1] = x1; X[2] = x2;
             }
-        } else if (lead) {
-            Xn[3 * (size_t)lm] = X[0]; Xn[3 * (size_t)lm + 1] = X[1]; Xn[3 * (size_t)lm + 2] = X[2];
         }
         STAMP(0);
 
         // ---- evaluate and linearise at the candidate (problem.cpp:285-331, :523-526) ----
+        // H_pp and b_p go straight to this lane's row of the pose-sum transpose
         double hll[6] = {0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
-        double hpp[21], bp[6], hpl[18];
-#pragma unroll
-        for (int i = 0; i < 21; ++i) hpp[i] = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) bp[i] = 0.0;
+        double hpl[18];
 #pragma unroll
         for (int i = 0; i < 18; ++i) hpl[i] = 0.0;
+        double* trow = scr + LH_TASKS * lane;
         if (has) {
-            const double* pt = ptn + (p * prm.ncam + cam) * LH_PT;
+            const double* pt = wt_n + (slot * ncam + cam) * LH_PT;
             EdgeEval E;
             edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
             edge_robust(E, prm);
@@ -465,7 +482,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
             edge_rho[o] = E.rho0;
             chi_acc += E.rho0;
             const double dr = (prm.huber_delta > 0.0) ? E.rho1 : 1.0;
-            double WJl[6], WJp[12];
+            double WJl[6];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 WJl[c] = E.W00 * E.Jl[c] + E.W01 * E.Jl[3 + c];
@@ -480,6 +497,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
 #pragma unroll
             for (int c = 0; c < 3; ++c) bl[c] = -((dr * E.Jl[c]) * E.r0 + (dr * E.Jl[3 + c]) * E.r1);
             if (!pfixed) {
+                double WJp[12];
 #pragma unroll
                 for (int a = 0; a < 6; ++a) {
                     WJp[a] = E.W00 * E.Jp[a] + E.W01 * E.Jp[6 + a];
@@ -489,12 +507,12 @@ __global__ __launch_bounds__(256, 2) void k_lin(
 #pragma unroll
                 for (int a = 0; a < 6; ++a)
 #pragma unroll
-                    for (int b = a; b < 6; ++b) hpp[k++] = E.Jp[a] * WJp[b] + E.Jp[6 + a] * WJp[6 + b];
+                    for (int b = a; b < 6; ++b) trow[k++] = E.Jp[a] * WJp[b] + E.Jp[6 + a] * WJp[6 + b];
 #pragma unroll
                 for (int a = 0; a < 6; ++a) {
 #pragma unroll
                     for (int c = 0; c < 3; ++c) hpl[3 * a + c] = E.Jp[a] * WJl[c] + E.Jp[6 + a] * WJl[3 + c];
-                    bp[a] = -((dr * E.Jp[a]) * E.r0 + (dr * E.Jp[6 + a]) * E.r1);
+                    trow[21 + a] = -((dr * E.Jp[a]) * E.r0 + (dr * E.Jp[6 + a]) * E.r1);
                 }
             }
         }
@@ -520,43 +538,43 @@ __global__ __launch_bounds__(256, 2) void k_lin(
         if (lead) {
             maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
             if (!pd) ndeg += 1.0;
-            double* cw = cn + (size_t)lm * LH_CACHE;
-            cw[0] = l00; cw[1] = l10; cw[2] = l11; cw[3] = l20; cw[4] = l21; cw[5] = l22;
-            cw[6] = h[6]; cw[7] = h[7]; cw[8] = h[8];
-            cw[9] = h[0]; cw[10] = h[3]; cw[11] = h[5];
+            double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
+            reinterpret_cast<double2*>(rw)[0] = double2{X[0], X[1]};
+            reinterpret_cast<double2*>(rw)[1] = double2{X[2], l00};
+            reinterpret_cast<double2*>(rw)[2] = double2{l10, l11};
+            reinterpret_cast<double2*>(rw)[3] = double2{l20, l21};
+            reinterpret_cast<double2*>(rw)[4] = double2{l22, h[6]};
+            reinterpret_cast<double2*>(rw)[5] = double2{h[7], h[8]};
+            reinterpret_cast<double2*>(rw)[6] = double2{h[0], h[3]};
+            reinterpret_cast<double2*>(rw)[7] = double2{h[5], 0.0};
         }
         STAMP(2);
 
         // ---- per observation: G = H_pl L^-T and bsd = G w = H_pl H_ll^-1 b_l ----
-        double G[18], bsd[6];
+        double G[18];
 #pragma unroll
         for (int i = 0; i < 18; ++i) G[i] = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) bsd[i] = 0.0;
-        if (has && !pfixed && !(prm.guard && !pd)) {
+        if (live && !(prm.guard && !pd)) {
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double g0 = hpl[3 * a] * i00;
                 const double g1 = (hpl[3 * a + 1] - l10 * g0) * i11;
                 const double g2 = (hpl[3 * a + 2] - l20 * g0 - l21 * g1) * i22;
                 G[3 * a] = g0; G[3 * a + 1] = g1; G[3 * a + 2] = g2;
-                bsd[a] = g0 * w0 + g1 * w1 + g2 * w2;
+                trow[27 + a] = g0 * w0 + g1 * w1 + g2 * w2;
             }
+        } else if (live) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) trow[27 + a] = 0.0;
         }
         STAMP(3);
 
         // ---- per-pose sums (H_pp, b_p, bsd): lanes 0..32 walk each pose's observations in lane order ----
-#pragma unroll
-        for (int i = 0; i < 21; ++i) scr[LH_TASKS * lane + i] = hpp[i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) scr[LH_TASKS * lane + 21 + i] = bp[i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) scr[LH_TASKS * lane + 27 + i] = bsd[i];
         wave_sync();
 #pragma unroll
         for (int uu = 0; uu < Cfg::UMAX; ++uu) {
             if (uu < U) {
-                uint64_t mk = __ballot(has && slot == uu);
+                uint64_t mk = __ballot(live && slot == uu);
                 if (lane < LH_TASKS) {
                     double sacc = task[uu];
                     while (mk) {
@@ -621,6 +639,7 @@ __global__ __launch_bounds__(256, 2) void k_lin(
         maxd = fmax(maxd, __shfl_xor(maxd, off));
     }
     __syncthreads();
+    double* smem = dsm;
     const int ntile = Cfg::NT * 256;
     const int ntask = U * LH_TASKS;
     for (int phase = 0; phase < 2; ++phase) {
@@ -767,7 +786,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 // The matrix is padded to NE = ceil8(n) with identity rows: no bounds tests in
 // the inner loops.
 // ============================================================================
-#define CT 256
+#define CT 512
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
 #define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
 #define XS 9                  // LDS row stride of the panel's unscaled columns
@@ -782,8 +801,15 @@ __device__ __forceinline__ double fast_rcp(double d) {
     return r;
 }
 
+// lower-triangular 16x16 tile enumeration x -> (I, J), x = I (I + 1) / 2 + J, I < 8
+__constant__ unsigned char c_triI[36] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5,
+                                         6, 6, 6, 6, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7, 7};
+__constant__ unsigned char c_triJ[36] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5,
+                                         0, 1, 2, 3, 4, 5, 6, 0, 1, 2, 3, 4, 5, 6, 7};
+
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
+                                             const uint32_t* __restrict__ rsmap,
                                              double* __restrict__ pose_mat, double* __restrict__ ptab,
                                              const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
@@ -791,32 +817,29 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     __shared__ double Xp[NP * XS];        // unscaled panel columns (W = L D) for the trailing update
     __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP], tmp8[8];
     __shared__ int perm[NP], iperm[NP];
-    __shared__ unsigned char pr_p[LH_PMAX * (LH_PMAX + 1) / 2], pr_q[LH_PMAX * (LH_PMAX + 1) / 2];
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int P = prm.P, n = 6 * P, NE = (n + 7) & ~7;
+    const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
     const lh_rs_layout LY = lh_rs_make(P);
     STAMP_DECL
 
     // ---------------- 1. prefetch (one round trip) ----------------
     double vs[NLD], vc[NLD];
+    uint32_t mp[NLD];
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
         const int i = u * CT + tid;
         const bool in = i < LY.total;
         vs[u] = in ? rs_stage[i] : 0.0;
         vc[u] = in ? rs_commit[i] : 0.0;
+        mp[u] = i < LY.off_bs ? rsmap[i] : 0u;
     }
     double pm0[12], pm1[12];
     if (tid < P) {
 #pragma unroll
         for (int i = 0; i < 12; ++i) { pm0[i] = pose_mat[(size_t)tid * 12 + i]; pm1[i] = pose_mat[((size_t)P + tid) * 12 + i]; }
-    }
-    if (tid < P) {
-        const int base = tid * P - (tid * (tid - 1)) / 2;
-        for (int q = tid; q < P; ++q) { pr_p[base + q - tid] = (unsigned char)tid; pr_q[base + q - tid] = (unsigned char)q; }
     }
     if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
         double mx = 0.0;
@@ -933,11 +956,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         vs[u] = v;
         if (accept && i < LY.total) rs_commit[i] = v;
         if (i < LY.off_bs) {
-            const int blk = i / 36, r = i - 36 * blk, a = r / 6, b = r - 6 * (r / 6);
-            if (a == b && pr_p[blk] == pr_q[blk]) {
-                const int g = 6 * pr_p[blk] + a;
-                dg[g] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
-            }
+            const int gi = mp[u] & 0xff, gj = (mp[u] >> 8) & 0xff;
+            if (gi == gj) dg[gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
         } else if (i < LY.off_bp) {
             bsv[i - LY.off_bs] = v;
         } else if (i < LY.off_hd) {
@@ -946,16 +966,23 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             hdv[i - LY.off_hd] = v;
         }
     }
+    if (tid >= n && tid < NP) dg[tid] = __builtin_nan("");   // key -1 at an index above every real row: never counted
     __syncthreads();
     if (tid < n) {
         // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation
         double di = fabs(dg[tid]);
         if (!(di == di)) di = -1.0;
         int r = 0;
-        for (int j = 0; j < n; ++j) {
-            double dj = fabs(dg[j]);
-            if (!(dj == dj)) dj = -1.0;
-            r += (dj > di) || (dj == di && j < tid);
+        for (int j0 = 0; j0 < n; j0 += 8) {
+            double dj[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) dj[u] = dg[j0 + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                double d = fabs(dj[u]);
+                if (!(d == d)) d = -1.0;
+                r += (d > di) || (d == di && j0 + u < tid);
+            }
         }
         perm[r] = tid;
         iperm[tid] = r;
@@ -968,9 +995,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     for (int u = 0; u < NLD; ++u) {
         const int i = u * CT + tid;
         if (i < LY.off_bs) {
-            const int blk = i / 36, r = i - 36 * blk, a = r / 6, b = r - 6 * (r / 6);
-            const int ri = iperm[6 * pr_p[blk] + a], rj = iperm[6 * pr_q[blk] + b];
-            if (pr_p[blk] != pr_q[blk]) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
+            const int ri = iperm[mp[u] & 0xff], rj = iperm[(mp[u] >> 8) & 0xff];
+            if (!(mp[u] >> 16)) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
             else if (ri > rj) A[ri * AS + rj] = vs[u];
         }
     }
@@ -1045,53 +1071,39 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
         __syncthreads();
         STAMP(15);
-        // trailing update: A[i][j] -= sum_c L[i][c] W[j][c], k0+8 <= j <= i < NE, 4x4 micro-tiles;
-        // plus 1x4 tiles of the rhs row
+        // trailing update A[i][j] -= sum_c L[i][c] W[j][c], k0+8 <= j <= i < NE, on f64 MFMA:
+        // 16x16 tiles anchored at tb = floor16(k0+8), two 16x16x4 steps each; rows/cols
+        // below k0+8 of the first tile row/col are computed and discarded
         const int m0 = k0 + 8;
-        const int mt = (NE - m0) >> 2;
+        const int tb = m0 & ~15;
+        const int mt = (NE - tb) >> 4;
         const int ntile = mt * (mt + 1) / 2;
-        for (int x = tid; x < ntile + mt; x += CT) {
-            int rb, cb, nr;
-            if (x < ntile) {
-                int I = (int)((sqrtf(8.0f * (float)x + 1.0f) - 1.0f) * 0.5f);
-                while ((I + 1) * (I + 2) / 2 <= x) ++I;
-                while (I * (I + 1) / 2 > x) --I;
-                const int J = x - I * (I + 1) / 2;
-                rb = m0 + 4 * I; cb = m0 + 4 * J; nr = 4;
-            } else {
-                rb = NP; cb = m0 + 4 * (x - ntile); nr = 1;
+        const int wv = __builtin_amdgcn_readfirstlane(wave);
+        for (int x = wv; x < ntile; x += CT / 64) {
+            const int rb = tb + 16 * c_triI[x], cb = tb + 16 * c_triJ[x];
+            const int li = lane & 15, lk = lane >> 4;
+            const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
+            const double b0 = Xp[(cb + li) * XS + lk], b1 = Xp[(cb + li) * XS + 4 + lk];
+            const int col = cb + li;
+            double old[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) old[r] = A[(rb + lk + 4 * r) * AS + col];
+            v4d acc = {0.0, 0.0, 0.0, 0.0};
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
+            // entries left of / above k0+8 are the panel's own L and D (written back unchanged)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = rb + lk + 4 * r;
+                A[row * AS + col] = (row >= m0 && col >= m0) ? old[r] - acc[r] : old[r];
             }
-            double Xc[4][8];
+        }
+        if (tid >= CT - 64) {   // the rhs row (forward substitution): last wave, after its tiles
+            for (int j = m0 + (tid - (CT - 64)); j < NE; j += 64) {
+                double acc = 0.0;
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-                for (int c = 0; c < 8; ++c) Xc[s2][c] = Xp[(cb + s2) * XS + c];
-            if (nr == 4) {
-                double Lr[4][8];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) Lr[r][c] = A[(rb + r) * AS + k0 + c];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2) {
-                        double acc = 0.0;
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) acc += Lr[r][c] * Xc[s2][c];
-                        A[(rb + r) * AS + cb + s2] -= acc;
-                    }
-            } else {
-                double Lr[8];
-#pragma unroll
-                for (int c = 0; c < 8; ++c) Lr[c] = A[NP * AS + k0 + c];
-#pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) {
-                    double acc = 0.0;
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) acc += Lr[c] * Xc[s2][c];
-                    A[NP * AS + cb + s2] -= acc;
-                }
+                for (int c = 0; c < 8; ++c) acc += A[NP * AS + k0 + c] * Xp[j * XS + c];
+                A[NP * AS + j] -= acc;
             }
         }
         __syncthreads();
@@ -1200,13 +1212,29 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 // ============================================================================
 extern "C" {
 
+size_t lh_lin_smem_bytes(int ncam) {
+    return sizeof(double) * ((size_t)LH_WAVES * SCR_SZ + 2 * (size_t)LH_UMAX * ncam * LH_PT + LH_UMAX * 6 + (size_t)ncam * LH_EXT);
+}
+
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
-                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta,
-                         double* Xbuf, double* cache, const double* ptab, const double* ext, const lh_ctrl* ctrl,
-                         const double* dxp, double* edge_rho, double* slabs, lh_params prm, int L, uint32_t fixed_mask) {
+                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
+                         const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
+                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint32_t fixed_mask) {
     if (nchunks <= 0) return hipSuccess;
+    const size_t smem = lh_lin_smem_bytes(prm.ncam);
     dim3 g(nchunks), b(256);
-#define LH_LIN(TT, TR) hipLaunchKernelGGL((k_lin<TT, TR>), g, b, 0, st, chunks, sbs, obs_uv, obs_meta, Xbuf, cache, ptab, ext, ctrl, dxp, edge_rho, slabs, prm, L, fixed_mask, chunk_base)
+#define LH_LIN(TT, TR)                                                                                             \
+    do {                                                                                                           \
+        static bool attr_set = false;                                                                              \
+        if (!attr_set) {                                                                                           \
+            hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lin<TT, TR>),                     \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);           \
+            if (e_ != hipSuccess) return e_;                                                                       \
+            attr_set = true;                                                                                       \
+        }                                                                                                          \
+        hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
+                           edge_rho, slabs, prm, nrec, fixed_mask, chunk_base);                                    \
+    } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
         case 3: LH_LIN(1, true); break;
@@ -1233,9 +1261,9 @@ hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double
 }
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
+                          const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
                           int* host_done) {
-    hipLaunchKernelGGL(k_ctrl, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pose_mat, ptab, ext, dxp, prm,
+    hipLaunchKernelGGL(k_ctrl, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp, prm,
                        mode, (volatile int*)host_done);
     return hipGetLastError();
 }
