@@ -72,7 +72,7 @@ typedef struct lh_options {
     int32_t rank;             /* this process's shard                                         */
     int32_t degenerate_guard; /* 0: reference semantics (rank-deficient H_ll poisons the step,
                                  problem.cpp:396-400); 1: skip such landmarks' Schur terms    */
-    int32_t trials_per_sync;  /* LM trials enqueued per host poll of the stop flag (0: auto)  */
+    int32_t trials_per_sync;  /* LM trials kept in flight ahead of the host poll (0: auto = 2)  */
     int32_t profile;          /* 1: time every kernel with HIP events (lh_kernel_stats)       */
     uint8_t comm_id[128];     /* ncclUniqueId from lh_comm_unique_id on rank 0 (world_size>1) */
 } lh_options;

@@ -39,6 +39,9 @@ hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
                           lh_params prm, int mode, int* host_done);
+hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, long nrec_doubles, double* qt,
+                           const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab, double* dxp,
+                           int ndxp, lh_ctrl* ctrl);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
 }
@@ -183,7 +186,8 @@ struct lh_handle {
         d_rs_stage, d_rs_commit, d_maxd, d_dxp;
     DevBuf<lh_ctrl> d_ctrl;
     lh_ctrl* h_ctrl = nullptr;   // pinned
-    int* h_done = nullptr;       // pinned
+    int* h_done = nullptr;       // pinned, mapped: k_ctrl raises it when the LM loop stops
+    int* d_done = nullptr;       // device alias of h_done
 
     // profiling
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -591,7 +595,7 @@ int enqueue_trial(lh_handle* h, int mode) {
     {
         Prof pr(h, KC_CTRL);
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p, h->d_ptab.p,
-                              h->d_ext.p, h->d_dxp.p, h->prm, mode, nullptr));
+                              h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -602,33 +606,39 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     hipStream_t s = h->stream;
     const int P = h->P;
     const size_t PT = (size_t)P * h->ncam * LH_PT;
-    // restart from the uploaded initial state
-    HIPCHK(hipMemcpyAsync(h->d_rec.p, h->d_rec_init.p, LH_REC * (size_t)h->L_act * sizeof(double), hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->d_qt.p, h->d_qt_init.p, 24 * (size_t)P * sizeof(double), hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->d_ptab.p, h->d_ptab_init.p, 2 * PT * sizeof(double), hipMemcpyDeviceToDevice, s));
-    std::memset(h->h_ctrl, 0, sizeof(lh_ctrl));
-    h->h_ctrl->cur = 0;
-    HIPCHK(hipMemcpyAsync(h->d_ctrl.p, h->h_ctrl, sizeof(lh_ctrl), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(h->d_dxp.p, 0, 6 * (size_t)std::max(P, 1) * sizeof(double), s));
-
+    // restart from the uploaded initial state (k_reset), then the LM trials.  Trials are
+    // enqueued two ahead of the one the host waits for, so the device never idles on the
+    // host; k_ctrl raises the mapped done flag and any trial enqueued after it is a no-op.
     hipEvent_t e0 = next_event(h), e1 = next_event(h);
     if (!e0 || !e1) return LH_E_HIP;
+    *h->h_done = 0;
     HIPCHK(hipEventRecord(e0, s));
+    HIPCHK(lh_launch_reset(s, h->d_rec.p, h->d_rec_init.p, LH_REC * (long)h->L_act, h->d_qt.p, h->d_qt_init.p, 24 * P,
+                           h->d_ptab.p, h->d_ptab_init.p, (int)(2 * PT), h->d_dxp.p, 6 * std::max(P, 1), h->d_ctrl.p));
+    DBGSYNC("k_reset");
     int st = enqueue_trial(h, 0);
     if (st != LH_OK) return st;
-    const int max_total = std::max(0, h->opt.max_iters) * std::max(1, h->opt.max_trials);
-    int batch = h->opt.trials_per_sync > 0 ? h->opt.trials_per_sync : 4;
-    int enq = 0;
-    while (enq < max_total) {
-        const int nb = std::min(batch, max_total - enq);
-        for (int i = 0; i < nb; ++i) {
-            st = enqueue_trial(h, 1);
-            if (st != LH_OK) return st;
-        }
-        enq += nb;
-        HIPCHK(hipMemcpyAsync(h->h_done, &h->d_ctrl.p->done, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (*h->h_done) break;
+    const int max_total = (h->opt.max_iters > 0) ? h->opt.max_iters * std::max(1, h->opt.max_trials) : 0;
+    const int depth = h->opt.trials_per_sync > 0 ? std::min(h->opt.trials_per_sync, 32) : 2;
+    hipEvent_t ring[64];
+    int head = 0, tail = 0, enq = 0;
+    auto push = [&]() -> int {
+        int r = enqueue_trial(h, 1);
+        if (r != LH_OK) return r;
+        hipEvent_t ev = next_event(h);
+        if (!ev) return LH_E_HIP;
+        if (hipEventRecord(ev, s) != hipSuccess) return LH_E_HIP;
+        ring[tail++ & 63] = ev;
+        ++enq;
+        return LH_OK;
+    };
+    while (enq < max_total && tail - head < depth)
+        if ((st = push()) != LH_OK) return st;
+    while (head < tail) {
+        HIPCHK(hipEventSynchronize(ring[head++ & 63]));
+        if (*(volatile int*)h->h_done) break;
+        if (enq < max_total)
+            if ((st = push()) != LH_OK) return st;
     }
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipMemcpyAsync(h->h_ctrl, h->d_ctrl.p, sizeof(lh_ctrl), hipMemcpyDeviceToHost, s));
@@ -755,7 +765,8 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     h->device = dev;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipHostMalloc((void**)&h->h_ctrl, sizeof(lh_ctrl), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_done, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&h->h_done, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->d_done, h->h_done, 0) != hipSuccess) {
         lh_destroy(h);
         return LH_E_HIP;
     }

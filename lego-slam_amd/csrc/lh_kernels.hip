@@ -13,6 +13,7 @@
 //             (VertexPose::add, lego_types.h:61-91).
 // Every reduction has a fixed order, so a solve is bitwise reproducible.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 
@@ -1265,6 +1266,33 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           int* host_done) {
     hipLaunchKernelGGL(k_ctrl, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp, prm,
                        mode, (volatile int*)host_done);
+    return hipGetLastError();
+}
+
+// ---- k_reset: restart a resident solve (one launch instead of five copies) ----
+__global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const double2* __restrict__ rec_init, long nrec2,
+                                               double* __restrict__ qt, const double* __restrict__ qt_init, int nqt,
+                                               double* __restrict__ ptab, const double* __restrict__ ptab_init, int nptab,
+                                               double* __restrict__ dxp, int ndxp, lh_ctrl* __restrict__ ctrl) {
+    const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
+    for (long i = i0; i < nrec2; i += st) rec[i] = rec_init[i];
+    if (blockIdx.x == 0) {
+        for (int i = threadIdx.x; i < nqt; i += 256) qt[i] = qt_init[i];
+        for (int i = threadIdx.x; i < nptab; i += 256) ptab[i] = ptab_init[i];
+        for (int i = threadIdx.x; i < ndxp; i += 256) dxp[i] = 0.0;
+        int* c = reinterpret_cast<int*>(ctrl);
+        for (int i = threadIdx.x; i < (int)(sizeof(lh_ctrl) / sizeof(int)); i += 256) c[i] = 0;   // cur = 0
+    }
+}
+
+hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, long nrec_doubles, double* qt,
+                           const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab, double* dxp,
+                           int ndxp, lh_ctrl* ctrl) {
+    const long n2 = nrec_doubles / 2;
+    const int blocks = (int)std::max(1L, std::min(2048L, (n2 + 255) / 256));
+    hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, st, reinterpret_cast<double2*>(rec),
+                       reinterpret_cast<const double2*>(rec_init), n2, qt, qt_init, nqt, ptab, ptab_init, nptab, dxp,
+                       ndxp, ctrl);
     return hipGetLastError();
 }
 
