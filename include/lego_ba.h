@@ -160,6 +160,9 @@ int lh_classify_outliers(const double *edge_robust_chi2, int64_t n_obs, double c
 /* ---- test hooks (not part of the reference interface) ---- */
 /* f64 MFMA accumulator-layout probe: D(16x16) = A(16x4) * B(4x16), device pointers, row-major */
 int lh_debug_mfma_probe(const double *A, const double *B, double *D);
+/* k_ctrl's reduced-system solve (Eigen-LDLT pivot order, blocked LDL^T, back substitution) on a
+   dense symmetric n x n S (row-major), n <= 128: x = S^-1 b.  Device pointers. */
+int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x);
 /* per-phase wave-cycle totals of a -DLH_STAMPS diagnostic build (all zero in the product build) */
 int lh_debug_stamps(unsigned long long *out, int n, int reset);
 

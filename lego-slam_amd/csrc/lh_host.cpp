@@ -42,6 +42,7 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, long nrec_doubles, double* qt,
                            const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab, double* dxp,
                            int ndxp, lh_ctrl* ctrl);
+hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
 }
@@ -880,6 +881,14 @@ int lh_debug_stamps(unsigned long long* out, int n, int reset) {
 }
 
 // test hook: f64 MFMA accumulator layout probe (A 16x4 row-major, B 4x16, D 16x16), device pointers
+int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x) {
+    if (!S || !b || !x) return LH_E_BADARG;
+    if (n < 1 || n > LH_NPAD) return LH_E_UNSUPPORTED;
+    HIPCHK(lh_launch_ldlt_probe(S, b, n, x));
+    HIPCHK(hipDeviceSynchronize());
+    return LH_OK;
+}
+
 int lh_debug_mfma_probe(const double* A, const double* B, double* D) {
     if (lh_launch_mfma_probe(A, B, D) != hipSuccess) return LH_E_HIP;
     if (hipDeviceSynchronize() != hipSuccess) return LH_E_HIP;

@@ -802,11 +802,211 @@ __device__ __forceinline__ double fast_rcp(double d) {
     return r;
 }
 
+#define TRI8(r, c) ((r) * ((r) - 1) / 2 + (c))   // packed strictly-lower 8x8 index, r > c
+
+// LDL^T of the 8x8 diagonal block at (k0, k0) of A (lower triangle), computed redundantly by
+// every lane of one wave; one lane writes D on A's diagonal and L below it (L = W where Eigen's
+// pivot_is_valid fails, ldlt_inplace).  Stores from one wave are slow: only these 36 values.
+__device__ __forceinline__ void factor_block8(double* A, int k0, int lane) {
+    double B[8][8], Wb[8][8], dv[8], inv[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) B[r][c] = A[(k0 + r) * AS + k0 + c];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        dv[c] = B[c][c];
+        const bool valid = fabs(dv[c]) > 0.0;     // Eigen ldlt_inplace: pivot_is_valid
+        inv[c] = valid ? fast_rcp(dv[c]) : 1.0;
+#pragma unroll
+        for (int r = c + 1; r < 8; ++r) Wb[r][c] = B[r][c];
+#pragma unroll
+        for (int r = c + 1; r < 8; ++r) {
+            const double l = Wb[r][c] * inv[c];
+            B[r][c] = l;
+#pragma unroll
+            for (int r2 = c + 1; r2 <= r; ++r2) B[r][r2] -= l * Wb[r2][c];
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+#pragma unroll
+            for (int c = 0; c < r; ++c) A[(k0 + r) * AS + k0 + c] = B[r][c];
+            A[(k0 + r) * AS + k0 + r] = dv[r];
+        }
+    }
+}
+
 // lower-triangular 16x16 tile enumeration x -> (I, J), x = I (I + 1) / 2 + J, I < 8
 __constant__ unsigned char c_triI[36] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5,
                                          6, 6, 6, 6, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7, 7};
 __constant__ unsigned char c_triJ[36] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5,
                                          0, 1, 2, 3, 4, 5, 6, 0, 1, 2, 3, 4, 5, 6, 7};
+
+// Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
+// blocked LDL^T and the solve; xsol[r] = solution in pivot order for r < n.  Shared with the
+// k_ldlt_probe test hook.  Must be called by all CT threads.
+__device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ Xp, double* __restrict__ xsol,
+                                               int n, int NE, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+#ifdef LH_STAMPS
+    unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_, sacc_[24] = {0};
+#endif
+    // ---------------- 3. blocked right-looking LDL^T (+ forward substitution in row NP) ----------------
+    // Each 8x8 diagonal block is factored by wave 0 as soon as the previous trailing update has
+    // produced it (look-ahead), while the other waves finish that update; the panel phase then
+    // only solves every row below against the factored block.
+    if (wave == 0) factor_block8(A, 0, lane);
+    __syncthreads();
+    STAMP(18);
+    for (int k0 = 0; k0 < NE; k0 += 8) {
+        const int m0 = k0 + 8;
+        const int nrow = NE - m0 + 1;                 // panel rows k0+8..NE-1 and the rhs row
+        if (tid < nrow) {
+            const int i = (tid == nrow - 1) ? NP : m0 + tid;
+            // the factored diagonal block: 1/D and W = L D (L itself where the pivot is invalid)
+            double inv[8], Wb[28], a[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const double d = A[(k0 + c) * AS + k0 + c];
+                const bool valid = fabs(d) > 0.0;
+                inv[c] = valid ? fast_rcp(d) : 1.0;
+#pragma unroll
+                for (int r = c + 1; r < 8; ++r) {
+                    const double l = A[(k0 + r) * AS + k0 + c];
+                    Wb[TRI8(r, c)] = valid ? l * d : l;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) a[c] = A[i * AS + k0 + c];
+            double w[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                w[c] = a[c];
+                const double l = a[c] * inv[c];
+                a[c] = l;
+#pragma unroll
+                for (int c2 = c + 1; c2 < 8; ++c2) a[c2] -= l * Wb[TRI8(c2, c)];
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) A[i * AS + k0 + c] = a[c];
+            if (i < NP) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) Xp[i * XS + c] = w[c];
+            }
+        }
+        __syncthreads();
+        STAMP(15);
+        if (m0 < NE) {
+            // trailing update A[i][j] -= sum_c L[i][c] W[j][c], k0+8 <= j <= i < NE, on f64 MFMA:
+            // 16x16 tiles anchored at tb = floor16(k0+8), two 16x16x4 steps each; rows/cols
+            // below k0+8 of the first tile row/col are the panel's own L and D (written back unchanged).
+            // Tile 0 holds the next diagonal block: wave 0 updates it first, then factors the block.
+            const int tb = m0 & ~15;
+            const int mt = (NE - tb) >> 4;
+            const int ntile = mt * (mt + 1) / 2;
+            const int wv = __builtin_amdgcn_readfirstlane(wave);
+            const int li = lane & 15, lk = lane >> 4;
+            // wave 4 shares wave 0's SIMD (waves w and w+4 of a workgroup do): it stays idle so the
+            // factor chain issues unimpeded; waves 1-3, 5-7 take tiles 1.. round-robin
+            const int tq = wv - 1 - (wv > 4 ? 1 : 0);
+            const int x0 = (wv == 0) ? 0 : (wv == 4 ? ntile : 1 + tq);
+            const int xs_ = (wv == 0) ? ntile : 6;
+            for (int x = x0; x < ntile; x += xs_) {
+                const int rb = tb + 16 * c_triI[x], cb = tb + 16 * c_triJ[x];
+                const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
+                const double b0 = Xp[(cb + li) * XS + lk], b1 = Xp[(cb + li) * XS + 4 + lk];
+                const int col = cb + li;
+                double old[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) old[r] = A[(rb + lk + 4 * r) * AS + col];
+                v4d acc = {0.0, 0.0, 0.0, 0.0};
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = rb + lk + 4 * r;
+                    A[row * AS + col] = (row >= m0 && col >= m0) ? old[r] - acc[r] : old[r];
+                }
+            }
+            if (wv == 0) { STAMP(22); } else { STAMP(23); }
+            if (wv == 0) {
+                wave_sync();
+                factor_block8(A, m0, lane);
+                STAMP(12);
+            }
+            if (tid >= CT - 64) {   // the rhs row (forward substitution): last wave, after its tiles
+                for (int j = m0 + (tid - (CT - 64)); j < NE; j += 64) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) acc += A[NP * AS + k0 + c] * Xp[j * XS + c];
+                    A[NP * AS + j] -= acc;
+                }
+            }
+            __syncthreads();
+        }
+        STAMP(16);
+    }
+
+    // ---------------- 4. z /= D (Eigen tolerance), back substitution L^T x = z ----------------
+    if (wave == 0) {
+        const double tol = 2.2250738585072014e-308;   // LDLT::_solve_impl: (numeric_limits::min)()
+        const int r0 = lane, r1 = lane + 64;
+        double t0 = 0.0, t1 = 0.0;
+        if (r0 < NE) { const double d = A[r0 * AS + r0]; t0 = fabs(d) > tol ? A[NP * AS + r0] : 0.0; }
+        if (r1 < NE) { const double d = A[r1 * AS + r1]; t1 = fabs(d) > tol ? A[NP * AS + r1] : 0.0; }
+        // the L columns of the rows above block kb (independent of the solution), one block ahead
+        double c0[8], c1[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            c0[v] = A[(NE - 8 + v) * AS + r0];
+            c1[v] = A[(NE - 8 + v) * AS + (r1 & (NP - 1))];
+        }
+        for (int kb = NE - 8; kb >= 0; kb -= 8) {
+            double Lb[28];
+#pragma unroll
+            for (int w2 = 1; w2 < 8; ++w2)
+#pragma unroll
+                for (int v = 0; v < w2; ++v) Lb[TRI8(w2, v)] = A[(kb + w2) * AS + kb + v];
+            double n0[8], n1[8];
+            const int kn = kb >= 8 ? kb - 8 : 0;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                n0[v] = A[(kn + v) * AS + r0];
+                n1[v] = A[(kn + v) * AS + (r1 & (NP - 1))];
+            }
+            // the block rows' right-hand sides, broadcast from their lanes
+            double x[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) x[v] = (kb < 64) ? readlane_d(t0, kb + v) : readlane_d(t1, kb + v - 64);
+#pragma unroll
+            for (int v = 7; v >= 0; --v) {
+#pragma unroll
+                for (int w2 = v + 1; w2 < 8; ++w2) x[v] -= Lb[TRI8(w2, v)] * x[w2];
+            }
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                if (r0 == kb + v) t0 = x[v];
+                if (r1 == kb + v) t1 = x[v];
+                s0 += c0[v] * x[v];
+                s1 += c1[v] * x[v];
+            }
+            if (r0 < kb) t0 -= s0;
+            if (r1 < kb) t1 -= s1;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) { c0[v] = n0[v]; c1[v] = n1[v]; }
+        }
+        if (r0 < n) xsol[r0] = t0;
+        if (r1 < n) xsol[r1] = t1;
+    }
+    __syncthreads();
+
+#ifdef LH_STAMPS
+    STAMP_FLUSH(10, 14);
+#endif
+}
 
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
@@ -816,7 +1016,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
     __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
     __shared__ double Xp[NP * XS];        // unscaled panel columns (W = L D) for the trailing update
-    __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP], tmp8[8];
+    __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP], yv[NP];
     __shared__ int perm[NP], iperm[NP];
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
@@ -826,7 +1026,17 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const lh_rs_layout LY = lh_rs_make(P);
     STAMP_DECL
 
-    // ---------------- 1. prefetch (one round trip) ----------------
+    // ---------------- 1. prefetch (one round trip); the controller's words first ----------------
+    double chi = 0.0, lam = 0.0, ni = 0.0, last = 0.0, spose = 0.0, chi0 = 0.0, tchi = 0.0, sl = 0.0;
+    int iter = 0, fc = 0, trials = 0, nacc = 0, done0 = 1, cur0 = 0, tl = 0;
+    if (tid == 0) {
+        chi = ctrl->chi; lam = ctrl->lambda; ni = ctrl->ni; last = ctrl->last_chi; spose = ctrl->spose;
+        chi0 = ctrl->chi2_initial;
+        iter = ctrl->iter; fc = ctrl->false_cnt; trials = ctrl->trials; nacc = ctrl->accepted;
+        done0 = ctrl->done; cur0 = ctrl->cur; tl = ctrl->trace_len;
+        tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
+        sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+    }
     double vs[NLD], vc[NLD];
     uint32_t mp[NLD];
 #pragma unroll
@@ -856,12 +1066,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 
     // ---------------- LM bookkeeping (thread 0) ----------------
     if (tid == 0) {
-        double chi = ctrl->chi, lam = ctrl->lambda, ni = ctrl->ni, last = ctrl->last_chi, spose = ctrl->spose;
-        double chi0 = ctrl->chi2_initial;
-        int iter = ctrl->iter, fc = ctrl->false_cnt, trials = ctrl->trials, nacc = ctrl->accepted;
-        int done = ctrl->done, cur = ctrl->cur, tl = ctrl->trace_len;
-        const double tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
-        const double sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+        int done = done0, cur = cur0;
         int accept = 0, trace = 0;
         if (!done) {
             if (mode == 0) {
@@ -969,29 +1174,38 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     if (tid >= n && tid < NP) dg[tid] = __builtin_nan("");   // key -1 at an index above every real row: never counted
     __syncthreads();
-    if (tid < n) {
-        // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation
-        double di = fabs(dg[tid]);
-        if (!(di == di)) di = -1.0;
+    STAMP(19);
+    {
+        // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation.
+        // Four threads per row, each counting over 32 of the 128 keys (dg[n..NP) are NaN).
+        const int row = tid >> 2, part = tid & 3;
         int r = 0;
-        for (int j0 = 0; j0 < n; j0 += 8) {
-            double dj[8];
+        if (row < n) {
+            double di = fabs(dg[row]);
+            if (!(di == di)) di = -1.0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) dj[u] = dg[j0 + u];
+            for (int j0 = 0; j0 < 32; j0 += 8) {
+                double dj[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                double d = fabs(dj[u]);
-                if (!(d == d)) d = -1.0;
-                r += (d > di) || (d == di && j0 + u < tid);
+                for (int u = 0; u < 8; ++u) dj[u] = dg[part * 32 + j0 + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    double d = fabs(dj[u]);
+                    if (!(d == d)) d = -1.0;
+                    r += (d > di) || (d == di && part * 32 + j0 + u < row);
+                }
             }
         }
-        perm[r] = tid;
-        iperm[tid] = r;
-    } else if (tid < NP) {
-        perm[tid] = tid;
-        iperm[tid] = tid;
+        r += __shfl_xor(r, 1);
+        r += __shfl_xor(r, 2);
+        if (part == 0 && row < NP) {
+            const int rr = row < n ? r : row;
+            perm[rr] = row;
+            iperm[row] = rr;
+        }
     }
     __syncthreads();
+    STAMP(21);
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
         const int i = u * CT + tid;
@@ -1012,147 +1226,15 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     __syncthreads();
     STAMP(11);
 
-    // ---------------- 3. blocked right-looking LDL^T (+ forward substitution in row NP) ----------------
-    for (int k0 = 0; k0 < NE; k0 += 8) {
-        const int nrow = NE - k0 + 1;                 // panel rows k0..NE-1 and the rhs row
-        if (tid < nrow) {
-            const int i = (tid == nrow - 1) ? NP : k0 + tid;
-            // 8x8 diagonal block, factored redundantly by every panel thread
-            double B[8][8], Wb[8][8], dv[8], inv[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-#pragma unroll
-                for (int c = 0; c <= r; ++c) B[r][c] = A[(k0 + r) * AS + k0 + c];
-            double a[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) a[c] = A[i * AS + k0 + c];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                dv[c] = B[c][c];
-                const bool valid = fabs(dv[c]) > 0.0;     // Eigen ldlt_inplace: pivot_is_valid
-                inv[c] = valid ? fast_rcp(dv[c]) : 1.0;
-#pragma unroll
-                for (int r = c + 1; r < 8; ++r) Wb[r][c] = B[r][c];
-#pragma unroll
-                for (int r = c + 1; r < 8; ++r) {
-                    const double l = Wb[r][c] * inv[c];
-                    B[r][c] = l;
-#pragma unroll
-                    for (int r2 = c + 1; r2 <= r; ++r2) B[r][r2] -= l * Wb[r2][c];
-                }
-            }
-            const int ri = i - k0;
-            if (ri < 8) {
-                // the diagonal block: the thread of its first row writes L and D of all 8 rows
-                if (ri == 0) {
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-#pragma unroll
-                        for (int c = 0; c < r; ++c) A[(k0 + r) * AS + k0 + c] = B[r][c];
-                        A[(k0 + r) * AS + k0 + r] = dv[r];
-                    }
-                }
-            } else {
-                double w[8];
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    w[c] = a[c];
-                    const double l = a[c] * inv[c];
-                    a[c] = l;
-#pragma unroll
-                    for (int c2 = c + 1; c2 < 8; ++c2) a[c2] -= l * Wb[c2][c];
-                }
-#pragma unroll
-                for (int c = 0; c < 8; ++c) A[i * AS + k0 + c] = a[c];
-                if (i < NP) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) Xp[i * XS + c] = w[c];
-                }
-            }
-        }
-        __syncthreads();
-        STAMP(15);
-        // trailing update A[i][j] -= sum_c L[i][c] W[j][c], k0+8 <= j <= i < NE, on f64 MFMA:
-        // 16x16 tiles anchored at tb = floor16(k0+8), two 16x16x4 steps each; rows/cols
-        // below k0+8 of the first tile row/col are computed and discarded
-        const int m0 = k0 + 8;
-        const int tb = m0 & ~15;
-        const int mt = (NE - tb) >> 4;
-        const int ntile = mt * (mt + 1) / 2;
-        const int wv = __builtin_amdgcn_readfirstlane(wave);
-        for (int x = wv; x < ntile; x += CT / 64) {
-            const int rb = tb + 16 * c_triI[x], cb = tb + 16 * c_triJ[x];
-            const int li = lane & 15, lk = lane >> 4;
-            const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
-            const double b0 = Xp[(cb + li) * XS + lk], b1 = Xp[(cb + li) * XS + 4 + lk];
-            const int col = cb + li;
-            double old[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) old[r] = A[(rb + lk + 4 * r) * AS + col];
-            v4d acc = {0.0, 0.0, 0.0, 0.0};
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
-            // entries left of / above k0+8 are the panel's own L and D (written back unchanged)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = rb + lk + 4 * r;
-                A[row * AS + col] = (row >= m0 && col >= m0) ? old[r] - acc[r] : old[r];
-            }
-        }
-        if (tid >= CT - 64) {   // the rhs row (forward substitution): last wave, after its tiles
-            for (int j = m0 + (tid - (CT - 64)); j < NE; j += 64) {
-                double acc = 0.0;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) acc += A[NP * AS + k0 + c] * Xp[j * XS + c];
-                A[NP * AS + j] -= acc;
-            }
-        }
-        __syncthreads();
-        STAMP(16);
-    }
-
-    // ---------------- 4. z /= D (Eigen tolerance), back substitution L^T x = z ----------------
-    if (wave == 0) {
-        const double tol = 2.2250738585072014e-308;   // LDLT::_solve_impl: (numeric_limits::min)()
-        const int r0 = lane, r1 = lane + 64;
-        double t0 = 0.0, t1 = 0.0;
-        if (r0 < NE) { const double d = A[r0 * AS + r0]; t0 = fabs(d) > tol ? A[NP * AS + r0] : 0.0; }
-        if (r1 < NE) { const double d = A[r1 * AS + r1]; t1 = fabs(d) > tol ? A[NP * AS + r1] : 0.0; }
-        for (int kb = NE - 8; kb >= 0; kb -= 8) {
-            // L columns of the rows above this block (independent of the block's solution)
-            double c0[8], c1[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                c0[v] = A[(kb + v) * AS + r0];
-                c1[v] = A[(kb + v) * AS + (r1 & (NP - 1))];
-            }
-            if (r0 >= kb && r0 < kb + 8) tmp8[r0 - kb] = t0;
-            if (r1 >= kb && r1 < kb + 8) tmp8[r1 - kb] = t1;
-            wave_sync();
-            double x[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) x[v] = tmp8[v];
-#pragma unroll
-            for (int v = 7; v >= 0; --v) {
-#pragma unroll
-                for (int w2 = v + 1; w2 < 8; ++w2) x[v] -= A[(kb + w2) * AS + kb + v] * x[w2];
-            }
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                if (r0 == kb + v) t0 = x[v];
-                if (r1 == kb + v) t1 = x[v];
-            }
-            double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-            for (int v = 0; v < 8; ++v) { s0 += c0[v] * x[v]; s1 += c1[v] * x[v]; }
-            if (r0 < kb) t0 -= s0;
-            if (r1 < kb) t1 -= s1;
-            wave_sync();
-        }
-        if (r0 < n) { xs[perm[r0]] = t0; dxp[perm[r0]] = t0; }
-        if (r1 < n) { xs[perm[r1]] = t1; dxp[perm[r1]] = t1; }
-    }
+    // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
+    STAMP_FLUSH(10, 14);
+    lds_ldlt_solve(A, Xp, yv, n, NE, tid);
+    if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
     __syncthreads();
+#ifdef LH_STAMPS
+    st0_ = __builtin_amdgcn_s_memtime();
+    for (int i_ = 0; i_ < 24; ++i_) sacc_[i_] = 0;
+#endif
     STAMP(13);
 
     // ---------------- pose part of the gain denominator; candidate poses ----------------
@@ -1205,7 +1287,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         ctrl->spose = s2;
     }
     STAMP(14);
-    STAMP_FLUSH(10, 8);
+    STAMP_FLUSH(10, 14);
 }
 
 // ============================================================================
@@ -1293,6 +1375,48 @@ hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, 
     hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, st, reinterpret_cast<double2*>(rec),
                        reinterpret_cast<const double2*>(rec_init), n2, qt, qt_init, nqt, ptab, ptab_init, nptab, dxp,
                        ndxp, ctrl);
+    return hipGetLastError();
+}
+
+// ---- LDL^T probe (tests): x = (S)^-1 b through k_ctrl's pivot order, LDS layout and
+//      lds_ldlt_solve, for a dense symmetric S (row-major n x n, n <= LH_NPAD) ----
+__global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
+                                                   double* __restrict__ x) {
+    __shared__ double A[(NP + 1) * AS];
+    __shared__ double Xp[NP * XS];
+    __shared__ double dg[NP], xsol[NP];
+    __shared__ int perm[NP];
+    const int tid = threadIdx.x, NE = (n + 15) & ~15;
+    if (tid < NP) dg[tid] = tid < n ? S[(size_t)tid * n + tid] : __builtin_nan("");
+    __syncthreads();
+    if (tid < n) {
+        double di = fabs(dg[tid]);
+        if (!(di == di)) di = -1.0;
+        int r = 0;
+        for (int j = 0; j < NP; ++j) {
+            double d = fabs(dg[j]);
+            if (!(d == d)) d = -1.0;
+            r += (d > di) || (d == di && j < tid);
+        }
+        perm[r] = tid;
+    } else if (tid < NP) {
+        perm[tid] = tid;
+    }
+    __syncthreads();
+    for (int e = tid; e < NE * NE; e += CT) {
+        const int r = e / NE, c = e - NE * (e / NE);
+        if (c <= r) A[r * AS + c] = (r < n) ? ((c < n) ? S[(size_t)perm[r] * n + perm[c]] : 0.0) : (r == c ? 1.0 : 0.0);
+    }
+    if (tid < NE) A[NP * AS + tid] = tid < n ? b[perm[tid]] : 0.0;
+    __syncthreads();
+    lds_ldlt_solve(A, Xp, xsol, n, NE, tid);
+    __syncthreads();
+    if (tid < n) x[perm[tid]] = xsol[tid];
+}
+
+hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x) {
+    if (n < 1 || n > LH_NPAD) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ldlt_probe, dim3(1), dim3(CT), 0, 0, S, b, n, x);
     return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ from windows import window  # noqa: E402
 
 NAMES = {0: "lin:backsub", 1: "lin:linearize", 2: "lin:Hll+chol", 3: "lin:G+bsd", 4: "lin:pose-tasks",
          5: "lin:G-image", 6: "lin:mfma", 7: "lin:combine+slab", 10: "ctrl:LM+copy", 11: "ctrl:S+perm+load",
-         12: "ctrl:LDLT(rest)", 13: "ctrl:solve", 14: "ctrl:poses", 15: "ctrl:LDLT panel", 16: "ctrl:LDLT update", 17: "ctrl:LM logic", 20: "reduce"}
+         12: "ctrl:factor8 (w0)", 13: "ctrl:solve", 14: "ctrl:poses", 15: "ctrl:LDLT panel", 16: "ctrl:LDLT update", 17: "ctrl:LM logic", 18: "ctrl:block0", 19: "ctrl:commit+dg", 21: "ctrl:rank", 22: "ctrl:upd tiles w0", 23: "ctrl:upd tiles w1-7", 20: "reduce"}
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 w = window(cfg, seed=0, family="stable_noout")
@@ -26,9 +26,9 @@ for _ in range(n):
     trials += s.solve_resident()["trials"] + 1
 st = lego_ba.debug_stamps(reset=True)
 lin = sum(int(st[i]) for i in range(8))
-ctrl = sum(int(st[i]) for i in range(10, 18))
+ctrl = sum(int(st[i]) for i in range(10, 24) if i != 20)
 print(f"{cfg}: {trials} k_lin launches; totals (wave-cycles/launch): lin {lin / trials:.3e} ctrl {ctrl / trials:.3e} reduce {int(st[20]) / trials:.3e}")
 for i, nm in NAMES.items():
     v = int(st[i])
-    base = lin if i < 10 else (ctrl if i < 20 else max(v, 1))
+    base = lin if i < 10 else (max(v, 1) if i == 20 else ctrl)
     print(f"  {nm:20s} {v / trials:12.3e} wave-cycles/launch  {100.0 * v / max(base, 1):5.1f}%")

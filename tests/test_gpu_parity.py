@@ -45,6 +45,52 @@ def test_mfma_f64_accumulator_layout():
     assert torch.equal(D, A @ B)
 
 
+def _ldlt_probe(S, b):
+    import torch
+    lib = lego_ba.ba_lib()
+    lib.lh_debug_ldlt_probe.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    St = torch.tensor(S, dtype=torch.float64, device="cuda").contiguous()
+    bt = torch.tensor(b, dtype=torch.float64, device="cuda")
+    xt = torch.zeros(len(b), dtype=torch.float64, device="cuda")
+    assert lib.lh_debug_ldlt_probe(St.data_ptr(), bt.data_ptr(), len(b), xt.data_ptr()) == 0
+    return xt.cpu().numpy()
+
+
+@pytest.mark.parametrize("n", [6, 12, 60, 96, 114, 120, 126])
+def test_reduced_solve_spd(n):
+    """k_ctrl's blocked LDL^T + solve (through the test hook) against numpy on SPD systems
+    shaped like S + lambda I (problem.cpp:404-420): block-banded, wide diagonal spread."""
+    rng = np.random.default_rng(n)
+    P = n // 6
+    S = np.zeros((n, n))
+    for p in range(P):
+        for q in range(p, min(P, p + 8)):
+            B = rng.standard_normal((6, 6)) * (10.0 ** rng.uniform(0, 4))
+            S[6 * p:6 * p + 6, 6 * q:6 * q + 6] += B
+    S = S @ S.T + np.diag(10.0 ** rng.uniform(2, 9, n))
+    b = rng.standard_normal(n) * 1e3
+    x = _ldlt_probe(S, b)
+    xr = np.linalg.solve(S, b)
+    assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
+
+
+def test_reduced_solve_zero_rows():
+    """STRATEGY1 with a fixed pose: exactly-zero rows and columns (diag 0 + lambda*0); Eigen's
+    LDLT pivots them last, skips the invalid pivots and returns 0 there (LDLT::_solve_impl)."""
+    rng = np.random.default_rng(7)
+    n = 60
+    M = rng.standard_normal((n, n))
+    S = M @ M.T + n * np.eye(n)
+    S[:6, :] = 0.0
+    S[:, :6] = 0.0
+    b = rng.standard_normal(n)
+    b[:6] = 0.0
+    x = _ldlt_probe(S, b)
+    assert np.all(x[:6] == 0.0)
+    xr = np.linalg.solve(S[6:, 6:], b[6:])
+    assert np.allclose(x[6:], xr, rtol=1e-11, atol=1e-13)
+
+
 @pytest.mark.parametrize("cfg,seed,family", [("C1", 0, "default"), ("C1", 1, "stable"), ("mini", 0, "default"),
                                               ("C2", 0, "default"), ("C2", 1, "stable")])
 def test_single_trial_parity(solver, cfg, seed, family):
@@ -77,18 +123,32 @@ def test_initial_edge_chi2_bitwise(solver, cfg, seed):
     assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-13
 
 
-@pytest.mark.parametrize("cfg,seed,family", [("C1", 0, "stable_noout"), ("C1", 1, "stable"), ("mini", 0, "stable"),
-                                              ("C2", 0, "stable_noout"), ("C2", 1, "stable"), ("C2", 2, "stable")])
-def test_full_solve_parity_stable(solver, cfg, seed, family):
-    """North-star bar on windows whose reference trajectory is reproducible."""
-    w = window(cfg, seed=seed, family=family)
-    o, spread, its = oracle_envelope(w)
-    assert spread < 1e-7, f"window not reproducible under reordering (spread {spread:.1e})"
+@pytest.mark.parametrize("cfg,seed", [("C1", 0), ("C1", 1), ("mini", 0), ("mini", 1), ("C2", 0), ("C2", 1),
+                                      ("C2", 2), ("C2", 3)])
+def test_full_solve_parity_stable(solver, cfg, seed):
+    """North-star bar (final chi2 within 1e-6) on windows whose reference trajectory is
+    reproducible: the oracle's final chi2 moves < 1e-12 across summation orders."""
+    w = window(cfg, seed=seed, family="stable_noout")
+    o, spread, its = oracle_envelope(w, threads=(1, 2, 8, 16))
+    assert spread < 1e-12, f"window not reproducible under reordering (spread {spread:.1e})"
     g = solver.solve(w)
     assert g["iterations"] in its
     assert rel(g["chi2_final"], o["chi2_final"]) < 1e-6
     assert rel(g["trace_chi2"][1], o["trace_chi2"][1]) < 1e-9      # after the first (bitwise-linearised) step
-    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-4)
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-6)
+
+
+@pytest.mark.parametrize("cfg,seed", [("C1", 1), ("mini", 0), ("C2", 1), ("C2", 2)])
+def test_full_solve_outlier_window_within_oracle_envelope(solver, cfg, seed):
+    """Windows with outliers: the Huber gate (base_edge.cpp:55) tests the sign of a rounding
+    residue on every outlier edge, so the reference itself lands in different basins under
+    summation reorders (e.g. C2 seed 1: 10 iterations for 14 of 16 thread counts, a 3-iteration
+    stall for the other two).  The GPU must match one of the oracle's own outcomes to 1e-6."""
+    w = window(cfg, seed=seed, family="stable")
+    runs = [ob.solve(w, n_threads=t) for t in range(1, 17)]
+    g = solver.solve(w)
+    assert min(rel(g["chi2_final"], r["chi2_final"]) for r in runs) < 1e-6
+    assert rel(g["trace_chi2"][1], runs[0]["trace_chi2"][1]) < 1e-9
 
 
 @pytest.mark.parametrize("cfg,seed", [("C2", 0), ("C2", 1), ("mini", 3)])
