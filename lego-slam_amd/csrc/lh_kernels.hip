@@ -692,6 +692,7 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
 
 #define RT 1024
 #define RW (RT / 64)
+#define RI_MAX 2048           // items (chunks) per pose pair staged in LDS at a time
 
 __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs, const uint32_t* __restrict__ pair_ptr,
                                                const uint32_t* __restrict__ items, const uint16_t* __restrict__ pair_pq,
@@ -729,25 +730,49 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
     const bool diag = p == q;
     const int a = lane / 6, bb = lane - 6 * (lane / 6);
     // lanes 0..35: S entry (a, bb) [+ H_pp entry on the diagonal]; 36..41: b_p; 42..47: bsd
-    int off_s = 0, off_h = 0;
+    int off_h = 0;
     if (lane < 36) off_h = LH_SLAB_TASK_OFF + (diag ? ((a < bb ? a : bb) * 6 - ((a < bb ? a : bb) * ((a < bb ? a : bb) - 1)) / 2 + ((a < bb ? bb : a) - (a < bb ? a : bb))) : 0);
     else if (lane < 42) off_h = LH_SLAB_TASK_OFF + 21 + (lane - 36);
     else if (lane < 48) off_h = LH_SLAB_TASK_OFF + 27 + (lane - 42);
     const bool act_s = lane < 36, act_h = (lane < 36 && diag) || (lane >= 36 && lane < 48 && diag);
-    double vs = 0.0, vh = 0.0;
-    const int it0 = pair_ptr[b], it1 = pair_ptr[b + 1];
-    for (int it = it0 + wave; it < it1; it += RW) {
-        const uint32_t item = items[it];
+    __shared__ uint32_t sitems[RI_MAX];
+    auto slab_off = [&](uint32_t item, int& off_s, const double*& sl) {
         const int ch = item >> 11, T = (item >> 8) & 7, sp = (item >> 4) & 15, sq = item & 15;
-        const double* sl = slabs + (size_t)ch * LH_SLAB_STRIDE;
-        if (act_s) {
-            int ra = 6 * sp + a, rc = 6 * sq + bb;
-            if ((ra >> 4) > (rc >> 4)) { const int t = ra; ra = rc; rc = t; }
-            const int R = ra >> 4, Cc = rc >> 4;
-            off_s = (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15);
-            vs += sl[off_s];
+        sl = slabs + (size_t)ch * LH_SLAB_STRIDE;
+        int ra = 6 * sp + a, rc = 6 * sq + bb;
+        if ((ra >> 4) > (rc >> 4)) { const int t = ra; ra = rc; rc = t; }
+        const int R = ra >> 4, Cc = rc >> 4;
+        off_s = act_s ? (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15) : 0;
+        return sp;
+    };
+    double vs = 0.0, vh = 0.0;
+    const int ib = pair_ptr[b], ie = pair_ptr[b + 1];
+    for (int seg = ib; seg < ie; seg += RI_MAX) {
+        // a segment of the pair's item list into LDS (one global round trip), then every wave
+        // walks its items (wave, wave + RW, ...) with four slab loads in flight
+        const int nit = min(ie - seg, RI_MAX);
+        __syncthreads();
+        for (int i = tid; i < nit; i += RT) sitems[i] = items[seg + i];
+        __syncthreads();
+        int it = wave;
+        for (; it + 3 * RW < nit; it += 4 * RW) {
+            double x[4], y[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int off_s; const double* sl;
+                const int sp = slab_off(sitems[it + u * RW], off_s, sl);
+                x[u] = act_s ? sl[off_s] : 0.0;
+                y[u] = act_h ? sl[off_h + sp * LH_TASKS] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { vs += x[u]; vh += y[u]; }
         }
-        if (act_h) vh += sl[off_h + sp * LH_TASKS];
+        for (; it < nit; it += RW) {
+            int off_s; const double* sl;
+            const int sp = slab_off(sitems[it], off_s, sl);
+            if (act_s) vs += sl[off_s];
+            if (act_h) vh += sl[off_h + sp * LH_TASKS];
+        }
     }
     part[0][wave][lane] = vs;
     part[1][wave][lane] = vh;
