@@ -336,7 +336,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const int cand = 1 - cur;
     const double lambda = ctrl->lambda;
     const int chunk = chunk_base + blockIdx.x;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loads, scalar loop
     const int ncam = prm.ncam;
     const int PT = prm.P * ncam * LH_PT;
     const int U = chunks[chunk].U;
@@ -375,22 +376,26 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     double chi_acc = 0.0, scale_acc = 0.0, maxd = 0.0, ndeg = 0.0;
     STAMP_DECL
 
-    // prefetch of the first sub-batch: observation words and the 8 landmark records
+    // prefetch of the first sub-batch: observation words and the 8 landmark records.  The
+    // prefetch is unconditional (index clamped to the chunk) so the compiler can keep it in
+    // flight with counted vmcnt waits across the iteration.
+    const int sb_last = (int)sb_end - 1;
     int sb = (int)sb_begin + wave;
-    uint32_t meta_n = 0u;
-    double u_n = 0.0, v_n = 0.0;
-    double2 r_n = double2{0.0, 0.0};
-    if (sb < (int)sb_end) {
-        const int o = sb * 64 + lane;
+    uint32_t meta_n;
+    double u_n, v_n;
+    double2 r_n;
+    {
+        const int sbc = min(sb, sb_last);
+        const int o = sbc * 64 + lane;
         meta_n = obs_meta[o];
         u_n = obs_uv[2 * (size_t)o];
         v_n = obs_uv[2 * (size_t)o + 1];
-        r_n = rc2[(size_t)sb * 64 + lane];
+        r_n = rc2[(size_t)sbc * 64 + lane];
     }
     __syncthreads();   // window tables
 
     for (; sb < (int)sb_end; sb += LH_WAVES) {
-        const lh_subbatch S = sbs[sb];
+        const lh_subbatch S = sbs[sb];   // scalar load (sb is wave-uniform)
         const int lg = S.lg, nlm = S.n_lm;
         const int ls = lane >> lg, gj = lane & ((1 << lg) - 1);
         const bool lmok = ls < nlm;
@@ -400,14 +405,12 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         const double2 rr = r_n;
         const int o = sb * 64 + lane;
         {
-            const int sbn = sb + LH_WAVES;
-            if (sbn < (int)sb_end) {
-                const int on = sbn * 64 + lane;
-                meta_n = obs_meta[on];
-                u_n = obs_uv[2 * (size_t)on];
-                v_n = obs_uv[2 * (size_t)on + 1];
-                r_n = rc2[(size_t)sbn * 64 + lane];
-            }
+            const int sbn = min(sb + LH_WAVES, sb_last);
+            const int on = sbn * 64 + lane;
+            meta_n = obs_meta[on];
+            u_n = obs_uv[2 * (size_t)on];
+            v_n = obs_uv[2 * (size_t)on + 1];
+            r_n = rc2[(size_t)sbn * 64 + lane];
         }
         // landmark records through LDS: lane -> its landmark's record
         reinterpret_cast<double2*>(scr)[lane] = rr;
