@@ -315,9 +315,28 @@ struct LinCfg {
     static constexpr int UMAX = (16 * T) / 6;           // window poses that fit 16T rows
 };
 
-// butterfly sum over the aligned lane group of G = 1 << lg lanes (every lane gets the total)
+// butterfly sum over the aligned lane group of G = 1 << lg lanes (every lane gets the total):
+// v + v[lane^1], + [lane^2], + [lane^4], ... in that order.  Partners within a 16-lane row come
+// through DPP (plain VALU: quad_perm for ^1 and ^2, row rotations for ^4 and ^8); ^16 and ^32
+// through ds_bpermute.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ double group_sum(double v, int lg) {
-    for (int off = 1; off < (1 << lg); off <<= 1) v += __shfl_xor(v, off);
+    if (lg >= 1) v += dpp_d<0xB1>(v);                       // quad_perm [1,0,3,2]: lane ^ 1
+    if (lg >= 2) v += dpp_d<0x4E>(v);                       // quad_perm [2,3,0,1]: lane ^ 2
+    if (lg >= 3) {                                          // lane ^ 4: row_ror 12 / row_ror 4
+        const double a = dpp_d<0x12C>(v), b = dpp_d<0x124>(v);
+        v += (__lane_id() & 4) ? b : a;
+    }
+    if (lg >= 4) v += dpp_d<0x128>(v);                      // row_ror 8: lane ^ 8
+    if (lg >= 5) v += __shfl_xor(v, 16);
+    if (lg >= 6) v += __shfl_xor(v, 32);
     return v;
 }
 
