@@ -21,7 +21,6 @@
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-#define SCR_SZ 2112                  // per-wave scratch: max(64*33, 24*80) doubles
 
 // Diagnostic build (-DLH_STAMPS): per-phase wave-cycle totals via s_memtime,
 // summed over all waves into lh_stamps[] (cdna_hip_programming.md §7 "In-kernel
@@ -308,11 +307,23 @@ __device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, co
 // k_lin: one workgroup (4 waves) per landmark chunk; one sub-batch (<= 8
 // landmarks, <= 64 observations, one observation per lane) per wave at a time.
 // ============================================================================
+// 1/d with one v_rcp_f64 and two Newton steps (the LDLT pivots and the H_ll Cholesky are not a bitwise-mirrored path)
+__device__ __forceinline__ double fast_rcp(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return r;
+}
+
 template <int T>
 struct LinCfg {
     static constexpr int NT = T * (T + 1) / 2;          // upper MFMA tiles of the window
     static constexpr int GS = (T == 1) ? 16 : (T == 4 ? 80 : 48);  // G row stride: 16T + pad, conflict-free b64 frag loads
     static constexpr int UMAX = (16 * T) / 6;           // window poses that fit 16T rows
+    // per-wave LDS scratch: pose-sum image [slot][landmark][33], G image [24][GS], the record
+    // stage (128), and (over the 4 waves) the two combine slabs
+    static constexpr int A_ = UMAX * LH_SB_LM * LH_TASKS, B_ = 3 * LH_SB_LM * GS, C_ = (2 * LH_SLAB_STRIDE + 3) / 4;
+    static constexpr int SCR = ((A_ > B_ ? (A_ > C_ ? A_ : C_) : (B_ > C_ ? B_ : C_)) + 1) & ~1;
 };
 
 // butterfly sum over the aligned lane group of G = 1 << lg lanes (every lane gets the total):
@@ -363,10 +374,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const uint32_t sb_begin = chunks[chunk].sb_begin, sb_end = chunks[chunk].sb_end;
     const uint16_t* __restrict__ cpose = chunks[chunk].pose;
 
-    double* scr = dsm + wave * SCR_SZ;
+    double* scr = dsm + wave * Cfg::SCR;
     // the chunk's window, LDS-resident: committed and candidate pose tables per (slot, camera),
     // the pending pose step per slot, the camera extrinsics
-    double* wt_c = dsm + LH_WAVES * SCR_SZ;
+    double* wt_c = dsm + LH_WAVES * Cfg::SCR;
     double* wt_n = wt_c + LH_UMAX * ncam * LH_PT;
     double* wdx = wt_n + LH_UMAX * ncam * LH_PT;
     double* wext = wdx + LH_UMAX * 6;
@@ -471,7 +482,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (lmok) {
                 const double l00 = cl[0], l10 = cl[1], l11 = cl[2], l20 = cl[3], l21 = cl[4], l22 = cl[5];
                 const double b0 = cl[6], b1 = cl[7], b2 = cl[8];
-                const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+                const double i00 = fast_rcp(l00), i11 = fast_rcp(l11), i22 = fast_rcp(l22);
                 const double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
                 const double y0 = t0 * i00, y1 = (t1 - l10 * y0) * i11, y2 = (t2 - l20 * y0 - l21 * y1) * i22;
                 double d2 = y2 * i22, d1 = (y1 - l21 * d2) * i11, d0 = (y0 - l10 * d1 - l20 * d2) * i00;
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         double hpl[18];
 #pragma unroll
         for (int i = 0; i < 18; ++i) hpl[i] = 0.0;
-        double* trow = scr + LH_TASKS * lane;
+        double* trow = scr + (slot * LH_SB_LM + (ls & 7)) * LH_TASKS;   // [slot][landmark][33]: unique writer
         if (has) {
             const double* pt = wt_n + (slot * ncam + cam) * LH_PT;
             EdgeEval E;
@@ -548,13 +559,13 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 #pragma unroll
         for (int i = 0; i < 3; ++i) h[6 + i] = group_sum(bl[i], lg);
         double l00 = sqrt(h[0]);
-        double i00 = 1.0 / l00;
+        double i00 = fast_rcp(l00);
         double l10 = h[1] * i00, l20 = h[2] * i00;
         const double a11 = h[3] - l10 * l10;
-        const double l11 = sqrt(a11), i11 = 1.0 / l11;
+        const double l11 = sqrt(a11), i11 = fast_rcp(l11);
         const double l21 = (h[4] - l20 * l10) * i11;
         const double a22 = h[5] - l20 * l20 - l21 * l21;
-        const double l22 = sqrt(a22), i22 = 1.0 / l22;
+        const double l22 = sqrt(a22), i22 = fast_rcp(l22);
         const bool pd = (h[0] > 0.0) && (a11 > 0.0) && (a22 > 0.0) && isfinite(l22) && isfinite(l21);
         if (!pd) { l00 = __builtin_nan(""); i00 = __builtin_nan(""); }   // poisons the step, like a singular LU inverse (problem.cpp:399)
         const double w0 = h[6] * i00, w1 = (h[7] - l10 * w0) * i11, w2 = (h[8] - l20 * w0 - l21 * w1) * i22;
@@ -592,28 +603,26 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         }
         STAMP(3);
 
-        // ---- per-pose sums (H_pp, b_p, bsd): lanes 0..32 walk each pose's observations in lane order ----
+        // ---- per-pose sums (H_pp, b_p, bsd): lane k < 33 adds task k of every landmark observing
+        //      the slot, in landmark (= lane) order ----
         wave_sync();
+        {
+            const int G = 1 << lg;
+            const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
 #pragma unroll
-        for (int uu = 0; uu < Cfg::UMAX; ++uu) {
-            if (uu < U) {
-                uint64_t mk = __ballot(live && slot == uu);
-                if (lane < LH_TASKS) {
-                    double sacc = task[uu];
-                    while (mk) {
-                        const int i0 = __builtin_ctzll(mk);
-                        mk &= mk - 1;
-                        if (mk) {
-                            const int i1 = __builtin_ctzll(mk);
-                            mk &= mk - 1;
-                            const double a0 = scr[LH_TASKS * i0 + lane], a1 = scr[LH_TASKS * i1 + lane];
-                            sacc += a0;
-                            sacc += a1;
-                        } else {
-                            sacc += scr[LH_TASKS * i0 + lane];
-                        }
+            for (int uu = 0; uu < Cfg::UMAX; ++uu) {
+                if (uu < U) {
+                    const uint64_t mk = __ballot(live && slot == uu);
+                    if (mk && lane < LH_TASKS) {
+                        double tv[LH_SB_LM];
+#pragma unroll
+                        for (int l = 0; l < LH_SB_LM; ++l) tv[l] = scr[(uu * LH_SB_LM + l) * LH_TASKS + lane];
+                        double sacc = task[uu];
+#pragma unroll
+                        for (int l = 0; l < LH_SB_LM; ++l)
+                            if (l < nlm && ((mk >> (l << lg)) & gmask)) sacc += tv[l];
+                        task[uu] = sacc;
                     }
-                    task[uu] = sacc;
                 }
             }
         }
@@ -841,13 +850,6 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 #define RS_MAX (LH_PMAX * (LH_PMAX + 1) / 2 * 36 + 18 * LH_PMAX + 8)
 #define NLD ((RS_MAX + CT - 1) / CT)
 
-// 1/d with one v_rcp_f64 and two Newton steps (the LDLT pivots are not a bitwise-mirrored path)
-__device__ __forceinline__ double fast_rcp(double d) {
-    double r = __builtin_amdgcn_rcp(d);
-    r = fma(r, fma(-d, r, 1.0), r);
-    r = fma(r, fma(-d, r, 1.0), r);
-    return r;
-}
 
 #define TRI8(r, c) ((r) * ((r) - 1) / 2 + (c))   // packed strictly-lower 8x8 index, r > c
 
@@ -1342,8 +1344,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 // ============================================================================
 extern "C" {
 
-size_t lh_lin_smem_bytes(int ncam) {
-    return sizeof(double) * ((size_t)LH_WAVES * SCR_SZ + 2 * (size_t)LH_UMAX * ncam * LH_PT + LH_UMAX * 6 + (size_t)ncam * LH_EXT);
+static size_t lin_smem_bytes(int scr, int ncam) {
+    return sizeof(double) * ((size_t)LH_WAVES * scr + 2 * (size_t)LH_UMAX * ncam * LH_PT + LH_UMAX * 6 + (size_t)ncam * LH_EXT);
 }
 
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
@@ -1351,7 +1353,6 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* slabs, lh_params prm, int nrec, uint32_t fixed_mask) {
     if (nchunks <= 0) return hipSuccess;
-    const size_t smem = lh_lin_smem_bytes(prm.ncam);
     dim3 g(nchunks), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
@@ -1362,6 +1363,7 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
             if (e_ != hipSuccess) return e_;                                                                       \
             attr_set = true;                                                                                       \
         }                                                                                                          \
+        const size_t smem = lin_smem_bytes(LinCfg<TT>::SCR, prm.ncam);                                 \
         hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
                            edge_rho, slabs, prm, nrec, fixed_mask, chunk_base);                                    \
     } while (0)
