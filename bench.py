@@ -28,26 +28,36 @@ import numpy as np  # noqa: E402
 
 import lego_ba  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
-FP64_PEAK_TFS = 78.6       # MI355X FP64 vector = matrix (spec)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFS = 78.6       # MI355X FP64 spec (vector = matrix); measured on the box:
+                           # v_mfma_f64_16x16x4 72.0 TF, v_fma_f64 60.5 TF (lego-slam_amd/tools/ubench_fp64_peak.hip)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_k_lin.json")
 
 
-def lin_algorithmic_bytes(n_obs, n_lm, n_chunks_slab_bytes):
-    """Compulsory HBM bytes of one k_lin launch (DESIGN.md "k_lin roofline"):
-    per observation uv (16 B) + meta (4 B) + rho0 write (8 B); per landmark
-    X read/write (48 B) + H_ll cache read/write (192 B) + CSR (4 B); plus the
-    chunk slabs written."""
-    return 28 * n_obs + 244 * n_lm + n_chunks_slab_bytes
+def survey_bytes_per_iteration(n_obs, n_lm):
+    """SURVEY.md 8(d) compulsory HBM bytes of one LM iteration (one k_lin launch fuses the
+    three passes: linearise + Schur, back-substitute, chi2-evaluate):
+    B = 3 (12 O + 28 L) + 24 L."""
+    return 3 * (12 * n_obs + 28 * n_lm) + 24 * n_lm
 
 
-def lin_algorithmic_flops(n_obs, k):
-    """fp64 flops of one k_lin TRIAL launch on a window with k observations per
-    landmark: back-substitution ~150/obs, evaluation + linearisation ~330/obs,
-    per-landmark Cholesky / solves ~60/k per obs, Schur pair blocks
-    108 * k(k+1)/2 MAC per landmark."""
-    per_obs = 150 + 330 + 60.0 / k
-    schur = 2 * 108 * k * (k + 1) / 2 / k
-    return n_obs * (per_obs + schur)
+def survey_flops_per_iteration(n_obs, n_lm, k):
+    """SURVEY.md 8(d) fp64 flops of one LM iteration: 400 O (projection, Jacobians, J^T W J,
+    H_pl H_ll^-1) + 216 sum_l k(k+1)/2 (Schur pair blocks) + 50 L (3x3 inverse) + 80 O
+    (back-substitution + chi2); the 6P x 6P solve (k_ctrl) is excluded."""
+    return 400 * n_obs + 216 * n_lm * k * (k + 1) / 2 + 50 * n_lm + 80 * n_obs
+
+
+def pmc_traffic(cfg_key):
+    """HBM bytes per k_lin launch from the committed rocprofv3 PMC passes (scripts/gpu_pmc.sh ->
+    scripts/pmc_traffic.py): 2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE,
+    or None when no pass for this workload is committed."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return d.get("bytes_per_launch") if d.get("workload") == cfg_key else None
 
 
 def main():
@@ -62,6 +72,7 @@ def main():
     ap.add_argument("--family", default="stable_noout", choices=["stable_noout", "stable", "default"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the cpu_baseline sample")
     ap.add_argument("--trials-per-sync", type=int, default=0)
     args = ap.parse_args()
 
@@ -145,12 +156,12 @@ def main():
     n_obs, n_lm = len(w["obs_pose"]), len(w["lm_xyz"])
     lin_n, lin_ms = ks.get("k_lin", (0, 0.0))
     lin_avg_ms = lin_ms / max(lin_n, 1)
-    n_chunks_est = max(1, (n_lm + 103) // 104)
-    slab_bytes = n_chunks_est * (6 * 256 + 8 * 33 + 4) * 8
-    bytes_per = lin_algorithmic_bytes(n_obs, n_lm, slab_bytes)
-    flops_per = lin_algorithmic_flops(n_obs, args.k)
-    achieved_gbs = bytes_per / (lin_avg_ms * 1e-3) / 1e9 if lin_avg_ms > 0 else 0.0
+    flops_per = survey_flops_per_iteration(n_obs, n_lm, args.k)
+    bytes_per = survey_bytes_per_iteration(n_obs, n_lm)
     achieved_tfs = flops_per / (lin_avg_ms * 1e-3) / 1e12 if lin_avg_ms > 0 else 0.0
+    achieved_gbs = bytes_per / (lin_avg_ms * 1e-3) / 1e9 if lin_avg_ms > 0 else 0.0
+    cfg_key = f"P{args.poses}-L{L}-k{args.k}-{args.family}-s{args.seed}"
+    traffic = pmc_traffic(cfg_key)
 
     out = {
         "metric": "LM iterations/sec + ms/solve, 20KF/50k-pts/400k-obs window; final chi2 vs ref",
@@ -174,22 +185,42 @@ def main():
         "trials_per_solve": trials / args.steps,
         "chi2_final": last["chi2_final"],
         "kernels_ms_per_solve": {k: round(v[1] / args.steps, 4) for k, v in ks.items()},
-        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_lin", "avg_launch_ms": round(lin_avg_ms, 5), "bytes_per_launch": bytes_per},
-        "roofline_fp64": {"achieved": round(achieved_tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                          "frac": round(achieved_tfs / FP64_PEAK_TFS, 4), "flops_per_launch": flops_per},
+        # dominant kernel k_lin (one launch = one LM iteration's linearise/back-substitute/chi2 pass);
+        # the path is FP64-bound (~29 flop/B > ridge 9.8 flop/B)
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": round(achieved_tfs / FP64_PEAK_TFS, 4), "traffic": traffic,
+                     "kernel": "k_lin", "avg_launch_ms": round(lin_avg_ms, 5), "flops_per_launch": flops_per,
+                     "peak_note": "FP64 spec (vector = matrix); measured here 72.0 TF MFMA, 60.5 TF VALU"},
+        "roofline_hbm": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": bytes_per,
+                         "traffic": traffic},
     }
+    # end-to-end host-buffer call (lh_solve: upload + solve + download over PCIe), rank 0 only
+    if world == 1:
+        solver_h = lego_ba.Solver(device=local)
+        solver_h.solve(w)
+        t = time.perf_counter()
+        solver_h.solve(w)
+        out["ms_per_solve_host_buffers"] = round((time.perf_counter() - t) * 1e3, 3)
+        solver_h.close()
     if world == 1 and not args.no_cpu:
         import oracle_bind
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        # bounded sample: repeated full solves of the same window for >= cpu_seconds of CPU work
         t = time.perf_counter()
-        o = oracle_bind.solve(w, n_threads=threads)
-        ct = time.perf_counter() - t
-        out["cpu_baseline"] = {"value": round(o["iterations"] / ct, 4), "unit": "LM iterations/s",
+        its = nsolve = 0
+        while True:
+            o = oracle_bind.solve(w, n_threads=threads)
+            its += o["iterations"]
+            nsolve += 1
+            ct = time.perf_counter() - t
+            if ct >= args.cpu_seconds:
+                break
+        out["cpu_baseline"] = {"value": round(its / ct, 4), "unit": "LM iterations/s",
                                "cores": threads, "kind": "port",
-                               "sample": "one full solve(10) of the same window by the block-sparse oracle "
-                                         f"(oracle/lego_oracle.c ref_sparse), {ct:.2f} s, {o['iterations']} iterations"}
+                               "sample": f"{nsolve} full solve(10)s of the same window by the block-sparse oracle "
+                                         f"(oracle/lego_oracle.c ref_sparse, OpenMP {threads} threads), {ct:.1f} s, "
+                                         f"{its} iterations"}
         out["chi2_rel_vs_oracle"] = abs(last["chi2_final"] - o["chi2_final"]) / o["chi2_final"]
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
     print(json.dumps(out))

@@ -191,7 +191,9 @@ struct lh_handle {
     int* d_done = nullptr;       // device alias of h_done
 
     // profiling
-    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    struct PendingEv { int kc; int trial; hipEvent_t a, b; };
+    std::vector<PendingEv> pending;   // profiled launches of the current solve
+    int cur_trial = 0;                 // trial index being enqueued (0 = initial linearisation)
     std::vector<hipEvent_t> event_pool;
     size_t event_next = 0;
     int64_t launches[KC_N] = {0};
@@ -243,17 +245,20 @@ struct Prof {
     ~Prof() {
         if (a && b) {
             (void)hipEventRecord(b, h->stream);
-            h->pending.push_back({kc, {a, b}});
+            h->pending.push_back({kc, h->cur_trial, a, b});
         }
     }
 };
 
-void collect_profile(lh_handle* h) {
+// Launches enqueued for trials past the device's stop (trial > trials_run) exit at their first
+// instruction; they are not counted as kernel work.
+void collect_profile(lh_handle* h, int trials_run) {
     for (auto& pe : h->pending) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, pe.second.first, pe.second.second) == hipSuccess) {
-            h->launches[pe.first] += 1;
-            h->total_ms[pe.first] += ms;
+        if (pe.trial > trials_run) continue;
+        if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            h->launches[pe.kc] += 1;
+            h->total_ms[pe.kc] += ms;
         }
     }
     h->pending.clear();
@@ -572,6 +577,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
 
 int enqueue_trial(lh_handle* h, int mode) {
     hipStream_t s = h->stream;
+    h->cur_trial = (mode == 0) ? 0 : h->cur_trial + 1;
     {
         Prof pr(h, mode == 0 ? KC_INIT : KC_LIN);
         for (int T = 1; T <= LH_TMAX; ++T) {
@@ -689,7 +695,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
             printf("Iteration = %d,\tChi = %g,\tLambda = %g\n", i, c.trace_chi[i], c.trace_lambda[i]);
         printf("\nInfo: \nTimeCost(SolveProblem) = %g ms\n", (double)ms);
     }
-    if (h->opt.profile) collect_profile(h);
+    if (h->opt.profile) collect_profile(h, c.trials);
     else h->event_next = 0;
     return LH_OK;
 }
@@ -771,9 +777,17 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
         lh_destroy(h);
         return LH_E_HIP;
     }
-    if (opt->world_size > 1) {
+    // LH_FORCE_RCCL=1 builds a one-rank communicator on a single GPU, so the data-path
+    // collectives (and their stream ordering) run in single-GPU tests too
+    const char* force = std::getenv("LH_FORCE_RCCL");
+    const bool force_comm = opt->world_size == 1 && force && force[0] == '1';
+    if (opt->world_size > 1 || force_comm) {
         ncclUniqueId id;
-        std::memcpy(&id, opt->comm_id, sizeof(id));
+        if (force_comm) {
+            if (ncclGetUniqueId(&id) != ncclSuccess) { lh_destroy(h); return LH_E_RCCL; }
+        } else {
+            std::memcpy(&id, opt->comm_id, sizeof(id));
+        }
         if (ncclCommInitRank(&h->comm, opt->world_size, id, opt->rank) != ncclSuccess) {
             h->comm = nullptr;
             lh_destroy(h);

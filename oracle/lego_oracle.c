@@ -325,6 +325,8 @@ typedef struct {
     int64_t *lm_ptr, *lm_edges;
     int64_t n;
     double chi, lambda, ni;
+    /* orc_reduced_system: capture the undamped reduced system instead of solving */
+    double *S_out, *bs_out;
 } prob_t;
 
 /* ---- EdgeProjection arithmetic (include/legoslam/lego_types.h:200-254) ---- */
@@ -654,6 +656,12 @@ static void solve_sparse(prob_t *pb) {
         for (int64_t j = 0; j < np; ++j)
             if (i / 6 != j / 6) S[i * np + j] = -S[i * np + j];
     for (int64_t i = 0; i < np; ++i) bs[i] = pb->bp[i] - bs[i];
+    if (pb->S_out) {   /* orc_reduced_system */
+        memcpy(pb->S_out, S, sizeof(double) * (size_t)(np * np));
+        memcpy(pb->bs_out, bs, sizeof(double) * (size_t)np);
+        free(S); free(bs); free(Hinv);
+        return;
+    }
     for (int64_t i = 0; i < np; ++i) {
         if (pb->opt.strategy == 0) S[i * np + i] += pb->lambda;
         else S[i * np + i] += pb->lambda * S[i * np + i];
@@ -821,11 +829,12 @@ double orc_now_ms(void);
  * Returns 0 on success, 1 for an empty problem (problem.cpp:157-161),
  * 2 for bad arguments.
  */
-int orc_solve(int variant, int32_t P, const double *pose_in, const uint8_t *fixed,
-              int32_t L, const double *lm_in, int64_t O, const uint32_t *op, const uint32_t *ol,
-              const uint8_t *oc, const double *uv, const double *K, int32_t ncam, const double *cam_ext,
-              const orc_options *opt, double *pose_out, double *lm_out, double *edge_rchi2,
-              double *trace_chi, double *trace_lambda, int32_t trace_cap, orc_stats *st) {
+static int orc_run(int variant, int32_t P, const double *pose_in, const uint8_t *fixed,
+                   int32_t L, const double *lm_in, int64_t O, const uint32_t *op, const uint32_t *ol,
+                   const uint8_t *oc, const double *uv, const double *K, int32_t ncam, const double *cam_ext,
+                   const orc_options *opt, double *pose_out, double *lm_out, double *edge_rchi2,
+                   double *trace_chi, double *trace_lambda, int32_t trace_cap, orc_stats *st,
+                   double *S_out, double *bs_out, double *chi2_out) {
     memset(st, 0, sizeof(*st));
     if (P < 0 || L < 0 || O < 0) return 2;
     if (O == 0 || (P + L) == 0) return 1;
@@ -876,6 +885,18 @@ int orc_solve(int variant, int32_t P, const double *pose_in, const uint8_t *fixe
     }
 
     /* ---- Problem::solve (problem.cpp:156-230) ---- */
+    if (S_out) {   /* orc_reduced_system: linearise at the input state, reduce, stop */
+        pb.S_out = S_out;
+        pb.bs_out = bs_out;
+        build_hessian(&pb);
+        *chi2_out = sum_rchi2(&pb, 0);   /* sum of rho0 (not halved) */
+        solve_linear(&pb);
+        free(pb.ext); free(pb.pose); free(pb.pose_bak); free(pb.lm); free(pb.lm_bak);
+        free(pb.res); free(pb.dx); free(pb.b); free(pb.hdiag);
+        free(pb.H); free(pb.Hpp); free(pb.bp); free(pb.Hll); free(pb.bl); free(pb.Hpl);
+        free(pb.lm_ptr); free(pb.lm_edges);
+        return 0;
+    }
     if (pb.opt.verbose) printf("==========LEGO OPTIMIZER==========\n");
     build_hessian(&pb);
     lambda_init(&pb);
@@ -922,6 +943,32 @@ int orc_solve(int variant, int32_t P, const double *pose_in, const uint8_t *fixe
     free(pb.H); free(pb.Hpp); free(pb.bp); free(pb.Hll); free(pb.bl); free(pb.Hpl);
     free(pb.lm_ptr); free(pb.lm_edges);
     return 0;
+}
+
+int orc_solve(int variant, int32_t P, const double *pose_in, const uint8_t *fixed,
+              int32_t L, const double *lm_in, int64_t O, const uint32_t *op, const uint32_t *ol,
+              const uint8_t *oc, const double *uv, const double *K, int32_t ncam, const double *cam_ext,
+              const orc_options *opt, double *pose_out, double *lm_out, double *edge_rchi2,
+              double *trace_chi, double *trace_lambda, int32_t trace_cap, orc_stats *st) {
+    return orc_run(variant, P, pose_in, fixed, L, lm_in, O, op, ol, oc, uv, K, ncam, cam_ext, opt, pose_out, lm_out,
+                   edge_rchi2, trace_chi, trace_lambda, trace_cap, st, NULL, NULL, NULL);
+}
+
+/*
+ * orc_reduced_system — the undamped reduced pose system of one window at its input state:
+ * S = H_pp - H_pl H_ll^-1 H_lp (6P x 6P, row-major, full), bs = b_p - H_pl H_ll^-1 b_l
+ * (problem.cpp:382-405 without the lambda of :406-418), chi2 = sum rho0.  Landmark shards
+ * contribute additively: the sum over shards equals the full window (the multi-GPU path's
+ * one all-reduce).  Block-sparse variant only.
+ */
+int orc_reduced_system(int32_t P, const double *pose_in, const uint8_t *fixed, int32_t L, const double *lm_in,
+                       int64_t O, const uint32_t *op, const uint32_t *ol, const uint8_t *oc, const double *uv,
+                       const double *K, int32_t ncam, const double *cam_ext, const orc_options *opt,
+                       double *S_out, double *bs_out, double *chi2_out) {
+    orc_stats st;
+    if (!S_out || !bs_out || !chi2_out) return 2;
+    return orc_run(1, P, pose_in, fixed, L, lm_in, O, op, ol, oc, uv, K, ncam, cam_ext, opt, NULL, NULL, NULL,
+                   NULL, NULL, 0, &st, S_out, bs_out, chi2_out);
 }
 
 #include <time.h>

@@ -46,6 +46,9 @@ def lib():
                                 C.c_int32, vp, C.POINTER(OrcOptions), vp, vp, vp, vp, vp, C.c_int32,
                                 C.POINTER(OrcStats)]
         L.orc_solve.restype = C.c_int
+        L.orc_reduced_system.argtypes = [C.c_int32, vp, vp, C.c_int32, vp, C.c_int64, vp, vp, vp, vp, vp,
+                                         C.c_int32, vp, C.POINTER(OrcOptions), vp, vp, vp]
+        L.orc_reduced_system.restype = C.c_int
         L.orc_se3_exp.argtypes = [vp, vp]
         L.orc_se3_left_update.argtypes = [vp, vp, vp]
         L.orc_huber.argtypes = [C.c_double, C.c_double, vp]
@@ -88,6 +91,39 @@ def solve(w, variant=1, trace_cap=64, **opt):
     for f in ("chi2_initial", "chi2_final", "lambda_final", "time_ms", "iterations", "trials", "accepted"):
         out[f] = getattr(st, f)
     return out
+
+
+def reduced_system(w, **opt):
+    """Undamped reduced pose system (S, bs) and sum rho0 of window `w` at its input state
+    (oracle/lego_oracle.c orc_reduced_system)."""
+    a = lambda k, dt: None if w.get(k) is None else np.ascontiguousarray(w[k], dtype=dt)
+    pose, lm = a("pose_Tcw", np.float64), a("lm_xyz", np.float64)
+    op, ol, oc, uv = a("obs_pose", np.uint32), a("obs_lm", np.uint32), a("obs_cam", np.uint8), a("obs_uv", np.float64)
+    fixed, ext = a("pose_fixed", np.uint8), a("cam_ext", np.float64)
+    K = np.ascontiguousarray(w["K"], np.float64)
+    P, L, O = pose.shape[0], lm.shape[0], op.shape[0]
+    S = np.zeros((6 * P, 6 * P))
+    bs = np.zeros(6 * P)
+    chi2 = C.c_double(0.0)
+    o = options(**opt)
+    rc = lib().orc_reduced_system(P, _p(pose), _p(fixed), L, _p(lm), O, _p(op), _p(ol), _p(oc), _p(uv), _p(K),
+                                  0 if ext is None else ext.shape[0], _p(ext), C.byref(o), _p(S), _p(bs),
+                                  C.byref(chi2))
+    assert rc == 0, rc
+    return S, bs, chi2.value
+
+
+def landmark_shard(w, l0, l1):
+    """The sub-window of landmarks [l0, l1) and their observations (poses replicated), the
+    unit one GPU owns in the landmark-sharded multi-GPU path."""
+    keep = (w["obs_lm"] >= l0) & (w["obs_lm"] < l1)
+    s = dict(w)
+    s["lm_xyz"] = w["lm_xyz"][l0:l1]
+    s["obs_lm"] = (w["obs_lm"][keep] - l0).astype(np.uint32)
+    for k in ("obs_pose", "obs_cam", "obs_uv"):
+        if w.get(k) is not None:
+            s[k] = w[k][keep]
+    return s
 
 
 def se3_exp(a):

@@ -264,3 +264,15 @@ def test_c3_window_parity_and_properties():
     assert np.all(np.isfinite(g["lm_xyz"])) and np.all(np.isfinite(g["pose_Tcw"]))
     R = g["pose_Tcw"].reshape(-1, 3, 4)[:, :, :3]
     assert np.allclose(R @ R.transpose(0, 2, 1), np.eye(3), atol=1e-12)
+
+
+def test_rccl_data_path_one_rank(monkeypatch):
+    """The multi-GPU data path (an RCCL all-reduce of the packed reduced system per trial, a MAX
+    all-reduce of max|H_ll diag| at the initial linearisation) on a one-rank communicator: the
+    collectives, their buffers and stream order run, and the result is bit-identical."""
+    w = window("C2", seed=0, family="stable_noout")
+    a = lego_ba.Solver().solve(w)
+    monkeypatch.setenv("LH_FORCE_RCCL", "1")
+    b = lego_ba.Solver().solve(w)
+    assert a["chi2_final"] == b["chi2_final"] and a["iterations"] == b["iterations"]
+    assert np.array_equal(a["pose_Tcw"], b["pose_Tcw"]) and np.array_equal(a["lm_xyz"], b["lm_xyz"])

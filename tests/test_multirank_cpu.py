@@ -1,0 +1,85 @@
+"""The N>1 path on CPU (gloo, world_size 2): landmark shards, one all-reduce.
+
+The multi-GPU solver shards landmarks across ranks, replicates poses, and
+all-reduces the packed reduced pose system (S, bs, chi2 and gain-scale partials) once per LM
+trial; every rank then runs the same deterministic solve.  This is correct iff the Schur
+reduction is additive over landmark shards.  Here two gloo ranks each reduce their shard with
+the oracle (oracle/lego_oracle.c orc_reduced_system), all-reduce, and must reproduce the
+full-window system; and the sharded window generator (bench.py's per-rank input) must hand
+each rank exactly its slice of the global window.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import lego_ba
+import oracle_bind as ob
+from windows import window
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, cfg, seed, family, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = window(cfg, seed=seed, family=family)
+        L = len(w["lm_xyz"])
+        l0, l1 = rank * L // world, (rank + 1) * L // world
+        S, bs, chi2 = ob.reduced_system(ob.landmark_shard(w, l0, l1), n_threads=1)
+        buf = torch.from_numpy(np.concatenate([S.ravel(), bs, [chi2]]))
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            q.put(buf.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg,seed,family", [("C1", 0, "default"), ("mini", 1, "stable")])
+def test_landmark_shards_allreduce_to_full_reduced_system(cfg, seed, family):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, cfg, seed, family, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    w = window(cfg, seed=seed, family=family)
+    S, bs, chi2 = ob.reduced_system(w, n_threads=1)
+    n = S.shape[0]
+    Sg, bsg, chi2g = got[:n * n].reshape(n, n), got[n * n:n * n + n], got[-1]
+    scale = np.abs(S).max()
+    assert np.abs(Sg - S).max() <= 1e-12 * scale
+    assert np.abs(bsg - bs).max() <= 1e-12 * np.abs(bs).max()
+    assert abs(chi2g - chi2) <= 1e-12 * chi2
+
+
+def test_sharded_window_generation_matches_global_window():
+    """bench.py generates each rank's shard directly (lm_begin/lm_end): it must equal the
+    global window restricted to that landmark range, poses identical on every rank."""
+    P, L, k, seed = 10, 3000, 8, 5
+    full = lego_ba.generate_window(P=P, L=L, k=k, seed=seed)
+    for r in range(3):
+        l0, l1 = r * L // 3, (r + 1) * L // 3
+        part = lego_ba.generate_window(P=P, L=L, k=k, seed=seed, lm_begin=l0, lm_end=l1)
+        ref = ob.landmark_shard(full, l0, l1)
+        assert np.array_equal(part["pose_Tcw"], full["pose_Tcw"])
+        assert np.array_equal(part["lm_xyz"], ref["lm_xyz"])
+        order_p = np.lexsort((part["obs_pose"], part["obs_lm"]))
+        order_r = np.lexsort((ref["obs_pose"], ref["obs_lm"]))
+        for key in ("obs_pose", "obs_lm", "obs_uv"):
+            assert np.array_equal(np.asarray(part[key])[order_p], np.asarray(ref[key])[order_r]), key
