@@ -999,58 +999,43 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     }
 
     // ---------------- 4. z /= D (Eigen tolerance), back substitution L^T x = z ----------------
+    // One wave; the right-hand side lives in LDS (xsol), block rows are read as broadcasts:
+    // no readlane chains (2.4x faster than a register-resident rhs, tools/ubench_backsub.hip).
     if (wave == 0) {
         const double tol = 2.2250738585072014e-308;   // LDLT::_solve_impl: (numeric_limits::min)()
-        const int r0 = lane, r1 = lane + 64;
-        double t0 = 0.0, t1 = 0.0;
-        if (r0 < NE) { const double d = A[r0 * AS + r0]; t0 = fabs(d) > tol ? A[NP * AS + r0] : 0.0; }
-        if (r1 < NE) { const double d = A[r1 * AS + r1]; t1 = fabs(d) > tol ? A[NP * AS + r1] : 0.0; }
-        // the L columns of the rows above block kb (independent of the solution), one block ahead
-        double c0[8], c1[8];
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            c0[v] = A[(NE - 8 + v) * AS + r0];
-            c1[v] = A[(NE - 8 + v) * AS + (r1 & (NP - 1))];
-        }
+        const int r0 = lane, r1 = lane + 64, r1m = r1 & (NP - 1);
+        if (r0 < NE) { const double d = A[r0 * AS + r0]; xsol[r0] = fabs(d) > tol ? A[NP * AS + r0] : 0.0; }
+        if (r1 < NE) { const double d = A[r1 * AS + r1]; xsol[r1] = fabs(d) > tol ? A[NP * AS + r1] : 0.0; }
+        wave_sync();
         for (int kb = NE - 8; kb >= 0; kb -= 8) {
-            double Lb[28];
+            double Lb[28], x[8], c0[8], c1[8];
 #pragma unroll
             for (int w2 = 1; w2 < 8; ++w2)
 #pragma unroll
                 for (int v = 0; v < w2; ++v) Lb[TRI8(w2, v)] = A[(kb + w2) * AS + kb + v];
-            double n0[8], n1[8];
-            const int kn = kb >= 8 ? kb - 8 : 0;
 #pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                n0[v] = A[(kn + v) * AS + r0];
-                n1[v] = A[(kn + v) * AS + (r1 & (NP - 1))];
-            }
-            // the block rows' right-hand sides, broadcast from their lanes
-            double x[8];
+            for (int v = 0; v < 8; ++v) { c0[v] = A[(kb + v) * AS + r0]; c1[v] = A[(kb + v) * AS + r1m]; }
 #pragma unroll
-            for (int v = 0; v < 8; ++v) x[v] = (kb < 64) ? readlane_d(t0, kb + v) : readlane_d(t1, kb + v - 64);
+            for (int v = 0; v < 8; ++v) x[v] = xsol[kb + v];
 #pragma unroll
-            for (int v = 7; v >= 0; --v) {
+            for (int v = 7; v >= 0; --v)
 #pragma unroll
                 for (int w2 = v + 1; w2 < 8; ++w2) x[v] -= Lb[TRI8(w2, v)] * x[w2];
-            }
             double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                if (r0 == kb + v) t0 = x[v];
-                if (r1 == kb + v) t1 = x[v];
-                s0 += c0[v] * x[v];
-                s1 += c1[v] * x[v];
+            for (int v = 0; v < 8; ++v) { s0 += c0[v] * x[v]; s1 += c1[v] * x[v]; }
+            if (lane == 0) {   // the block's solution: four 16-B stores from one lane (NaN-safe, no selects)
+                double2* xb = reinterpret_cast<double2*>(xsol + kb);
+                xb[0] = double2{x[0], x[1]}; xb[1] = double2{x[2], x[3]};
+                xb[2] = double2{x[4], x[5]}; xb[3] = double2{x[6], x[7]};
             }
-            if (r0 < kb) t0 -= s0;
-            if (r1 < kb) t1 -= s1;
-#pragma unroll
-            for (int v = 0; v < 8; ++v) { c0[v] = n0[v]; c1[v] = n1[v]; }
+            if (r0 < kb) xsol[r0] -= s0;
+            if (r1 < kb) xsol[r1] -= s1;
+            wave_sync();
         }
-        if (r0 < n) xsol[r0] = t0;
-        if (r1 < n) xsol[r1] = t1;
     }
     __syncthreads();
+    STAMP(13);
 
 #ifdef LH_STAMPS
     STAMP_FLUSH(10, 14);
@@ -1065,7 +1050,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
     __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
     __shared__ double Xp[NP * XS];        // unscaled panel columns (W = L D) for the trailing update
-    __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP], yv[NP];
+    __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP];
+    __shared__ __attribute__((aligned(16))) double yv[NP];
     __shared__ int perm[NP], iperm[NP];
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
@@ -1284,7 +1270,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     st0_ = __builtin_amdgcn_s_memtime();
     for (int i_ = 0; i_ < 24; ++i_) sacc_[i_] = 0;
 #endif
-    STAMP(13);
+    STAMP(10);
 
     // ---------------- pose part of the gain denominator; candidate poses ----------------
     double sp = 0.0;
@@ -1433,7 +1419,8 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
                                                    double* __restrict__ x) {
     __shared__ double A[(NP + 1) * AS];
     __shared__ double Xp[NP * XS];
-    __shared__ double dg[NP], xsol[NP];
+    __shared__ double dg[NP];
+    __shared__ __attribute__((aligned(16))) double xsol[NP];
     __shared__ int perm[NP];
     const int tid = threadIdx.x, NE = (n + 15) & ~15;
     if (tid < NP) dg[tid] = tid < n ? S[(size_t)tid * n + tid] : __builtin_nan("");
