@@ -33,7 +33,8 @@
 #define LH_SC_MAXD 3          // max |H_ll diag| (a max, not a sum)
 
 // per-landmark record (one 128-B line, double-buffered committed/candidate):
-// X (3) | Cholesky of H_ll (6) | b_l (3) | diag H_ll (3) | pad.  A sub-batch owns 8
+// X (3) | Cholesky of H_ll with reciprocal diagonal {1/L00, L10, 1/L11, L20, L21, 1/L22} (6) |
+// b_l (3) | diag H_ll (3) | pad.  A sub-batch owns 8
 // consecutive records, so one wave moves its landmarks with one 16-B access per lane.
 #define LH_REC 16
 #define LH_REC_X 0

@@ -315,6 +315,15 @@ __device__ __forceinline__ double fast_rcp(double d) {
     return r;
 }
 
+// 1/sqrt(a) with v_rsq_f64 and two Newton steps (the H_ll Cholesky is not a mirrored path)
+__device__ __forceinline__ double fast_rsq(double a) {
+    double y = __builtin_amdgcn_rsq(a);
+    const double h = 0.5 * a;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
 template <int T>
 struct LinCfg {
     static constexpr int NT = T * (T + 1) / 2;          // upper MFMA tiles of the window
@@ -480,13 +489,13 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             }
             const double s0 = group_sum(v3[0], lg), s1 = group_sum(v3[1], lg), s2 = group_sum(v3[2], lg);
             if (lmok) {
-                const double l00 = cl[0], l10 = cl[1], l11 = cl[2], l20 = cl[3], l21 = cl[4], l22 = cl[5];
+                // the cached factor holds 1/L_ii on the diagonal
+                const double i00 = cl[0], l10 = cl[1], i11 = cl[2], l20 = cl[3], l21 = cl[4], i22 = cl[5];
                 const double b0 = cl[6], b1 = cl[7], b2 = cl[8];
-                const double i00 = fast_rcp(l00), i11 = fast_rcp(l11), i22 = fast_rcp(l22);
                 const double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
                 const double y0 = t0 * i00, y1 = (t1 - l10 * y0) * i11, y2 = (t2 - l20 * y0 - l21 * y1) * i22;
                 double d2 = y2 * i22, d1 = (y1 - l21 * d2) * i11, d0 = (y0 - l10 * d1 - l20 * d2) * i00;
-                if (prm.guard && !(l00 == l00)) { d0 = d1 = d2 = 0.0; }   // skipped degenerate landmark
+                if (prm.guard && !(i00 == i00)) { d0 = d1 = d2 = 0.0; }   // skipped degenerate landmark
                 double x0 = X[0], x1 = X[1], x2 = X[2];
                 if (isfinite(d0) && isfinite(d1) && isfinite(d2)) { x0 += d0; x1 += d1; x2 += d2; }   // VertexXYZ::add
                 if (lead) {
@@ -558,26 +567,26 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         for (int i = 0; i < 6; ++i) h[i] = group_sum(hll[i], lg);
 #pragma unroll
         for (int i = 0; i < 3; ++i) h[6 + i] = group_sum(bl[i], lg);
-        double l00 = sqrt(h[0]);
-        double i00 = fast_rcp(l00);
-        double l10 = h[1] * i00, l20 = h[2] * i00;
+        // Cholesky of H_ll through reciprocal square roots: i_jj = 1/L_jj directly
+        double i00 = fast_rsq(h[0]);
+        const double l10 = h[1] * i00, l20 = h[2] * i00;
         const double a11 = h[3] - l10 * l10;
-        const double l11 = sqrt(a11), i11 = fast_rcp(l11);
+        const double i11 = fast_rsq(a11);
         const double l21 = (h[4] - l20 * l10) * i11;
         const double a22 = h[5] - l20 * l20 - l21 * l21;
-        const double l22 = sqrt(a22), i22 = fast_rcp(l22);
-        const bool pd = (h[0] > 0.0) && (a11 > 0.0) && (a22 > 0.0) && isfinite(l22) && isfinite(l21);
-        if (!pd) { l00 = __builtin_nan(""); i00 = __builtin_nan(""); }   // poisons the step, like a singular LU inverse (problem.cpp:399)
+        const double i22 = fast_rsq(a22);
+        const bool pd = (h[0] > 0.0) && (a11 > 0.0) && (a22 > 0.0) && isfinite(i22) && isfinite(l21);
+        if (!pd) i00 = __builtin_nan("");   // poisons the step, like a singular LU inverse (problem.cpp:399)
         const double w0 = h[6] * i00, w1 = (h[7] - l10 * w0) * i11, w2 = (h[8] - l20 * w0 - l21 * w1) * i22;
         if (lead) {
             maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
             if (!pd) ndeg += 1.0;
             double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
             reinterpret_cast<double2*>(rw)[0] = double2{X[0], X[1]};
-            reinterpret_cast<double2*>(rw)[1] = double2{X[2], l00};
-            reinterpret_cast<double2*>(rw)[2] = double2{l10, l11};
+            reinterpret_cast<double2*>(rw)[1] = double2{X[2], i00};
+            reinterpret_cast<double2*>(rw)[2] = double2{l10, i11};
             reinterpret_cast<double2*>(rw)[3] = double2{l20, l21};
-            reinterpret_cast<double2*>(rw)[4] = double2{l22, h[6]};
+            reinterpret_cast<double2*>(rw)[4] = double2{i22, h[6]};
             reinterpret_cast<double2*>(rw)[5] = double2{h[7], h[8]};
             reinterpret_cast<double2*>(rw)[6] = double2{h[0], h[3]};
             reinterpret_cast<double2*>(rw)[7] = double2{h[5], 0.0};
@@ -588,7 +597,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         double G[18];
 #pragma unroll
         for (int i = 0; i < 18; ++i) G[i] = 0.0;
-        if (live && !(prm.guard && !pd)) {
+        const bool gl = live && !(prm.guard && !pd);
+        if (gl) {
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double g0 = hpl[3 * a] * i00;
@@ -636,7 +646,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             for (int i = lane; i < nz; i += 64) z[i] = double2{0.0, 0.0};
         }
         wave_sync();
-        if (has) {
+        if (gl) {
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
