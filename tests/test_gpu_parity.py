@@ -276,3 +276,35 @@ def test_rccl_data_path_one_rank(monkeypatch):
     b = lego_ba.Solver().solve(w)
     assert a["chi2_final"] == b["chi2_final"] and a["iterations"] == b["iterations"]
     assert np.array_equal(a["pose_Tcw"], b["pose_Tcw"]) and np.array_equal(a["lm_xyz"], b["lm_xyz"])
+
+
+@pytest.mark.parametrize("kmin,kmax", [(3, 10), (2, 6)])
+def test_random_pose_subsets_all_tile_counts(kmin, kmax):
+    """Landmarks seen by random subsets of 2..10 keyframes: chunks with T = 1..4 MFMA tiles
+    (one k_lin launch per T), windows unions up to 10 poses, sub-batches with 2..16-lane groups."""
+    w = window("C2", seed=3, family="stable_noout", pose_mode=1, k_min=kmin, k_max=kmax)
+    g = lego_ba.Solver(max_iters=1, max_trials=1).solve(w)
+    o = ob.solve(w, max_iters=1, max_trials=1)
+    assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-12
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-7)
+    gf = lego_ba.Solver().solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 2, 8))
+    assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+
+
+def test_largest_supported_window_p21():
+    """P = 21 keyframes: the 126 x 126 reduced system (two identity padding rows in LDS)."""
+    w = lego_ba.generate_window(P=21, L=3000, k=8, seed=4, **dict(__import__("windows").STABLE, outlier_frac=0.0))
+    f = np.zeros(21, np.uint8)
+    f[0] = 1
+    w["pose_fixed"] = f
+    g = lego_ba.Solver().solve(w)
+    o, spread, its = oracle_envelope(w, threads=(1, 2, 8))
+    assert g["iterations"] in its
+    assert rel(g["chi2_final"], o["chi2_final"]) < max(1e-6, 10 * spread)
+    with pytest.raises(lego_ba.LhError) as e:     # one keyframe more is outside the envelope
+        w22 = lego_ba.generate_window(P=22, L=500, k=8, seed=4)
+        lego_ba.Solver().solve(w22)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED
