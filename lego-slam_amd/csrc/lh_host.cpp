@@ -29,6 +29,7 @@
 #include "lh_common.h"
 
 extern "C" {
+hipError_t lh_prepare_lin();
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
@@ -770,6 +771,7 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return LH_E_HIP; }
     h->device = dev;
+    if (lh_prepare_lin() != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipHostMalloc((void**)&h->h_ctrl, sizeof(lh_ctrl), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_done, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||

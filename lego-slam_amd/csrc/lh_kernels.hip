@@ -1344,6 +1344,22 @@ static size_t lin_smem_bytes(int scr, int ncam) {
     return sizeof(double) * ((size_t)LH_WAVES * scr + 2 * (size_t)LH_UMAX * ncam * LH_PT + LH_UMAX * 6 + (size_t)ncam * LH_EXT);
 }
 
+// Raise the dynamic-LDS limit of every k_lin instantiation on the current device (lh_create), before any
+// launch or stream capture.
+hipError_t lh_prepare_lin() {
+    {
+        const void* fns[] = {reinterpret_cast<const void*>(&k_lin<1, false>), reinterpret_cast<const void*>(&k_lin<1, true>),
+                             reinterpret_cast<const void*>(&k_lin<2, false>), reinterpret_cast<const void*>(&k_lin<2, true>),
+                             reinterpret_cast<const void*>(&k_lin<3, false>), reinterpret_cast<const void*>(&k_lin<3, true>),
+                             reinterpret_cast<const void*>(&k_lin<4, false>), reinterpret_cast<const void*>(&k_lin<4, true>)};
+        for (const void* f : fns) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+}
+
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
@@ -1352,13 +1368,6 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     dim3 g(nchunks), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
-        static bool attr_set = false;                                                                              \
-        if (!attr_set) {                                                                                           \
-            hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lin<TT, TR>),                     \
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);           \
-            if (e_ != hipSuccess) return e_;                                                                       \
-            attr_set = true;                                                                                       \
-        }                                                                                                          \
         const size_t smem = lin_smem_bytes(LinCfg<TT>::SCR, prm.ncam);                                 \
         hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
                            edge_rho, slabs, prm, nrec, fixed_mask, chunk_base);                                    \

@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out
 ok() { [ "$1" -le 1 ]; }
-LH_DEBUG=1 timeout -k 10 900 python -m pytest tests -q -m gpu -rf -p no:cacheprovider > gpurun_out/t.log 2>&1; rc=$?; echo "rc=$rc" >> gpurun_out/t.log
+timeout -k 10 900 python -m pytest tests -q -m gpu -rf -p no:cacheprovider > gpurun_out/t.log 2>&1; rc=$?; echo "rc=$rc" >> gpurun_out/t.log
 ok $rc || exit $rc
 timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/b.log 2>&1; rc=$?; echo "rc=$rc" >> gpurun_out/b.log
 [ $rc -eq 0 ] || exit $rc
