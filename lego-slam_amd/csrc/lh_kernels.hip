@@ -837,7 +837,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 }
 
 // ============================================================================
-// k_ctrl: LM controller + reduced-system solve, one workgroup of 256 threads.
+// k_ctrl: LM controller + reduced-system solve, one workgroup of 512 threads.
 //
 //  1. one global round trip: every thread prefetches its slice of BOTH reduced
 //     systems (staged candidate linearisation and committed one) plus the
@@ -845,204 +845,285 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 //  2. the chosen system is scattered straight from registers into LDS in Eigen's
 //     LDLT pivot order (problem.cpp:420; left-looking Eigen LDLT pivots on the
 //     ORIGINAL |diag|, so the order is a static sort), committing it on accept;
-//  3. right-looking blocked LDL^T, panel 8: every panel thread factors the 8x8
-//     diagonal block redundantly in registers (no cross-lane chain), then its
-//     own row; the right-hand side rides along as an extra row (row NP), so the
-//     forward substitution is part of the factorisation;
+//  3. right-looking blocked LDL^T (8-column blocks, one barrier per block), see
+//     lds_ldlt_solve; the right-hand side rides along as row NP (forward substitution);
 //  4. blocked back substitution in one wave; candidate poses (VertexPose::add).
-// The matrix is padded to NE = ceil8(n) with identity rows: no bounds tests in
+// The matrix is padded to NE = ceil16(n) with identity rows: no bounds tests in
 // the inner loops.
 // ============================================================================
 #define CT 512
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
 #define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
-#define XS 9                  // LDS row stride of the panel's unscaled columns
+#define NBLK (LH_NPAD / 8)
 #define RS_MAX (LH_PMAX * (LH_PMAX + 1) / 2 * 36 + 18 * LH_PMAX + 8)
 #define NLD ((RS_MAX + CT - 1) / CT)
 
+// Per-block products of the 8x8 diagonal-block factor (LDS, shared by all waves).
+struct LdltBlockLds {
+    double N[2][64];          // N = (Delta L^T)^-1 of the block being eliminated (row-major), by step parity
+    double ND[NBLK][64];      // N Delta = L_bb^-T of every block (row-major): trailing-update operand
+                              // and the back substitution's block solve
+    double z[NP];             // z = D^-1 L^-1 b (zero where |D| <= DBL_MIN)
+};
 
-#define TRI8(r, c) ((r) * ((r) - 1) / 2 + (c))   // packed strictly-lower 8x8 index, r > c
+// 64-bit broadcast of lane L of each 16-lane row (DPP row_newbcast, two 32-bit moves): a few
+// cycles, where a readlane round trip through an SGPR costs ~45 on a dependent chain.  (A single
+// v_fmac_f64_dpp from inline asm measured 10% faster but lost precision: not used.)
+template <int L>
+__device__ __forceinline__ double bcast16(double v) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)x, 0x150 + L, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), 0x150 + L, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
-// LDL^T of the 8x8 diagonal block at (k0, k0) of A (lower triangle), computed redundantly by
-// every lane of one wave; one lane writes D on A's diagonal and L below it (L = W where Eigen's
-// pivot_is_valid fails, ldlt_inplace).  Stores from one wave are slow: only these 36 values.
-__device__ __forceinline__ void factor_block8(double* A, int k0, int lane) {
-    double B[8][8], Wb[8][8], dv[8], inv[8];
+template <int Q>
+__device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
+    const double d = bcast16<Q>(R[Q]);
+    dl[Q] = fabs(d) > 0.0 ? d : 1.0;          // Eigen ldlt_inplace: no scaling where !pivot_is_valid
+    const double inv = fast_rcp(dl[Q]);
+    const double coef = R[Q] * inv;
+    double u[8];
+    // W[j][Q] = lane j's R[Q], read before R[Q] becomes coef
+    if (Q < 1) u[1] = bcast16<1>(R[Q]);
+    if (Q < 2) u[2] = bcast16<2>(R[Q]);
+    if (Q < 3) u[3] = bcast16<3>(R[Q]);
+    if (Q < 4) u[4] = bcast16<4>(R[Q]);
+    if (Q < 5) u[5] = bcast16<5>(R[Q]);
+    if (Q < 6) u[6] = bcast16<6>(R[Q]);
+    if (Q < 7) u[7] = bcast16<7>(R[Q]);
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
+    for (int j = Q + 1; j < 8; ++j) R[j] -= coef * u[j];
+    R[Q] = coef;
+}
+
+// LDL^T of the 8x8 diagonal block at (k0, k0) of A by one wave, Eigen ldlt_inplace order (L = W
+// where pivot_is_valid fails).  In each 16-lane row (four identical replicas), lane r < 8 holds
+// row r of the block and lane 8 + r row r of the identity: the same column eliminations turn
+// the first into L and the second into N = (Delta L^T)^-1, Delta = diag(D, 1 where invalid), so
+// one instruction stream computes both.  Column q's pivot and entries move by DPP broadcast.
+// Writes D on A's diagonal and L^T above it (L[r][c] at A[c][r]), N, and ND = N Delta = L^-T.
+// For a row a below the block, l = a N is its forward substitution through the block and
+// l Delta its partially eliminated entries, so the trailing update of rows i, j is
+// L_i Delta L_j^T = T_i a_j^T with T_i = L_i ND^T.
+__device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __restrict__ No, double* __restrict__ NDo,
+                                              int k0, int lane) {
+    const int p = lane & 15, r = p & 7;
+    const bool ident = p >= 8;
+    double R[8], dl[8];
+    double v[8];
 #pragma unroll
-        for (int c = 0; c <= r; ++c) B[r][c] = A[(k0 + r) * AS + k0 + c];
+    for (int q = 0; q < 8; ++q) v[q] = A[(k0 + r) * AS + k0 + q];   // upper entries: garbage confined to this lane's upper part
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        dv[c] = B[c][c];
-        const bool valid = fabs(dv[c]) > 0.0;     // Eigen ldlt_inplace: pivot_is_valid
-        inv[c] = valid ? fast_rcp(dv[c]) : 1.0;
+    for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
+    factor_column<0>(R, dl);
+    factor_column<1>(R, dl);
+    factor_column<2>(R, dl);
+    factor_column<3>(R, dl);
+    factor_column<4>(R, dl);
+    factor_column<5>(R, dl);
+    factor_column<6>(R, dl);
+    factor_column<7>(R, dl);
+    if (lane < 8) {
 #pragma unroll
-        for (int r = c + 1; r < 8; ++r) Wb[r][c] = B[r][c];
+        for (int q = 0; q < 8; ++q)
+            if (q <= r) A[(k0 + q) * AS + k0 + r] = (q == r) ? dl[q] : R[q];
+    } else if (lane < 16) {
+        double2* n2 = reinterpret_cast<double2*>(No + 8 * r);
+        double2* d2 = reinterpret_cast<double2*>(NDo + 8 * r);
 #pragma unroll
-        for (int r = c + 1; r < 8; ++r) {
-            const double l = Wb[r][c] * inv[c];
-            B[r][c] = l;
-#pragma unroll
-            for (int r2 = c + 1; r2 <= r; ++r2) B[r][r2] -= l * Wb[r2][c];
-        }
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-#pragma unroll
-            for (int c = 0; c < r; ++c) A[(k0 + r) * AS + k0 + c] = B[r][c];
-            A[(k0 + r) * AS + k0 + r] = dv[r];
+        for (int q = 0; q < 4; ++q) {
+            n2[q] = double2{R[2 * q], R[2 * q + 1]};
+            d2[q] = double2{R[2 * q] * dl[2 * q], R[2 * q + 1] * dl[2 * q + 1]};
         }
     }
 }
 
-// lower-triangular 16x16 tile enumeration x -> (I, J), x = I (I + 1) / 2 + J, I < 8
-__constant__ unsigned char c_triI[36] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5,
-                                         6, 6, 6, 6, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7, 7};
-__constant__ unsigned char c_triJ[36] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5,
-                                         0, 1, 2, 3, 4, 5, 6, 0, 1, 2, 3, 4, 5, 6, 7};
+// Step k0 of the elimination for the 16-row tile row at rb (one wave): with the raw block column
+// a_I = A[rb..rb+15][k0..k0+7] (rows below k0+8 only; the block's own rows are masked),
+//   L_I^T = N^T a_I^T              (MFMA; lands in A-operand layout: lane (li, lk) holds L[li][lk], L[li][lk+4])
+//   T_I^T = ND L_I^T               (T_I = L_I Delta N^T, again in A-operand layout)
+//   L^T -> A[k0+c][i]              (upper triangle; only when store_l)
+//   b_i -= T_I . b_blk             (forward substitution of the rhs row; only when store_l)
+//   A_IJ -= T_I a_J^T  for the tile columns J in [jb0, jb1) except skip_cb (lower part, cols >= m0).
+// Every operand is the block column as it was before this step: no panel pass and no barrier
+// between the elimination of the column and the trailing update.
+__device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const double* __restrict__ N,
+                                              const double* __restrict__ ND, int k0, int rb, int jb0, int jb1,
+                                              int skip_cb, bool store_l, int lane) {
+    const int li = lane & 15, lk = lane >> 4, m0 = k0 + 8;
+    const bool lo = li < 8;
+    // every LDS read of this tile row is issued up front (tiles are disjoint and this step's
+    // writes never touch block column k0, so no read here can see a write of this step)
+    const double na0 = lo ? N[lk * 8 + li] : 0.0, na1 = lo ? N[(lk + 4) * 8 + li] : 0.0;
+    const double da0 = lo ? ND[li * 8 + lk] : 0.0, da1 = lo ? ND[li * 8 + 4 + lk] : 0.0;
+    const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
+    int cb = (jb0 == skip_cb) ? jb0 + 16 : jb0;
+    double b0 = 0.0, b1 = 0.0, old[4] = {0.0, 0.0, 0.0, 0.0};
+    if (cb < jb1) {
+        b0 = A[(cb + li) * AS + k0 + lk];
+        b1 = A[(cb + li) * AS + k0 + 4 + lk];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[q] = A[(rb + lk + 4 * q) * AS + cb + li];
+    }
+    v4d l = {0.0, 0.0, 0.0, 0.0};
+    l = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, a0, l, 0, 0, 0);
+    l = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, a1, l, 0, 0, 0);
+    // l[q] = L[rb+li][k0+lk+4q] (q = 0, 1)
+    v4d t = {0.0, 0.0, 0.0, 0.0};
+    t = __builtin_amdgcn_mfma_f64_16x16x4f64(da0, l[0], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f64_16x16x4f64(da1, l[1], t, 0, 0, 0);
+    // t[q] = T[rb+li][lk+4q] (q = 0, 1)
+    if (store_l) {
+        const double rb0 = (li == 0) ? A[NP * AS + k0 + lk] : 0.0, rb1 = (li == 0) ? A[NP * AS + k0 + 4 + lk] : 0.0;
+        double rold[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rold[q] = A[NP * AS + rb + lk + 4 * q];
+        if (rb + li >= m0) {
+            A[(k0 + lk) * AS + rb + li] = l[0];
+            A[(k0 + 4 + lk) * AS + rb + li] = l[1];
+        }
+        v4d u = {0.0, 0.0, 0.0, 0.0};
+        u = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], rb0, u, 0, 0, 0);
+        u = __builtin_amdgcn_mfma_f64_16x16x4f64(t[1], rb1, u, 0, 0, 0);
+        // u[q] = (T b_blk)[rb+lk+4q] in column li = 0
+        if (li == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = rb + lk + 4 * q;
+                if (row >= m0) A[NP * AS + row] = rold[q] - u[q];
+            }
+        }
+    }
+    // trailing tiles, software-pipelined: the next tile's operands are in flight during this one's MFMAs
+    while (cb < jb1) {
+        int nc = cb + 16;
+        if (nc == skip_cb) nc += 16;
+        double nb0 = 0.0, nb1 = 0.0, nold[4] = {0.0, 0.0, 0.0, 0.0};
+        if (nc < jb1) {
+            nb0 = A[(nc + li) * AS + k0 + lk];
+            nb1 = A[(nc + li) * AS + k0 + 4 + lk];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nold[q] = A[(rb + lk + 4 * q) * AS + nc + li];
+        }
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[1], b1, acc, 0, 0, 0);
+        const int col = cb + li;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = rb + lk + 4 * q;
+            if (row >= m0 && col >= m0 && col <= row) A[row * AS + col] = old[q] - acc[q];
+        }
+        cb = nc;
+        b0 = nb0; b1 = nb1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[q] = nold[q];
+    }
+}
+
+// tile row -> wave: waves w and w+4 share a SIMD; wave 0 runs the critical chain (the next
+// diagonal tile + factor), so its SIMD-mate takes the lightest rows and the heavy bottom rows
+// go one per SIMD
+__device__ __forceinline__ int row_wave(int g) { return g < 4 ? 4 + g : 8 - g; }   // 4 5 6 7 4 3 2 1
 
 // Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
-// blocked LDL^T and the solve; xsol[r] = solution in pivot order for r < n.  Shared with the
-// k_ldlt_probe test hook.  Must be called by all CT threads.
-__device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ Xp, double* __restrict__ xsol,
-                                               int n, int NE, int tid) {
+// blocked LDL^T with the forward substitution, then the back substitution; xsol[r] = solution in
+// pivot order for r < n.  Shared with the k_ldlt_probe test hook.  Must be called by all CT threads.
+//
+// Step t eliminates block column k0 = 8t.  Interval t (one barrier each):
+//   wave 0:       the trailing update of the diagonal tile holding block t+1, then the factor
+//                 of block t+1 (N by step parity, ND per block);
+//   tile-row owners: L_I (stored transposed), T_I, the rhs update and A_IJ -= T_I a_J^T for
+//                 their tile row (row_wave), skipping wave 0's tile;
+//   wave 4 first: z_t = b_t N_t (Eigen's solve tolerance applied).
+// L lives in the upper triangle, so the raw block columns stay readable for the whole step.
+__device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
+    __shared__ __attribute__((aligned(16))) LdltBlockLds F;
 #ifdef LH_STAMPS
     unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_, sacc_[24] = {0};
 #endif
-    // ---------------- 3. blocked right-looking LDL^T (+ forward substitution in row NP) ----------------
-    // Each 8x8 diagonal block is factored by wave 0 as soon as the previous trailing update has
-    // produced it (look-ahead), while the other waves finish that update; the panel phase then
-    // only solves every row below against the factored block.
-    if (wave == 0) factor_block8(A, 0, lane);
+    const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if (wv == 0) factor_block8(A, F.N[0], F.ND[0], 0, lane);
     __syncthreads();
     STAMP(18);
-    for (int k0 = 0; k0 < NE; k0 += 8) {
-        const int m0 = k0 + 8;
-        const int nrow = NE - m0 + 1;                 // panel rows k0+8..NE-1 and the rhs row
-        if (tid < nrow) {
-            const int i = (tid == nrow - 1) ? NP : m0 + tid;
-            // the factored diagonal block: 1/D and W = L D (L itself where the pivot is invalid)
-            double inv[8], Wb[28], a[8];
+    for (int k0 = 0; k0 < nb; k0 += 8) {
+        const int t = k0 >> 3, par = t & 1, m0 = k0 + 8;
+        const double* N = F.N[par];
+        const double* ND = F.ND[t];
+        if (wv == 4 && lane < 8) {        // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
+            double z = 0.0;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const double d = A[(k0 + c) * AS + k0 + c];
-                const bool valid = fabs(d) > 0.0;
-                inv[c] = valid ? fast_rcp(d) : 1.0;
-#pragma unroll
-                for (int r = c + 1; r < 8; ++r) {
-                    const double l = A[(k0 + r) * AS + k0 + c];
-                    Wb[TRI8(r, c)] = valid ? l * d : l;
-                }
+            for (int q = 0; q < 8; ++q) z += A[NP * AS + k0 + q] * N[q * 8 + lane];
+            const double d = A[(k0 + lane) * AS + k0 + lane];
+            F.z[k0 + lane] = fabs(d) > 2.2250738585072014e-308 ? z : 0.0;
+        }
+        if (m0 < nb) {
+            const int g0 = m0 >> 4;               // tile row/col of the next diagonal block
+            const int tg = g0;                    // first tile row with rows >= m0 (and first tile column)
+            if (wv == 0) {
+                ldlt_tile_row(A, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
+                wave_sync();
+                factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
+                STAMP(12);
             }
-#pragma unroll
-            for (int c = 0; c < 8; ++c) a[c] = A[i * AS + k0 + c];
-            double w[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                w[c] = a[c];
-                const double l = a[c] * inv[c];
-                a[c] = l;
-#pragma unroll
-                for (int c2 = c + 1; c2 < 8; ++c2) a[c2] -= l * Wb[TRI8(c2, c)];
-            }
-#pragma unroll
-            for (int c = 0; c < 8; ++c) A[i * AS + k0 + c] = a[c];
-            if (i < NP) {
-#pragma unroll
-                for (int c = 0; c < 8; ++c) Xp[i * XS + c] = w[c];
+            for (int g = tg; 16 * g < NE; ++g) {
+                if (row_wave(g) != wv) continue;
+                ldlt_tile_row(A, N, ND, k0, 16 * g, 16 * tg, 16 * g + 16, g == g0 ? 16 * g0 : -1, true, lane);
             }
         }
         __syncthreads();
-        STAMP(15);
-        if (m0 < NE) {
-            // trailing update A[i][j] -= sum_c L[i][c] W[j][c], k0+8 <= j <= i < NE, on f64 MFMA:
-            // 16x16 tiles anchored at tb = floor16(k0+8), two 16x16x4 steps each; rows/cols
-            // below k0+8 of the first tile row/col are the panel's own L and D (written back unchanged).
-            // Tile 0 holds the next diagonal block: wave 0 updates it first, then factors the block.
-            const int tb = m0 & ~15;
-            const int mt = (NE - tb) >> 4;
-            const int ntile = mt * (mt + 1) / 2;
-            const int wv = __builtin_amdgcn_readfirstlane(wave);
-            const int li = lane & 15, lk = lane >> 4;
-            // wave 4 shares wave 0's SIMD (waves w and w+4 of a workgroup do): it stays idle so the
-            // factor chain issues unimpeded; waves 1-3, 5-7 take tiles 1.. round-robin
-            const int tq = wv - 1 - (wv > 4 ? 1 : 0);
-            const int x0 = (wv == 0) ? 0 : (wv == 4 ? ntile : 1 + tq);
-            const int xs_ = (wv == 0) ? ntile : 6;
-            for (int x = x0; x < ntile; x += xs_) {
-                const int rb = tb + 16 * c_triI[x], cb = tb + 16 * c_triJ[x];
-                const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
-                const double b0 = Xp[(cb + li) * XS + lk], b1 = Xp[(cb + li) * XS + 4 + lk];
-                const int col = cb + li;
-                double old[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) old[r] = A[(rb + lk + 4 * r) * AS + col];
-                v4d acc = {0.0, 0.0, 0.0, 0.0};
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = rb + lk + 4 * r;
-                    A[row * AS + col] = (row >= m0 && col >= m0) ? old[r] - acc[r] : old[r];
-                }
-            }
-            if (wv == 0) { STAMP(22); } else { STAMP(23); }
-            if (wv == 0) {
-                wave_sync();
-                factor_block8(A, m0, lane);
-                STAMP(12);
-            }
-            if (tid >= CT - 64) {   // the rhs row (forward substitution): last wave, after its tiles
-                for (int j = m0 + (tid - (CT - 64)); j < NE; j += 64) {
-                    double acc = 0.0;
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) acc += A[NP * AS + k0 + c] * Xp[j * XS + c];
-                    A[NP * AS + j] -= acc;
-                }
-            }
-            __syncthreads();
-        }
         STAMP(16);
     }
 
-    // ---------------- 4. z /= D (Eigen tolerance), back substitution L^T x = z ----------------
-    // One wave; the right-hand side lives in LDS (xsol), block rows are read as broadcasts:
-    // no readlane chains (2.4x faster than a register-resident rhs, tools/ubench_backsub.hip).
-    if (wave == 0) {
-        const double tol = 2.2250738585072014e-308;   // LDLT::_solve_impl: (numeric_limits::min)()
-        const int r0 = lane, r1 = lane + 64, r1m = r1 & (NP - 1);
-        if (r0 < NE) { const double d = A[r0 * AS + r0]; xsol[r0] = fabs(d) > tol ? A[NP * AS + r0] : 0.0; }
-        if (r1 < NE) { const double d = A[r1 * AS + r1]; xsol[r1] = fabs(d) > tol ? A[NP * AS + r1] : 0.0; }
-        wave_sync();
-        for (int kb = NE - 8; kb >= 0; kb -= 8) {
-            double Lb[28], x[8], c0[8], c1[8];
+    // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
+    // Block b: x_b = ND_b y_b, then every row r above it: y_r -= sum_v L[kb+v][r] x_b[v] (L^T rows
+    // r of the upper triangle).  y lives in registers (rows lane and lane + 64), moved by readlane;
+    // lane kb+v (mod 64) computes x_b[v], so it already holds its own row's result.  The next
+    // block's L^T and ND operands are loaded one block ahead.
+    if (wv == 0) {
+        const int r0 = lane, r1 = lane + 64;
+        double y0 = (r0 < nb) ? F.z[r0] : 0.0, y1 = (r1 < nb) ? F.z[r1] : 0.0;
+        double lt0[8], lt1[8], ndr[8];
+        int kb = nb - 8;
 #pragma unroll
-            for (int w2 = 1; w2 < 8; ++w2)
-#pragma unroll
-                for (int v = 0; v < w2; ++v) Lb[TRI8(w2, v)] = A[(kb + w2) * AS + kb + v];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) { c0[v] = A[(kb + v) * AS + r0]; c1[v] = A[(kb + v) * AS + r1m]; }
-#pragma unroll
-            for (int v = 0; v < 8; ++v) x[v] = xsol[kb + v];
-#pragma unroll
-            for (int v = 7; v >= 0; --v)
-#pragma unroll
-                for (int w2 = v + 1; w2 < 8; ++w2) x[v] -= Lb[TRI8(w2, v)] * x[w2];
-            double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-            for (int v = 0; v < 8; ++v) { s0 += c0[v] * x[v]; s1 += c1[v] * x[v]; }
-            if (lane == 0) {   // the block's solution: four 16-B stores from one lane (NaN-safe, no selects)
-                double2* xb = reinterpret_cast<double2*>(xsol + kb);
-                xb[0] = double2{x[0], x[1]}; xb[1] = double2{x[2], x[3]};
-                xb[2] = double2{x[4], x[5]}; xb[3] = double2{x[6], x[7]};
-            }
-            if (r0 < kb) xsol[r0] -= s0;
-            if (r1 < kb) xsol[r1] -= s1;
-            wave_sync();
+        for (int v = 0; v < 8; ++v) {
+            lt0[v] = A[r0 * AS + kb + v];
+            lt1[v] = A[(r1 & (NP - 1)) * AS + kb + v];
+            ndr[v] = F.ND[kb >> 3][(lane & 7) * 8 + v];
         }
+        for (; kb >= 0; kb -= 8) {
+            const int kn = kb >= 8 ? kb - 8 : 0;
+            double nlt0[8], nlt1[8], nndr[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                nlt0[v] = A[r0 * AS + kn + v];
+                nlt1[v] = A[(r1 & (NP - 1)) * AS + kn + v];
+                nndr[v] = F.ND[kn >> 3][(lane & 7) * 8 + v];
+            }
+            const bool hi = kb >= 64;
+            const double ysrc = hi ? y1 : y0;
+            double yb[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) yb[w] = readlane_d(ysrc, (kb + w) & 63);
+            const double xv = ((ndr[0] * yb[0] + ndr[1] * yb[1]) + (ndr[2] * yb[2] + ndr[3] * yb[3])) +
+                              ((ndr[4] * yb[4] + ndr[5] * yb[5]) + (ndr[6] * yb[6] + ndr[7] * yb[7]));
+            double xb[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, ((kb & 63) + v));
+            const double s0 = ((lt0[0] * xb[0] + lt0[1] * xb[1]) + (lt0[2] * xb[2] + lt0[3] * xb[3])) +
+                              ((lt0[4] * xb[4] + lt0[5] * xb[5]) + (lt0[6] * xb[6] + lt0[7] * xb[7]));
+            const double s1 = ((lt1[0] * xb[0] + lt1[1] * xb[1]) + (lt1[2] * xb[2] + lt1[3] * xb[3])) +
+                              ((lt1[4] * xb[4] + lt1[5] * xb[5]) + (lt1[6] * xb[6] + lt1[7] * xb[7]));
+            y0 = (r0 < kb) ? y0 - s0 : ((r0 < kb + 8) ? xv : y0);
+            y1 = (r1 < kb) ? y1 - s1 : ((r1 < kb + 8) ? xv : y1);
+#pragma unroll
+            for (int v = 0; v < 8; ++v) { lt0[v] = nlt0[v]; lt1[v] = nlt1[v]; ndr[v] = nndr[v]; }
+        }
+        if (r0 < NE) xsol[r0] = y0;
+        if (r1 < NE) xsol[r1] = y1;
     }
     __syncthreads();
     STAMP(13);
@@ -1059,7 +1140,6 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                                              const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
     __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
-    __shared__ double Xp[NP * XS];        // unscaled panel columns (W = L D) for the trailing update
     __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP];
     __shared__ __attribute__((aligned(16))) double yv[NP];
     __shared__ int perm[NP], iperm[NP];
@@ -1273,7 +1353,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
     STAMP_FLUSH(10, 14);
-    lds_ldlt_solve(A, Xp, yv, n, NE, tid);
+    lds_ldlt_solve(A, yv, n, NE, tid);
     if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
     __syncthreads();
 #ifdef LH_STAMPS
@@ -1437,7 +1517,6 @@ hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, 
 __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
                                                    double* __restrict__ x) {
     __shared__ double A[(NP + 1) * AS];
-    __shared__ double Xp[NP * XS];
     __shared__ double dg[NP];
     __shared__ __attribute__((aligned(16))) double xsol[NP];
     __shared__ int perm[NP];
@@ -1464,7 +1543,7 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     }
     if (tid < NE) A[NP * AS + tid] = tid < n ? b[perm[tid]] : 0.0;
     __syncthreads();
-    lds_ldlt_solve(A, Xp, xsol, n, NE, tid);
+    lds_ldlt_solve(A, xsol, n, NE, tid);
     __syncthreads();
     if (tid < n) x[perm[tid]] = xsol[tid];
 }
