@@ -837,7 +837,8 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 }
 
 // ============================================================================
-// k_ctrl: LM controller + reduced-system solve, one workgroup of 512 threads.
+// k_ctrl: LM controller + reduced-system solve, one workgroup of 1024 threads (16 waves: the
+// LDLT's trailing updates are latency-bound MFMA chains, four waves per SIMD overlap them).
 //
 //  1. one global round trip: every thread prefetches its slice of BOTH reduced
 //     systems (staged candidate linearisation and committed one) plus the
@@ -851,7 +852,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 // The matrix is padded to NE = ceil16(n) with identity rows: no bounds tests in
 // the inner loops.
 // ============================================================================
-#define CT 512
+#define CT 1024
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
 #define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
 #define NBLK (LH_NPAD / 8)
@@ -1022,10 +1023,17 @@ __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const doub
     }
 }
 
-// tile row -> wave: waves w and w+4 share a SIMD; wave 0 runs the critical chain (the next
-// diagonal tile + factor), so its SIMD-mate takes the lightest rows and the heavy bottom rows
-// go one per SIMD
-__device__ __forceinline__ int row_wave(int g) { return g < 4 ? 4 + g : 8 - g; }   // 4 5 6 7 4 3 2 1
+// Work units of one elimination step over the active tile rows tg..7: unit 2i and 2i+1 are the
+// two halves of the tile columns of row 7 - i (i < R - 1; the first half also stores L^T and
+// updates the rhs), the last unit is row tg's L^T and rhs (its one tile is wave 0's).  Units
+// go to waves in this order: waves w, w+4, w+8, w+12 share a SIMD, and wave 0 runs the
+// critical chain, so its SIMD-mates 4, 8, 12 come last (lightest units).
+__device__ __forceinline__ int wave_unit(int w) {
+    // order: 1 2 3 5 6 7 9 10 11 13 14 15 4 8 12
+    if (w == 0) return -1;
+    if (w & 3) return (w >> 2) * 3 + (w & 3) - 1;
+    return 11 + (w >> 2);
+}
 
 // Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
 // blocked LDL^T with the forward substitution, then the back substitution; xsol[r] = solution in
@@ -1034,9 +1042,9 @@ __device__ __forceinline__ int row_wave(int g) { return g < 4 ? 4 + g : 8 - g; }
 // Step t eliminates block column k0 = 8t.  Interval t (one barrier each):
 //   wave 0:       the trailing update of the diagonal tile holding block t+1, then the factor
 //                 of block t+1 (N by step parity, ND per block);
-//   tile-row owners: L_I (stored transposed), T_I, the rhs update and A_IJ -= T_I a_J^T for
-//                 their tile row (row_wave), skipping wave 0's tile;
-//   wave 4 first: z_t = b_t N_t (Eigen's solve tolerance applied).
+//   the other waves: L_I (stored transposed), T_I, the rhs update and A_IJ -= T_I a_J^T, by
+//                 half tile rows (wave_unit), skipping wave 0's tile;
+//   wave 12 first: z_t = b_t N_t (Eigen's solve tolerance applied).
 // L lives in the upper triangle, so the raw block columns stay readable for the whole step.
 __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
@@ -1053,7 +1061,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         const int t = k0 >> 3, par = t & 1, m0 = k0 + 8;
         const double* N = F.N[par];
         const double* ND = F.ND[t];
-        if (wv == 4 && lane < 8) {        // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
+        if (wv == 12 && lane < 8) {       // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
             double z = 0.0;
 #pragma unroll
             for (int q = 0; q < 8; ++q) z += A[NP * AS + k0 + q] * N[q * 8 + lane];
@@ -1069,9 +1077,15 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
                 STAMP(12);
             }
-            for (int g = tg; 16 * g < NE; ++g) {
-                if (row_wave(g) != wv) continue;
-                ldlt_tile_row(A, N, ND, k0, 16 * g, 16 * tg, 16 * g + 16, g == g0 ? 16 * g0 : -1, true, lane);
+            const int gl = (NE >> 4) - 1, R = gl - tg + 1;
+            const int u = wave_unit(wv);
+            if (u >= 0 && u < 2 * (R - 1)) {
+                const int g = gl - (u >> 1), nt = g - tg + 1, split = tg + ((nt + 1) >> 1);
+                const bool first = (u & 1) == 0;
+                ldlt_tile_row(A, N, ND, k0, 16 * g, first ? 16 * tg : 16 * split, first ? 16 * split : 16 * g + 16, -1,
+                              first, lane);
+            } else if (u == 2 * (R - 1)) {
+                ldlt_tile_row(A, N, ND, k0, 16 * g0, 0, 0, -1, true, lane);   // row tg: L^T and rhs only
             }
         }
         __syncthreads();
@@ -1145,6 +1159,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     __shared__ int perm[NP], iperm[NP];
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
+    __shared__ double s_pm[2][LH_PMAX * 12];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
@@ -1172,10 +1187,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         vc[u] = in ? rs_commit[i] : 0.0;
         mp[u] = i < LY.off_bs ? rsmap[i] : 0u;
     }
-    double pm0[12], pm1[12];
-    if (tid < P) {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) { pm0[i] = pose_mat[(size_t)tid * 12 + i]; pm1[i] = pose_mat[((size_t)P + tid) * 12 + i]; }
+    if (tid < 24 * P) {   // both pose-matrix buffers into LDS (used after the solve)
+        const int b = tid / (12 * P), i = tid - b * 12 * P;
+        s_pm[b][i] = pose_mat[(size_t)b * P * 12 + i];
     }
     if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
         double mx = 0.0;
@@ -1386,7 +1400,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         d_se3_exp(up, qe, te);
         double Tc[12];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) Tc[i] = cur ? pm1[i] : pm0[i];
+        for (int i = 0; i < 12; ++i) Tc[i] = s_pm[cur][pidx * 12 + i];
         const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
         const double tc[3] = {Tc[3], Tc[7], Tc[11]};
         d_q_from_R(Rc, qT);

@@ -7,7 +7,9 @@ for b in ubench_ldlt_old ubench_ldlt ubench_ldlt_st; do
   [ -x $B/$b ] || continue
   echo "== $b"; for n in ${NS:-120 42 6}; do timeout -k 5 60 $B/$b $n || exit 1; done
 done
-if [ -x $B/ubench_ldlt_parts ]; then echo "== parts"; timeout -k 5 60 $B/ubench_ldlt_parts || exit 1; fi
+for b in ubench_ldlt_parts exp_ldlt; do
+  if [ -x $B/$b ]; then echo "== $b"; timeout -k 5 60 $B/$b || exit 1; fi
+done
 } > gpurun_out/u.log 2>&1
 if [ "${RUN_TESTS:-1}" = 1 ]; then
 timeout -k 10 600 python -m pytest tests -q -m gpu -rf -p no:cacheprovider -k "${TESTS_K:-reduced_solve or parity_stable or p21 or subsets}" > gpurun_out/t.log 2>&1; rc=$?; echo rc=$rc >> gpurun_out/t.log
