@@ -1035,6 +1035,48 @@ __device__ __forceinline__ int wave_unit(int w) {
     return 11 + (w >> 2);
 }
 
+// Back substitution x = L^-T z for block KB (compile-time, so every lane index below is an
+// immediate), one wave: y holds rows lane (y0) and lane + 64 (y1), already reduced by every block
+// above KB.  x_b = ND_b y_b: the block's 8 y values sit in lanes KB..KB+7 (mod 64), inside one
+// 16-lane row, and reach that row's lanes by DPP broadcast; lane KB+v computes x_b[v], so it
+// holds its own row's result.  Every row r above the block then takes y_r -= sum_v L[KB+v][r]
+// x_b[v] (L^T row r in the upper triangle), x_b broadcast by readlane.  No LDS writes: the
+// compiler may hoist every block's operand loads.
+template <int KB>
+__device__ __forceinline__ void backsub_block(const double* __restrict__ A, const LdltBlockLds& F, int nb, int lane,
+                                              double& y0, double& y1) {
+    if (KB >= nb) return;
+    constexpr bool HI = KB >= 64;
+    constexpr int KL = KB & 63, R16 = KL & 15;
+    const double ys = HI ? y1 : y0;
+    double yb[8], nd[8];
+    yb[0] = bcast16<R16 + 0>(ys); yb[1] = bcast16<R16 + 1>(ys); yb[2] = bcast16<R16 + 2>(ys); yb[3] = bcast16<R16 + 3>(ys);
+    yb[4] = bcast16<R16 + 4>(ys); yb[5] = bcast16<R16 + 5>(ys); yb[6] = bcast16<R16 + 6>(ys); yb[7] = bcast16<R16 + 7>(ys);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) nd[w] = F.ND[KB >> 3][(lane & 7) * 8 + w];
+    const double xv = ((nd[0] * yb[0] + nd[1] * yb[1]) + (nd[2] * yb[2] + nd[3] * yb[3])) +
+                      ((nd[4] * yb[4] + nd[5] * yb[5]) + (nd[6] * yb[6] + nd[7] * yb[7]));
+    double xb[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, KL + v);
+    double l0[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) l0[v] = A[lane * AS + KB + v];
+    const double s0 = ((l0[0] * xb[0] + l0[1] * xb[1]) + (l0[2] * xb[2] + l0[3] * xb[3])) +
+                      ((l0[4] * xb[4] + l0[5] * xb[5]) + (l0[6] * xb[6] + l0[7] * xb[7]));
+    if (HI) {
+        double l1[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) l1[v] = A[(lane + 64) * AS + KB + v];
+        const double s1 = ((l1[0] * xb[0] + l1[1] * xb[1]) + (l1[2] * xb[2] + l1[3] * xb[3])) +
+                          ((l1[4] * xb[4] + l1[5] * xb[5]) + (l1[6] * xb[6] + l1[7] * xb[7]));
+        y0 -= s0;
+        y1 = (lane + 64 < KB) ? y1 - s1 : ((lane + 64 < KB + 8) ? xv : y1);
+    } else {
+        y0 = (lane < KB) ? y0 - s0 : ((lane < KB + 8) ? xv : y0);
+    }
+}
+
 // Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
 // blocked LDL^T with the forward substitution, then the back substitution; xsol[r] = solution in
 // pivot order for r < n.  Shared with the k_ldlt_probe test hook.  Must be called by all CT threads.
@@ -1093,51 +1135,26 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     }
 
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
-    // Block b: x_b = ND_b y_b, then every row r above it: y_r -= sum_v L[kb+v][r] x_b[v] (L^T rows
-    // r of the upper triangle).  y lives in registers (rows lane and lane + 64), moved by readlane;
-    // lane kb+v (mod 64) computes x_b[v], so it already holds its own row's result.  The next
-    // block's L^T and ND operands are loaded one block ahead.
     if (wv == 0) {
-        const int r0 = lane, r1 = lane + 64;
-        double y0 = (r0 < nb) ? F.z[r0] : 0.0, y1 = (r1 < nb) ? F.z[r1] : 0.0;
-        double lt0[8], lt1[8], ndr[8];
-        int kb = nb - 8;
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            lt0[v] = A[r0 * AS + kb + v];
-            lt1[v] = A[(r1 & (NP - 1)) * AS + kb + v];
-            ndr[v] = F.ND[kb >> 3][(lane & 7) * 8 + v];
-        }
-        for (; kb >= 0; kb -= 8) {
-            const int kn = kb >= 8 ? kb - 8 : 0;
-            double nlt0[8], nlt1[8], nndr[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                nlt0[v] = A[r0 * AS + kn + v];
-                nlt1[v] = A[(r1 & (NP - 1)) * AS + kn + v];
-                nndr[v] = F.ND[kn >> 3][(lane & 7) * 8 + v];
-            }
-            const bool hi = kb >= 64;
-            const double ysrc = hi ? y1 : y0;
-            double yb[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) yb[w] = readlane_d(ysrc, (kb + w) & 63);
-            const double xv = ((ndr[0] * yb[0] + ndr[1] * yb[1]) + (ndr[2] * yb[2] + ndr[3] * yb[3])) +
-                              ((ndr[4] * yb[4] + ndr[5] * yb[5]) + (ndr[6] * yb[6] + ndr[7] * yb[7]));
-            double xb[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, ((kb & 63) + v));
-            const double s0 = ((lt0[0] * xb[0] + lt0[1] * xb[1]) + (lt0[2] * xb[2] + lt0[3] * xb[3])) +
-                              ((lt0[4] * xb[4] + lt0[5] * xb[5]) + (lt0[6] * xb[6] + lt0[7] * xb[7]));
-            const double s1 = ((lt1[0] * xb[0] + lt1[1] * xb[1]) + (lt1[2] * xb[2] + lt1[3] * xb[3])) +
-                              ((lt1[4] * xb[4] + lt1[5] * xb[5]) + (lt1[6] * xb[6] + lt1[7] * xb[7]));
-            y0 = (r0 < kb) ? y0 - s0 : ((r0 < kb + 8) ? xv : y0);
-            y1 = (r1 < kb) ? y1 - s1 : ((r1 < kb + 8) ? xv : y1);
-#pragma unroll
-            for (int v = 0; v < 8; ++v) { lt0[v] = nlt0[v]; lt1[v] = nlt1[v]; ndr[v] = nndr[v]; }
-        }
-        if (r0 < NE) xsol[r0] = y0;
-        if (r1 < NE) xsol[r1] = y1;
+        double y0 = (lane < nb) ? F.z[lane] : 0.0, y1 = (lane + 64 < nb) ? F.z[lane + 64] : 0.0;
+        backsub_block<120>(A, F, nb, lane, y0, y1);
+        backsub_block<112>(A, F, nb, lane, y0, y1);
+        backsub_block<104>(A, F, nb, lane, y0, y1);
+        backsub_block<96>(A, F, nb, lane, y0, y1);
+        backsub_block<88>(A, F, nb, lane, y0, y1);
+        backsub_block<80>(A, F, nb, lane, y0, y1);
+        backsub_block<72>(A, F, nb, lane, y0, y1);
+        backsub_block<64>(A, F, nb, lane, y0, y1);
+        backsub_block<56>(A, F, nb, lane, y0, y1);
+        backsub_block<48>(A, F, nb, lane, y0, y1);
+        backsub_block<40>(A, F, nb, lane, y0, y1);
+        backsub_block<32>(A, F, nb, lane, y0, y1);
+        backsub_block<24>(A, F, nb, lane, y0, y1);
+        backsub_block<16>(A, F, nb, lane, y0, y1);
+        backsub_block<8>(A, F, nb, lane, y0, y1);
+        backsub_block<0>(A, F, nb, lane, y0, y1);
+        if (lane < NE) xsol[lane] = y0;
+        if (lane + 64 < NE) xsol[lane + 64] = y1;
     }
     __syncthreads();
     STAMP(13);
