@@ -150,21 +150,27 @@ __device__ inline void d_q_mul(const double* a, const double* b, double o[4]) {
     o[0] = w; o[1] = x; o[2] = y; o[3] = z;
 }
 
-// Sophus SE3::exp, twist (upsilon, omega) -> (q, t)   (Sophus 1.0 se3.hpp)
-__device__ inline void d_se3_exp(const double a[6], double q[4], double t[3]) {
+// rotation angle of a twist (upsilon, omega): theta = |omega|
+__device__ inline double d_twist_theta(const double a[6]) {
+    return sqrt(a[3] * a[3] + a[4] * a[4] + a[5] * a[5]);
+}
+
+// Sophus SE3::exp, twist (upsilon, omega) -> (q, t)   (Sophus 1.0 se3.hpp), with the
+// transcendentals given: sh, ch = sin, cos(theta / 2) and st, ct = sin, cos(theta)
+__device__ inline void d_se3_exp_trig(const double a[6], double sh, double ch, double st, double ct, double q[4],
+                                      double t[3]) {
     const double eps = 1e-10;
     const double* w = a + 3;
     const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     const double th = sqrt(th2);
-    const double half = 0.5 * th;
     double im, re;
     if (th < eps) {
         const double th4 = th2 * th2;
         im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
         re = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
     } else {
-        im = sin(half) / th;
-        re = cos(half);
+        im = sh / th;
+        re = ch;
     }
     q[0] = re; q[1] = im * w[0]; q[2] = im * w[1]; q[3] = im * w[2];
     double V[9];
@@ -176,12 +182,13 @@ __device__ inline void d_se3_exp(const double a[6], double q[4], double t[3]) {
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j)
                 Om2[3 * i + j] = Om[3 * i] * Om[j] + Om[3 * i + 1] * Om[3 + j] + Om[3 * i + 2] * Om[6 + j];
-        const double c1 = (1.0 - cos(th)) / th2;
-        const double c2 = (th - sin(th)) / (th2 * th);
+        const double c1 = (1.0 - ct) / th2;
+        const double c2 = (th - st) / (th2 * th);
         for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * Om[i] + c2 * Om2[i];
     }
     for (int i = 0; i < 3; ++i) t[i] = V[3 * i] * a[0] + V[3 * i + 1] * a[1] + V[3 * i + 2] * a[2];
 }
+
 
 // estimate_ (row-major [R|t]) -> pose table entry for camera extrinsic e (LH_EXT layout)
 __device__ inline void d_pose_table(const double* T12, const double* __restrict__ e, double* pt) {
@@ -1177,6 +1184,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
     __shared__ double s_pm[2][LH_PMAX * 12];
+    __shared__ double s_trig[LH_PMAX][4], s_qT[LH_PMAX][4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
@@ -1402,9 +1410,10 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
     if (lane == 0) s_red[wave] = sp;
     const int cand = 1 - cur;
-    if (tid < P) {
-        const int pidx = tid;
-        double up[6];
+    // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix(), one pose per
+    // lane in three steps: (1) wave 0 sin/cos(theta/2), wave 1 sin/cos(theta), wave 2 the current
+    // quaternion; (2) wave 0 composes; (3) one lane per (pose, camera) builds the pose table
+    auto pose_step = [&](int pidx, double up[6]) {
         bool bad = false;
 #pragma unroll
         for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
@@ -1412,29 +1421,46 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #pragma unroll
             for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
         }
-        // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix()
-        double qe[4], te[3], qT[4], qn[4], tr[3], Rn[9];
-        d_se3_exp(up, qe, te);
-        double Tc[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) Tc[i] = s_pm[cur][pidx * 12 + i];
+    };
+    if (wave < 2 && lane < P) {
+        double up[6];
+        pose_step(lane, up);
+        const double th = d_twist_theta(up);
+        double sn, cs;
+        sincos(wave == 0 ? 0.5 * th : th, &sn, &cs);
+        s_trig[lane][2 * wave] = sn;
+        s_trig[lane][2 * wave + 1] = cs;
+    } else if (wave == 2 && lane < P) {
+        const double* Tc = &s_pm[cur][lane * 12];
         const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
+        d_q_from_R(Rc, s_qT[lane]);
+    }
+    __syncthreads();
+    if (wave == 0 && lane < P) {
+        const int pidx = lane;
+        double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
+        pose_step(pidx, up);
+        d_se3_exp_trig(up, s_trig[pidx][0], s_trig[pidx][1], s_trig[pidx][2], s_trig[pidx][3], qe, te);
+        const double* Tc = &s_pm[cur][pidx * 12];
         const double tc[3] = {Tc[3], Tc[7], Tc[11]};
-        d_q_from_R(Rc, qT);
-        d_q_mul(qe, qT, qn);
+        d_q_mul(qe, s_qT[pidx], qn);
         d_q_rotate(qe, tc, tr);
         d_R_from_q(qn, Rn);
-        double To[12];
+        double* To = &s_pm[cand][pidx * 12];   // the candidate buffer's LDS copy is free after the solve
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
             To[4 * i + 3] = te[i] + tr[i];
         }
-        double* Tg = pose_mat + ((size_t)cand * P + pidx) * 12;
+    }
+    __syncthreads();
+    if (tid < 12 * P) pose_mat[(size_t)cand * P * 12 + tid] = s_pm[cand][tid];
+    if (tid >= 64 && tid < 64 + P * prm.ncam) {
+        const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
+        double To[12];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) Tg[i] = To[i];
-        for (int cam = 0; cam < prm.ncam; ++cam)
-            d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
+        for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pidx * 12 + i];
+        d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
     }
     __syncthreads();
     if (tid == 0) {

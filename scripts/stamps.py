@@ -12,7 +12,7 @@ from windows import window  # noqa: E402
 
 NAMES = {0: "lin:backsub", 1: "lin:linearize", 2: "lin:Hll+chol", 3: "lin:G+bsd", 4: "lin:pose-tasks",
          5: "lin:G-image", 6: "lin:mfma", 7: "lin:combine+slab", 10: "ctrl:dx scatter", 11: "ctrl:S+perm+load",
-         12: "ctrl:factor8 (w0)", 13: "ctrl:back-subst", 14: "ctrl:poses", 15: "ctrl:LDLT panel", 16: "ctrl:LDLT update", 17: "ctrl:LM logic", 18: "ctrl:block0", 19: "ctrl:commit+dg", 21: "ctrl:rank", 22: "ctrl:upd tiles w0", 23: "ctrl:upd tiles w1-7", 20: "reduce"}
+         12: "ctrl:diag tile+factor (w0)", 13: "ctrl:back-subst", 14: "ctrl:poses", 16: "ctrl:LDLT steps", 17: "ctrl:LM logic", 18: "ctrl:block0", 19: "ctrl:commit+dg", 21: "ctrl:rank", 20: "reduce"}
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 w = window(cfg, seed=0, family="stable_noout")
