@@ -1265,7 +1265,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                 const bool ok = rho > 0 && isfinite(tchi);
                 if (prm.strategy == 0) {
                     if (ok) {
-                        double alpha = 1.0 - pow((2 * rho - 1), 3);
+                        const double m = 2 * rho - 1;
+                        double alpha = 1.0 - m * m * m;   // std::pow(2 rho - 1, 3), problem.cpp:541 (within an ulp)
                         alpha = fmin(alpha, 2.0 / 3.0);
                         lam *= fmax(1.0 / 3.0, alpha);
                         ni = 2;
@@ -1341,27 +1342,25 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     STAMP(19);
     {
         // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation.
-        // Four threads per row, each counting over 32 of the 128 keys (dg[n..NP) are NaN).
-        const int row = tid >> 2, part = tid & 3;
+        // Eight threads per row, each counting over 16 of the 128 keys (dg[n..NP) are NaN).
+        const int row = tid >> 3, part = tid & 7;
         int r = 0;
         if (row < n) {
             double di = fabs(dg[row]);
             if (!(di == di)) di = -1.0;
+            double dj[16];
 #pragma unroll
-            for (int j0 = 0; j0 < 32; j0 += 8) {
-                double dj[8];
+            for (int u = 0; u < 16; ++u) dj[u] = dg[part * 16 + u];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) dj[u] = dg[part * 32 + j0 + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    double d = fabs(dj[u]);
-                    if (!(d == d)) d = -1.0;
-                    r += (d > di) || (d == di && part * 32 + j0 + u < row);
-                }
+            for (int u = 0; u < 16; ++u) {
+                double d = fabs(dj[u]);
+                if (!(d == d)) d = -1.0;
+                r += (d > di) || (d == di && part * 16 + u < row);
             }
         }
         r += __shfl_xor(r, 1);
         r += __shfl_xor(r, 2);
+        r += __shfl_xor(r, 4);
         if (part == 0 && row < NP) {
             const int rr = row < n ? r : row;
             perm[rr] = row;
