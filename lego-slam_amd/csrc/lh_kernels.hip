@@ -61,6 +61,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier ordering LDS only.  __syncthreads() also releases global memory, i.e. waits
+// (s_waitcnt vmcnt(0)) for every global store and prefetch load the wave has in flight; these
+// kernels never hand global data between threads of a workgroup, so that wait is pure stall
+// (measured: ~15k cycles per wave at the end of k_lin).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ============================================================================
 // Eigen / Sophus arithmetic and the per-edge path, in the reference's
 // expression order with contraction off.  This is a bitwise mirror of the
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         v_n = obs_uv[2 * (size_t)o + 1];
         r_n = rc2[(size_t)sbc * 64 + lane];
     }
-    __syncthreads();   // window tables
+    lds_barrier();   // window tables
 
     for (; sb < (int)sb_end; sb += LH_WAVES) {
         const lh_subbatch S = sbs[sb];   // scalar load (sb is wave-uniform)
@@ -687,7 +697,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         ndeg += __shfl_xor(ndeg, off);
         maxd = fmax(maxd, __shfl_xor(maxd, off));
     }
-    __syncthreads();
+    STAMP(9);
+    lds_barrier();
+    STAMP(8);
     double* smem = dsm;
     const int ntile = Cfg::NT * 256;
     const int ntask = U * LH_TASKS;
@@ -717,8 +729,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
                 else { sc[0] += chi_acc; sc[1] += scale_acc; sc[2] += ndeg; sc[3] = fmax(sc[3], maxd); }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
+    STAMP(9);
     const double* s0 = smem;
     const double* s1 = smem + LH_SLAB_STRIDE;
     double* gs = slabs + (size_t)chunk * LH_SLAB_STRIDE;
@@ -726,8 +739,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = s0[LH_SLAB_TASK_OFF + i] + s1[LH_SLAB_TASK_OFF + i];
     if (tid < 3) gs[LH_SLAB_SC_OFF + tid] = s0[LH_SLAB_SC_OFF + tid] + s1[LH_SLAB_SC_OFF + tid];
     if (tid == 3) gs[LH_SLAB_SC_OFF + 3] = fmax(s0[LH_SLAB_SC_OFF + 3], s1[LH_SLAB_SC_OFF + 3]);
-    STAMP(7);
-    STAMP_FLUSH(0, 8);
+    STAMP(10);
+    STAMP_FLUSH(0, 11);
 }
 
 // ============================================================================
@@ -762,7 +775,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
             mx = fmax(mx, __shfl_xor(mx, off));
         }
         if (lane == 0) { part[0][wave][0] = s0; part[1][wave][0] = s1; part[2][wave][0] = s2; part[0][wave][1] = mx; }
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) {
             double a0 = 0.0, a1 = 0.0, a2 = 0.0, m = 0.0;
             for (int w = 0; w < RW; ++w) { a0 += part[0][w][0]; a1 += part[1][w][0]; a2 += part[2][w][0]; m = fmax(m, part[0][w][1]); }
@@ -799,9 +812,9 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
         // a segment of the pair's item list into LDS (one global round trip), then every wave
         // walks its items (wave, wave + RW, ...) with four slab loads in flight
         const int nit = min(ie - seg, RI_MAX);
-        __syncthreads();
+        lds_barrier();
         for (int i = tid; i < nit; i += RT) sitems[i] = items[seg + i];
-        __syncthreads();
+        lds_barrier();
         int it = wave;
         for (; it + 3 * RW < nit; it += 4 * RW) {
             double x[4], y[4];
@@ -824,7 +837,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
     }
     part[0][wave][lane] = vs;
     part[1][wave][lane] = vh;
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
         double s = 0.0, h = 0.0;
         for (int w = 0; w < RW; ++w) { s += part[0][w][lane]; h += part[1][w][lane]; }
@@ -1104,7 +1117,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     if (wv == 0) factor_block8(A, F.N[0], F.ND[0], 0, lane);
-    __syncthreads();
+    lds_barrier();
     STAMP(18);
     for (int k0 = 0; k0 < nb; k0 += 8) {
         const int t = k0 >> 3, par = t & 1, m0 = k0 + 8;
@@ -1137,7 +1150,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 ldlt_tile_row(A, N, ND, k0, 16 * g0, 0, 0, -1, true, lane);   // row tg: L^T and rhs only
             }
         }
-        __syncthreads();
+        lds_barrier();
         STAMP(16);
     }
 
@@ -1163,7 +1176,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         if (lane < NE) xsol[lane] = y0;
         if (lane + 64 < NE) xsol[lane + 64] = y1;
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(13);
 
 #ifdef LH_STAMPS
@@ -1225,7 +1238,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
         for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
         if (lane == 0) s_red[wave] = mx;
-        __syncthreads();
+        lds_barrier();
     }
 
     // ---------------- LM bookkeeping (thread 0) ----------------
@@ -1313,7 +1326,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         s_flags[2] = cur;
         s_lam = lam;
     }
-    __syncthreads();
+    lds_barrier();
     const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
     if (done) return;
     const double lambda = s_lam;
@@ -1338,7 +1351,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
     }
     if (tid >= n && tid < NP) dg[tid] = __builtin_nan("");   // key -1 at an index above every real row: never counted
-    __syncthreads();
+    lds_barrier();
     STAMP(19);
     {
         // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation.
@@ -1367,7 +1380,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             iperm[row] = rr;
         }
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(21);
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
@@ -1386,14 +1399,14 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         const int r = n + x / NE, c = x - NE * (x / NE);
         if (c < r) A[r * AS + c] = 0.0;
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(11);
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
     STAMP_FLUSH(10, 14);
     lds_ldlt_solve(A, yv, n, NE, tid);
     if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
-    __syncthreads();
+    lds_barrier();
 #ifdef LH_STAMPS
     st0_ = __builtin_amdgcn_s_memtime();
     for (int i_ = 0; i_ < 24; ++i_) sacc_[i_] = 0;
@@ -1434,7 +1447,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
         d_q_from_R(Rc, s_qT[lane]);
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == 0 && lane < P) {
         const int pidx = lane;
         double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
@@ -1452,7 +1465,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             To[4 * i + 3] = te[i] + tr[i];
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 12 * P) pose_mat[(size_t)cand * P * 12 + tid] = s_pm[cand][tid];
     if (tid >= 64 && tid < 64 + P * prm.ncam) {
         const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
@@ -1461,7 +1474,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pidx * 12 + i];
         d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
     }
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
         double s2 = 0.0;
         for (int w = 0; w < CT / 64; ++w) s2 += s_red[w];
@@ -1578,7 +1591,7 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     __shared__ int perm[NP];
     const int tid = threadIdx.x, NE = (n + 15) & ~15;
     if (tid < NP) dg[tid] = tid < n ? S[(size_t)tid * n + tid] : __builtin_nan("");
-    __syncthreads();
+    lds_barrier();
     if (tid < n) {
         double di = fabs(dg[tid]);
         if (!(di == di)) di = -1.0;
@@ -1592,15 +1605,15 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     } else if (tid < NP) {
         perm[tid] = tid;
     }
-    __syncthreads();
+    lds_barrier();
     for (int e = tid; e < NE * NE; e += CT) {
         const int r = e / NE, c = e - NE * (e / NE);
         if (c <= r) A[r * AS + c] = (r < n) ? ((c < n) ? S[(size_t)perm[r] * n + perm[c]] : 0.0) : (r == c ? 1.0 : 0.0);
     }
     if (tid < NE) A[NP * AS + tid] = tid < n ? b[perm[tid]] : 0.0;
-    __syncthreads();
+    lds_barrier();
     lds_ldlt_solve(A, xsol, n, NE, tid);
-    __syncthreads();
+    lds_barrier();
     if (tid < n) x[perm[tid]] = xsol[tid];
 }
 

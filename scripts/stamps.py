@@ -11,7 +11,7 @@ import lego_ba  # noqa: E402
 from windows import window  # noqa: E402
 
 NAMES = {0: "lin:backsub", 1: "lin:linearize", 2: "lin:Hll+chol", 3: "lin:G+bsd", 4: "lin:pose-tasks",
-         5: "lin:G-image", 6: "lin:mfma", 7: "lin:combine+slab", 10: "ctrl:dx scatter", 11: "ctrl:S+perm+load",
+         5: "lin:G-image", 6: "lin:mfma", 7: "lin:combine", 8: "lin:epilogue barrier", 9: "lin:shfl reductions", 10: "lin:slab write", 11: "ctrl:S+perm+load",
          12: "ctrl:diag tile+factor (w0)", 13: "ctrl:back-subst", 14: "ctrl:poses", 16: "ctrl:LDLT steps", 17: "ctrl:LM logic", 18: "ctrl:block0", 19: "ctrl:commit+dg", 21: "ctrl:rank", 20: "reduce"}
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
@@ -25,7 +25,7 @@ trials = 0
 for _ in range(n):
     trials += s.solve_resident()["trials"] + 1
 st = lego_ba.debug_stamps(reset=True)
-lin = sum(int(st[i]) for i in range(8))
+lin = sum(int(st[i]) for i in range(10))  # 10 is shared with ctrl:dx scatter
 ctrl = sum(int(st[i]) for i in range(10, 24) if i != 20)
 print(f"{cfg}: {trials} k_lin launches; totals (wave-cycles/launch): lin {lin / trials:.3e} ctrl {ctrl / trials:.3e} reduce {int(st[20]) / trials:.3e}")
 for i, nm in NAMES.items():
