@@ -364,17 +364,38 @@ __device__ __forceinline__ double dpp_d(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ __forceinline__ double group_sum(double v, int lg) {
-    if (lg >= 1) v += dpp_d<0xB1>(v);                       // quad_perm [1,0,3,2]: lane ^ 1
-    if (lg >= 2) v += dpp_d<0x4E>(v);                       // quad_perm [2,3,0,1]: lane ^ 2
-    if (lg >= 3) {                                          // lane ^ 4: row_ror 12 / row_ror 4
-        const double a = dpp_d<0x12C>(v), b = dpp_d<0x124>(v);
-        v += (__lane_id() & 4) ? b : a;
+// N values at once: one uniform branch per level and N independent DPP + add chains per level
+// (a sum at a time serialises the branches and the DPP latencies)
+template <int N>
+__device__ __forceinline__ void group_sum(double (&v)[N], int lg) {
+    if (lg >= 1) {                                          // quad_perm [1,0,3,2]: lane ^ 1
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] += dpp_d<0xB1>(v[i]);
     }
-    if (lg >= 4) v += dpp_d<0x128>(v);                      // row_ror 8: lane ^ 8
-    if (lg >= 5) v += __shfl_xor(v, 16);
-    if (lg >= 6) v += __shfl_xor(v, 32);
-    return v;
+    if (lg >= 2) {                                          // quad_perm [2,3,0,1]: lane ^ 2
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] += dpp_d<0x4E>(v[i]);
+    }
+    if (lg >= 3) {                                          // lane ^ 4: row_ror 12 / row_ror 4
+        const bool up = (__lane_id() & 4) != 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const double a = dpp_d<0x12C>(v[i]), b = dpp_d<0x124>(v[i]);
+            v[i] += up ? b : a;
+        }
+    }
+    if (lg >= 4) {                                          // row_ror 8: lane ^ 8
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] += dpp_d<0x128>(v[i]);
+    }
+    if (lg >= 5) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], 16);
+    }
+    if (lg >= 6) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], 32);
+    }
 }
 
 template <int T, bool TRIAL>
@@ -504,7 +525,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 #pragma unroll
                 for (int c = 0; c < 3; ++c) v3[c] = E.Jl[c] * y0 + E.Jl[3 + c] * y1;
             }
-            const double s0 = group_sum(v3[0], lg), s1 = group_sum(v3[1], lg), s2 = group_sum(v3[2], lg);
+            group_sum(v3, lg);
+            const double s0 = v3[0], s1 = v3[1], s2 = v3[2];
             if (lmok) {
                 // the cached factor holds 1/L_ii on the diagonal
                 const double i00 = cl[0], l10 = cl[1], i11 = cl[2], l20 = cl[3], l21 = cl[4], i22 = cl[5];
@@ -579,11 +601,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         STAMP(1);
 
         // ---- per-landmark H_ll, b_l over the lane group; Cholesky (redundant per lane) ----
-        double h[9];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) h[i] = group_sum(hll[i], lg);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) h[6 + i] = group_sum(bl[i], lg);
+        double h[9] = {hll[0], hll[1], hll[2], hll[3], hll[4], hll[5], bl[0], bl[1], bl[2]};
+        group_sum(h, lg);
         // Cholesky of H_ll through reciprocal square roots: i_jj = 1/L_jj directly
         double i00 = fast_rsq(h[0]);
         const double l10 = h[1] * i00, l20 = h[2] * i00;
