@@ -500,6 +500,16 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             for (int i = 0; i < 12; ++i) cl[i] = myrec[LH_REC_L + i];
         }
         wave_sync();
+        {
+            // the pose-sum image [landmark][slot][33] starts at zero: cells without a live
+            // observation then add exact zeros, and the per-slot sums need no masks or branches
+            double2* z = reinterpret_cast<double2*>(scr);
+            constexpr int nz = (LH_SB_LM * Cfg::UMAX * LH_TASKS) / 2;
+#pragma unroll
+            for (int k = 0; k < (nz + 63) / 64; ++k)
+                if (k * 64 + lane < nz) z[k * 64 + lane] = double2{0.0, 0.0};
+        }
+        wave_sync();
 
         const bool has = (meta & LH_META_VALID) != 0u;
         const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta);
@@ -554,7 +564,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         double hpl[18];
 #pragma unroll
         for (int i = 0; i < 18; ++i) hpl[i] = 0.0;
-        double* trow = scr + (slot * LH_SB_LM + (ls & 7)) * LH_TASKS;   // [slot][landmark][33]: unique writer
+        // [landmark][slot][33]: unique writer; a wave's 16-lane store group covers distinct cells
+        double* trow = scr + ((ls & 7) * Cfg::UMAX + slot) * LH_TASKS;
         if (has) {
             const double* pt = wt_n + (slot * ncam + cam) * LH_PT;
             EdgeEval E;
@@ -643,32 +654,25 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
                 G[3 * a] = g0; G[3 * a + 1] = g1; G[3 * a + 2] = g2;
                 trow[27 + a] = g0 * w0 + g1 * w1 + g2 * w2;
             }
-        } else if (live) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) trow[27 + a] = 0.0;
         }
         STAMP(3);
 
         // ---- per-pose sums (H_pp, b_p, bsd): lane k < 33 adds task k of every landmark observing
         //      the slot, in landmark (= lane) order ----
         wave_sync();
-        {
-            const int G = 1 << lg;
-            const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+        if (lane < LH_TASKS) {
+            // every (landmark, slot) cell in landmark order: absent cells are +0.0, and adding
+            // them leaves every sum bit-identical to adding the present cells only
 #pragma unroll
             for (int uu = 0; uu < Cfg::UMAX; ++uu) {
                 if (uu < U) {
-                    const uint64_t mk = __ballot(live && slot == uu);
-                    if (mk && lane < LH_TASKS) {
-                        double tv[LH_SB_LM];
+                    double tv[LH_SB_LM];
 #pragma unroll
-                        for (int l = 0; l < LH_SB_LM; ++l) tv[l] = scr[(uu * LH_SB_LM + l) * LH_TASKS + lane];
-                        double sacc = task[uu];
+                    for (int l = 0; l < LH_SB_LM; ++l) tv[l] = scr[(l * Cfg::UMAX + uu) * LH_TASKS + lane];
+                    double sacc = task[uu];
 #pragma unroll
-                        for (int l = 0; l < LH_SB_LM; ++l)
-                            if (l < nlm && ((mk >> (l << lg)) & gmask)) sacc += tv[l];
-                        task[uu] = sacc;
-                    }
+                    for (int l = 0; l < LH_SB_LM; ++l) sacc += tv[l];
+                    task[uu] = sacc;
                 }
             }
         }
