@@ -163,6 +163,9 @@ int lh_debug_mfma_probe(const double *A, const double *B, double *D);
 /* k_ctrl's reduced-system solve (Eigen-LDLT pivot order, blocked LDL^T, back substitution) on a
    dense symmetric n x n S (row-major), n <= 128: x = S^-1 b.  Device pointers. */
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x);
+/* mean HIP-event bracket (ms) of an empty kernel on the handle's stream: the launch floor of the
+   per-kernel times lh_set_profiling reports (bench.py subtracts it for the roofline) */
+int lh_debug_event_floor(lh_handle *h, double *ms);
 /* per-phase wave-cycle totals of a -DLH_STAMPS diagnostic build (all zero in the product build) */
 int lh_debug_stamps(unsigned long long *out, int n, int reset);
 

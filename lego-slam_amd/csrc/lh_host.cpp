@@ -30,6 +30,7 @@
 
 extern "C" {
 hipError_t lh_prepare_lin();
+hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
@@ -896,13 +897,39 @@ int lh_debug_stamps(unsigned long long* out, int n, int reset) {
     return lh_read_stamps(out, n, reset) == hipSuccess ? LH_OK : LH_E_HIP;
 }
 
-// test hook: f64 MFMA accumulator layout probe (A 16x4 row-major, B 4x16, D 16x16), device pointers
+// test hook: k_ctrl's reduced-system solve on a dense symmetric S, device pointers
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x) {
     if (!S || !b || !x) return LH_E_BADARG;
     if (n < 1 || n > LH_NPAD) return LH_E_UNSUPPORTED;
     HIPCHK(lh_launch_ldlt_probe(S, b, n, x));
     HIPCHK(hipDeviceSynchronize());
     return LH_OK;
+}
+
+// The per-kernel HIP-event bracket of lh_set_profiling includes the launch itself: this is the
+// same bracket around an empty kernel on the handle's stream (mean of 64 after 8 warm-ups).
+int lh_debug_event_floor(lh_handle* h, double* ms) {
+    if (!h || !ms) return LH_E_BADARG;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return LH_E_HIP;
+    if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return LH_E_HIP; }
+    double tot = 0.0;
+    int st = LH_OK;
+    for (int i = 0; i < 72 && st == LH_OK; ++i) {
+        if (hipEventRecord(a, h->stream) != hipSuccess || lh_launch_nop(h->stream) != hipSuccess ||
+            hipEventRecord(b, h->stream) != hipSuccess || hipEventSynchronize(b) != hipSuccess) {
+            st = LH_E_HIP;
+            break;
+        }
+        float e = 0.f;
+        if (hipEventElapsedTime(&e, a, b) != hipSuccess) st = LH_E_HIP;
+        if (i >= 8) tot += e;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (st == LH_OK) *ms = tot / 64.0;
+    return st;
 }
 
 int lh_debug_mfma_probe(const double* A, const double* B, double* D) {

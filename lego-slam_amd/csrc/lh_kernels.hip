@@ -1646,6 +1646,14 @@ hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double*
     return hipGetLastError();
 }
 
+// ---- empty kernel: the HIP-event bracket floor of one launch (bench.py's roofline timing) ----
+__global__ void k_nop() {}
+
+hipError_t lh_launch_nop(hipStream_t st) {
+    hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, st);
+    return hipGetLastError();
+}
+
 // ---- MFMA f64 layout probe (tests): D = A * B for 16x4 A, 4x16 B ----
 __global__ void k_mfma_probe(const double* A, const double* B, double* D) {
     const int l = threadIdx.x;

@@ -320,6 +320,14 @@ class Solver:
     def set_profiling(self, on):
         _check(ba_lib().lh_set_profiling(self.h, int(on)), "lh_set_profiling")
 
+    def event_floor_ms(self):
+        """HIP-event bracket of an empty kernel on this solver's stream (lh_debug_event_floor)."""
+        ms = C.c_double(0.0)
+        lib = ba_lib()
+        lib.lh_debug_event_floor.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        _check(lib.lh_debug_event_floor(self.h, C.byref(ms)), "lh_debug_event_floor")
+        return ms.value
+
 
 def debug_stamps(reset=True):
     """Per-phase wave-cycle totals from the LH_STAMPS diagnostic build (zeros otherwise)."""
