@@ -200,6 +200,25 @@ def main():
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": bytes_per,
                          "traffic": traffic},
     }
+    # the same window through the PCG reduced solve (BASELINE config 3 names "Schur + PCG"; the
+    # reference's own solver, and value above, is the LDLT): reported beside value, never as it
+    if world == 1:
+        sp = lego_ba.Solver(device=local, linear_solver=lego_ba.LH_SOLVER_PCG)
+        sp.upload(w)
+        sp.solve_resident()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        pits = pcgs = 0
+        for _ in range(args.steps):
+            r = sp.solve_resident()
+            pits += r["iterations"]
+            pcgs += r["pcg_iterations"]
+        torch.cuda.synchronize()
+        dtp = time.perf_counter() - t
+        out["pcg"] = {"ms_per_solve": round(dtp / args.steps * 1e3, 4), "iterations_per_s": round(pits / dtp, 3),
+                      "iterations_per_solve": pits / args.steps, "pcg_steps_per_solve": pcgs / args.steps,
+                      "chi2_rel_vs_ldlt": abs(r["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
+        sp.close()
     # end-to-end host-buffer call (lh_solve: upload + solve + download over PCIe), rank 0 only
     if world == 1:
         solver_h = lego_ba.Solver(device=local)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define LH_ABI_VERSION 1
+#define LH_ABI_VERSION 2
 
 typedef enum lh_status {
     LH_OK = 0,
@@ -52,7 +52,8 @@ typedef enum lh_status {
 typedef enum lh_strategy { LH_STRATEGY_DEFAULT = 0, LH_STRATEGY_1 = 1 } lh_strategy;
 
 /* Reduced pose-system solver: the reference uses Eigen LDLT (problem.cpp:420);
-   PCG is the correct Jacobi-PCG the reference left commented out (:422). */
+   PCG is the reference's Jacobi-PCG (Problem::PCGSolver, :584-614), which it left commented out
+   (:422), with its first-step bug fixed (:595-596 never add alpha*p to x). */
 typedef enum lh_linear_solver { LH_SOLVER_LDLT = 0, LH_SOLVER_PCG = 1 } lh_linear_solver;
 
 typedef struct lh_options {
@@ -74,6 +75,8 @@ typedef struct lh_options {
                                  problem.cpp:396-400); 1: skip such landmarks' Schur terms    */
     int32_t trials_per_sync;  /* LM trials kept in flight ahead of the host poll (0: auto = 2)  */
     int32_t profile;          /* 1: time every kernel with HIP events (lh_kernel_stats)       */
+    int32_t pcg_max_iters;    /* PCG: iteration cap; <= 0: 2 * rows (problem.cpp:422)          */
+    double pcg_tol;           /* PCG: stop when ||r|| <= pcg_tol * ||b|| (1e-6, problem.cpp:597) */
     uint8_t comm_id[128];     /* ncclUniqueId from lh_comm_unique_id on rank 0 (world_size>1) */
 } lh_options;
 
@@ -118,6 +121,7 @@ typedef struct lh_result {
     double chi2_final;         /* currentChi_ at exit                                              */
     double lambda_final;
     double time_ms;            /* wall time of the LM solve on the device (excludes upload)        */
+    int32_t pcg_iterations;    /* PCG iterations summed over all trials (0 with LH_SOLVER_LDLT)    */
 } lh_result;
 
 typedef struct lh_kernel_stats {
@@ -163,6 +167,9 @@ int lh_debug_mfma_probe(const double *A, const double *B, double *D);
 /* k_ctrl's reduced-system solve (Eigen-LDLT pivot order, blocked LDL^T, back substitution) on a
    dense symmetric n x n S (row-major), n <= 128: x = S^-1 b.  Device pointers. */
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x);
+/* k_ctrl's PCG solve (same LDS layout and pivot order) on a dense symmetric n x n S, n <= 128:
+   x ~= S^-1 b to ||r|| <= tol ||b|| within max_iters (<= 0: 2n).  Device pointers; *iters host. */
+int lh_debug_pcg_probe(const double* S, const double* b, int n, double tol, int max_iters, double* x, int* iters);
 /* mean HIP-event bracket (ms) of an empty kernel on the handle's stream: the launch floor of the
    per-kernel times lh_set_profiling reports (bench.py subtracts it for the roofline) */
 int lh_debug_event_floor(lh_handle *h, double *ms);

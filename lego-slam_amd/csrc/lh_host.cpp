@@ -40,11 +40,12 @@ hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double
                             double* maxd, lh_params prm, int n_chunks);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
-                          lh_params prm, int mode, int* host_done);
+                          lh_params prm, int mode, int* host_done, int seq);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, long nrec_doubles, double* qt,
                            const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab, double* dxp,
                            int ndxp, lh_ctrl* ctrl);
-hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x);
+hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x, int solver, double tol, int max_it,
+                                int* iters);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
 }
@@ -205,6 +206,7 @@ struct lh_handle {
 namespace {
 
 bool g_debug = getenv("LH_DEBUG") != nullptr;
+bool g_event_sync = getenv("LH_EVENT_SYNC") != nullptr;   // A/B: the per-trial event scheme
 
 #define HIPCHK(x)                                                                                        \
     do {                                                                                                 \
@@ -505,6 +507,9 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     prm.tau = h->opt.tau;
     prm.lambda_cap = h->opt.lambda_cap;
     prm.lambda_init = h->opt.lambda_init;
+    prm.solver = h->opt.linear_solver;
+    prm.pcg_tol = h->opt.pcg_tol;
+    prm.pcg_max_it = h->opt.pcg_max_iters;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     h->LY = lh_rs_make(P);
     h->L_act = (int)h->lm_perm.size();   // landmark records (padded to 8 per sub-batch)
@@ -604,7 +609,7 @@ int enqueue_trial(lh_handle* h, int mode) {
     {
         Prof pr(h, KC_CTRL);
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p, h->d_ptab.p,
-                              h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done));
+                              h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -620,7 +625,9 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     // host; k_ctrl raises the mapped done flag and any trial enqueued after it is a no-op.
     hipEvent_t e0 = next_event(h), e1 = next_event(h);
     if (!e0 || !e1) return LH_E_HIP;
-    *h->h_done = 0;
+    volatile int* hd = h->h_done;   // [0] done, [1] last trial whose k_ctrl has started
+    hd[0] = 0;
+    hd[1] = -1;
     HIPCHK(hipEventRecord(e0, s));
     HIPCHK(lh_launch_reset(s, h->d_rec.p, h->d_rec_init.p, LH_REC * (long)h->L_act, h->d_qt.p, h->d_qt_init.p, 24 * P,
                            h->d_ptab.p, h->d_ptab_init.p, (int)(2 * PT), h->d_dxp.p, 6 * std::max(P, 1), h->d_ctrl.p));
@@ -629,25 +636,46 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     if (st != LH_OK) return st;
     const int max_total = (h->opt.max_iters > 0) ? h->opt.max_iters * std::max(1, h->opt.max_trials) : 0;
     const int depth = h->opt.trials_per_sync > 0 ? std::min(h->opt.trials_per_sync, 32) : 2;
-    hipEvent_t ring[64];
-    int head = 0, tail = 0, enq = 0;
-    auto push = [&]() -> int {
-        int r = enqueue_trial(h, 1);
-        if (r != LH_OK) return r;
-        hipEvent_t ev = next_event(h);
-        if (!ev) return LH_E_HIP;
-        if (hipEventRecord(ev, s) != hipSuccess) return LH_E_HIP;
-        ring[tail++ & 63] = ev;
-        ++enq;
-        return LH_OK;
-    };
-    while (enq < max_total && tail - head < depth)
-        if ((st = push()) != LH_OK) return st;
-    while (head < tail) {
-        HIPCHK(hipEventSynchronize(ring[head++ & 63]));
-        if (*(volatile int*)h->h_done) break;
-        if (enq < max_total)
+    int enq = 0;
+    if (g_event_sync) {
+        // previous scheme (A/B reference): one event per trial, host waits on the oldest
+        hipEvent_t ring[64];
+        int head = 0, tail = 0;
+        auto push = [&]() -> int {
+            int r = enqueue_trial(h, 1);
+            if (r != LH_OK) return r;
+            hipEvent_t ev = next_event(h);
+            if (!ev) return LH_E_HIP;
+            if (hipEventRecord(ev, s) != hipSuccess) return LH_E_HIP;
+            ring[tail++ & 63] = ev;
+            ++enq;
+            return LH_OK;
+        };
+        while (enq < max_total && tail - head < depth)
             if ((st = push()) != LH_OK) return st;
+        while (head < tail) {
+            HIPCHK(hipEventSynchronize(ring[head++ & 63]));
+            if (hd[0]) break;
+            if (enq < max_total)
+                if ((st = push()) != LH_OK) return st;
+        }
+    } else {
+        // No per-trial events: k_ctrl writes the trial it starts into the mapped progress word,
+        // and the host keeps `depth` trials enqueued past it until the device raises done.
+        // hipStreamQuery every few thousand polls turns a device fault into an error return.
+        unsigned spin = 0;
+        while (!hd[0] && enq < max_total) {
+            if (enq - hd[1] < depth) {
+                if ((st = enqueue_trial(h, 1)) != LH_OK) return st;
+                ++enq;
+                continue;
+            }
+            if ((++spin & 4095) == 0) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q != hipSuccess && q != hipErrorNotReady) return LH_E_HIP;
+            }
+            __builtin_ia32_pause();
+        }
     }
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipMemcpyAsync(h->h_ctrl, h->d_ctrl.p, sizeof(lh_ctrl), hipMemcpyDeviceToHost, s));
@@ -665,6 +693,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         out->chi2_final = c.chi;
         out->lambda_final = c.lambda;
         out->time_ms = ms;
+        out->pcg_iterations = c.pcg_iters;
         out->trace_len = std::min(c.trace_len, std::min(out->trace_cap, LH_TRACE));
         for (int i = 0; i < out->trace_len; ++i) {
             if (out->trace_chi2) out->trace_chi2[i] = c.trace_chi[i];
@@ -744,6 +773,8 @@ void lh_default_options(lh_options* o) {
     o->degenerate_guard = 0;
     o->trials_per_sync = 0;
     o->profile = 0;
+    o->pcg_max_iters = 0;
+    o->pcg_tol = 1e-6;
 }
 
 int lh_comm_unique_id(uint8_t out[128]) {
@@ -762,7 +793,8 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     if (opt->max_iters < 0 || opt->max_trials < 0 || opt->world_size < 1 || opt->rank < 0 ||
         opt->rank >= opt->world_size || (opt->strategy != 0 && opt->strategy != 1))
         return LH_E_BADARG;
-    if (opt->linear_solver != LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
+    if (opt->linear_solver != LH_SOLVER_LDLT && opt->linear_solver != LH_SOLVER_PCG) return LH_E_BADARG;
+    if (opt->linear_solver == LH_SOLVER_PCG && !(opt->pcg_tol >= 0.0)) return LH_E_BADARG;
     lh_handle* h = new (std::nothrow) lh_handle();
     if (!h) return LH_E_HIP;
     h->opt = *opt;
@@ -775,7 +807,7 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     if (lh_prepare_lin() != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipHostMalloc((void**)&h->h_ctrl, sizeof(lh_ctrl), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_done, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_done, 2 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&h->d_done, h->h_done, 0) != hipSuccess) {
         lh_destroy(h);
         return LH_E_HIP;
@@ -901,8 +933,22 @@ int lh_debug_stamps(unsigned long long* out, int n, int reset) {
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x) {
     if (!S || !b || !x) return LH_E_BADARG;
     if (n < 1 || n > LH_NPAD) return LH_E_UNSUPPORTED;
-    HIPCHK(lh_launch_ldlt_probe(S, b, n, x));
+    HIPCHK(lh_launch_ldlt_probe(S, b, n, x, 0, 0.0, 0, nullptr));
     HIPCHK(hipDeviceSynchronize());
+    return LH_OK;
+}
+
+int lh_debug_pcg_probe(const double* S, const double* b, int n, double tol, int max_iters, double* x, int* iters) {
+    if (!S || !b || !x || !(tol >= 0.0)) return LH_E_BADARG;
+    if (n < 1 || n > LH_NPAD) return LH_E_UNSUPPORTED;
+    int* d_it = nullptr;
+    HIPCHK(hipMalloc(&d_it, sizeof(int)));
+    hipError_t e = lh_launch_ldlt_probe(S, b, n, x, 1, tol, max_iters, d_it);
+    int it = 0;
+    if (e == hipSuccess) e = hipMemcpy(&it, d_it, sizeof(int), hipMemcpyDeviceToHost);
+    (void)hipFree(d_it);
+    if (e != hipSuccess) return LH_E_HIP;
+    if (iters) *iters = it;
     return LH_OK;
 }
 

@@ -1207,18 +1207,112 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
 #endif
 }
 
+// Phases 3-4 of k_ctrl, PCG variant (lh_options.linear_solver = LH_SOLVER_PCG): Jacobi-preconditioned
+// conjugate gradients on the same permuted, padded system (A lower triangle + rhs row NP).  This is
+// the solver the reference left commented out (problem.cpp:421-422 -> Problem::PCGSolver :584-614)
+// with its stop rule, ||r|| <= 1e-6 ||b|| (:597), and iteration cap, 2 * rows (:422), but corrected:
+// the reference never adds the first step alpha*p to x (:595-596); here every step is applied.
+// A zero diagonal entry (STRATEGY1 with a fixed pose: 0 + lambda*0) preconditions with 0 instead of
+// Eigen's inf (which would turn the whole step into NaN).
+// Layout: eight threads per row (row = tid >> 3), each holding 16 entries of its row in registers and
+// summing those columns of A p; every thread of a row keeps that row's x, r, p, 1/d.  Three barriers per iteration (A p | p.q | r.r and r.z, p).
+// At most max_it steps (callers pass the reference cap + 1: its first step precedes its loop).
+// Returns the iteration count.  Must be called by all CT threads; xsol[r] = x in pivot order.
+__device__ __forceinline__ int lds_pcg_solve(const double* __restrict__ A, double* __restrict__ xsol, double* __restrict__ pv,
+                             double* __restrict__ s_red2, int n, int tid, double tol_rel, int max_it) {
+    const int row = tid >> 3, part = tid & 7, lane = tid & 63, wave = tid >> 6;
+    const bool live = row < n;
+    auto Aij = [&](int i, int j) { return i >= j ? A[i * AS + j] : A[j * AS + i]; };
+    // this thread's 16 entries of its row, kept in registers for the whole solve (zero outside n x n)
+    double arow[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int c = part * 16 + u;
+        arow[u] = (live && c < n) ? Aij(row, c) : 0.0;
+    }
+    const double d = live ? Aij(row, row) : 0.0;
+    const double dinv = (d != 0.0) ? 1.0 / d : 0.0;
+    double r = live ? A[NP * AS + row] : 0.0;
+    double x = 0.0;
+    double z = r * dinv;
+    double p = z;
+    // wave partial of a per-row value (counted once per row: part 0), then the 16 waves in order
+    auto wsum = [&](double v) {
+        v = (part == 0) ? v : 0.0;
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        return v;
+    };
+    auto total = [&](int slot) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < CT / 64; ++w) t += s_red2[slot * 16 + w];
+        return t;
+    };
+    {
+        const double a = wsum(r * z), c = wsum(r * r);
+        if (lane == 0) { s_red2[wave] = a; s_red2[16 + wave] = c; }
+        if (part == 0 && row < NP) pv[row] = live ? p : 0.0;   // rows n..NP-1 stay 0
+    }
+    lds_barrier();
+    double rz = total(0);
+    const double bnorm = sqrt(total(1));
+    const double thr = tol_rel * bnorm;
+    int it = 0;
+    if (bnorm > 0.0) {
+#pragma clang loop unroll(disable)
+        while (it < max_it) {
+            // q = A p over this thread's 16 columns, then across the row's 8 threads
+            double q = 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) q += arow[u] * pv[part * 16 + u];
+            q += __shfl_xor(q, 1);
+            q += __shfl_xor(q, 2);
+            q += __shfl_xor(q, 4);
+            {
+                const double a = wsum(p * q);
+                if (lane == 0) s_red2[32 + wave] = a;
+            }
+            lds_barrier();
+            const double alpha = rz / total(2);
+            x += alpha * p;
+            r -= alpha * q;
+            z = r * dinv;
+            {
+                const double a = wsum(r * z), c = wsum(r * r);
+                if (lane == 0) { s_red2[wave] = a; s_red2[16 + wave] = c; }
+            }
+            ++it;
+            lds_barrier();
+            const double rzn = total(0), rr = total(1);
+            if (!(sqrt(rr) > thr)) break;       // also stops on NaN
+            const double beta = rzn / rz;
+            rz = rzn;
+            p = z + beta * p;
+            if (part == 0 && live) pv[row] = p;
+            lds_barrier();
+        }
+    }
+    if (part == 0 && live) xsol[row] = x;
+    lds_barrier();
+    return it;
+}
+
+template <int SOLVER>
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                              const uint32_t* __restrict__ rsmap,
                                              double* __restrict__ pose_mat, double* __restrict__ ptab,
                                              const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
-                                             int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done) {
+                                             int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done,
+                                             int seq) {
     __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
     __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP];
     __shared__ __attribute__((aligned(16))) double yv[NP];
     __shared__ int perm[NP], iperm[NP];
     __shared__ int s_flags[4];
-    __shared__ double s_red[CT / 64], s_lam;
+    __shared__ double s_red[CT / 64], s_lam, s_pcg[48];
     __shared__ double s_pm[2][LH_PMAX * 12];
     __shared__ double s_trig[LH_PMAX][4], s_qT[LH_PMAX][4];
 
@@ -1226,6 +1320,10 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
     const lh_rs_layout LY = lh_rs_make(P);
     STAMP_DECL
+
+    // host progress word: this trial's controller has started (its k_lin and k_reduce are done);
+    // the host keeps the queue filled from it instead of recording an event per trial
+    if (tid == 0 && host_done) host_done[1] = seq;
 
     // ---------------- 1. prefetch (one round trip); the controller's words first ----------------
     double chi = 0.0, lam = 0.0, ni = 0.0, last = 0.0, spose = 0.0, chi0 = 0.0, tchi = 0.0, sl = 0.0;
@@ -1427,7 +1525,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
     STAMP_FLUSH(10, 14);
-    lds_ldlt_solve(A, yv, n, NE, tid);
+    if constexpr (SOLVER == 1) {
+        const int its = lds_pcg_solve(A, yv, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
+        if (tid == 0) ctrl->pcg_iters += its;
+    } else {
+        lds_ldlt_solve(A, yv, n, NE, tid);
+    }
     if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
     lds_barrier();
 #ifdef LH_STAMPS
@@ -1571,9 +1674,13 @@ hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
-                          int* host_done) {
-    hipLaunchKernelGGL(k_ctrl, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp, prm,
-                       mode, (volatile int*)host_done);
+                          int* host_done, int seq) {
+    if (prm.solver == 1)
+        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
+                           prm, mode, (volatile int*)host_done, seq);
+    else
+        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
+                           prm, mode, (volatile int*)host_done, seq);
     return hipGetLastError();
 }
 
@@ -1607,7 +1714,8 @@ hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, 
 // ---- LDL^T probe (tests): x = (S)^-1 b through k_ctrl's pivot order, LDS layout and
 //      lds_ldlt_solve, for a dense symmetric S (row-major n x n, n <= LH_NPAD) ----
 __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
-                                                   double* __restrict__ x) {
+                                                   double* __restrict__ x, int solver, double tol, int max_it,
+                                                   int* __restrict__ iters) {
     __shared__ double A[(NP + 1) * AS];
     __shared__ double dg[NP];
     __shared__ __attribute__((aligned(16))) double xsol[NP];
@@ -1635,14 +1743,21 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     }
     if (tid < NE) A[NP * AS + tid] = tid < n ? b[perm[tid]] : 0.0;
     lds_barrier();
-    lds_ldlt_solve(A, xsol, n, NE, tid);
+    if (solver == 1) {
+        __shared__ double s_pcg[48];
+        const int its = lds_pcg_solve(A, xsol, dg, s_pcg, n, tid, tol, (max_it > 0 ? max_it : 2 * n) + 1);
+        if (tid == 0 && iters) *iters = its;
+    } else {
+        lds_ldlt_solve(A, xsol, n, NE, tid);
+    }
     lds_barrier();
     if (tid < n) x[perm[tid]] = xsol[tid];
 }
 
-hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x) {
+hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x, int solver, double tol, int max_it,
+                                int* iters) {
     if (n < 1 || n > LH_NPAD) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ldlt_probe, dim3(1), dim3(CT), 0, 0, S, b, n, x);
+    hipLaunchKernelGGL(k_ldlt_probe, dim3(1), dim3(CT), 0, 0, S, b, n, x, solver, tol, max_it, iters);
     return hipGetLastError();
 }
 

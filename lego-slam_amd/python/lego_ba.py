@@ -119,6 +119,8 @@ def config_window(name, seed=0, **kw):
 # --------------------------------------------------------------------------
 
 LH_OK, LH_E_EMPTY, LH_E_BADARG, LH_E_HIP, LH_E_RCCL, LH_E_UNSUPPORTED, LH_E_STATE = range(7)
+LH_ABI_VERSION = 2
+LH_SOLVER_LDLT, LH_SOLVER_PCG = 0, 1
 
 
 class LhOptions(C.Structure):
@@ -128,7 +130,8 @@ class LhOptions(C.Structure):
         ("tau", C.c_double), ("lambda_cap", C.c_double), ("lambda_init", C.c_double),
         ("linear_solver", C.c_int32), ("verbose", C.c_int32), ("device", C.c_int32),
         ("world_size", C.c_int32), ("rank", C.c_int32), ("degenerate_guard", C.c_int32),
-        ("trials_per_sync", C.c_int32), ("profile", C.c_int32), ("comm_id", C.c_uint8 * 128),
+        ("trials_per_sync", C.c_int32), ("profile", C.c_int32), ("pcg_max_iters", C.c_int32),
+        ("pcg_tol", C.c_double), ("comm_id", C.c_uint8 * 128),
     ]
 
 
@@ -148,7 +151,7 @@ class LhResult(C.Structure):
         ("trace_chi2", C.c_void_p), ("trace_lambda", C.c_void_p), ("trace_cap", C.c_int32),
         ("trace_len", C.c_int32), ("iterations", C.c_int32), ("trials", C.c_int32),
         ("accepted", C.c_int32), ("chi2_initial", C.c_double), ("chi2_final", C.c_double),
-        ("lambda_final", C.c_double), ("time_ms", C.c_double),
+        ("lambda_final", C.c_double), ("time_ms", C.c_double), ("pcg_iterations", C.c_int32),
     ]
 
 
@@ -161,6 +164,7 @@ ABI_SYMBOLS = [
     "lh_strerror", "lh_default_options", "lh_kernel_name", "lh_comm_unique_id",
     "lh_create", "lh_destroy", "lh_solve", "lh_upload", "lh_solve_resident",
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
+    "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
 ]
 
 _balib = None
@@ -288,7 +292,8 @@ class Solver:
         n = r.trace_len
         out["trace_chi2"] = out["trace_chi2"][:n]
         out["trace_lambda"] = out["trace_lambda"][:n]
-        for f in ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "time_ms"):
+        for f in ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "time_ms",
+                  "pcg_iterations"):
             out[f] = getattr(r, f)
         return out
 

@@ -48,11 +48,15 @@ typedef struct orc_options {
     double tau;            /* 1e-5 */
     double lambda_cap;     /* 5e10 */
     double lambda_init;    /* < 0 computed */
+    int32_t linear_solver; /* 0 Eigen LDLT (problem.cpp:420); 1 PCG (PCGSolver :584-614, fixed) */
+    int32_t pcg_max_iters; /* <= 0: 2 * rows (problem.cpp:422) */
+    double pcg_tol;        /* 1e-6 (problem.cpp:597) */
 } orc_options;
 
 typedef struct orc_stats {
     double chi2_initial, chi2_final, lambda_final, time_ms;
     int32_t iterations, trials, accepted, trace_len;
+    int32_t pcg_iterations, pad_;
 } orc_stats;
 
 /* ======================= Eigen / Sophus restatements ======================= */
@@ -296,6 +300,70 @@ static void ldlt_solve(double *A, int n, const double *b, double *x) {
     free(temp);
 }
 
+/* Problem::PCGSolver (problem.cpp:584-614), the Jacobi-PCG the reference left commented out at
+   :421-422 (called there with maxIter = 2 * rows), restated with its bug fixed: the reference
+   computes the first step alpha * p but never adds it to x (:595-596).  Same stop rule
+   (||r|| > 1e-6 ||b||, :597-598), same update order.  A zero diagonal entry preconditions with 0
+   (Eigen's inverse would give inf and a NaN step).  A is read through its lower triangle.
+   Returns the number of steps (the reference's first step plus its loop iterations). */
+static int pcg_solve(const double *A, int n, const double *b, double *x, double tol, int max_iters) {
+#define AL_(i, j) ((i) >= (j) ? A[(size_t)(i) * (size_t)n + (size_t)(j)] : A[(size_t)(j) * (size_t)n + (size_t)(i)])
+    const int maxit = max_iters > 0 ? max_iters : 2 * n;
+    double *minv = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double *r = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double *z = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double *p = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double *w = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double rz = 0.0, bb = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double d = AL_(i, i);
+        minv[i] = d != 0.0 ? 1.0 / d : 0.0;
+        x[i] = 0.0;
+        r[i] = b[i];
+        z[i] = minv[i] * r[i];
+        p[i] = z[i];
+        rz += r[i] * z[i];
+        bb += r[i] * r[i];
+    }
+    const double thr = tol * sqrt(bb);
+    int steps = 0;
+    if (bb > 0.0) {
+        for (;;) {
+            double pw = 0.0;
+            for (int i = 0; i < n; ++i) {
+                double s = 0.0;
+                for (int j = 0; j < n; ++j) s += AL_(i, j) * p[j];
+                w[i] = s;
+                pw += p[i] * s;
+            }
+            const double alpha = rz / pw;
+            double rr = 0.0, rzn = 0.0;
+            for (int i = 0; i < n; ++i) {
+                x[i] += alpha * p[i];
+                r[i] -= alpha * w[i];
+                z[i] = minv[i] * r[i];
+                rr += r[i] * r[i];
+                rzn += r[i] * z[i];
+            }
+            ++steps;
+            if (!(sqrt(rr) > thr) || steps >= maxit + 1) break;
+            const double beta = rzn / rz;
+            rz = rzn;
+            for (int i = 0; i < n; ++i) p[i] = beta * p[i] + z[i];
+        }
+    }
+    free(minv); free(r); free(z); free(p); free(w);
+#undef AL_
+    return steps;
+}
+
+/* The reduced pose solve: Eigen LDLT (the reference) or the fixed PCG (its commented-out option). */
+static int reduced_solve(const orc_options *o, double *S, int n, const double *bs, double *x) {
+    if (o->linear_solver == 1) return pcg_solve(S, n, bs, x, o->pcg_tol, o->pcg_max_iters);
+    ldlt_solve(S, n, bs, x);
+    return 0;
+}
+
 /* ============================ problem state ============================== */
 
 typedef struct {
@@ -327,6 +395,7 @@ typedef struct {
     double chi, lambda, ni;
     /* orc_reduced_system: capture the undamped reduced system instead of solving */
     double *S_out, *bs_out;
+    int64_t pcg_iters;       /* PCG steps summed over the solve's trials */
 } prob_t;
 
 /* ---- EdgeProjection arithmetic (include/legoslam/lego_types.h:200-254) ---- */
@@ -507,7 +576,7 @@ static void solve_dense(prob_t *pb) {
         if (pb->opt.strategy == 0) S[i * np + i] += pb->lambda;
         else S[i * np + i] += pb->lambda * S[i * np + i];
     }
-    ldlt_solve(S, (int)np, bs, pb->dx);
+    pb->pcg_iters += reduced_solve(&pb->opt, S, (int)np, bs, pb->dx);
     /* dxl = Hmm_inv * (bmm - Hmp * dxp) */
     double *tmp = (double *)malloc(sizeof(double) * (size_t)(nm > 0 ? nm : 1));
     for (int64_t k = 0; k < nm; ++k) {
@@ -666,7 +735,7 @@ static void solve_sparse(prob_t *pb) {
         if (pb->opt.strategy == 0) S[i * np + i] += pb->lambda;
         else S[i * np + i] += pb->lambda * S[i * np + i];
     }
-    ldlt_solve(S, (int)np, bs, pb->dx);
+    pb->pcg_iters += reduced_solve(&pb->opt, S, (int)np, bs, pb->dx);
     free(S); free(bs);
     /* back substitution: dxl = Hll^-1 (bl - Hlp * dxp) */
 #pragma omp parallel for schedule(static) num_threads(nt)
@@ -930,6 +999,7 @@ static int orc_run(int variant, int32_t P, const double *pose_in, const uint8_t 
     st->iterations = iter;
     st->chi2_final = pb.chi;
     st->lambda_final = pb.lambda;
+    st->pcg_iterations = (int32_t)pb.pcg_iters;
     if (st->trace_len > trace_cap) st->trace_len = trace_cap;
 
     if (pose_out) memcpy(pose_out, pb.pose, sizeof(double) * 12 * (size_t)P);
@@ -994,6 +1064,9 @@ void orc_ldlt_solve(const double *A, int n, const double *b, double *x) {
     memcpy(M, A, sizeof(double) * (size_t)n * (size_t)n);
     ldlt_solve(M, n, b, x);
     free(M);
+}
+int orc_pcg_solve(const double *A, int n, const double *b, double *x, double tol, int max_iters) {
+    return pcg_solve(A, n, b, x, tol, max_iters);
 }
 /* residual / Jacobians / robust weight of one edge, for finite-difference tests */
 void orc_edge_eval(const double T12[12], const double X[3], const double uv[2], const double K[4],

@@ -20,6 +20,7 @@ class OrcOptions(C.Structure):
         ("verbose", C.c_int32), ("n_threads", C.c_int32), ("gate_mode", C.c_int32),
         ("huber_delta", C.c_double), ("stop_dchi2", C.c_double), ("tau", C.c_double),
         ("lambda_cap", C.c_double), ("lambda_init", C.c_double),
+        ("linear_solver", C.c_int32), ("pcg_max_iters", C.c_int32), ("pcg_tol", C.c_double),
     ]
 
 
@@ -28,6 +29,7 @@ class OrcStats(C.Structure):
         ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("lambda_final", C.c_double),
         ("time_ms", C.c_double), ("iterations", C.c_int32), ("trials", C.c_int32),
         ("accepted", C.c_int32), ("trace_len", C.c_int32),
+        ("pcg_iterations", C.c_int32), ("pad_", C.c_int32),
     ]
 
 
@@ -54,6 +56,8 @@ def lib():
         L.orc_huber.argtypes = [C.c_double, C.c_double, vp]
         L.orc_lu_inverse3.argtypes = [vp, vp]
         L.orc_ldlt_solve.argtypes = [vp, C.c_int, vp, vp]
+        L.orc_pcg_solve.argtypes = [vp, C.c_int, vp, vp, C.c_double, C.c_int]
+        L.orc_pcg_solve.restype = C.c_int
         L.orc_edge_eval.argtypes = [vp] * 5 + [C.c_double] + [vp] * 6
         _lib = L
     return _lib
@@ -64,9 +68,10 @@ def _p(a):
 
 
 def options(max_iters=10, max_trials=10, strategy=0, huber_delta=5.991, stop_dchi2=1e-5, tau=1e-5,
-            lambda_cap=5e10, lambda_init=-1.0, verbose=0, n_threads=0, gate_mode=0):
+            lambda_cap=5e10, lambda_init=-1.0, verbose=0, n_threads=0, gate_mode=0, linear_solver=0,
+            pcg_max_iters=0, pcg_tol=1e-6):
     return OrcOptions(max_iters, max_trials, strategy, verbose, n_threads, gate_mode, huber_delta, stop_dchi2,
-                      tau, lambda_cap, lambda_init)
+                      tau, lambda_cap, lambda_init, linear_solver, pcg_max_iters, pcg_tol)
 
 
 def solve(w, variant=1, trace_cap=64, **opt):
@@ -88,7 +93,8 @@ def solve(w, variant=1, trace_cap=64, **opt):
     out["status"] = rc
     out["trace_chi2"] = out["trace_chi2"][:st.trace_len]
     out["trace_lambda"] = out["trace_lambda"][:st.trace_len]
-    for f in ("chi2_initial", "chi2_final", "lambda_final", "time_ms", "iterations", "trials", "accepted"):
+    for f in ("chi2_initial", "chi2_final", "lambda_final", "time_ms", "iterations", "trials", "accepted",
+              "pcg_iterations"):
         out[f] = getattr(st, f)
     return out
 
@@ -155,6 +161,14 @@ def ldlt_solve(A, b):
     x = np.zeros(A.shape[0])
     lib().orc_ldlt_solve(_p(A), A.shape[0], _p(np.ascontiguousarray(b, np.float64)), _p(x))
     return x
+
+
+def pcg_solve(A, b, tol=1e-6, max_iters=0):
+    """The fixed reference PCG (oracle pcg_solve): (x, steps)."""
+    A = np.ascontiguousarray(A, np.float64)
+    x = np.zeros(A.shape[0])
+    it = lib().orc_pcg_solve(_p(A), A.shape[0], _p(np.ascontiguousarray(b, np.float64)), _p(x), tol, max_iters)
+    return x, it
 
 
 def edge_eval(T12, X, uv, K, ext12=None, huber_delta=5.991):

@@ -52,8 +52,9 @@ int main(void) {
   printf("lh_result %zu\n", sizeof(lh_result));
   printf("lh_kernel_stats %zu\n", sizeof(lh_kernel_stats));
   P(lh_options, huber_delta) P(lh_options, linear_solver) P(lh_options, comm_id) P(lh_options, profile)
+  P(lh_options, pcg_max_iters) P(lh_options, pcg_tol)
   P(lh_window, n_obs) P(lh_window, K) P(lh_window, cam_ext)
-  P(lh_result, trace_cap) P(lh_result, chi2_initial) P(lh_result, time_ms)
+  P(lh_result, trace_cap) P(lh_result, chi2_initial) P(lh_result, time_ms) P(lh_result, pcg_iterations)
   return 0;
 }
 """
@@ -79,7 +80,9 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
 
 def test_default_options_mirror_reference_constants():
     o = lego_ba.default_options()
-    assert o.abi_version == 1
+    assert o.abi_version == lego_ba.LH_ABI_VERSION == 2
+    assert o.linear_solver == lego_ba.LH_SOLVER_LDLT   # Eigen LDLT     problem.cpp:420
+    assert o.pcg_tol == 1e-6 and o.pcg_max_iters <= 0   # PCGSolver stop rule / cap  problem.cpp:597, :422
     assert o.max_iters == 10          # problem.solve(10)      backend_lego.cpp:161
     assert o.max_trials == 10         # false_cnt_threshold    problem.cpp:178
     assert o.huber_delta == 5.991     # HuberCost(chi2_th)     backend_lego.cpp:92-94
