@@ -219,6 +219,24 @@ def main():
                       "iterations_per_solve": pits / args.steps, "pcg_steps_per_solve": pcgs / args.steps,
                       "chi2_rel_vs_ldlt": abs(r["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
         sp.close()
+    # the frontend's pose-only LM (Frontend::EstimateCurrentPose) on a batch of
+    # frames through lh_estimate_pose: device time of one launch over the batch, beside value
+    if world == 1:
+        import frames
+        nf = 2048
+        fb = frames.batch(args.seed, nf, n_obs=150)
+        sf = lego_ba.Solver(device=local)
+        sf.estimate_pose(fb)
+        tms = [sf.estimate_pose(fb)["time_ms"] for _ in range(3)]
+        out["estimate_pose"] = {"frames": nf, "obs_per_frame": 150, "ms_per_batch": round(min(tms), 4),
+                                "frames_per_s": round(nf / (min(tms) * 1e-3), 1),
+                                "note": "device time of one lh_estimate_pose launch (4 rounds of solve(10) per frame)"}
+        if not args.no_cpu:
+            import oracle_bind
+            t = time.perf_counter()
+            oracle_bind.estimate_pose(frames.batch(args.seed, 256, n_obs=150))
+            out["estimate_pose"]["cpu_frames_per_s_1core"] = round(256 / (time.perf_counter() - t), 1)
+        sf.close()
     # end-to-end host-buffer call (lh_solve: upload + solve + download over PCIe), rank 0 only
     if world == 1:
         solver_h = lego_ba.Solver(device=local)

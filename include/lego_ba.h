@@ -18,6 +18,7 @@
  *     edge->getRobustChi2()        base_edge.cpp:33 lh_result.edge_robust_chi2
  *     vertex->getEstimate()        base_vertex.h:34 lh_result.pose_Tcw / lm_xyz
  *     outlier threshold loop       backend_lego.cpp:163-194 lh_classify_outliers
+ *     Frontend::EstimateCurrentPose frontend_lego.cpp:157-250 lh_estimate_pose (batched)
  *     ~Problem                     problem.cpp:32 lh_destroy
  *
  * Plain C types only (no torch, Eigen or Sophus in any signature).  No C++
@@ -160,6 +161,39 @@ void lh_kernel_stats_reset(lh_handle *h);
  */
 int lh_classify_outliers(const double *edge_robust_chi2, int64_t n_obs, double chi2_th,
                          uint8_t *is_outlier, double *th_out, int64_t *n_inlier, int64_t *n_outlier);
+
+/*
+ * Frontend pose-only LM: Frontend::EstimateCurrentPose
+ * (src/frontend_lego.cpp:157-250) for a batch of independent frames.  Per frame:
+ * one VertexPose, one EdgeProjectionPoseOnly per observation (lego_types.h:116-180),
+ * four rounds of problem.solve(max_iters) each restarting from the frame's pose,
+ * the outlier flags refreshed after each round (robust chi2 > 5.991, :205-226;
+ * flagged features recomputed at the final estimate first), Huber(huber_delta) on
+ * rounds one to three and none on round four (:223-225).  Flags never remove an
+ * edge (the reference's setLevel is commented out).  Uses the handle's options
+ * (max_iters, max_trials, strategy, huber_delta, stop_dchi2, tau, lambda_cap,
+ * lambda_init); one workgroup per frame, the whole batch in one launch.
+ */
+typedef struct lh_frames {
+    int32_t n_frames;
+    const int64_t *obs_ptr;     /* [n_frames + 1] CSR: frame f owns observations [obs_ptr[f], obs_ptr[f+1]) */
+    const double *pose_Tcw;     /* [n_frames][12] row-major [R | t]: current_frame_->Pose()           */
+    const double *pts_w;        /* [n_obs][3] map-point world positions (mp->pos_)                     */
+    const double *obs_uv;       /* [n_obs][2] feature pixels (toVec2(feat->position_.pt))              */
+    const uint8_t *is_outlier;  /* [n_obs] the features' is_outlier_ on entry, or NULL (all false)     */
+    double K[4];                /* fx, fy, cx, cy (camera_left_->K())                                   */
+} lh_frames;
+
+typedef struct lh_frames_result {
+    double *pose_Tcw;           /* [n_frames][12] SE3(vertex_pose->getEstimate()) after round four     */
+    uint8_t *is_outlier;        /* [n_obs] flags after round four, or NULL                             */
+    double *edge_chi2;          /* [n_obs] chi2 the last classification compared with 5.991, or NULL  */
+    int32_t *n_inliers;         /* [n_frames] EstimateCurrentPose's return value, or NULL               */
+    int32_t *iterations;        /* [n_frames] LM iterations summed over the four rounds, or NULL       */
+    double time_ms;             /* device time of the batch (upload and download excluded)             */
+} lh_frames_result;
+
+int lh_estimate_pose(lh_handle *h, const lh_frames *in, lh_frames_result *out);
 
 /* ---- test hooks (not part of the reference interface) ---- */
 /* f64 MFMA accumulator-layout probe: D(16x16) = A(16x4) * B(4x16), device pointers, row-major */

@@ -48,6 +48,10 @@ hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double*
                                 int* iters);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
+hipError_t lh_launch_frames(hipStream_t st, int n_frames, const int64_t* obs_ptr, const double* pose_in,
+                            const double* pts, const double* uv, const uint8_t* flag_in, lh_params prm, double* res,
+                            double* pose_out, uint8_t* flag_out, double* rchi2_out, int32_t* iters_out,
+                            int32_t* inliers_out);
 }
 
 namespace {
@@ -189,6 +193,11 @@ struct lh_handle {
     DevBuf<double> d_uv, d_rec, d_rec_init, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs,
         d_rs_stage, d_rs_commit, d_maxd, d_dxp;
     DevBuf<lh_ctrl> d_ctrl;
+    // frontend pose-only batch (lh_estimate_pose)
+    DevBuf<int64_t> f_ptr;
+    DevBuf<double> f_pose_in, f_pts, f_uv, f_res, f_pose_out, f_rchi2;
+    DevBuf<uint8_t> f_flag_in, f_flag_out;
+    DevBuf<int32_t> f_iters, f_inl;
     lh_ctrl* h_ctrl = nullptr;   // pinned
     int* h_done = nullptr;       // pinned, mapped: k_ctrl raises it when the LM loop stops
     int* d_done = nullptr;       // device alias of h_done
@@ -839,6 +848,9 @@ void lh_destroy(lh_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm) ncclCommDestroy(h->comm);
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
+    h->f_ptr.release(); h->f_pose_in.release(); h->f_pts.release(); h->f_uv.release(); h->f_res.release();
+    h->f_pose_out.release(); h->f_rchi2.release(); h->f_flag_in.release(); h->f_flag_out.release();
+    h->f_iters.release(); h->f_inl.release();
     h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release();
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release();
     h->d_uv.release(); h->d_rec.release(); h->d_rec_init.release(); h->d_ptab.release();
@@ -894,6 +906,73 @@ int lh_set_profiling(lh_handle* h, int on) {
 void lh_kernel_stats_reset(lh_handle* h) {
     if (!h) return;
     for (int i = 0; i < KC_N; ++i) { h->launches[i] = 0; h->total_ms[i] = 0.0; }
+}
+
+// Frontend::EstimateCurrentPose for a batch of frames (frontend_lego.cpp:157-250): upload, one
+// k_frames launch (one workgroup per frame), download.
+int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
+    if (!h || !in || !out) return LH_E_BADARG;
+    const int F = in->n_frames;
+    if (F < 0 || (F > 0 && (!in->obs_ptr || !in->pose_Tcw))) return LH_E_BADARG;
+    if (F == 0) { out->time_ms = 0.0; return LH_OK; }
+    if (in->obs_ptr[0] != 0) return LH_E_BADARG;
+    for (int f = 0; f < F; ++f)
+        if (in->obs_ptr[f + 1] < in->obs_ptr[f] || in->obs_ptr[f + 1] - in->obs_ptr[f] > (int64_t)INT32_MAX)
+            return LH_E_BADARG;
+    const int64_t O = in->obs_ptr[F];
+    if (O > 0 && (!in->pts_w || !in->obs_uv)) return LH_E_BADARG;
+    if (!out->pose_Tcw) return LH_E_BADARG;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    hipStream_t s = h->stream;
+    HIPCHK(h->f_ptr.ensure(F + 1));
+    HIPCHK(h->f_pose_in.ensure(12 * (size_t)F));
+    HIPCHK(h->f_pose_out.ensure(12 * (size_t)F));
+    HIPCHK(h->f_pts.ensure(3 * (size_t)O));
+    HIPCHK(h->f_uv.ensure(2 * (size_t)O));
+    HIPCHK(h->f_res.ensure(2 * (size_t)O));
+    HIPCHK(h->f_rchi2.ensure((size_t)O));
+    HIPCHK(h->f_flag_in.ensure((size_t)O));
+    HIPCHK(h->f_flag_out.ensure((size_t)O));
+    HIPCHK(h->f_iters.ensure((size_t)F));
+    HIPCHK(h->f_inl.ensure((size_t)F));
+    auto up = [&](void* d, const void* src, size_t bytes) { return hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, s); };
+    HIPCHK(up(h->f_ptr.p, in->obs_ptr, sizeof(int64_t) * (F + 1)));
+    HIPCHK(up(h->f_pose_in.p, in->pose_Tcw, sizeof(double) * 12 * (size_t)F));
+    if (O > 0) {
+        HIPCHK(up(h->f_pts.p, in->pts_w, sizeof(double) * 3 * (size_t)O));
+        HIPCHK(up(h->f_uv.p, in->obs_uv, sizeof(double) * 2 * (size_t)O));
+        if (in->is_outlier) HIPCHK(up(h->f_flag_in.p, in->is_outlier, (size_t)O));
+    }
+    lh_params prm{};
+    prm.max_iters = h->opt.max_iters;
+    prm.max_trials = h->opt.max_trials;
+    prm.strategy = h->opt.strategy;
+    prm.lambda_given = h->opt.lambda_init >= 0.0;
+    prm.huber_delta = h->opt.huber_delta;
+    prm.stop_dchi2 = h->opt.stop_dchi2;
+    prm.tau = h->opt.tau;
+    prm.lambda_cap = h->opt.lambda_cap;
+    prm.lambda_init = h->opt.lambda_init;
+    for (int i = 0; i < 4; ++i) prm.K[i] = in->K[i];
+    hipEvent_t e0 = next_event(h), e1 = next_event(h);
+    if (!e0 || !e1) return LH_E_HIP;
+    HIPCHK(hipEventRecord(e0, s));
+    HIPCHK(lh_launch_frames(s, F, h->f_ptr.p, h->f_pose_in.p, h->f_pts.p, h->f_uv.p,
+                            in->is_outlier ? h->f_flag_in.p : nullptr, prm, h->f_res.p, h->f_pose_out.p,
+                            h->f_flag_out.p, h->f_rchi2.p, h->f_iters.p, h->f_inl.p));
+    HIPCHK(hipEventRecord(e1, s));
+    auto down = [&](void* dst, const void* d, size_t bytes) { return hipMemcpyAsync(dst, d, bytes, hipMemcpyDeviceToHost, s); };
+    HIPCHK(down(out->pose_Tcw, h->f_pose_out.p, sizeof(double) * 12 * (size_t)F));
+    if (out->is_outlier && O > 0) HIPCHK(down(out->is_outlier, h->f_flag_out.p, (size_t)O));
+    if (out->edge_chi2 && O > 0) HIPCHK(down(out->edge_chi2, h->f_rchi2.p, sizeof(double) * (size_t)O));
+    if (out->n_inliers) HIPCHK(down(out->n_inliers, h->f_inl.p, sizeof(int32_t) * (size_t)F));
+    if (out->iterations) HIPCHK(down(out->iterations, h->f_iters.p, sizeof(int32_t) * (size_t)F));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    out->time_ms = ms;
+    h->event_next = 0;
+    return LH_OK;
 }
 
 int lh_classify_outliers(const double* rchi2, int64_t n_obs, double chi2_th, uint8_t* is_outlier, double* th_out,

@@ -1611,6 +1611,366 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 }
 
 // ============================================================================
+// k_frames: the frontend's pose-only LM, Frontend::EstimateCurrentPose
+// (src/frontend_lego.cpp:157-250), one workgroup per frame, the whole thing in
+// one launch: four rounds of problem.solve(10) on one VertexPose with
+// EdgeProjectionPoseOnly edges (lego_types.h:116-180), each round restarting
+// from the frame's pose, then the outlier flags (:205-226); the edges lose the
+// Huber cost after round three (:223-225).  Edges are never removed (the
+// reference's setLevel is commented out).  n = 6: the Schur complement is H_pp
+// itself (problem.cpp:380-430 with no landmark vertex), solved by thread 0 with
+// Eigen's pivoted LDLT.  Per-edge arithmetic is the bitwise mirror of
+// oracle/lego_oracle.c (po_residual / po_jacobian); sums have a fixed order
+// (thread-strided, then a fixed tree), so a batch is bitwise reproducible.
+// ============================================================================
+#define FT 256                 // threads per frame
+#define FV 28                  // per-edge sums: H_pp upper (21) | b (6) | rho0
+#pragma clang fp contract(off)
+
+// EdgeProjectionPoseOnly residual + Jacobian at pos_cam = T X (one transform for both)
+__device__ __forceinline__ void po_edge(const double* q, const double* t, const double X[3], double u, double v,
+                                        const double* K, double& r0, double& r1, double J[12], bool want_j) {
+    double Pc[3];
+    d_q_rotate(q, X, Pc);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Pc[i] = Pc[i] + t[i];
+    double p0 = K[0] * Pc[0] + K[2] * Pc[2];
+    double p1 = K[1] * Pc[1] + K[3] * Pc[2];
+    const double den = Pc[2] + 1e-18;
+    p0 /= den;
+    p1 /= den;
+    r0 = u - p0;
+    r1 = v - p1;
+    if (want_j) {
+        const double fx = K[0], fy = K[1];
+        const double x = Pc[0], y = Pc[1], z = Pc[2];
+        const double zi = 1.0 / (z + 1e-18);
+        const double zi2 = zi * zi;
+        J[0] = -fx * zi;              J[1] = 0.0;                  J[2] = fx * x * zi2;
+        J[3] = fx * x * y * zi2;      J[4] = -fx - fx * x * x * zi2; J[5] = fx * y * zi;
+        J[6] = 0.0;                   J[7] = -fy * zi;             J[8] = fy * y * zi2;
+        J[9] = fy + fy * y * y * zi2; J[10] = -fy * x * y * zi2;   J[11] = -fy * x * zi;
+    }
+}
+
+__device__ __forceinline__ double po_rho0(double r0, double r1, double delta) {
+    const double e2 = r0 * r0 + r1 * r1;
+    if (delta > 0.0) {
+        const double d2 = delta * delta;
+        if (e2 <= d2) return e2;
+        const double s = sqrt(e2);
+        return 2 * s * delta - d2;
+    }
+    return e2;
+}
+
+// one edge's contributions: (J^T W) J upper triangle, -(rho1 J)^T r, rho0  (problem.cpp:300-330)
+__device__ __forceinline__ void po_accumulate(double r0, double r1, const double J[12], double delta, double acc[FV]) {
+    EdgeEval E;
+    E.r0 = r0; E.r1 = r1;
+    lh_params pr;
+    pr.huber_delta = delta;
+    edge_robust(E, pr);
+    double JtW[12];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        JtW[2 * a] = J[a] * E.W00 + J[6 + a] * E.W10;
+        JtW[2 * a + 1] = J[a] * E.W01 + J[6 + a] * E.W11;
+    }
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = a; c < 6; ++c) acc[k++] += JtW[2 * a] * J[c] + JtW[2 * a + 1] * J[6 + c];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] -= (E.rho1 * J[a]) * r0 + (E.rho1 * J[6 + a]) * r1;
+    acc[27] += E.rho0;
+}
+
+// Eigen LDLT<Lower> (diagonal pivoting) + solve on a 6x6 (the oracle's ldlt_solve, n = 6).
+// A, x, tr, temp live in LDS: the pivot swaps index dynamically (registers would go to scratch).
+__device__ void po_ldlt6(double* A, const double* b, double* x, int* tr, double* temp) {
+    int all_zero = 0;
+    for (int k = 0; k < 6; ++k) {
+        int idx = k;
+        double big = fabs(A[7 * k]);
+        for (int i = k + 1; i < 6; ++i)
+            if (fabs(A[7 * i]) > big) { big = fabs(A[7 * i]); idx = i; }
+        tr[k] = idx;
+        if (k != idx) {
+            for (int j = 0; j < k; ++j) { double t = A[6 * k + j]; A[6 * k + j] = A[6 * idx + j]; A[6 * idx + j] = t; }
+            for (int i = idx + 1; i < 6; ++i) { double t = A[6 * i + k]; A[6 * i + k] = A[6 * i + idx]; A[6 * i + idx] = t; }
+            { double t = A[7 * k]; A[7 * k] = A[7 * idx]; A[7 * idx] = t; }
+            for (int i = k + 1; i < idx; ++i) { double t = A[6 * i + k]; A[6 * i + k] = A[6 * idx + i]; A[6 * idx + i] = t; }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = A[7 * j] * A[6 * k + j];
+            double s = 0.0;
+            for (int j = 0; j < k; ++j) s += A[6 * k + j] * temp[j];
+            A[7 * k] -= s;
+            for (int i = k + 1; i < 6; ++i) {
+                double si = 0.0;
+                for (int j = 0; j < k; ++j) si += A[6 * i + j] * temp[j];
+                A[6 * i + k] -= si;
+            }
+        }
+        const double akk = A[7 * k];
+        const bool valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            for (int j = 0; j < 6; ++j) tr[j] = j;
+            all_zero = 1;
+            break;
+        }
+        if (k < 5 && valid)
+            for (int i = k + 1; i < 6; ++i) A[6 * i + k] /= akk;
+    }
+    for (int i = 0; i < 6; ++i) x[i] = b[i];
+    for (int k = 0; k < 6; ++k) { const int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
+    if (!all_zero)
+        for (int k = 0; k < 6; ++k)
+            for (int i = k + 1; i < 6; ++i) x[i] -= A[6 * i + k] * x[k];
+    for (int i = 0; i < 6; ++i) {
+        const double d = A[7 * i];
+        x[i] = (fabs(d) > 2.2250738585072014e-308) ? x[i] / d : 0.0;
+    }
+    if (!all_zero)
+        for (int k = 5; k >= 0; --k)
+            for (int i = 0; i < k; ++i) x[i] -= A[6 * k + i] * x[k];
+    for (int k = 5; k >= 0; --k) { const int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
+}
+
+// VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91)
+__device__ void po_pose_add(const double d_in[6], const double* T12, double* out12) {
+    double d[6];
+    bool bad = false;
+    for (int a = 0; a < 6; ++a) { d[a] = d_in[a]; bad |= !isfinite(d[a]); }
+    if (bad)
+        for (int a = 0; a < 6; ++a) d[a] = 0.0;
+    const double th = d_twist_theta(d);
+    double sh, ch, st, ct;
+    sincos(0.5 * th, &sh, &ch);
+    sincos(th, &st, &ct);
+    double qe[4], te[3], qT[4], qn[4], tr[3], Rn[9];
+    d_se3_exp_trig(d, sh, ch, st, ct, qe, te);
+    const double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
+    d_q_from_R(R, qT);
+    const double tc[3] = {T12[3], T12[7], T12[11]};
+    d_q_mul(qe, qT, qn);
+    d_q_rotate(qe, tc, tr);
+    d_R_from_q(qn, Rn);
+    for (int i = 0; i < 3; ++i) {
+        out12[4 * i] = Rn[3 * i]; out12[4 * i + 1] = Rn[3 * i + 1]; out12[4 * i + 2] = Rn[3 * i + 2];
+        out12[4 * i + 3] = te[i] + tr[i];
+    }
+}
+
+#pragma clang fp contract(fast)
+
+struct PoShared {
+    double pose[12], cand[12], q[4], t[3], K[4];
+    double H[36], b[6], dx[6], A[36], tmp[6];
+    int tr[6];
+    double red[FT / 64][FV];
+    double sum[FV];
+    double chi, lam, ni, last, delta;
+    int flags[4];              // 0: trial loop running, 1: iteration loop running
+};
+
+// all FT threads: the workgroup's fixed-order sum of acc[FV] into S.sum
+__device__ __forceinline__ void po_reduce(double acc[FV], PoShared& S, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < FV; ++k) {
+        double v = acc[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) S.red[wave][k] = v;
+    }
+    lds_barrier();
+    if (tid < FV) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < FT / 64; ++w) s += S.red[w][tid];
+        S.sum[tid] = s;
+    }
+    lds_barrier();
+}
+
+// SE3(estimate_) of S.cand (or S.pose) into S.q / S.t (one thread)
+__device__ __forceinline__ void po_table(PoShared& S, const double* T12) {
+    const double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
+    d_q_from_R(R, S.q);
+    S.t[0] = T12[3]; S.t[1] = T12[7]; S.t[2] = T12[11];
+}
+
+__global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_ptr, const double* __restrict__ pose_in,
+                                               const double* __restrict__ pts, const double* __restrict__ uv,
+                                               const uint8_t* __restrict__ flag_in, lh_params prm,
+                                               double* __restrict__ res, double* __restrict__ pose_out,
+                                               uint8_t* __restrict__ flag_out, double* __restrict__ rchi2_out,
+                                               int32_t* __restrict__ iters_out, int32_t* __restrict__ inliers_out) {
+    __shared__ PoShared S;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int64_t o0 = obs_ptr[f];
+    const int O = (int)(obs_ptr[f + 1] - o0);
+    const double* X = pts + 3 * o0;
+    const double* Z = uv + 2 * o0;
+    double* R = res + 2 * o0;
+    uint8_t* flag = flag_out + o0;
+    for (int e = tid; e < O; e += FT) flag[e] = flag_in ? (flag_in[o0 + e] != 0) : 0;
+    if (tid < 4) S.K[tid] = prm.K[tid];
+    if (tid == 0) S.delta = prm.huber_delta;
+    int its = 0;
+
+    // linearise at T12 (S.q / S.t already its table): residuals -> R, H, b, sum rho0 -> S.sum
+    auto linearise = [&]() {
+        double acc[FV];
+#pragma unroll
+        for (int k = 0; k < FV; ++k) acc[k] = 0.0;
+        const double delta = S.delta;
+        for (int e = tid; e < O; e += FT) {
+            double r0, r1, J[12];
+            const double Xe[3] = {X[3 * e], X[3 * e + 1], X[3 * e + 2]};
+            po_edge(S.q, S.t, Xe, Z[2 * e], Z[2 * e + 1], S.K, r0, r1, J, true);
+            R[2 * e] = r0;
+            R[2 * e + 1] = r1;
+            po_accumulate(r0, r1, J, delta, acc);
+        }
+        po_reduce(acc, S, tid);
+    };
+    auto load_system = [&]() {   // thread 0: S.sum -> H (full symmetric), b
+        int k = 0;
+        for (int a = 0; a < 6; ++a)
+            for (int c = a; c < 6; ++c) { S.H[6 * a + c] = S.sum[k]; S.H[6 * c + a] = S.sum[k]; ++k; }
+        for (int a = 0; a < 6; ++a) S.b[a] = S.sum[21 + a];
+    };
+
+    for (int round = 0; round < 4; ++round) {
+        if (tid < 12) S.pose[tid] = pose_in[12 * (size_t)f + tid];   // setEstimate(current_frame_->Pose()) :201
+        lds_barrier();
+        if (O > 0) {   // Problem::solve returns false with no edge (problem.cpp:157-161)
+            if (tid == 0) po_table(S, S.pose);
+            lds_barrier();
+            linearise();
+            if (tid == 0) {
+                load_system();
+                // computeLambdaInitLM (problem.cpp:470-504)
+                S.ni = 2.0;
+                S.chi = 0.5 * S.sum[27];
+                if (prm.strategy == 0) {
+                    if (prm.lambda_given) {
+                        S.lam = prm.lambda_init;
+                    } else {
+                        double m = 0.0;
+                        for (int i = 0; i < 6; ++i) m = fmax(fabs(S.H[7 * i]), m);
+                        S.lam = prm.tau * fmin(prm.lambda_cap, m);
+                    }
+                } else {
+                    S.lam = 1e-5;
+                }
+                S.last = 1e20;
+                S.flags[1] = prm.max_iters > 0;
+            }
+            lds_barrier();
+            int iter = 0;
+            while (S.flags[1]) {
+                if (tid == 0) { S.flags[0] = 1; S.flags[2] = 0; }   // trial loop, false_cnt
+                lds_barrier();
+                while (S.flags[0]) {
+                    if (tid == 0) {
+                        for (int i = 0; i < 36; ++i) S.A[i] = S.H[i];
+                        for (int i = 0; i < 6; ++i) S.A[7 * i] += (prm.strategy == 0) ? S.lam : S.lam * S.A[7 * i];
+                        po_ldlt6(S.A, S.b, S.dx, S.tr, S.tmp);
+                        po_pose_add(S.dx, S.pose, S.cand);
+                        po_table(S, S.cand);
+                    }
+                    lds_barrier();
+                    linearise();   // isGoodStepInLM's residuals (:524) and, if accepted, buildHessian's
+                    if (tid == 0) {
+                        const double tchi = 0.5 * S.sum[27];
+                        double scale = 0.0;
+                        for (int i = 0; i < 6; ++i)
+                            scale += (prm.strategy == 0) ? S.dx[i] * (S.lam * S.dx[i] + S.b[i])
+                                                         : S.dx[i] * (S.lam * S.H[7 * i] * S.dx[i] + S.b[i]);
+                        scale = 0.5 * scale;
+                        scale += 1e-10;
+                        const double rho = (S.chi - tchi) / scale;
+                        const bool ok = rho > 0 && isfinite(tchi);
+                        if (prm.strategy == 0) {
+                            if (ok) {
+                                const double m = 2 * rho - 1;
+                                double alpha = 1.0 - m * m * m;
+                                alpha = fmin(alpha, 2.0 / 3.0);
+                                S.lam *= fmax(1.0 / 3.0, alpha);
+                                S.ni = 2;
+                                S.chi = tchi;
+                            } else {
+                                S.lam *= S.ni;
+                                S.ni *= 2;
+                            }
+                        } else {
+                            if (ok) { S.lam = fmax(S.lam / 9.0, 1e-7); S.chi = tchi; }
+                            else S.lam = fmin(S.lam * 11.0, 1e7);
+                        }
+                        if (ok) {
+                            for (int i = 0; i < 12; ++i) S.pose[i] = S.cand[i];
+                            load_system();
+                            S.flags[0] = 0;
+                        } else {
+                            S.flags[2] += 1;                   // rollbackStates: S.pose untouched
+                            if (S.flags[2] >= prm.max_trials) S.flags[0] = 0;
+                        }
+                    }
+                    lds_barrier();
+                }
+                ++iter;
+                if (tid == 0) {
+                    if (S.last - S.chi < prm.stop_dchi2 || iter >= prm.max_iters) S.flags[1] = 0;
+                    S.last = S.chi;
+                }
+                lds_barrier();
+            }
+            its += iter;
+        }
+        // outlier flags (frontend_lego.cpp:205-226); residual_ is "as last evaluated" except for the
+        // features already flagged, which are recomputed at the final estimate
+        if (tid == 0) po_table(S, S.pose);
+        lds_barrier();
+        const double delta = S.delta;
+        for (int e = tid; e < O; e += FT) {
+            double r0 = R[2 * e], r1 = R[2 * e + 1];
+            if (flag[e]) {
+                double J[12];
+                const double Xe[3] = {X[3 * e], X[3 * e + 1], X[3 * e + 2]};
+                po_edge(S.q, S.t, Xe, Z[2 * e], Z[2 * e + 1], S.K, r0, r1, J, false);
+                R[2 * e] = r0;
+                R[2 * e + 1] = r1;
+            }
+            const double rc = po_rho0(r0, r1, delta);
+            flag[e] = rc > 5.991;                       // chi2_th (frontend_lego.cpp:171)
+            if (round == 3 && rchi2_out) rchi2_out[o0 + e] = rc;
+        }
+        lds_barrier();
+        if (round == 2 && tid == 0) S.delta = 0.0;     // setCostFunction(nullptr) (:223-225)
+        lds_barrier();
+    }
+    if (tid < 12) pose_out[12 * (size_t)f + tid] = S.pose[tid];
+    // inliers: features.size() - cnt_outlier (:249)
+    int cnt = 0;
+    for (int e = tid; e < O; e += FT) cnt += flag[e] ? 1 : 0;
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    __shared__ int s_cnt[FT / 64];
+    if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
+    lds_barrier();
+    if (tid == 0) {
+        int c = 0;
+        for (int w = 0; w < FT / 64; ++w) c += s_cnt[w];
+        if (inliers_out) inliers_out[f] = O - c;
+        if (iters_out) iters_out[f] = its;
+    }
+}
+
+// ============================================================================
 // launchers (host side)
 // ============================================================================
 extern "C" {
@@ -1795,6 +2155,16 @@ hipError_t lh_read_stamps(unsigned long long* out, int n, int reset) {
 
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D) {
     hipLaunchKernelGGL(k_mfma_probe, dim3(1), dim3(64), 0, 0, A, B, D);
+    return hipGetLastError();
+}
+
+hipError_t lh_launch_frames(hipStream_t st, int n_frames, const int64_t* obs_ptr, const double* pose_in,
+                            const double* pts, const double* uv, const uint8_t* flag_in, lh_params prm, double* res,
+                            double* pose_out, uint8_t* flag_out, double* rchi2_out, int32_t* iters_out,
+                            int32_t* inliers_out) {
+    if (n_frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_frames, dim3(n_frames), dim3(FT), 0, st, obs_ptr, pose_in, pts, uv, flag_in, prm, res, pose_out,
+                       flag_out, rchi2_out, iters_out, inliers_out);
     return hipGetLastError();
 }
 

@@ -155,6 +155,20 @@ class LhResult(C.Structure):
     ]
 
 
+class LhFrames(C.Structure):
+    _fields_ = [
+        ("n_frames", C.c_int32), ("obs_ptr", C.c_void_p), ("pose_Tcw", C.c_void_p), ("pts_w", C.c_void_p),
+        ("obs_uv", C.c_void_p), ("is_outlier", C.c_void_p), ("K", C.c_double * 4),
+    ]
+
+
+class LhFramesResult(C.Structure):
+    _fields_ = [
+        ("pose_Tcw", C.c_void_p), ("is_outlier", C.c_void_p), ("edge_chi2", C.c_void_p),
+        ("n_inliers", C.c_void_p), ("iterations", C.c_void_p), ("time_ms", C.c_double),
+    ]
+
+
 class LhKernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64 * 8), ("total_ms", C.c_double * 8)]
 
@@ -164,6 +178,7 @@ ABI_SYMBOLS = [
     "lh_strerror", "lh_default_options", "lh_kernel_name", "lh_comm_unique_id",
     "lh_create", "lh_destroy", "lh_solve", "lh_upload", "lh_solve_resident",
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
+    "lh_estimate_pose",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
 ]
 
@@ -191,6 +206,7 @@ def ba_lib():
         lib.lh_kernel_stats_get.argtypes = [C.c_void_p, C.POINTER(LhKernelStats)]
         lib.lh_kernel_stats_reset.argtypes = [C.c_void_p]
         lib.lh_set_profiling.argtypes = [C.c_void_p, C.c_int]
+        lib.lh_estimate_pose.argtypes = [C.c_void_p, C.POINTER(LhFrames), C.POINTER(LhFramesResult)]
         lib.lh_classify_outliers.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p, C.c_void_p]
         _balib = lib
@@ -312,6 +328,30 @@ class Solver:
         r, out = self._result(s.n_poses, s.n_landmarks, s.n_obs, trace_cap, want_states, want_edges)
         _check(ba_lib().lh_solve_resident(self.h, C.byref(r)), "lh_solve_resident")
         return self._finish(r, out)
+
+    def estimate_pose(self, fb, is_outlier_in=None):
+        """Frontend::EstimateCurrentPose on every frame of batch `fb` (obs_ptr CSR, pose_Tcw, pts,
+        obs_uv, K: the tests/frames.py layout) through lh_estimate_pose."""
+        F = int(fb["n_frames"])
+        keep = dict(ptr=_as(fb["obs_ptr"], np.int64), pose=_as(np.reshape(fb["pose_Tcw"], (F, 12)), np.float64),
+                    pts=_as(fb["pts"], np.float64), uv=_as(fb["obs_uv"], np.float64),
+                    fin=_as(is_outlier_in, np.uint8))
+        O = int(keep["ptr"][-1]) if F else 0
+        s = LhFrames()
+        s.n_frames = F
+        s.obs_ptr, s.pose_Tcw, s.pts_w, s.obs_uv = _ptr(keep["ptr"]), _ptr(keep["pose"]), _ptr(keep["pts"]), _ptr(keep["uv"])
+        s.is_outlier = _ptr(keep["fin"])
+        for i in range(4):
+            s.K[i] = float(fb["K"][i])
+        out = dict(pose_Tcw=np.zeros((F, 12)), is_outlier=np.zeros(O, np.uint8), edge_chi2=np.zeros(O),
+                   n_inliers=np.zeros(F, np.int32), iterations=np.zeros(F, np.int32))
+        r = LhFramesResult()
+        r.pose_Tcw, r.is_outlier, r.edge_chi2 = _ptr(out["pose_Tcw"]), _ptr(out["is_outlier"]), _ptr(out["edge_chi2"])
+        r.n_inliers, r.iterations = _ptr(out["n_inliers"]), _ptr(out["iterations"])
+        _check(ba_lib().lh_estimate_pose(self.h, C.byref(s), C.byref(r)), "lh_estimate_pose")
+        out["is_outlier"] = out["is_outlier"].astype(bool)
+        out["time_ms"] = r.time_ms
+        return out
 
     def kernel_stats(self):
         st = LhKernelStats()

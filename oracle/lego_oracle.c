@@ -1090,3 +1090,227 @@ void orc_edge_eval(const double T12[12], const double X[3], const double uv[2], 
     robust_info(&pb, r, W, drho);
     *rchi2 = robust_chi2(&pb, r);
 }
+
+/* ============================ frontend pose-only ============================
+ * Frontend::EstimateCurrentPose (src/frontend_lego.cpp:157-250): one VertexPose, one
+ * EdgeProjectionPoseOnly per tracked feature with a map point (include/legoslam/lego_types.h:116-180),
+ * Huber(5.991); four rounds, each restarting from the frame's pose and running
+ * problem.solve(10); after each round the outlier flags are refreshed (:205-226) and after the
+ * third round the edges lose their cost function (:223-225, so round four is plain least
+ * squares).  The flags never remove an edge from the problem (setLevel is commented out, :219,
+ * :222).  The Problem is SLAM mode with no landmark vertex: n = 6, the Schur complement is H_pp
+ * itself (problem.cpp:380-430 with marg_size 0), and the LM loop is problem.cpp:156-230.
+ * Sequential per-edge sums (edge order), LDLT as the backend path.
+ */
+
+/* EdgeProjectionPoseOnly::computeResidual (lego_types.h:128-143): K (T X), pi, z - pi */
+static void po_residual(const se3_t *T, const double *X, const double *uv, const double *K, double r[2]) {
+    double Pc[3];
+    se3_apply(T, X, Pc);
+    double p0 = K[0] * Pc[0] + 0.0 * Pc[1] + K[2] * Pc[2];
+    double p1 = 0.0 * Pc[0] + K[1] * Pc[1] + K[3] * Pc[2];
+    double p2 = 0.0 * Pc[0] + 0.0 * Pc[1] + 1.0 * Pc[2];
+    double den = p2 + 1e-18;
+    p0 /= den; p1 /= den;
+    r[0] = uv[0] - p0;
+    r[1] = uv[1] - p1;
+}
+
+/* EdgeProjectionPoseOnly::computeJacobians (lego_types.h:145-176): J at pos_cam = T X */
+static void po_jacobian(const se3_t *T, const double *X, const double *K, double J[12]) {
+    double Pc[3];
+    se3_apply(T, X, Pc);
+    const double fx = K[0], fy = K[1];
+    const double x = Pc[0], y = Pc[1], z = Pc[2];
+    const double zi = 1.0 / (z + 1e-18);
+    const double zi2 = zi * zi;
+    J[0] = -fx * zi;              J[1] = 0.0;               J[2] = fx * x * zi2;
+    J[3] = fx * x * y * zi2;      J[4] = -fx - fx * x * x * zi2; J[5] = fx * y * zi;
+    J[6] = 0.0;                   J[7] = -fy * zi;          J[8] = fy * y * zi2;
+    J[9] = fy + fy * y * y * zi2; J[10] = -fy * x * y * zi2; J[11] = -fy * x * zi;
+}
+
+typedef struct {
+    int32_t O;
+    const double *X, *uv;
+    double K[4];
+    double delta;            /* Huber delta of the edges' cost function, <= 0: none */
+    orc_options opt;
+    double pose[12], pose_bak[12];
+    double *res;             /* O x 2: residual_ as last computed */
+    double H[36], b[6], dx[6];
+    double chi, lambda, ni;
+} po_t;
+
+static double po_rchi2(const po_t *p, const double r[2]) {
+    double e2 = r[0] * r[0] + r[1] * r[1];
+    if (p->delta > 0) { double rho[3]; huber(p->delta, e2, rho); return rho[0]; }
+    return e2;
+}
+
+/* buildHessian (problem.cpp:273-358) for the single pose vertex */
+static void po_build(po_t *p) {
+    se3_t T;
+    se3_from_mat(p->pose, &T);
+    memset(p->H, 0, sizeof(p->H));
+    memset(p->b, 0, sizeof(p->b));
+    for (int32_t e = 0; e < p->O; ++e) {
+        double r[2], J[12], W[4], drho, Hpp[36];
+        po_residual(&T, p->X + 3 * (size_t)e, p->uv + 2 * (size_t)e, p->K, r);
+        p->res[2 * e] = r[0]; p->res[2 * e + 1] = r[1];
+        po_jacobian(&T, p->X + 3 * (size_t)e, p->K, J);
+        if (p->delta > 0) {
+            double e2 = r[0] * r[0] + r[1] * r[1], rho[3];
+            huber(p->delta, e2, rho);
+            W[0] = rho[1]; W[1] = 0.0; W[2] = 0.0; W[3] = rho[1];
+            if (rho[1] + 2 * rho[2] * e2 > 0.0) {
+                double s = 2 * rho[2];
+                W[0] += s * r[0] * r[0]; W[1] += s * r[0] * r[1];
+                W[2] += s * r[1] * r[0]; W[3] += s * r[1] * r[1];
+            }
+            drho = rho[1];
+        } else {
+            W[0] = 1.0; W[1] = 0.0; W[2] = 0.0; W[3] = 1.0;
+            drho = 1.0;
+        }
+        jtwj(J, 6, W, J, 6, Hpp);
+        for (int i = 0; i < 36; ++i) p->H[i] += Hpp[i];
+        for (int a = 0; a < 6; ++a) p->b[a] -= (drho * J[a]) * r[0] + (drho * J[6 + a]) * r[1];
+    }
+    memset(p->dx, 0, sizeof(p->dx));
+}
+
+static double po_sum_rchi2(po_t *p, int recompute) {
+    se3_t T;
+    se3_from_mat(p->pose, &T);
+    double s = 0.0;
+    for (int32_t e = 0; e < p->O; ++e) {
+        if (recompute) po_residual(&T, p->X + 3 * (size_t)e, p->uv + 2 * (size_t)e, p->K, p->res + 2 * e);
+        s += po_rchi2(p, p->res + 2 * e);
+    }
+    return s;
+}
+
+/* Problem::solve(max_iters) (problem.cpp:156-230) on the pose-only problem; returns iterations */
+static int po_solve(po_t *p, int *trials_out) {
+    int trials = 0;
+    po_build(p);
+    p->ni = 2.0;
+    p->chi = 0.5 * po_sum_rchi2(p, 0);
+    if (p->opt.strategy == 0) {
+        double m = 0.0;
+        for (int i = 0; i < 6; ++i) m = fmax(fabs(p->H[7 * i]), m);
+        p->lambda = p->opt.lambda_init >= 0 ? p->opt.lambda_init : p->opt.tau * fmin(p->opt.lambda_cap, m);
+    } else {
+        p->lambda = 1e-5;
+    }
+    int stop = 0, iter = 0;
+    double last_chi = 1e20;
+    while (!stop && iter < p->opt.max_iters) {
+        int ok = 0, false_cnt = 0;
+        while (!ok && false_cnt < p->opt.max_trials) {
+            double S[36];
+            memcpy(S, p->H, sizeof(S));
+            for (int i = 0; i < 6; ++i) {
+                if (p->opt.strategy == 0) S[7 * i] += p->lambda;
+                else S[7 * i] += p->lambda * S[7 * i];
+            }
+            ldlt_solve(S, 6, p->b, p->dx);
+            memcpy(p->pose_bak, p->pose, sizeof(p->pose));
+            {
+                double u[6];
+                int bad = 0;
+                for (int a = 0; a < 6; ++a) if (isnan(p->dx[a]) || isinf(p->dx[a])) bad = 1;
+                for (int a = 0; a < 6; ++a) u[a] = bad ? 0.0 : p->dx[a];
+                se3_t E, T, R;
+                se3_exp(u, &E);
+                se3_from_mat(p->pose, &T);
+                se3_mul(&E, &T, &R);
+                se3_to_mat(&R, p->pose);
+            }
+            double temp_chi = 0.5 * po_sum_rchi2(p, 1);
+            double scale = 0.0;
+            for (int i = 0; i < 6; ++i) {
+                if (p->opt.strategy == 0) scale += p->dx[i] * (p->lambda * p->dx[i] + p->b[i]);
+                else scale += p->dx[i] * (p->lambda * p->H[7 * i] * p->dx[i] + p->b[i]);
+            }
+            scale = 0.5 * scale;
+            scale += 1e-10;
+            double rho = (p->chi - temp_chi) / scale;
+            ok = rho > 0 && isfinite(temp_chi);
+            if (p->opt.strategy == 0) {
+                if (ok) {
+                    double alpha = 1.0 - pow((2 * rho - 1), 3);
+                    alpha = fmin(alpha, 2.0 / 3.0);
+                    p->lambda *= fmax(1.0 / 3.0, alpha);
+                    p->ni = 2;
+                    p->chi = temp_chi;
+                } else {
+                    p->lambda *= p->ni;
+                    p->ni *= 2;
+                }
+            } else {
+                if (ok) { p->lambda = fmax(p->lambda / 9.0, 1e-7); p->chi = temp_chi; }
+                else p->lambda = fmin(p->lambda * 11.0, 1e7);
+            }
+            trials++;
+            if (ok) po_build(p);
+            else { false_cnt++; memcpy(p->pose, p->pose_bak, sizeof(p->pose)); }
+        }
+        ++iter;
+        if (last_chi - p->chi < p->opt.stop_dchi2) stop = 1;
+        last_chi = p->chi;
+    }
+    if (trials_out) *trials_out += trials;
+    return iter;
+}
+
+/*
+ * orc_estimate_pose — Frontend::EstimateCurrentPose for n_frames independent frames (CSR over
+ * observations: frame f owns obs [obs_ptr[f], obs_ptr[f+1])).  pose_in/pose_out [n_frames][12];
+ * pts [O][3] map-point positions, uv [O][2]; is_outlier: in = the features' flags on entry
+ * (NULL: all false), out = flags after the fourth round.  rchi2_out [O] (optional): each edge's
+ * robust chi2 as the last round's classification saw it.  iters_out/trials_out [n_frames]
+ * (optional): summed over the four rounds.  Returns 0, or 2 for bad arguments.
+ */
+int orc_estimate_pose(int32_t n_frames, const int64_t *obs_ptr, const double *pose_in, const double *pts,
+                      const double *uv, const double *K, const orc_options *opt, const uint8_t *is_outlier_in,
+                      double *pose_out, uint8_t *is_outlier_out, double *rchi2_out, int32_t *iters_out,
+                      int32_t *trials_out) {
+    if (n_frames < 0 || !obs_ptr || !pose_in || !pose_out || !K || !opt) return 2;
+    for (int32_t f = 0; f < n_frames; ++f) {
+        const int64_t o0 = obs_ptr[f], O = obs_ptr[f + 1] - o0;
+        if (O < 0) return 2;
+        po_t p;
+        memset(&p, 0, sizeof(p));
+        p.O = (int32_t)O;
+        p.X = pts + 3 * o0;
+        p.uv = uv + 2 * o0;
+        memcpy(p.K, K, sizeof(p.K));
+        p.opt = *opt;
+        p.delta = opt->huber_delta;
+        p.res = (double *)calloc(2 * (size_t)(O > 0 ? O : 1), sizeof(double));
+        uint8_t *flag = is_outlier_out + o0;
+        for (int64_t e = 0; e < O; ++e) flag[e] = is_outlier_in ? is_outlier_in[o0 + e] : 0;
+        int its = 0, trials = 0;
+        memcpy(p.pose, pose_in + 12 * (size_t)f, sizeof(p.pose));
+        for (int round = 0; round < 4; ++round) {
+            memcpy(p.pose, pose_in + 12 * (size_t)f, sizeof(p.pose));   /* setEstimate(Pose()) :201 */
+            if (O > 0) its += po_solve(&p, &trials);                   /* solve(10): false on no edge */
+            se3_t T;
+            se3_from_mat(p.pose, &T);
+            for (int64_t e = 0; e < O; ++e) {
+                if (flag[e]) po_residual(&T, p.X + 3 * e, p.uv + 2 * e, p.K, p.res + 2 * e);   /* :208-210 */
+                const double rc = po_rchi2(&p, p.res + 2 * e);
+                flag[e] = rc > 5.991;                                   /* chi2_th :171, :211-217 */
+                if (rchi2_out) rchi2_out[o0 + e] = rc;
+            }
+            if (round == 2) p.delta = 0.0;                              /* setCostFunction(nullptr) :223-225 */
+        }
+        memcpy(pose_out + 12 * (size_t)f, p.pose, sizeof(p.pose));
+        if (iters_out) iters_out[f] = its;
+        if (trials_out) trials_out[f] = trials;
+        free(p.res);
+    }
+    return 0;
+}

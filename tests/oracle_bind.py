@@ -163,6 +163,30 @@ def ldlt_solve(A, b):
     return x
 
 
+def estimate_pose(fb, is_outlier_in=None, **opt):
+    """Frontend::EstimateCurrentPose on every frame of batch `fb` (tests/frames.py layout)."""
+    L = lib()
+    vp = C.c_void_p
+    L.orc_estimate_pose.argtypes = [C.c_int32, vp, vp, vp, vp, vp, C.POINTER(OrcOptions), vp, vp, vp, vp, vp, vp]
+    L.orc_estimate_pose.restype = C.c_int
+    F = int(fb["n_frames"])
+    O = int(fb["obs_ptr"][-1])
+    ptr = np.ascontiguousarray(fb["obs_ptr"], np.int64)
+    pose = np.ascontiguousarray(fb["pose_Tcw"], np.float64).reshape(F, 12)
+    pts = np.ascontiguousarray(fb["pts"], np.float64)
+    uv = np.ascontiguousarray(fb["obs_uv"], np.float64)
+    K = np.ascontiguousarray(fb["K"], np.float64)
+    fin = None if is_outlier_in is None else np.ascontiguousarray(is_outlier_in, np.uint8)
+    out = dict(pose_Tcw=np.zeros((F, 12)), is_outlier=np.zeros(O, np.uint8), rchi2=np.zeros(O),
+               iterations=np.zeros(F, np.int32), trials=np.zeros(F, np.int32))
+    o = options(**opt)
+    rc = L.orc_estimate_pose(F, _p(ptr), _p(pose), _p(pts), _p(uv), _p(K), C.byref(o), _p(fin), _p(out["pose_Tcw"]),
+                             _p(out["is_outlier"]), _p(out["rchi2"]), _p(out["iterations"]), _p(out["trials"]))
+    assert rc == 0, rc
+    out["is_outlier"] = out["is_outlier"].astype(bool)
+    return out
+
+
 def pcg_solve(A, b, tol=1e-6, max_iters=0):
     """The fixed reference PCG (oracle pcg_solve): (x, steps)."""
     A = np.ascontiguousarray(A, np.float64)

@@ -51,6 +51,10 @@ int main(void) {
   printf("lh_window %zu\n", sizeof(lh_window));
   printf("lh_result %zu\n", sizeof(lh_result));
   printf("lh_kernel_stats %zu\n", sizeof(lh_kernel_stats));
+  printf("lh_frames %zu\n", sizeof(lh_frames));
+  printf("lh_frames_result %zu\n", sizeof(lh_frames_result));
+  P(lh_frames, obs_ptr) P(lh_frames, is_outlier) P(lh_frames, K)
+  P(lh_frames_result, iterations) P(lh_frames_result, time_ms)
   P(lh_options, huber_delta) P(lh_options, linear_solver) P(lh_options, comm_id) P(lh_options, profile)
   P(lh_options, pcg_max_iters) P(lh_options, pcg_tol)
   P(lh_window, n_obs) P(lh_window, K) P(lh_window, cam_ext)
@@ -71,10 +75,13 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     assert got["lh_window"] == C.sizeof(lego_ba.LhWindow)
     assert got["lh_result"] == C.sizeof(lego_ba.LhResult)
     assert got["lh_kernel_stats"] == C.sizeof(lego_ba.LhKernelStats)
+    assert got["lh_frames"] == C.sizeof(lego_ba.LhFrames)
+    assert got["lh_frames_result"] == C.sizeof(lego_ba.LhFramesResult)
     for key, v in got.items():
         if "." in key:
             s, f = key.split(".")
-            cls = {"lh_options": lego_ba.LhOptions, "lh_window": lego_ba.LhWindow, "lh_result": lego_ba.LhResult}[s]
+            cls = {"lh_options": lego_ba.LhOptions, "lh_window": lego_ba.LhWindow, "lh_result": lego_ba.LhResult,
+                   "lh_frames": lego_ba.LhFrames, "lh_frames_result": lego_ba.LhFramesResult}[s]
             assert getattr(cls, f).offset == v, key
 
 
