@@ -9,9 +9,15 @@ i0, i1 = resets[-3], resets[-2]          # one whole timed solve (k_reset .. nex
 prev = None
 print("one solve(10) of the C3 bench window under rocprofv3 --kernel-trace")
 print(f"{'kernel':24s} {'dur us':>8s} {'gap us':>8s}")
-for r in rows[i0:i1]:
+last = i0
+for i in range(i0, i1):
+    r = rows[i]
+    if not r["Kernel_Name"].startswith(("k_reset", "void k_lin", "k_reduce", "k_ctrl")):
+        break                              # the solve ends at its last controller launch
+    last = i
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     gap = (s - prev) / 1000 if prev else 0.0
     print(f"{r['Kernel_Name'].split('(')[0]:24s} {(e - s) / 1000:8.2f} {gap:8.2f}")
     prev = e
-print(f"total {(int(rows[i1 - 1]['End_Timestamp']) - int(rows[i0]['Start_Timestamp'])) / 1000:.1f} us")
+print(f"total {(int(rows[last]['End_Timestamp']) - int(rows[i0]['Start_Timestamp'])) / 1000:.1f} us "
+      "(the last launches are trials enqueued past the device's stop: they exit at once)")
