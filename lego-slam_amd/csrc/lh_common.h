@@ -11,8 +11,9 @@
 
 // ---- envelope ---------------------------------------------------------------
 #define LH_PMAX 21            // poses per window (reduced system n = 6P <= 126 fits LDS)
-#define LH_UMAX 10            // distinct poses in one chunk window (6U <= 64 rows)
-#define LH_TMAX 4             // 16-row MFMA tiles per window side
+#define LH_UMAX 16            // distinct poses in one chunk window (6U <= 96 rows); the reference window is
+                              // 15 keyframes (map.h:82), so any landmark of it fits one chunk window
+#define LH_TMAX 6             // 16-row MFMA tiles per window side
 #define LH_SB_LM 8            // landmarks per sub-batch (one wave)
 #define LH_SB_OBS 64          // observations per sub-batch (one per lane)
 #define LH_WAVES 4            // waves per k_lin workgroup

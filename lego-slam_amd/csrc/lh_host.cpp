@@ -30,6 +30,7 @@
 
 extern "C" {
 hipError_t lh_prepare_lin();
+size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
@@ -447,6 +448,9 @@ int upload_impl(lh_handle* h, const lh_window* w) {
             while (c < h->n_chunks && chunks[c].T == T) ++c;
         }
         h->tgroup_begin[LH_TMAX + 1] = h->n_chunks;
+        // a chunk window must fit one CU's LDS (a T = 6 window with 4 cameras does not)
+        for (int T = 1; T <= LH_TMAX; ++T)
+            if (h->tgroup_begin[T + 1] > h->tgroup_begin[T] && lh_lin_smem(T, ncam) > 160 * 1024) return LH_E_UNSUPPORTED;
     }
 
     // ---- reduce plan: for every pose pair (p <= q) the chunks touching it ----

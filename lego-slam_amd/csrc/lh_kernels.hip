@@ -344,11 +344,15 @@ __device__ __forceinline__ double fast_rsq(double a) {
 template <int T>
 struct LinCfg {
     static constexpr int NT = T * (T + 1) / 2;          // upper MFMA tiles of the window
-    static constexpr int GS = (T == 1) ? 16 : (T == 4 ? 80 : 48);  // G row stride: 16T + pad, conflict-free b64 frag loads
+    // G row stride: >= 16T and = 16 mod 32 doubles (conflict-free b64 fragment loads)
+    static constexpr int GS = (T == 1) ? 16 : (T <= 3 ? 48 : (T <= 5 ? 80 : 112));
     static constexpr int UMAX = (16 * T) / 6;           // window poses that fit 16T rows
+    // the chunk slab as combined in LDS: NT tiles | UMAX x 33 per-pose sums | 4 scalars (written to
+    // the global slab at LH_SLAB_* offsets)
+    static constexpr int LS_TASK = NT * 256, LS_SC = LS_TASK + UMAX * LH_TASKS, LS = LS_SC + 8;
     // per-wave LDS scratch: pose-sum image [slot][landmark][33], G image [24][GS], the record
     // stage (128), and (over the 4 waves) the two combine slabs
-    static constexpr int A_ = UMAX * LH_SB_LM * LH_TASKS, B_ = 3 * LH_SB_LM * GS, C_ = (2 * LH_SLAB_STRIDE + 3) / 4;
+    static constexpr int A_ = UMAX * LH_SB_LM * LH_TASKS, B_ = 3 * LH_SB_LM * GS, C_ = (2 * LS + 3) / 4;
     static constexpr int SCR = ((A_ > B_ ? (A_ > C_ ? A_ : C_) : (B_ > C_ ? B_ : C_)) + 1) & ~1;
 };
 
@@ -425,9 +429,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // the chunk's window, LDS-resident: committed and candidate pose tables per (slot, camera),
     // the pending pose step per slot, the camera extrinsics
     double* wt_c = dsm + LH_WAVES * Cfg::SCR;
-    double* wt_n = wt_c + LH_UMAX * ncam * LH_PT;
-    double* wdx = wt_n + LH_UMAX * ncam * LH_PT;
-    double* wext = wdx + LH_UMAX * 6;
+    double* wt_n = wt_c + Cfg::UMAX * ncam * LH_PT;     // a chunk of T tiles has U <= UMAX poses
+    double* wdx = wt_n + Cfg::UMAX * ncam * LH_PT;
+    double* wext = wdx + Cfg::UMAX * 6;
     {
         const int per = ncam * LH_PT, ne = U * per;
         for (int i = tid; i < ne; i += 256) {
@@ -461,9 +465,11 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     uint32_t meta_n;
     double u_n, v_n;
     double2 r_n;
+    lh_subbatch S_n;
     {
         const int sbc = min(sb, sb_last);
         const int o = sbc * 64 + lane;
+        S_n = sbs[sbc];
         meta_n = obs_meta[o];
         u_n = obs_uv[2 * (size_t)o];
         v_n = obs_uv[2 * (size_t)o + 1];
@@ -472,7 +478,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     lds_barrier();   // window tables
 
     for (; sb < (int)sb_end; sb += LH_WAVES) {
-        const lh_subbatch S = sbs[sb];   // scalar load (sb is wave-uniform)
+        const lh_subbatch S = S_n;       // scalar words, prefetched one sub-batch ahead (sb is wave-uniform)
         const int lg = S.lg, nlm = S.n_lm;
         const int ls = lane >> lg, gj = lane & ((1 << lg) - 1);
         const bool lmok = ls < nlm;
@@ -484,6 +490,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         {
             const int sbn = min(sb + LH_WAVES, sb_last);
             const int on = sbn * 64 + lane;
+            S_n = sbs[sbn];
             meta_n = obs_meta[on];
             u_n = obs_uv[2 * (size_t)on];
             v_n = obs_uv[2 * (size_t)on + 1];
@@ -728,7 +735,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const int ntask = U * LH_TASKS;
     for (int phase = 0; phase < 2; ++phase) {
         if ((wave >> 1) == phase) {
-            double* sl = smem + (wave & 1) * LH_SLAB_STRIDE;
+            double* sl = smem + (wave & 1) * Cfg::LS;
             const bool first = phase == 0;
 #pragma unroll
             for (int t = 0; t < Cfg::NT; ++t)
@@ -741,13 +748,13 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 #pragma unroll
                 for (int uu = 0; uu < Cfg::UMAX; ++uu) {
                     if (uu < U) {
-                        const int idx = LH_SLAB_TASK_OFF + uu * LH_TASKS + lane;
+                        const int idx = Cfg::LS_TASK + uu * LH_TASKS + lane;
                         sl[idx] = (first ? 0.0 : sl[idx]) + task[uu];
                     }
                 }
             }
             if (lane == 0) {
-                double* sc = sl + LH_SLAB_SC_OFF;
+                double* sc = sl + Cfg::LS_SC;
                 if (first) { sc[0] = chi_acc; sc[1] = scale_acc; sc[2] = ndeg; sc[3] = maxd; }
                 else { sc[0] += chi_acc; sc[1] += scale_acc; sc[2] += ndeg; sc[3] = fmax(sc[3], maxd); }
             }
@@ -756,12 +763,12 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     }
     STAMP(9);
     const double* s0 = smem;
-    const double* s1 = smem + LH_SLAB_STRIDE;
+    const double* s1 = smem + Cfg::LS;
     double* gs = slabs + (size_t)chunk * LH_SLAB_STRIDE;
     for (int i = tid; i < ntile; i += 256) gs[i] = s0[i] + s1[i];
-    for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = s0[LH_SLAB_TASK_OFF + i] + s1[LH_SLAB_TASK_OFF + i];
-    if (tid < 3) gs[LH_SLAB_SC_OFF + tid] = s0[LH_SLAB_SC_OFF + tid] + s1[LH_SLAB_SC_OFF + tid];
-    if (tid == 3) gs[LH_SLAB_SC_OFF + 3] = fmax(s0[LH_SLAB_SC_OFF + 3], s1[LH_SLAB_SC_OFF + 3]);
+    for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = s0[Cfg::LS_TASK + i] + s1[Cfg::LS_TASK + i];
+    if (tid < 3) gs[LH_SLAB_SC_OFF + tid] = s0[Cfg::LS_SC + tid] + s1[Cfg::LS_SC + tid];
+    if (tid == 3) gs[LH_SLAB_SC_OFF + 3] = fmax(s0[Cfg::LS_SC + 3], s1[Cfg::LS_SC + 3]);
     STAMP(10);
     STAMP_FLUSH(0, 11);
 }
@@ -776,17 +783,21 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
 
 #define RT 1024
 #define RW (RT / 64)
-#define RI_MAX 2048           // items (chunks) per pose pair staged in LDS at a time
 
 __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs, const uint32_t* __restrict__ pair_ptr,
                                                const uint32_t* __restrict__ items, const uint16_t* __restrict__ pair_pq,
                                                const lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
                                                double* __restrict__ maxd_out, lh_params prm, int n_chunks) {
-    if (__builtin_amdgcn_readfirstlane(ctrl->done)) return;
     STAMP_DECL
     __shared__ double part[3][RW][64];
     const lh_rs_layout LY = lh_rs_make(prm.P);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the stop flag and this block's pair words are independent loads: one round trip for all
+    const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
+    const int bq = b < LY.npairs ? b : 0;
+    const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
+    const int ib = pair_ptr[bq], ie = pair_ptr[bq + 1];
+    if (done) return;
     if (b == LY.npairs) {
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
         for (int c = tid; c < n_chunks; c += RT) {
@@ -810,7 +821,6 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
         }
         return;
     }
-    const int p = pair_pq[2 * b], q = pair_pq[2 * b + 1];
     const bool diag = p == q;
     const int a = lane / 6, bb = lane - 6 * (lane / 6);
     // lanes 0..35: S entry (a, bb) [+ H_pp entry on the diagonal]; 36..41: b_p; 42..47: bsd
@@ -819,7 +829,6 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
     else if (lane < 42) off_h = LH_SLAB_TASK_OFF + 21 + (lane - 36);
     else if (lane < 48) off_h = LH_SLAB_TASK_OFF + 27 + (lane - 42);
     const bool act_s = lane < 36, act_h = (lane < 36 && diag) || (lane >= 36 && lane < 48 && diag);
-    __shared__ uint32_t sitems[RI_MAX];
     auto slab_off = [&](uint32_t item, int& off_s, const double*& sl) {
         const int ch = item >> 11, T = (item >> 8) & 7, sp = (item >> 4) & 15, sq = item & 15;
         sl = slabs + (size_t)ch * LH_SLAB_STRIDE;
@@ -829,34 +838,25 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
         off_s = act_s ? (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15) : 0;
         return sp;
     };
+    // Each wave walks its items (wave, wave + RW, ...) in order, eight at a time: the item words are
+    // wave-uniform (scalar loads straight from global, no LDS staging or barrier) and all eight
+    // items' slab loads are in flight together.  Same per-wave order as one item at a time.
     double vs = 0.0, vh = 0.0;
-    const int ib = pair_ptr[b], ie = pair_ptr[b + 1];
-    for (int seg = ib; seg < ie; seg += RI_MAX) {
-        // a segment of the pair's item list into LDS (one global round trip), then every wave
-        // walks its items (wave, wave + RW, ...) with four slab loads in flight
-        const int nit = min(ie - seg, RI_MAX);
-        lds_barrier();
-        for (int i = tid; i < nit; i += RT) sitems[i] = items[seg + i];
-        lds_barrier();
-        int it = wave;
-        for (; it + 3 * RW < nit; it += 4 * RW) {
-            double x[4], y[4];
+    const int w_u = __builtin_amdgcn_readfirstlane(wave);
+    for (int base = ib + w_u; base < ie; base += 8 * RW) {
+        double x[8], y[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                int off_s; const double* sl;
-                const int sp = slab_off(sitems[it + u * RW], off_s, sl);
-                x[u] = act_s ? sl[off_s] : 0.0;
-                y[u] = act_h ? sl[off_h + sp * LH_TASKS] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) { vs += x[u]; vh += y[u]; }
-        }
-        for (; it < nit; it += RW) {
+        for (int u = 0; u < 8; ++u) {
+            const int it = base + u * RW;
+            const bool in = it < ie;
+            const uint32_t item = items[in ? it : ib];
             int off_s; const double* sl;
-            const int sp = slab_off(sitems[it], off_s, sl);
-            if (act_s) vs += sl[off_s];
-            if (act_h) vh += sl[off_h + sp * LH_TASKS];
+            const int sp = slab_off(item, off_s, sl);
+            x[u] = (in && act_s) ? sl[off_s] : 0.0;
+            y[u] = (in && act_h) ? sl[off_h + sp * LH_TASKS] : 0.0;
         }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { vs += x[u]; vh += y[u]; }
     }
     part[0][wave][lane] = vs;
     part[1][wave][lane] = vh;
@@ -1970,13 +1970,31 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
     }
 }
 
+// dynamic LDS of k_lin<T>: 4 wave scratches + the chunk's pose tables, step and extrinsics
+template <int T>
+static size_t lin_smem_bytes(int ncam) {
+    using Cfg = LinCfg<T>;
+    return sizeof(double) * ((size_t)LH_WAVES * Cfg::SCR + 2 * (size_t)Cfg::UMAX * ncam * LH_PT + Cfg::UMAX * 6 +
+                             (size_t)ncam * LH_EXT);
+}
+
 // ============================================================================
 // launchers (host side)
 // ============================================================================
 extern "C" {
 
-static size_t lin_smem_bytes(int scr, int ncam) {
-    return sizeof(double) * ((size_t)LH_WAVES * scr + 2 * (size_t)LH_UMAX * ncam * LH_PT + LH_UMAX * 6 + (size_t)ncam * LH_EXT);
+
+// dynamic LDS of k_lin<T> for ncam cameras (the host rejects windows whose chunks would not fit a CU)
+size_t lh_lin_smem(int T, int ncam) {
+    switch (T) {
+        case 1: return lin_smem_bytes<1>(ncam);
+        case 2: return lin_smem_bytes<2>(ncam);
+        case 3: return lin_smem_bytes<3>(ncam);
+        case 4: return lin_smem_bytes<4>(ncam);
+        case 5: return lin_smem_bytes<5>(ncam);
+        case 6: return lin_smem_bytes<6>(ncam);
+        default: return (size_t)-1;
+    }
 }
 
 // Raise the dynamic-LDS limit of every k_lin instantiation on the current device (lh_create), before any
@@ -1986,7 +2004,9 @@ hipError_t lh_prepare_lin() {
         const void* fns[] = {reinterpret_cast<const void*>(&k_lin<1, false>), reinterpret_cast<const void*>(&k_lin<1, true>),
                              reinterpret_cast<const void*>(&k_lin<2, false>), reinterpret_cast<const void*>(&k_lin<2, true>),
                              reinterpret_cast<const void*>(&k_lin<3, false>), reinterpret_cast<const void*>(&k_lin<3, true>),
-                             reinterpret_cast<const void*>(&k_lin<4, false>), reinterpret_cast<const void*>(&k_lin<4, true>)};
+                             reinterpret_cast<const void*>(&k_lin<4, false>), reinterpret_cast<const void*>(&k_lin<4, true>),
+                             reinterpret_cast<const void*>(&k_lin<5, false>), reinterpret_cast<const void*>(&k_lin<5, true>),
+                             reinterpret_cast<const void*>(&k_lin<6, false>), reinterpret_cast<const void*>(&k_lin<6, true>)};
         for (const void* f : fns) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
@@ -2003,7 +2023,7 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     dim3 g(nchunks), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
-        const size_t smem = lin_smem_bytes(LinCfg<TT>::SCR, prm.ncam);                                 \
+        const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
         hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
                            edge_rho, slabs, prm, nrec, fixed_mask, chunk_base);                                    \
     } while (0)
@@ -2016,6 +2036,10 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
         case 7: LH_LIN(3, true); break;
         case 8: LH_LIN(4, false); break;
         case 9: LH_LIN(4, true); break;
+        case 10: LH_LIN(5, false); break;
+        case 11: LH_LIN(5, true); break;
+        case 12: LH_LIN(6, false); break;
+        case 13: LH_LIN(6, true); break;
         default: return hipErrorInvalidValue;
     }
 #undef LH_LIN

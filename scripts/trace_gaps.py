@@ -12,7 +12,7 @@ print(f"{'kernel':24s} {'dur us':>8s} {'gap us':>8s}")
 last = i0
 for i in range(i0, i1):
     r = rows[i]
-    if not r["Kernel_Name"].startswith(("k_reset", "void k_lin", "k_reduce", "k_ctrl")):
+    if not r["Kernel_Name"].startswith(("k_reset", "void k_lin", "k_reduce", "k_ctrl", "void k_ctrl")):
         break                              # the solve ends at its last controller launch
     last = i
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])

@@ -308,3 +308,32 @@ def test_largest_supported_window_p21():
         w22 = lego_ba.generate_window(P=22, L=500, k=8, seed=4)
         lego_ba.Solver().solve(w22)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("kmin,kmax,mode", [(11, 16, 1), (2, 16, 1), (8, 15, 0)])
+def test_wide_landmarks_up_to_16_poses(kmin, kmax, mode):
+    """Landmarks seen by up to 16 keyframes (the reference window is 15 keyframes, map.h:82, so a
+    landmark can be seen by all of them): chunk windows of T = 5 and 6 MFMA tiles (k_lin<5>,
+    k_lin<6>, accumulators in AGPRs), slots up to 15, lane groups of 16."""
+    p = dict(__import__("windows").STABLE, outlier_frac=0.0)
+    w = lego_ba.generate_window(P=20, L=3000, k=kmin, k_max=kmax, seed=2, pose_mode=mode, **p)
+    f = np.zeros(20, np.uint8)
+    f[0] = 1
+    w["pose_fixed"] = f
+    g = lego_ba.Solver(max_iters=1, max_trials=1).solve(w)
+    o = ob.solve(w, max_iters=1, max_trials=1)
+    assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-12
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-7)
+    gf = lego_ba.Solver().solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 2, 8))
+    assert gf["iterations"] in its
+    assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+
+
+def test_landmark_seen_by_17_poses_is_unsupported():
+    w = lego_ba.generate_window(P=20, L=200, k=17, seed=1, pose_mode=1)
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.Solver().solve(w)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED
