@@ -314,7 +314,7 @@ def test_largest_supported_window_p21():
 def test_wide_landmarks_up_to_16_poses(kmin, kmax, mode):
     """Landmarks seen by up to 16 keyframes (the reference window is 15 keyframes, map.h:82, so a
     landmark can be seen by all of them): chunk windows of T = 5 and 6 MFMA tiles (k_lin<5>,
-    k_lin<6>, accumulators in AGPRs), slots up to 15, lane groups of 16."""
+    k_lin<6>), slots up to 15, lane groups of 16."""
     p = dict(__import__("windows").STABLE, outlier_frac=0.0)
     w = lego_ba.generate_window(P=20, L=3000, k=kmin, k_max=kmax, seed=2, pose_mode=mode, **p)
     f = np.zeros(20, np.uint8)
