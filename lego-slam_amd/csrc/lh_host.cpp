@@ -353,6 +353,10 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     int chunk_lm = (int)((Lact + 511) / 512);
     chunk_lm = ((chunk_lm + 4 * LH_SB_LM - 1) / (4 * LH_SB_LM)) * (4 * LH_SB_LM);
     chunk_lm = std::max(32, std::min(256, chunk_lm));
+    if (const char* e = getenv("LH_CHUNK_LM")) {   // A/B knob for the chunk size (scripts/gpu_ab_chunk.sh)
+        const int v = atoi(e);
+        if (v >= LH_SB_LM && v <= 512) chunk_lm = v;
+    }
 
     struct ChunkTmp { std::vector<int32_t> lms; uint32_t mask; };
     std::vector<ChunkTmp> ctmp;
