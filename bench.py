@@ -1,23 +1,27 @@
 """bench.py — LM iterations/s and ms/solve of the MI355X BA solver.
 
-A "step" is one complete Backend::Optimize solve (problem.solve(10),
-src/backend_lego.cpp:161) of a device-resident sliding window: restart from the
-uploaded initial state, run every LM trial to the reference stop rule.
-value = LM iterations completed per second, summed over ranks.
+A "step" is one complete Backend::Optimize solve (problem.solve(10), src/backend_lego.cpp:161) of a
+device-resident sliding window: restart from the uploaded initial state, run every LM trial to the
+reference stop rule.  value = LM iterations (of the whole window) completed per second.
 
-Workload (BASELINE.json metric window, configs[2]): 20 keyframes, 50 000
-landmarks, 400 000 observations per GPU, fp64 throughout (>= the reference's
-double).  With N GPUs the window grows to N x 50 000 landmarks (landmark
-shards, poses replicated, one RCCL all-reduce of the reduced pose system per
-LM trial) -> "scaling": "weak"; value counts shard-iterations (iterations x N).
+Workloads (BASELINE.json configs); fp64 throughout (>= the reference's double):
+  C3  20 KF / 50 000 landmarks / 400 000 obs on one GPU: the metric window (the N = 1 default).
+  C4  20 KF / 500 000 landmarks / 4 000 000 obs, landmark-sharded over N GPUs (500 000 / N landmarks
+      and their observations per rank, poses replicated, one RCCL all-reduce of the reduced pose
+      system per LM trial): the multi-GPU window (the N > 1 default), "scaling": "strong".  value
+      counts iterations of the whole window (no factor N).  The N = 1 line carries the same window on
+      one GPU ("c4_1gpu") as the base of the scaling ratio.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]
+Usage: python bench.py [--gpus N --steps K --warmup W] [--workload C3|C4]
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -31,13 +35,13 @@ import lego_ba  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFS = 78.6       # MI355X FP64 spec (vector = matrix); measured on the box:
                            # v_mfma_f64_16x16x4 72.0 TF, v_fma_f64 60.5 TF (lego-slam_amd/tools/ubench_fp64_peak.hip)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_k_lin.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_k_lin.json")
+WORKLOADS = {"C3": dict(P=20, L=50_000, k=8), "C4": dict(P=20, L=500_000, k=8)}
 
 
 def survey_bytes_per_iteration(n_obs, n_lm):
-    """SURVEY.md 8(d) compulsory HBM bytes of one LM iteration (one k_lin launch fuses the
-    three passes: linearise + Schur, back-substitute, chi2-evaluate):
-    B = 3 (12 O + 28 L) + 24 L."""
+    """SURVEY.md 8(d) compulsory HBM bytes of one LM iteration (one k_lin launch fuses the three
+    passes: linearise + Schur, back-substitute, chi2-evaluate): B = 3 (12 O + 28 L) + 24 L."""
     return 3 * (12 * n_obs + 28 * n_lm) + 24 * n_lm
 
 
@@ -60,19 +64,105 @@ def pmc_traffic(cfg_key):
     return d.get("bytes_per_launch") if d.get("workload") == cfg_key else None
 
 
+def host_info():
+    """The host the CPU baseline ran on: core counts and CPU model."""
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "cpus_available": avail, "cpu_model": model}
+
+
+def native_oracle():
+    """The timed CPU baseline build: the oracle at -O3 -march=native, compiled
+    here for this host's CPU (the parity build in oracle/ is portable).  -ffp-contract=off keeps the
+    reference's roundings (no FMA), so it computes the same numbers.  Falls back to the parity build."""
+    src = os.path.join(ROOT, "oracle", "lego_oracle.c")
+    out = os.path.join(tempfile.gettempdir(), f"liblego_oracle_native_{os.getpid()}.so")
+    flags = ["-O3", "-march=native", "-fPIC", "-std=gnu11", "-ffp-contract=off", "-fopenmp", "-shared"]
+    try:
+        subprocess.run(["gcc", *flags, "-o", out, src, "-lm"], check=True, timeout=120, capture_output=True)
+        return out, " ".join(flags)
+    except (OSError, subprocess.SubprocessError):
+        return None, "-O3 -ffp-contract=off -fopenmp (parity build; native build failed)"
+
+
+def make_window(name, family, seed, rank, world):
+    """Rank `rank`'s landmark shard of workload `name` (all of it with world = 1), generated directly."""
+    from windows import STABLE
+    c = WORKLOADS[name]
+    params = {}
+    if family.startswith("stable"):
+        params.update(STABLE)
+    if family == "stable_noout":
+        params["outlier_frac"] = 0.0
+    L = c["L"]
+    w = lego_ba.generate_window(P=c["P"], L=L, k=c["k"], seed=seed, lm_begin=rank * L // world,
+                                lm_end=(rank + 1) * L // world, **params)
+    if family.startswith("stable"):
+        f = np.zeros(c["P"], np.uint8)
+        f[0] = 1
+        w["pose_fixed"] = f
+    return w
+
+
+def time_solves(solver, steps, barrier):
+    import torch
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    it = tr = 0
+    res = None
+    for _ in range(steps):
+        res = solver.solve_resident()
+        it += res["iterations"]
+        tr += res["trials"]
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0, it, tr, res
+
+
+def roofline(solver, n_obs, n_lm, k, cfg_key, reps=50):
+    """k_lin (the dominant kernel; one launch = one LM trial's linearise / back-substitute / chi2 pass)
+    against the FP64 peak: SURVEY 8(d) flops per iteration / k_lin's duration, the latter measured by
+    replaying the solve's trial-mode launch `reps` times back to back between HIP events on the
+    solver's stream (lh_debug_time_lin)."""
+    ms = solver.time_lin_ms(reps)
+    flops = survey_flops_per_iteration(n_obs, n_lm, k)
+    nbytes = survey_bytes_per_iteration(n_obs, n_lm)
+    tfs = flops / (ms * 1e-3) / 1e12
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    traffic = pmc_traffic(cfg_key)
+    return ({"bound": "mfma", "achieved": round(tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+             "frac": round(tfs / FP64_PEAK_TFS, 4), "traffic": traffic, "kernel": "k_lin",
+             "avg_launch_ms": round(ms, 5), "timing": f"{reps} back-to-back replays between HIP events",
+             "flops_per_launch": flops,
+             "peak_note": "FP64 spec (vector = matrix); measured here 72.0 TF MFMA, 60.5 TF VALU"},
+            {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes, "traffic": traffic})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--landmarks", type=int, default=50000, help="landmarks per GPU")
-    ap.add_argument("--poses", type=int, default=20)
-    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--workload", default="auto", choices=["auto", "C3", "C4"],
+                    help="auto: C3 on one GPU, C4 sharded over N > 1")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--family", default="stable_noout", choices=["stable_noout", "stable", "default"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the cpu_baseline sample")
+    ap.add_argument("--no-extras", action="store_true", help="only the timed line (no side measurements)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="length of the cpu_baseline sample")
     ap.add_argument("--trials-per-sync", type=int, default=0)
     args = ap.parse_args()
 
@@ -81,6 +171,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world != 1:
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+    name = args.workload if args.workload != "auto" else ("C3" if world == 1 else "C4")
 
     import torch
     dist = None
@@ -89,18 +180,7 @@ def main():
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
 
-    from windows import STABLE
-    params = dict(STABLE) if args.family.startswith("stable") else {}
-    if args.family == "stable_noout":
-        params["outlier_frac"] = 0.0
-    L = args.landmarks
-    w = lego_ba.generate_window(P=args.poses, L=L * world, k=args.k, seed=args.seed,
-                                lm_begin=rank * L, lm_end=(rank + 1) * L, **params)
-    if args.family.startswith("stable"):
-        f = np.zeros(args.poses, np.uint8)
-        f[0] = 1
-        w["pose_fixed"] = f
-
+    w = make_window(name, args.family, args.seed, rank, world)
     comm_id = bytes(128)
     if world > 1:
         obj = [lego_ba.comm_unique_id() if rank == 0 else None]
@@ -116,36 +196,22 @@ def main():
 
     for _ in range(args.warmup):
         solver.solve_resident()
-
-    def timed(profile):
-        solver.set_profiling(profile)
-        solver.kernel_stats_reset()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        it = tr = 0
-        res = None
-        for _ in range(args.steps):
-            res = solver.solve_resident()
-            it += res["iterations"]
-            tr += res["trials"]
-        torch.cuda.synchronize()
-        barrier()
-        dt = time.perf_counter() - t0
-        if dist is not None:
-            t = torch.tensor([dt], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return dt, it, tr, res
-
-    # ---- timed region: K whole solves, no per-kernel instrumentation ----
-    dt, iters, trials, last = timed(False)
-    # ---- the same K solves again with a HIP event pair around every kernel (on the solver's
-    #      stream): per-kernel average durations for the roofline ----
-    dt_prof, _, _, _ = timed(True)
+    # ---- timed region: K whole solves of the resident window, no per-kernel instrumentation ----
+    dt, iters, trials, last = time_solves(solver, args.steps, barrier)
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # the same solves with a HIP event pair around every kernel: per-kernel ms per solve
+    solver.set_profiling(True)
+    solver.kernel_stats_reset()
+    time_solves(solver, max(2, args.steps // 4), barrier)
     ks = solver.kernel_stats()
     solver.set_profiling(False)
-    event_floor_ms = solver.event_floor_ms()   # the same event bracket around an empty kernel
+    n_obs, n_lm = len(w["obs_pose"]), len(w["lm_xyz"])
+    c = WORKLOADS[name]
+    cfg_key = f"{name}-{args.family}-s{args.seed}"
+    rl, rl_hbm = roofline(solver, n_obs, n_lm, c["k"], cfg_key)
 
     if rank != 0:
         if dist is not None:
@@ -153,20 +219,8 @@ def main():
             dist.destroy_process_group()
         return
 
-    value = world * iters / dt
-    n_obs, n_lm = len(w["obs_pose"]), len(w["lm_xyz"])
-    lin_n, lin_ms = ks.get("k_lin", (0, 0.0))
-    lin_bracket_ms = lin_ms / max(lin_n, 1)
-    # the event pair brackets the launch too: its empty-kernel floor is subtracted (rocprofv3's
-    # kernel-trace average of the same command is committed under profiles/ for comparison)
-    lin_avg_ms = max(lin_bracket_ms - event_floor_ms, 1e-6)
-    flops_per = survey_flops_per_iteration(n_obs, n_lm, args.k)
-    bytes_per = survey_bytes_per_iteration(n_obs, n_lm)
-    achieved_tfs = flops_per / (lin_avg_ms * 1e-3) / 1e12 if lin_avg_ms > 0 else 0.0
-    achieved_gbs = bytes_per / (lin_avg_ms * 1e-3) / 1e9 if lin_avg_ms > 0 else 0.0
-    cfg_key = f"P{args.poses}-L{L}-k{args.k}-{args.family}-s{args.seed}"
-    traffic = pmc_traffic(cfg_key)
-
+    value = iters / dt
+    nprof = max(2, args.steps // 4)
     out = {
         "metric": "LM iterations/sec + ms/solve, 20KF/50k-pts/400k-obs window; final chi2 vs ref",
         "value": round(value, 3),
@@ -175,100 +229,139 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
-        "ms_per_step_with_kernel_events": round(dt_prof / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic (tools/window_gen.c, family={args.family}, seed={args.seed})",
-        "config": {"workload": f"sliding-window BA solve(10): {args.poses} KF / {L * world} landmarks / "
-                               f"{n_obs * world} obs ({L} landmarks per GPU)",
-                   "keyframes": args.poses, "landmarks_per_gpu": L, "obs_per_gpu": n_obs,
-                   "parallelism": f"landmark-shard x{world}"},
+        "config": {"workload": f"{name}: sliding-window BA solve(10), {c['P']} KF / {c['L']} landmarks / "
+                               f"{c['L'] * c['k']} obs" + (f", landmark-sharded over {world} GPUs" if world > 1 else ""),
+                   "keyframes": c["P"], "landmarks": c["L"], "landmarks_per_gpu": c["L"] // world,
+                   "obs_this_rank": n_obs, "parallelism": f"landmark-shard x{world}"},
         "iterations_per_solve": iters / args.steps,
         "trials_per_solve": trials / args.steps,
+        "trials_per_s": round(trials / dt, 3),
         "chi2_final": last["chi2_final"],
-        "kernels_ms_per_solve": {k: round(v[1] / args.steps, 4) for k, v in ks.items()},
-        # dominant kernel k_lin (one launch = one LM iteration's linearise/back-substitute/chi2 pass);
-        # the path is FP64-bound (~29 flop/B > ridge 9.8 flop/B)
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": round(achieved_tfs / FP64_PEAK_TFS, 4), "traffic": traffic,
-                     "kernel": "k_lin", "avg_launch_ms": round(lin_avg_ms, 5), "event_bracket_ms": round(lin_bracket_ms, 5),
-                     "event_floor_ms": round(event_floor_ms, 5), "flops_per_launch": flops_per,
-                     "peak_note": "FP64 spec (vector = matrix); measured here 72.0 TF MFMA, 60.5 TF VALU"},
-        "roofline_hbm": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": bytes_per,
-                         "traffic": traffic},
+        "kernels_ms_per_solve_event_bracketed": {k: round(v[1] / nprof, 4) for k, v in ks.items()},
+        "roofline": rl,
+        "roofline_hbm": rl_hbm,
     }
+    if world > 1 or args.no_extras:
+        print(json.dumps(out))
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # ---------------- side measurements (one GPU), reported beside value, never as it ----------------
+    # the drop-in call Backend::Optimize pays: lh_solve on host buffers (preprocess + copies + solve +
+    # download), median of 5
+    sh = lego_ba.Solver(device=local)
+    sh.solve(w)
+    runs = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        r = sh.solve(w)
+        runs.append(((time.perf_counter() - t0) * 1e3, r))
+    runs.sort(key=lambda x: x[0])
+    ms_h, rh = runs[2]
+    out["host_buffer_path"] = {"ms_per_solve": round(ms_h, 3), "iterations_per_s": round(rh["iterations"] / ms_h * 1e3, 3),
+                               "prep_ms": round(rh["time_prep_ms"], 3), "upload_ms": round(rh["time_upload_ms"], 3),
+                               "solve_ms": round(rh["time_ms"], 3), "download_ms": round(rh["time_download_ms"], 3),
+                               "note": "lh_solve(window in host memory): planner + pinned copies + solve + "
+                                       "outputs (poses, landmarks, per-edge rho) back; median of 5"}
+    sh.close()
+    # C4 on one GPU: the base of the N-GPU scaling ratio (SCALE lines run C4 sharded)
+    if name == "C3":
+        w4 = make_window("C4", args.family, args.seed, 0, 1)
+        s4 = lego_ba.Solver(device=local)
+        s4.upload(w4)
+        s4.solve_resident()
+        d4, i4, t4, l4 = time_solves(s4, 5, barrier)
+        r4, _ = roofline(s4, len(w4["obs_pose"]), len(w4["lm_xyz"]), 8, f"C4-{args.family}-s{args.seed}", reps=10)
+        out["c4_1gpu"] = {"iterations_per_s": round(i4 / d4, 3), "ms_per_solve": round(d4 / 5 * 1e3, 3),
+                          "iterations_per_solve": i4 / 5, "trials_per_solve": t4 / 5, "chi2_final": l4["chi2_final"],
+                          "k_lin_ms": r4["avg_launch_ms"], "k_lin_frac_fp64": r4["frac"]}
+        s4.close()
+        del w4
+    # survey-default family (the reference's live configuration: free gauge, 2 % outliers, left image
+    # only).  Its C3 windows have landmarks running off to ~1e15 and are not reproducible under
+    # summation reorders even in the oracle; seed 5 is, with the Huber-gate residue
+    # taken as 0 on both sides (gate_mode 1): parity is checked on it.
+    wd = make_window("C3", "default", 5, 0, 1)
+    sd = lego_ba.Solver(device=local, gate_mode=1)
+    sd.upload(wd)
+    sd.solve_resident()
+    dd, idd, tdd, ld = time_solves(sd, 5, barrier)
+    out["survey_default_c3"] = {"seed": 5, "gate_mode": 1, "iterations_per_s": round(idd / dd, 3),
+                                "ms_per_solve": round(dd / 5 * 1e3, 3), "iterations_per_solve": idd / 5,
+                                "trials_per_solve": tdd / 5, "chi2_final": ld["chi2_final"]}
+    sd.close()
     # the same window through the PCG reduced solve (BASELINE config 3 names "Schur + PCG"; the
-    # reference's own solver, and value above, is the LDLT): reported beside value, never as it
-    if world == 1:
-        sp = lego_ba.Solver(device=local, linear_solver=lego_ba.LH_SOLVER_PCG)
-        sp.upload(w)
-        sp.solve_resident()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        pits = pcgs = 0
-        for _ in range(args.steps):
-            r = sp.solve_resident()
-            pits += r["iterations"]
-            pcgs += r["pcg_iterations"]
-        torch.cuda.synchronize()
-        dtp = time.perf_counter() - t
-        out["pcg"] = {"ms_per_solve": round(dtp / args.steps * 1e3, 4), "iterations_per_s": round(pits / dtp, 3),
-                      "iterations_per_solve": pits / args.steps, "pcg_steps_per_solve": pcgs / args.steps,
-                      "chi2_rel_vs_ldlt": abs(r["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
-        sp.close()
-    # the frontend's pose-only LM (Frontend::EstimateCurrentPose) on a batch of
-    # frames through lh_estimate_pose: device time of one launch over the batch, beside value
-    if world == 1:
-        import frames
-        nf = 2048
-        fb = frames.batch(args.seed, nf, n_obs=150)
-        sf = lego_ba.Solver(device=local)
-        sf.estimate_pose(fb)
-        tms = [sf.estimate_pose(fb)["time_ms"] for _ in range(3)]
-        out["estimate_pose"] = {"frames": nf, "obs_per_frame": 150, "ms_per_batch": round(min(tms), 4),
-                                "frames_per_s": round(nf / (min(tms) * 1e-3), 1),
-                                "note": "device time of one lh_estimate_pose launch (4 rounds of solve(10) per frame)"}
-        if not args.no_cpu:
-            import oracle_bind
-            t = time.perf_counter()
-            oracle_bind.estimate_pose(frames.batch(args.seed, 256, n_obs=150))
-            out["estimate_pose"]["cpu_frames_per_s_1core"] = round(256 / (time.perf_counter() - t), 1)
-        sf.close()
-    # end-to-end host-buffer call (lh_solve: upload + solve + download over PCIe), rank 0 only
-    if world == 1:
-        solver_h = lego_ba.Solver(device=local)
-        solver_h.solve(w)
-        t = time.perf_counter()
-        solver_h.solve(w)
-        out["ms_per_solve_host_buffers"] = round((time.perf_counter() - t) * 1e3, 3)
-        solver_h.close()
-    if world == 1 and not args.no_cpu:
+    # reference's own solver, and value above, is the LDLT)
+    sp = lego_ba.Solver(device=local, linear_solver=lego_ba.LH_SOLVER_PCG)
+    sp.upload(w)
+    sp.solve_resident()
+    dp, ip, _, rp = time_solves(sp, max(3, args.steps // 4), barrier)
+    npcg = max(3, args.steps // 4)
+    out["pcg"] = {"ms_per_solve": round(dp / npcg * 1e3, 4), "iterations_per_s": round(ip / dp, 3),
+                  "iterations_per_solve": ip / npcg, "pcg_steps_per_solve": rp["pcg_iterations"],
+                  "chi2_rel_vs_ldlt": abs(rp["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
+    sp.close()
+    # the frontend's pose-only LM (Frontend::EstimateCurrentPose): one frame the way
+    # the reference calls it (frontend_lego.cpp:157, once per frame), and a batch of frames
+    import frames
+    sf = lego_ba.Solver(device=local)
+    one = frames.batch(args.seed, 1, n_obs=150)
+    sf.estimate_pose(one)
+    lat = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        sf.estimate_pose(one)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    nf = 2048
+    fb = frames.batch(args.seed, nf, n_obs=150)
+    sf.estimate_pose(fb)
+    tms = [sf.estimate_pose(fb)["time_ms"] for _ in range(3)]
+    out["estimate_pose"] = {"single_frame_ms": round(float(np.median(lat)), 4), "obs_per_frame": 150,
+                            "batch_frames": nf, "batch_ms": round(min(tms), 4),
+                            "batch_frames_per_s": round(nf / (min(tms) * 1e-3), 1),
+                            "note": "single frame: host-to-host lh_estimate_pose call (4 rounds of solve(10)); "
+                                    "batch: device time of one launch"}
+    sf.close()
+    if not args.no_cpu:
         import oracle_bind
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        # bounded sample: repeated full solves of the same window for >= cpu_seconds of CPU work
-        t = time.perf_counter()
+        lib_path, flags = native_oracle()
+        hi = host_info()
+        threads = hi["cpus_available"]
+        o = oracle_bind.solve(w, n_threads=threads, lib_path=lib_path)   # warm-up
+        t0 = time.perf_counter()
         its = nsolve = 0
         while True:
-            o = oracle_bind.solve(w, n_threads=threads)
+            o = oracle_bind.solve(w, n_threads=threads, lib_path=lib_path)
             its += o["iterations"]
             nsolve += 1
-            ct = time.perf_counter() - t
+            ct = time.perf_counter() - t0
             if ct >= args.cpu_seconds:
                 break
-        out["cpu_baseline"] = {"value": round(its / ct, 4), "unit": "LM iterations/s",
-                               "cores": threads, "kind": "port",
-                               "sample": f"{nsolve} full solve(10)s of the same window by the block-sparse oracle "
-                                         f"(oracle/lego_oracle.c ref_sparse, OpenMP {threads} threads), {ct:.1f} s, "
-                                         f"{its} iterations"}
+        out["cpu_baseline"] = {"value": round(its / ct, 4), "unit": "LM iterations/s", "cores": threads, "kind": "port",
+                               "sample": f"{nsolve} full solve(10)s of the same C3 window by the block-sparse oracle "
+                                         f"(oracle/lego_oracle.c ref_sparse, gcc {flags}, OpenMP {threads} threads = "
+                                         f"every CPU available to this process), {ct:.1f} s, {its} iterations",
+                               "host": hi}
         out["chi2_rel_vs_oracle"] = abs(last["chi2_final"] - o["chi2_final"]) / o["chi2_final"]
+        op = oracle_bind.solve(w, n_threads=threads)
+        out["native_build_matches_parity_build"] = bool(op["chi2_final"] == o["chi2_final"])
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+        od = oracle_bind.solve(wd, n_threads=threads, gate_mode=1, lib_path=lib_path)
+        out["survey_default_c3"]["chi2_rel_vs_oracle"] = abs(ld["chi2_final"] - od["chi2_final"]) / od["chi2_final"]
+        out["survey_default_c3"]["oracle_iterations"] = od["iterations"]
+        if lib_path:
+            try:
+                os.unlink(lib_path)
+            except OSError:
+                pass
     print(json.dumps(out))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define LH_ABI_VERSION 2
+#define LH_ABI_VERSION 3
 
 typedef enum lh_status {
     LH_OK = 0,
@@ -57,6 +57,13 @@ typedef enum lh_strategy { LH_STRATEGY_DEFAULT = 0, LH_STRATEGY_1 = 1 } lh_strat
    (:422), with its first-step bug fixed (:595-596 never add alpha*p to x). */
 typedef enum lh_linear_solver { LH_SOLVER_LDLT = 0, LH_SOLVER_PCG = 1 } lh_linear_solver;
 
+/* The per-trial exchange of a landmark-sharded solve (world_size > 1): RCCL on the handle's stream
+   (one process per GPU), or a caller-supplied all-reduce over host buffers (any transport: MPI, gloo,
+   sockets), called once per LM trial from inside lh_solve on the calling thread. */
+typedef enum lh_comm_mode { LH_COMM_RCCL = 0, LH_COMM_HOST = 1 } lh_comm_mode;
+/* in-place all-reduce of count doubles over the ranks; op 0 = sum, 1 = max; returns 0 on success */
+typedef int (*lh_allreduce_fn)(void *user, double *buf, int64_t count, int32_t op);
+
 typedef struct lh_options {
     int32_t abi_version;      /* must be LH_ABI_VERSION                                      */
     int32_t max_iters;        /* outer LM iterations, solve(10)          backend_lego.cpp:161 */
@@ -72,13 +79,24 @@ typedef struct lh_options {
     int32_t device;           /* HIP device ordinal, -1 = current device                      */
     int32_t world_size;       /* landmark shards (one process per GPU); 1 = single GPU        */
     int32_t rank;             /* this process's shard                                         */
-    int32_t degenerate_guard; /* 0: reference semantics (rank-deficient H_ll poisons the step,
-                                 problem.cpp:396-400); 1: skip such landmarks' Schur terms    */
+    int32_t degenerate_guard; /* 0: reference semantics: a landmark with one edge (rank-2 H_ll) or a
+                                 non-positive-definite H_ll poisons the step, as the LU inverse's
+                                 inf does (problem.cpp:396-400; the solve then rejects every trial);
+                                 1: such landmarks are held fixed (no Schur term, no update)   */
     int32_t trials_per_sync;  /* LM trials kept in flight ahead of the host poll (0: auto = 2)  */
     int32_t profile;          /* 1: time every kernel with HIP events (lh_kernel_stats)       */
     int32_t pcg_max_iters;    /* PCG: iteration cap; <= 0: 2 * rows (problem.cpp:422)          */
     double pcg_tol;           /* PCG: stop when ||r|| <= pcg_tol * ||b|| (1e-6, problem.cpp:597) */
     uint8_t comm_id[128];     /* ncclUniqueId from lh_comm_unique_id on rank 0 (world_size>1) */
+    /* ---- ABI 3 ---- */
+    int32_t gate_mode;        /* 0: the reference's Huber gate rho1 + 2 rho2 e2 > 0 (base_edge.cpp:55);
+                                 1: diagnostic, its analytically-zero residue on outlier edges taken
+                                 as 0 (the oracle's gate_mode 1; parity tests only)            */
+    int32_t chunk_landmarks;  /* landmarks per k_lin chunk; 0 = auto (~2 workgroups per CU)     */
+    int32_t comm_mode;        /* lh_comm_mode (world_size > 1)                                  */
+    int32_t host_threads;     /* window-preprocessing threads; 0 = auto (<= 8)                   */
+    lh_allreduce_fn allreduce;  /* LH_COMM_HOST: the exchange                                    */
+    void *allreduce_user;       /* its first argument                                            */
 } lh_options;
 
 /*
@@ -123,6 +141,10 @@ typedef struct lh_result {
     double lambda_final;
     double time_ms;            /* wall time of the LM solve on the device (excludes upload)        */
     int32_t pcg_iterations;    /* PCG iterations summed over all trials (0 with LH_SOLVER_LDLT)    */
+    int32_t degenerate;        /* landmarks with a rank-deficient H_ll at the initial linearisation */
+    double time_prep_ms;       /* lh_solve / lh_upload: host preprocessing of the window           */
+    double time_upload_ms;     /* lh_solve / lh_upload: preprocessing + host-to-device copies      */
+    double time_download_ms;   /* device-to-host copies of the requested outputs                   */
 } lh_result;
 
 typedef struct lh_kernel_stats {
@@ -209,6 +231,12 @@ int lh_debug_pcg_probe(const double* S, const double* b, int n, double tol, int 
 int lh_debug_event_floor(lh_handle *h, double *ms);
 /* per-phase wave-cycle totals of a -DLH_STAMPS diagnostic build (all zero in the product build) */
 int lh_debug_stamps(unsigned long long *out, int n, int reset);
+/* k_lin's duration per LM trial, measured after a solve: the trial-mode k_lin launch(es) replayed
+   reps times back to back between two HIP events on the handle's stream (ms per replay).  The
+   replay rewrites the candidate buffers and the per-edge chi2: read the solve's outputs first. */
+int lh_debug_time_lin(lh_handle *h, int reps, double *ms);
+/* reduced-system all-reduces (data-path collectives) the last solve issued on this rank */
+int lh_debug_comm_count(lh_handle *h, int64_t *n);
 
 #ifdef __cplusplus
 }

@@ -1,50 +1,48 @@
-// lh_host.cpp — C ABI (include/lego_ba.h) of the MI355X BA solver: window
-// preprocessing, device buffers, the LM launch loop and the RCCL exchange.
+// lh_host.cpp — C ABI (include/lego_ba.h) of the MI355X BA solver: device buffers, the upload of
+// a window (lh_plan.cpp preprocessing into pinned staging, one async copy per array), the LM launch
+// loop, the per-trial exchange of a landmark-sharded solve, and the download of the results.
 //
-// Host-side work per window (once, at lh_upload):
-//   * landmark-major CSR of the observations, each landmark's observations in
-//     ascending pose order (the reference visits edges in hash order; any order
-//     is the same problem);
-//   * landmarks sorted by observation span and packed into chunks whose union
-//     of observing poses fits one MFMA window (<= LH_UMAX poses), chunks split
-//     into wave sub-batches (<= 8 landmarks, <= 64 observations);
-//   * the reduce plan: for every pose pair, the chunks that touch it.
-// Per solve nothing but kernel launches (and, with >1 rank, one RCCL all-reduce
-// per LM trial) happens on the host; it polls the device stop flag every few
-// trials.
+// Per solve nothing but kernel launches happens on the host: the whole LM loop (accept/reject,
+// lambda schedule, stop rule) runs on the device, and the host keeps `depth` trials enqueued ahead
+// of the device's progress word.  With >1 rank each trial carries one all-reduce of the packed
+// reduced pose system; every rank issues exactly the same number of them (see solve_resident_impl).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
-#include <numeric>
 #include <vector>
 
 #include "../../include/lego_ba.h"
 #include "lh_common.h"
+#include "lh_plan.h"
 
 extern "C" {
-hipError_t lh_prepare_lin();
+hipError_t lh_prepare_lin(int lds_limit);
 size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* slabs, lh_params prm, int nrec, uint32_t fixed_mask);
-hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double* slabs, const uint32_t* pair_ptr,
-                            const uint32_t* items, const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage,
-                            double* maxd, lh_params prm, int n_chunks);
+hipError_t lh_launch_reduce(hipStream_t st, const double* slabs, const uint32_t* pair_ptr, const uint32_t* items,
+                            const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
+                            lh_params prm, int n_chunks);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
                           lh_params prm, int mode, int* host_done, int seq);
-hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, long nrec_doubles, double* qt,
-                           const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab, double* dxp,
-                           int ndxp, lh_ctrl* ctrl);
+hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
+                           double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
+                           double* dxp, int ndxp, lh_ctrl* ctrl);
+hipError_t lh_launch_gather(hipStream_t st, const lh_ctrl* ctrl, const double* rec, const int32_t* lm_perm, int nrec,
+                            const double* rho, const int32_t* obs_perm, long nslots, double* out_xyz, double* out_rho);
 hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x, int solver, double tol, int max_it,
                                 int* iters);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
@@ -69,13 +67,35 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
-        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-        hipError_t e = hipMalloc(&p, bytes);
-        if (e == hipSuccess) n = std::max<size_t>(count, 1);
+        const size_t c = std::max<size_t>(count, 1);
+        hipError_t e = hipMalloc(&p, c * sizeof(T));
+        if (e == hipSuccess) n = c;
         return e;
     }
     void release() {
         if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+// pinned host staging, grown on demand and reused across windows
+template <typename T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        const size_t c = std::max<size_t>(count + count / 4, 1);   // headroom: the next window is similar
+        hipError_t e = hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = c;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
     }
@@ -165,34 +185,53 @@ void pose_table(const double* T12, const double* e, double* pt) {
     pt[23] = 0.0;
 }
 
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int auto_host_threads() {
+    cpu_set_t set;
+    int n = 8;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    return std::max(1, std::min(8, n));
+}
+
 }  // namespace
 
 struct lh_handle {
     lh_options opt;
     int device = 0;
+    int lds_limit = 160 * 1024;   // hipDeviceAttributeMaxSharedMemoryPerBlock of the device
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
+    bool host_comm = false;       // LH_COMM_HOST with world_size > 1
     bool uploaded = false;
+    lh::Pool* pool = nullptr;
 
-    // window (host copies needed to answer a solve)
-    int P = 0, L = 0, L_act = 0, ncam = 1;
-    int64_t O = 0;
-    uint32_t fixed_mask = 0;
+    // window
+    lh::Plan plan;
+    int P = 0, L = 0, ncam = 1, n_rec = 0;
+    int64_t O = 0, n_slots = 0;
     lh_params prm{};
-    std::vector<int32_t> lm_perm;      // landmark record slot -> window landmark (-1: padding)
-    std::vector<int64_t> obs_perm;     // chunked obs -> window obs
-    std::vector<double> lm_in;         // window input positions (landmarks with no edge keep them)
-    int n_chunks = 0;
-    int tgroup_begin[LH_TMAX + 2] = {0};
     lh_rs_layout LY{};
+    double last_prep_ms = 0.0, last_upload_ms = 0.0;
+
+    // pinned staging of the upload
+    HostBuf<lh_chunk> s_chunks;
+    HostBuf<lh_subbatch> s_sbs;
+    HostBuf<uint32_t> s_meta, s_items, s_pair_ptr, s_rsmap;
+    HostBuf<uint16_t> s_pair_pq;
+    HostBuf<int32_t> s_obs_perm, s_lm_perm;
+    HostBuf<double> s_uv, s_lm, s_qt, s_ptab, s_ext, s_rs;   // s_rs: the host-exchange buffer
 
     // device buffers
     DevBuf<lh_chunk> d_chunks;
     DevBuf<lh_subbatch> d_sbs;
     DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
     DevBuf<uint16_t> d_pair_pq;
-    DevBuf<double> d_uv, d_rec, d_rec_init, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs,
-        d_rs_stage, d_rs_commit, d_maxd, d_dxp;
+    DevBuf<int32_t> d_obs_perm, d_lm_perm;
+    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs, d_rs_stage,
+        d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
     // frontend pose-only batch (lh_estimate_pose)
     DevBuf<int64_t> f_ptr;
@@ -200,13 +239,16 @@ struct lh_handle {
     DevBuf<uint8_t> f_flag_in, f_flag_out;
     DevBuf<int32_t> f_iters, f_inl;
     lh_ctrl* h_ctrl = nullptr;   // pinned
-    int* h_done = nullptr;       // pinned, mapped: k_ctrl raises it when the LM loop stops
+    int* h_done = nullptr;       // pinned, mapped: [0] k_ctrl raises it when the LM loop stops, [1] progress
     int* d_done = nullptr;       // device alias of h_done
+
+    // per-solve bookkeeping
+    int64_t n_coll = 0;          // data-path all-reduces of the last solve
 
     // profiling
     struct PendingEv { int kc; int trial; hipEvent_t a, b; };
-    std::vector<PendingEv> pending;   // profiled launches of the current solve
-    int cur_trial = 0;                 // trial index being enqueued (0 = initial linearisation)
+    std::vector<PendingEv> pending;
+    int cur_trial = 0;
     std::vector<hipEvent_t> event_pool;
     size_t event_next = 0;
     int64_t launches[KC_N] = {0};
@@ -216,13 +258,12 @@ struct lh_handle {
 namespace {
 
 bool g_debug = getenv("LH_DEBUG") != nullptr;
-bool g_event_sync = getenv("LH_EVENT_SYNC") != nullptr;   // A/B: the per-trial event scheme
 
 #define HIPCHK(x)                                                                                        \
     do {                                                                                                 \
         hipError_t e_ = (x);                                                                             \
         if (e_ != hipSuccess) {                                                                          \
-            if (g_debug) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            if (g_debug) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, hipGetErrorString(e_));       \
             return LH_E_HIP;                                                                             \
         }                                                                                                \
     } while (0)
@@ -231,7 +272,7 @@ bool g_event_sync = getenv("LH_EVENT_SYNC") != nullptr;   // A/B: the per-trial 
     do {                                                                                                 \
         ncclResult_t r_ = (x);                                                                           \
         if (r_ != ncclSuccess) {                                                                         \
-            if (g_debug) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, ncclGetErrorString(r_)); \
+            if (g_debug) fprintf(stderr, "lego_ba: %s failed: %s\n", #x, ncclGetErrorString(r_));      \
             return LH_E_RCCL;                                                                            \
         }                                                                                                \
     } while (0)
@@ -279,210 +320,46 @@ void collect_profile(lh_handle* h, int trials_run) {
     h->event_next = 0;
 }
 
-int validate(const lh_window* w) {
-    if (!w) return LH_E_BADARG;
-    if (w->n_poses < 0 || w->n_landmarks < 0 || w->n_obs < 0) return LH_E_BADARG;
-    if (w->n_poses > 0 && !w->pose_Tcw) return LH_E_BADARG;
-    if (w->n_landmarks > 0 && !w->lm_xyz) return LH_E_BADARG;
-    if (w->n_obs > 0 && (!w->obs_pose || !w->obs_lm || !w->obs_uv)) return LH_E_BADARG;
-    if (w->n_cams < 0 || w->n_cams > LH_MAX_CAMS || (w->n_cams > 0 && !w->cam_ext)) return LH_E_BADARG;
-    const int ncam = w->n_cams > 0 ? w->n_cams : 1;
-    for (int64_t o = 0; o < w->n_obs; ++o) {
-        if (w->obs_pose[o] >= (uint32_t)w->n_poses || w->obs_lm[o] >= (uint32_t)w->n_landmarks) return LH_E_BADARG;
-        if (w->obs_cam && w->obs_cam[o] >= ncam) return LH_E_BADARG;
-    }
-    return LH_OK;
-}
-
 int upload_impl(lh_handle* h, const lh_window* w) {
-    int st = validate(w);
-    if (st != LH_OK) return st;
+    const double t0 = now_ms();
     h->uploaded = false;
-    const int P = w->n_poses, L = w->n_landmarks;
-    const int64_t O = w->n_obs;
-    if (h->opt.world_size <= 1 && (O == 0 || (P + L) == 0)) return LH_E_EMPTY;   // problem.cpp:157-161
-    if (P > LH_PMAX) return LH_E_UNSUPPORTED;
-    const int ncam = w->n_cams > 0 ? w->n_cams : 1;
-    h->P = P; h->L = L; h->O = O; h->ncam = ncam;
-    h->fixed_mask = 0;
-    if (w->pose_fixed)
-        for (int p = 0; p < P; ++p)
-            if (w->pose_fixed[p]) h->fixed_mask |= 1u << p;
+    lh::PlanCfg cfg;
+    cfg.chunk_lm = h->opt.chunk_landmarks;
+    lh::Plan& pl = h->plan;
+    int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
+    if (st != LH_OK) return st;
+    // a chunk window must fit one CU's LDS
+    for (int T = 1; T <= LH_TMAX; ++T)
+        if (pl.tgroup_begin[T + 1] > pl.tgroup_begin[T] && lh_lin_smem(T, pl.ncam) > (size_t)h->lds_limit)
+            return LH_E_UNSUPPORTED;
+    const int P = pl.P, ncam = pl.ncam;
+    h->P = P; h->L = pl.L; h->O = pl.O; h->ncam = ncam;
+    h->n_rec = pl.n_rec;
+    h->n_slots = pl.n_slots;
+    h->LY = lh_rs_make(P);
 
-    // ---- landmark-major CSR, observations in ascending pose order ----
-    std::vector<int64_t> cnt(L + 1, 0);
-    for (int64_t o = 0; o < O; ++o) cnt[w->obs_lm[o] + 1]++;
-    for (int l = 0; l < L; ++l) cnt[l + 1] += cnt[l];
-    std::vector<int64_t> csr(O);
-    {
-        std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
-        for (int64_t o = 0; o < O; ++o) csr[pos[w->obs_lm[o]]++] = o;
-    }
-    std::vector<uint32_t> lm_mask(L, 0);
-    std::vector<int> lm_first(L, 0), lm_last(L, 0);
-    for (int l = 0; l < L; ++l) {
-        auto b = csr.begin() + cnt[l], e = csr.begin() + cnt[l + 1];
-        std::sort(b, e, [&](int64_t x, int64_t y) {
-            if (w->obs_pose[x] != w->obs_pose[y]) return w->obs_pose[x] < w->obs_pose[y];
-            return x < y;
-        });
-        uint32_t m = 0;
-        for (auto it = b; it != e; ++it) {
-            const uint32_t bit = 1u << w->obs_pose[*it];
-            if (m & bit) return LH_E_UNSUPPORTED;   // two edges landmark->same pose (DESIGN.md "Limits")
-            m |= bit;
-        }
-        if (e - b > LH_SB_OBS) return LH_E_UNSUPPORTED;
-        if (__builtin_popcount(m) > LH_UMAX) return LH_E_UNSUPPORTED;
-        lm_mask[l] = m;
-        if (m) { lm_first[l] = __builtin_ctz(m); lm_last[l] = 31 - __builtin_clz(m); }
-    }
+    // ---- staging ----
+    HIPCHK(h->s_chunks.ensure(pl.n_chunks));
+    HIPCHK(h->s_sbs.ensure(pl.n_sb));
+    HIPCHK(h->s_meta.ensure(pl.n_slots));
+    HIPCHK(h->s_uv.ensure(2 * pl.n_slots));
+    HIPCHK(h->s_obs_perm.ensure(pl.n_slots));
+    HIPCHK(h->s_lm_perm.ensure(pl.n_rec));
+    HIPCHK(h->s_items.ensure(pl.n_items));
+    HIPCHK(h->s_pair_ptr.ensure(pl.npairs + 1));
+    HIPCHK(h->s_pair_pq.ensure(2 * (size_t)pl.npairs));
+    HIPCHK(h->s_rsmap.ensure((size_t)pl.npairs * 36));
+    HIPCHK(h->s_lm.ensure(3 * (size_t)pl.L));
+    lh::PlanOut po{h->s_chunks.p, h->s_sbs.p, h->s_meta.p, h->s_uv.p, h->s_obs_perm.p, h->s_lm_perm.p,
+                   h->s_items.p, h->s_pair_pq.p, h->s_rsmap.p, h->s_lm.p};
+    lh::plan_fill(w, pl, po, h->pool);
+    std::memcpy(h->s_pair_ptr.p, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
 
-    // ---- landmark order: by observation span, so chunks share small windows ----
-    std::vector<int32_t> order;
-    order.reserve(L);
-    for (int l = 0; l < L; ++l)
-        if (lm_mask[l]) order.push_back(l);   // landmarks without edges are not vertices (backend_lego.cpp:126)
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-        if (lm_first[a] != lm_first[b]) return lm_first[a] < lm_first[b];
-        if (lm_last[a] != lm_last[b]) return lm_last[a] < lm_last[b];
-        return lm_mask[a] < lm_mask[b];
-    });
-    const int Lact = (int)order.size();
-    // ~512 chunks (2 workgroups per CU), 4*8-landmark multiples so the 4 waves get equal work
-    int chunk_lm = (int)((Lact + 511) / 512);
-    chunk_lm = ((chunk_lm + 4 * LH_SB_LM - 1) / (4 * LH_SB_LM)) * (4 * LH_SB_LM);
-    chunk_lm = std::max(32, std::min(256, chunk_lm));
-    if (const char* e = getenv("LH_CHUNK_LM")) {   // A/B knob for the chunk size (scripts/gpu_ab_chunk.sh)
-        const int v = atoi(e);
-        if (v >= LH_SB_LM && v <= 512) chunk_lm = v;
-    }
-
-    struct ChunkTmp { std::vector<int32_t> lms; uint32_t mask; };
-    std::vector<ChunkTmp> ctmp;
-    // a chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new
-    // chunk rather than let the union grow past the larger of the two tile counts
-    auto chunkT = [](uint32_t mask) { return (6 * __builtin_popcount(mask) + 15) / 16; };
-    for (int32_t l : order) {
-        const uint32_t m = lm_mask[l];
-        if (ctmp.empty() || (int)ctmp.back().lms.size() >= chunk_lm ||
-            __builtin_popcount(ctmp.back().mask | m) > LH_UMAX ||
-            chunkT(ctmp.back().mask | m) > std::max(chunkT(ctmp.back().mask), chunkT(m))) {
-            ctmp.push_back(ChunkTmp{{}, 0u});
-        }
-        ctmp.back().lms.push_back(l);
-        ctmp.back().mask |= m;
-    }
-    // group chunks by MFMA tile count T (one launch per T)
-    std::vector<int> corder(ctmp.size());
-    std::iota(corder.begin(), corder.end(), 0);
-    std::stable_sort(corder.begin(), corder.end(), [&](int a, int b) { return chunkT(ctmp[a].mask) < chunkT(ctmp[b].mask); });
-
-    std::vector<lh_chunk> chunks;
-    std::vector<lh_subbatch> sbs;
-    std::vector<uint32_t> meta;
-    std::vector<double> uv, rec_init;
-    h->lm_perm.clear();
-    h->obs_perm.clear();
-    for (int T = 0; T <= LH_TMAX + 1; ++T) h->tgroup_begin[T] = 0;
-    int slot_of[32];
-    auto pow2ceil = [](int k) { int g = 1, lg = 0; while (g < k) { g <<= 1; ++lg; } return lg; };
-    for (int ci : corder) {
-        const ChunkTmp& c = ctmp[ci];
-        lh_chunk ck{};
-        const int U = __builtin_popcount(c.mask);
-        ck.U = (uint8_t)U;
-        ck.T = (uint8_t)chunkT(c.mask);
-        {
-            int s = 0;
-            for (int p = 0; p < 32; ++p) {
-                if (c.mask & (1u << p)) { ck.pose[s] = (uint16_t)p; slot_of[p] = s; ++s; }
-            }
-        }
-        ck.sb_begin = (uint32_t)sbs.size();
-        // sub-batches: landmark l owns the aligned lane group [l*G, l*G + k_l) of 64 slots
-        size_t i = 0;
-        while (i < c.lms.size()) {
-            int lg = 0, n = 0;
-            while (i + n < c.lms.size() && n < LH_SB_LM) {
-                const int32_t l = c.lms[i + n];
-                const int lgn = std::max(lg, pow2ceil((int)(cnt[l + 1] - cnt[l])));
-                if ((n + 1) << lgn > LH_SB_OBS) break;
-                lg = lgn;
-                ++n;
-            }
-            lh_subbatch sb{};
-            sb.lm_begin = (uint32_t)(sbs.size() * LH_SB_LM);   // records sb*8 .. sb*8+7
-            h->lm_perm.resize(sb.lm_begin + LH_SB_LM, -1);
-            rec_init.resize((size_t)(sb.lm_begin + LH_SB_LM) * LH_REC, 0.0);
-            sb.n_lm = (uint8_t)n;
-            sb.lg = (uint8_t)lg;
-            const size_t base = meta.size();
-            meta.resize(base + LH_SB_OBS, 0u);
-            uv.resize(2 * (base + LH_SB_OBS), 0.0);
-            h->obs_perm.resize(base + LH_SB_OBS, -1);
-            for (int q = 0; q < n; ++q) {
-                const int32_t l = c.lms[i + q];
-                h->lm_perm[sb.lm_begin + q] = l;
-                for (int a = 0; a < 3; ++a) rec_init[(size_t)(sb.lm_begin + q) * LH_REC + LH_REC_X + a] = w->lm_xyz[3 * (size_t)l + a];
-                int j = 0;
-                for (int64_t r = cnt[l]; r < cnt[l + 1]; ++r, ++j) {
-                    const int64_t o = csr[r];
-                    const uint32_t p = w->obs_pose[o];
-                    const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
-                    const size_t slot = base + ((size_t)q << lg) + (size_t)j;
-                    meta[slot] = LH_META(p, cam, slot_of[p], q);
-                    uv[2 * slot] = w->obs_uv[2 * o];
-                    uv[2 * slot + 1] = w->obs_uv[2 * o + 1];
-                    h->obs_perm[slot] = o;
-                }
-            }
-            sbs.push_back(sb);
-            i += n;
-        }
-        ck.sb_end = (uint32_t)sbs.size();
-        chunks.push_back(ck);
-    }
-    h->n_chunks = (int)chunks.size();
-    // T group boundaries
-    {
-        int c = 0;
-        for (int T = 1; T <= LH_TMAX + 1; ++T) {
-            h->tgroup_begin[T] = c;
-            while (c < h->n_chunks && chunks[c].T == T) ++c;
-        }
-        h->tgroup_begin[LH_TMAX + 1] = h->n_chunks;
-        // a chunk window must fit one CU's LDS (a T = 6 window with 4 cameras does not)
-        for (int T = 1; T <= LH_TMAX; ++T)
-            if (h->tgroup_begin[T + 1] > h->tgroup_begin[T] && lh_lin_smem(T, ncam) > 160 * 1024) return LH_E_UNSUPPORTED;
-    }
-
-    // ---- reduce plan: for every pose pair (p <= q) the chunks touching it ----
-    const int npairs = P * (P + 1) / 2;
-    std::vector<uint16_t> pair_pq(2 * (size_t)std::max(npairs, 1));
-    std::vector<std::vector<uint32_t>> plist(npairs);
-    {
-        int b = 0;
-        for (int p = 0; p < P; ++p)
-            for (int q = p; q < P; ++q, ++b) { pair_pq[2 * b] = (uint16_t)p; pair_pq[2 * b + 1] = (uint16_t)q; }
-    }
-    for (int ci = 0; ci < h->n_chunks; ++ci) {
-        const lh_chunk& ck = chunks[ci];
-        for (int s = 0; s < ck.U; ++s)
-            for (int t = s; t < ck.U; ++t) {
-                const int p = ck.pose[s], q = ck.pose[t];
-                const int b = p * P - (p * (p - 1)) / 2 + (q - p);
-                plist[b].push_back(((uint32_t)ci << 11) | ((uint32_t)ck.T << 8) | ((uint32_t)s << 4) | (uint32_t)t);
-            }
-    }
-    std::vector<uint32_t> pair_ptr(npairs + 1, 0), items;
-    for (int b = 0; b < npairs; ++b) {
-        pair_ptr[b + 1] = pair_ptr[b] + (uint32_t)plist[b].size();
-        items.insert(items.end(), plist[b].begin(), plist[b].end());
-    }
-
-    // ---- camera extrinsics (Sophus SE3 of Camera::pose_) and initial pose tables ----
-    std::vector<double> ext(LH_EXT * (size_t)ncam);
+    // ---- camera extrinsics (Sophus SE3 of Camera::pose_) and the initial pose tables ----
+    HIPCHK(h->s_ext.ensure(LH_EXT * (size_t)ncam));
+    HIPCHK(h->s_qt.ensure(24 * (size_t)std::max(P, 1)));
+    HIPCHK(h->s_ptab.ensure(2 * (size_t)std::max(P, 1) * ncam * LH_PT));
+    double* ext = h->s_ext.p;
     int ext_identity = 0;
     for (int c = 0; c < ncam; ++c) {
         static const double I12[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
@@ -491,20 +368,19 @@ int upload_impl(lh_handle* h, const lh_window* w) {
         double q[4], Rq[9];
         q_from_R(R, q);
         R_from_q(q, Rq);
-        double* e = &ext[LH_EXT * (size_t)c];
+        double* e = ext + LH_EXT * (size_t)c;
         for (int i = 0; i < 4; ++i) e[i] = q[i];
         e[4] = E[3]; e[5] = E[7]; e[6] = E[11];
         for (int i = 0; i < 9; ++i) e[7 + i] = Rq[i];
         if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0 && e[4] == 0.0 && e[5] == 0.0 && e[6] == 0.0)
             ext_identity |= 1 << c;
     }
-    std::vector<double> pose(24 * (size_t)P), ptab(2 * (size_t)P * ncam * LH_PT);
     for (int p = 0; p < P; ++p) {
         const double* T = w->pose_Tcw + 12 * p;
         for (int s = 0; s < 2; ++s) {
-            std::memcpy(&pose[12 * ((size_t)s * P + p)], T, 12 * sizeof(double));
+            std::memcpy(h->s_qt.p + 12 * ((size_t)s * P + p), T, 12 * sizeof(double));
             for (int c = 0; c < ncam; ++c)
-                pose_table(T, &ext[LH_EXT * (size_t)c], &ptab[((size_t)s * P * ncam + (size_t)p * ncam + c) * LH_PT]);
+                pose_table(T, ext + LH_EXT * (size_t)c, h->s_ptab.p + ((size_t)s * P * ncam + (size_t)p * ncam + c) * LH_PT);
         }
     }
 
@@ -517,6 +393,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     prm.max_trials = h->opt.max_trials;
     prm.strategy = h->opt.strategy;
     prm.guard = h->opt.degenerate_guard;
+    prm.gate_mode = h->opt.gate_mode;
     prm.lambda_given = h->opt.lambda_init >= 0.0;
     prm.ext_identity = ext_identity;
     prm.huber_delta = h->opt.huber_delta;
@@ -528,61 +405,59 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     prm.pcg_tol = h->opt.pcg_tol;
     prm.pcg_max_it = h->opt.pcg_max_iters;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
-    h->LY = lh_rs_make(P);
-    h->L_act = (int)h->lm_perm.size();   // landmark records (padded to 8 per sub-batch)
-    // reduced-system element map for k_ctrl's register scatter: S element i of pose pair
-    // (pi, pj), pi <= pj, row a, col b  ->  global rows gi = 6 pi + a, gj = 6 pj + b
-    std::vector<uint32_t> rsmap((size_t)h->LY.npairs * 36);
-    for (int pi = 0, blk = 0; pi < P; ++pi)
-        for (int pj = pi; pj < P; ++pj, ++blk)
-            for (int a = 0; a < 6; ++a)
-                for (int b = 0; b < 6; ++b)
-                    rsmap[(size_t)blk * 36 + 6 * a + b] = (uint32_t)(6 * pi + a) | ((uint32_t)(6 * pj + b) << 8) |
-                                                        ((pi == pj ? 1u : 0u) << 16);
-    h->lm_in.assign(w->lm_xyz, w->lm_xyz + 3 * (size_t)L);
+    const double t1 = now_ms();
 
-    // ---- device buffers ----
+    // ---- device buffers and the copies ----
     const size_t PT = (size_t)P * ncam * LH_PT;
-    HIPCHK(h->d_chunks.ensure(chunks.size()));
-    HIPCHK(h->d_sbs.ensure(sbs.size()));
-    HIPCHK(h->d_meta.ensure(meta.size()));
-    HIPCHK(h->d_uv.ensure(uv.size()));
-    HIPCHK(h->d_pair_ptr.ensure(pair_ptr.size()));
-    HIPCHK(h->d_items.ensure(items.size()));
-    HIPCHK(h->d_pair_pq.ensure(pair_pq.size()));
-    HIPCHK(h->d_rec_init.ensure(rec_init.size()));
-    HIPCHK(h->d_rec.ensure(2 * rec_init.size()));
+    HIPCHK(h->d_chunks.ensure(pl.n_chunks));
+    HIPCHK(h->d_sbs.ensure(pl.n_sb));
+    HIPCHK(h->d_meta.ensure(pl.n_slots));
+    HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
+    HIPCHK(h->d_obs_perm.ensure(pl.n_slots));
+    HIPCHK(h->d_lm_perm.ensure(pl.n_rec));
+    HIPCHK(h->d_lm_in.ensure(3 * (size_t)pl.L));
+    HIPCHK(h->d_pair_ptr.ensure(pl.npairs + 1));
+    HIPCHK(h->d_items.ensure(pl.n_items));
+    HIPCHK(h->d_pair_pq.ensure(2 * (size_t)pl.npairs));
+    HIPCHK(h->d_rec.ensure(2 * (size_t)pl.n_rec * LH_REC));
     HIPCHK(h->d_ptab.ensure(2 * PT));
     HIPCHK(h->d_ptab_init.ensure(2 * PT));
-    HIPCHK(h->d_qt.ensure(pose.size()));
-    HIPCHK(h->d_qt_init.ensure(pose.size()));
-    HIPCHK(h->d_ext.ensure(ext.size()));
-    HIPCHK(h->d_rho.ensure(meta.size()));
-    HIPCHK(h->d_slabs.ensure((size_t)h->n_chunks * LH_SLAB_STRIDE));
+    HIPCHK(h->d_qt.ensure(24 * (size_t)P));
+    HIPCHK(h->d_qt_init.ensure(24 * (size_t)P));
+    HIPCHK(h->d_ext.ensure(LH_EXT * (size_t)ncam));
+    HIPCHK(h->d_rho.ensure(pl.n_slots));
+    HIPCHK(h->d_slabs.ensure((size_t)pl.n_chunks * LH_SLAB_STRIDE));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
-    HIPCHK(h->d_rsmap.ensure(rsmap.size()));
+    HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
     HIPCHK(h->d_maxd.ensure(1));
     HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
     HIPCHK(h->d_ctrl.ensure(1));
+    HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
+    HIPCHK(h->d_out_rho.ensure(pl.O));
+    if (h->host_comm) HIPCHK(h->s_rs.ensure(h->LY.total + 1));
     hipStream_t s = h->stream;
     auto up = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
         if (!bytes) return hipSuccess;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
     };
-    HIPCHK(up(h->d_chunks.p, chunks.data(), chunks.size() * sizeof(lh_chunk)));
-    HIPCHK(up(h->d_sbs.p, sbs.data(), sbs.size() * sizeof(lh_subbatch)));
-    HIPCHK(up(h->d_meta.p, meta.data(), meta.size() * sizeof(uint32_t)));
-    HIPCHK(up(h->d_uv.p, uv.data(), uv.size() * sizeof(double)));
-    HIPCHK(up(h->d_pair_ptr.p, pair_ptr.data(), pair_ptr.size() * sizeof(uint32_t)));
-    HIPCHK(up(h->d_items.p, items.data(), items.size() * sizeof(uint32_t)));
-    HIPCHK(up(h->d_pair_pq.p, pair_pq.data(), pair_pq.size() * sizeof(uint16_t)));
-    HIPCHK(up(h->d_rec_init.p, rec_init.data(), rec_init.size() * sizeof(double)));
-    HIPCHK(up(h->d_ptab_init.p, ptab.data(), ptab.size() * sizeof(double)));
-    HIPCHK(up(h->d_qt_init.p, pose.data(), pose.size() * sizeof(double)));
-    HIPCHK(up(h->d_ext.p, ext.data(), ext.size() * sizeof(double)));
-    HIPCHK(up(h->d_rsmap.p, rsmap.data(), rsmap.size() * sizeof(uint32_t)));
-    HIPCHK(hipStreamSynchronize(s));   // host vectors die at return
+    HIPCHK(up(h->d_meta.p, h->s_meta.p, pl.n_slots * sizeof(uint32_t)));
+    HIPCHK(up(h->d_uv.p, h->s_uv.p, 2 * pl.n_slots * sizeof(double)));
+    HIPCHK(up(h->d_obs_perm.p, h->s_obs_perm.p, pl.n_slots * sizeof(int32_t)));
+    HIPCHK(up(h->d_lm_perm.p, h->s_lm_perm.p, (size_t)pl.n_rec * sizeof(int32_t)));
+    HIPCHK(up(h->d_lm_in.p, h->s_lm.p, 3 * (size_t)pl.L * sizeof(double)));
+    HIPCHK(up(h->d_chunks.p, h->s_chunks.p, (size_t)pl.n_chunks * sizeof(lh_chunk)));
+    HIPCHK(up(h->d_sbs.p, h->s_sbs.p, (size_t)pl.n_sb * sizeof(lh_subbatch)));
+    HIPCHK(up(h->d_pair_ptr.p, h->s_pair_ptr.p, ((size_t)pl.npairs + 1) * sizeof(uint32_t)));
+    HIPCHK(up(h->d_items.p, h->s_items.p, (size_t)pl.n_items * sizeof(uint32_t)));
+    HIPCHK(up(h->d_pair_pq.p, h->s_pair_pq.p, 2 * (size_t)pl.npairs * sizeof(uint16_t)));
+    HIPCHK(up(h->d_rsmap.p, h->s_rsmap.p, (size_t)pl.npairs * 36 * sizeof(uint32_t)));
+    HIPCHK(up(h->d_ptab_init.p, h->s_ptab.p, 2 * PT * sizeof(double)));
+    HIPCHK(up(h->d_qt_init.p, h->s_qt.p, 24 * (size_t)P * sizeof(double)));
+    HIPCHK(up(h->d_ext.p, h->s_ext.p, LH_EXT * (size_t)ncam * sizeof(double)));
+    HIPCHK(hipStreamSynchronize(s));   // the staging is reused by the next upload
+    h->last_prep_ms = t1 - t0;
+    h->last_upload_ms = now_ms() - t0;
     h->uploaded = true;
     return LH_OK;
 }
@@ -599,36 +474,95 @@ int upload_impl(lh_handle* h, const lh_window* w) {
         }                                                                                               \
     } while (0)
 
-int enqueue_trial(lh_handle* h, int mode) {
+int launch_lin(lh_handle* h, int trial) {
+    hipStream_t s = h->stream;
+    for (int T = 1; T <= LH_TMAX; ++T) {
+        const int c0 = h->plan.tgroup_begin[T], c1 = h->plan.tgroup_begin[T + 1];
+        HIPCHK(lh_launch_lin(T, trial, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p, h->d_meta.p, h->d_rec.p,
+                             h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p, h->d_rho.p, h->d_slabs.p, h->prm,
+                             h->n_rec, h->plan.fixed_mask));
+        DBGSYNC("k_lin");
+    }
+    return LH_OK;
+}
+
+// host-transport exchange: the reduced system (and at the initial linearisation max|diag H_ll|)
+// through the caller's all-reduce, synchronously
+int host_exchange(lh_handle* h, int mode) {
+    hipStream_t s = h->stream;
+    const size_t n = (size_t)h->LY.total;
+    HIPCHK(hipMemcpyAsync(h->s_rs.p, h->d_rs_stage.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (mode == 0) HIPCHK(hipMemcpyAsync(h->s_rs.p + n, h->d_maxd.p, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (mode == 0 && h->opt.allreduce(h->opt.allreduce_user, h->s_rs.p + n, 1, 1) != 0) return LH_E_RCCL;
+    if (h->opt.allreduce(h->opt.allreduce_user, h->s_rs.p, (int64_t)n, 0) != 0) return LH_E_RCCL;
+    ++h->n_coll;
+    HIPCHK(hipMemcpyAsync(h->d_rs_stage.p, h->s_rs.p, n * sizeof(double), hipMemcpyHostToDevice, s));
+    if (mode == 0) HIPCHK(hipMemcpyAsync(h->d_maxd.p, h->s_rs.p + n, sizeof(double), hipMemcpyHostToDevice, s));
+    return LH_OK;
+}
+
+// One LM trial (mode 1) or the initial linearisation (mode 0).  *stopped is set (host transport
+// only) when the device had already stopped: no exchange and no k_ctrl were issued.
+int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     hipStream_t s = h->stream;
     h->cur_trial = (mode == 0) ? 0 : h->cur_trial + 1;
     {
         Prof pr(h, mode == 0 ? KC_INIT : KC_LIN);
-        for (int T = 1; T <= LH_TMAX; ++T) {
-            const int c0 = h->tgroup_begin[T], c1 = h->tgroup_begin[T + 1];
-            HIPCHK(lh_launch_lin(T, mode, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p,
-                                 h->d_meta.p, h->d_rec.p, h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p,
-                                 h->d_rho.p, h->d_slabs.p, h->prm, h->L_act, h->fixed_mask));
-            DBGSYNC("k_lin");
-        }
+        int st = launch_lin(h, mode);
+        if (st != LH_OK) return st;
     }
     {
         Prof pr(h, KC_REDUCE);
-        HIPCHK(lh_launch_reduce(s, h->d_chunks.p, h->d_slabs.p, h->d_pair_ptr.p, h->d_items.p, h->d_pair_pq.p,
-                                h->d_ctrl.p, h->d_rs_stage.p, h->d_maxd.p, h->prm, h->n_chunks));
+        HIPCHK(lh_launch_reduce(s, h->d_slabs.p, h->d_pair_ptr.p, h->d_items.p, h->d_pair_pq.p, h->d_ctrl.p,
+                                h->d_rs_stage.p, h->d_maxd.p, h->prm, h->plan.n_chunks));
         DBGSYNC("k_reduce");
     }
     if (h->comm) {
         Prof pr(h, KC_ALLREDUCE);
         if (mode == 0) NCCLCHK(ncclAllReduce(h->d_maxd.p, h->d_maxd.p, 1, ncclFloat64, ncclMax, h->comm, s));
         NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
+        ++h->n_coll;
+    } else if (h->host_comm) {
+        HIPCHK(hipStreamSynchronize(s));
+        if (mode != 0 && h->h_done[0]) {   // device-determined, identical on every rank
+            *stopped = true;
+            return LH_OK;
+        }
+        int st = host_exchange(h, mode);
+        if (st != LH_OK) return st;
     }
     {
         Prof pr(h, KC_CTRL);
-        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p, h->d_ptab.p,
-                              h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial));
+        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p,
+                              h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial));
         DBGSYNC("k_ctrl");
     }
+    return LH_OK;
+}
+
+int download(lh_handle* h, lh_result* out, int cur) {
+    hipStream_t s = h->stream;
+    const int P = h->P;
+    const double t0 = now_ms();
+    if (out->pose_Tcw && P)   // estimate_ of every VertexPose (backend_lego.cpp:198-213)
+        HIPCHK(hipMemcpyAsync(out->pose_Tcw, h->d_qt.p + 12 * (size_t)cur * P, 12 * (size_t)P * sizeof(double),
+                              hipMemcpyDeviceToHost, s));
+    if (out->lm_xyz || out->edge_robust_chi2) {
+        // landmarks without an edge are not vertices (backend_lego.cpp:126): they keep their input
+        if (out->lm_xyz && h->L)
+            HIPCHK(hipMemcpyAsync(h->d_out_xyz.p, h->d_lm_in.p, 3 * (size_t)h->L * sizeof(double), hipMemcpyDeviceToDevice, s));
+        HIPCHK(lh_launch_gather(s, h->d_ctrl.p, h->d_rec.p, h->d_lm_perm.p, out->lm_xyz ? h->n_rec : 0, h->d_rho.p,
+                                h->d_obs_perm.p, out->edge_robust_chi2 ? (long)h->n_slots : 0L, h->d_out_xyz.p,
+                                h->d_out_rho.p));
+        if (out->lm_xyz && h->L)
+            HIPCHK(hipMemcpyAsync(out->lm_xyz, h->d_out_xyz.p, 3 * (size_t)h->L * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (out->edge_robust_chi2 && h->O)
+            HIPCHK(hipMemcpyAsync(out->edge_robust_chi2, h->d_out_rho.p, (size_t)h->O * sizeof(double),
+                                  hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    out->time_download_ms = now_ms() - t0;
     return LH_OK;
 }
 
@@ -637,53 +571,37 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     hipStream_t s = h->stream;
     const int P = h->P;
     const size_t PT = (size_t)P * h->ncam * LH_PT;
-    // restart from the uploaded initial state (k_reset), then the LM trials.  Trials are
-    // enqueued two ahead of the one the host waits for, so the device never idles on the
-    // host; k_ctrl raises the mapped done flag and any trial enqueued after it is a no-op.
     hipEvent_t e0 = next_event(h), e1 = next_event(h);
     if (!e0 || !e1) return LH_E_HIP;
-    volatile int* hd = h->h_done;   // [0] done, [1] last trial whose k_ctrl has started
+    volatile int* hd = h->h_done;   // [0] done, [1] last trial whose k_ctrl started live
     hd[0] = 0;
     hd[1] = -1;
+    h->n_coll = 0;
     HIPCHK(hipEventRecord(e0, s));
-    HIPCHK(lh_launch_reset(s, h->d_rec.p, h->d_rec_init.p, LH_REC * (long)h->L_act, h->d_qt.p, h->d_qt_init.p, 24 * P,
+    HIPCHK(lh_launch_reset(s, h->d_rec.p, h->d_lm_perm.p, h->d_lm_in.p, h->n_rec, h->d_qt.p, h->d_qt_init.p, 24 * P,
                            h->d_ptab.p, h->d_ptab_init.p, (int)(2 * PT), h->d_dxp.p, 6 * std::max(P, 1), h->d_ctrl.p));
     DBGSYNC("k_reset");
-    int st = enqueue_trial(h, 0);
+    bool stopped = false;
+    int st = enqueue_trial(h, 0, &stopped);
     if (st != LH_OK) return st;
     const int max_total = (h->opt.max_iters > 0) ? h->opt.max_iters * std::max(1, h->opt.max_trials) : 0;
-    const int depth = h->opt.trials_per_sync > 0 ? std::min(h->opt.trials_per_sync, 32) : 2;
+    const int depth = h->host_comm ? 1 : (h->opt.trials_per_sync > 0 ? std::min(h->opt.trials_per_sync, 32) : 2);
     int enq = 0;
-    if (g_event_sync) {
-        // previous scheme (A/B reference): one event per trial, host waits on the oldest
-        hipEvent_t ring[64];
-        int head = 0, tail = 0;
-        auto push = [&]() -> int {
-            int r = enqueue_trial(h, 1);
-            if (r != LH_OK) return r;
-            hipEvent_t ev = next_event(h);
-            if (!ev) return LH_E_HIP;
-            if (hipEventRecord(ev, s) != hipSuccess) return LH_E_HIP;
-            ring[tail++ & 63] = ev;
-            ++enq;
-            return LH_OK;
-        };
-        while (enq < max_total && tail - head < depth)
-            if ((st = push()) != LH_OK) return st;
-        while (head < tail) {
-            HIPCHK(hipEventSynchronize(ring[head++ & 63]));
-            if (hd[0]) break;
-            if (enq < max_total)
-                if ((st = push()) != LH_OK) return st;
+    if (h->host_comm) {
+        // synchronous: each trial's exchange waits for the previous k_ctrl, whose stop flag every
+        // rank reads at the same point
+        while (enq < max_total && !stopped) {
+            if ((st = enqueue_trial(h, 1, &stopped)) != LH_OK) return st;
+            if (!stopped) ++enq;
         }
     } else {
-        // No per-trial events: k_ctrl writes the trial it starts into the mapped progress word,
-        // and the host keeps `depth` trials enqueued past it until the device raises done.
+        // k_ctrl writes the trial it starts (when the loop is still live) into the mapped progress
+        // word; the host keeps `depth` trials enqueued past it until the device raises done.
         // hipStreamQuery every few thousand polls turns a device fault into an error return.
         unsigned spin = 0;
         while (!hd[0] && enq < max_total) {
             if (enq - hd[1] < depth) {
-                if ((st = enqueue_trial(h, 1)) != LH_OK) return st;
+                if ((st = enqueue_trial(h, 1, &stopped)) != LH_OK) return st;
                 ++enq;
                 continue;
             }
@@ -697,9 +615,22 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipMemcpyAsync(h->h_ctrl, h->d_ctrl.p, sizeof(lh_ctrl), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    const lh_ctrl& c = *h->h_ctrl;
+    if (h->comm) {
+        // Equal collective counts on every rank.  The progress word only advances on live trials,
+        // so no rank enqueued more than (stop trial) + depth trials; the stop trial is decided by
+        // identical all-reduced data, so every rank tops up to the same target.  The extra
+        // all-reduces carry no data anyone reads (the device has stopped).
+        const int target = std::min(c.trials + depth, max_total);
+        if (enq > target) return LH_E_STATE;   // cannot happen: the bound above
+        for (; enq < target; ++enq) {
+            NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
+            ++h->n_coll;
+        }
+        HIPCHK(hipStreamSynchronize(s));
+    }
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    const lh_ctrl& c = *h->h_ctrl;
     const int cur = c.cur;
 
     if (out) {
@@ -711,31 +642,17 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         out->lambda_final = c.lambda;
         out->time_ms = ms;
         out->pcg_iterations = c.pcg_iters;
+        out->degenerate = c.nonpd;
         out->trace_len = std::min(c.trace_len, std::min(out->trace_cap, LH_TRACE));
         for (int i = 0; i < out->trace_len; ++i) {
             if (out->trace_chi2) out->trace_chi2[i] = c.trace_chi[i];
             if (out->trace_lambda) out->trace_lambda[i] = c.trace_lambda[i];
         }
-        if (out->pose_Tcw && P)   // estimate_ of every VertexPose (backend_lego.cpp:198-213)
-            HIPCHK(hipMemcpy(out->pose_Tcw, h->d_qt.p + 12 * (size_t)cur * P, 12 * (size_t)P * sizeof(double),
-                             hipMemcpyDeviceToHost));
-        if (out->lm_xyz) {
-            std::memcpy(out->lm_xyz, h->lm_in.data(), h->lm_in.size() * sizeof(double));
-            std::vector<double> R(LH_REC * (size_t)h->L_act);
-            if (h->L_act)
-                HIPCHK(hipMemcpy(R.data(), h->d_rec.p + LH_REC * (size_t)cur * h->L_act, R.size() * sizeof(double),
-                                 hipMemcpyDeviceToHost));
-            for (int i = 0; i < h->L_act; ++i)
-                if (h->lm_perm[i] >= 0)
-                    for (int a = 0; a < 3; ++a)
-                        out->lm_xyz[3 * (size_t)h->lm_perm[i] + a] = R[LH_REC * (size_t)i + LH_REC_X + a];
-        }
-        if (out->edge_robust_chi2) {
-            std::vector<double> r(h->obs_perm.size());
-            if (!r.empty()) HIPCHK(hipMemcpy(r.data(), h->d_rho.p, r.size() * sizeof(double), hipMemcpyDeviceToHost));
-            for (size_t i = 0; i < r.size(); ++i)
-                if (h->obs_perm[i] >= 0) out->edge_robust_chi2[h->obs_perm[i]] = r[i];
-        }
+        out->time_prep_ms = h->last_prep_ms;
+        out->time_upload_ms = h->last_upload_ms;
+        out->time_download_ms = 0.0;
+        st = download(h, out, cur);
+        if (st != LH_OK) return st;
     }
     if (h->opt.verbose) {
         printf("==========LEGO OPTIMIZER (MI355X)==========\n");
@@ -761,7 +678,7 @@ const char* lh_strerror(int status) {
         case LH_E_EMPTY: return "empty problem: no vertices or no edges";
         case LH_E_BADARG: return "bad argument";
         case LH_E_HIP: return "HIP runtime error";
-        case LH_E_RCCL: return "RCCL error";
+        case LH_E_RCCL: return "RCCL / exchange error";
         case LH_E_UNSUPPORTED: return "window outside the supported envelope";
         case LH_E_STATE: return "call out of order";
         default: return "unknown status";
@@ -792,6 +709,12 @@ void lh_default_options(lh_options* o) {
     o->profile = 0;
     o->pcg_max_iters = 0;
     o->pcg_tol = 1e-6;
+    o->gate_mode = 0;
+    o->chunk_landmarks = 0;
+    o->comm_mode = LH_COMM_RCCL;
+    o->host_threads = 0;
+    o->allreduce = nullptr;
+    o->allreduce_user = nullptr;
 }
 
 int lh_comm_unique_id(uint8_t out[128]) {
@@ -812,6 +735,11 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
         return LH_E_BADARG;
     if (opt->linear_solver != LH_SOLVER_LDLT && opt->linear_solver != LH_SOLVER_PCG) return LH_E_BADARG;
     if (opt->linear_solver == LH_SOLVER_PCG && !(opt->pcg_tol >= 0.0)) return LH_E_BADARG;
+    if (opt->gate_mode != 0 && opt->gate_mode != 1) return LH_E_BADARG;
+    if (opt->degenerate_guard != 0 && opt->degenerate_guard != 1) return LH_E_BADARG;
+    if (opt->chunk_landmarks < 0 || opt->host_threads < 0) return LH_E_BADARG;
+    if (opt->comm_mode != LH_COMM_RCCL && opt->comm_mode != LH_COMM_HOST) return LH_E_BADARG;
+    if (opt->world_size > 1 && opt->comm_mode == LH_COMM_HOST && !opt->allreduce) return LH_E_BADARG;
     lh_handle* h = new (std::nothrow) lh_handle();
     if (!h) return LH_E_HIP;
     h->opt = *opt;
@@ -821,7 +749,10 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return LH_E_HIP; }
     h->device = dev;
-    if (lh_prepare_lin() != hipSuccess) { delete h; return LH_E_HIP; }
+    int lds = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && lds > 0)
+        h->lds_limit = lds;
+    if (lh_prepare_lin(h->lds_limit) != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return LH_E_HIP; }
     if (hipHostMalloc((void**)&h->h_ctrl, sizeof(lh_ctrl), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_done, 2 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -829,11 +760,14 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
         lh_destroy(h);
         return LH_E_HIP;
     }
+    h->pool = new (std::nothrow) lh::Pool(opt->host_threads > 0 ? std::min(opt->host_threads, 64) : auto_host_threads());
+    if (!h->pool) { lh_destroy(h); return LH_E_HIP; }
+    h->host_comm = opt->world_size > 1 && opt->comm_mode == LH_COMM_HOST;
     // LH_FORCE_RCCL=1 builds a one-rank communicator on a single GPU, so the data-path
     // collectives (and their stream ordering) run in single-GPU tests too
     const char* force = std::getenv("LH_FORCE_RCCL");
     const bool force_comm = opt->world_size == 1 && force && force[0] == '1';
-    if (opt->world_size > 1 || force_comm) {
+    if ((opt->world_size > 1 && !h->host_comm) || force_comm) {
         ncclUniqueId id;
         if (force_comm) {
             if (ncclGetUniqueId(&id) != ncclSuccess) { lh_destroy(h); return LH_E_RCCL; }
@@ -856,15 +790,19 @@ void lh_destroy(lh_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm) ncclCommDestroy(h->comm);
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
+    delete h->pool;
     h->f_ptr.release(); h->f_pose_in.release(); h->f_pts.release(); h->f_uv.release(); h->f_res.release();
     h->f_pose_out.release(); h->f_rchi2.release(); h->f_flag_in.release(); h->f_flag_out.release();
     h->f_iters.release(); h->f_inl.release();
-    h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release();
-    h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release();
-    h->d_uv.release(); h->d_rec.release(); h->d_rec_init.release(); h->d_ptab.release();
+    h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release(); h->d_obs_perm.release(); h->d_lm_perm.release();
+    h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
+    h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
-    h->d_slabs.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release(); h->d_dxp.release();
-    h->d_ctrl.release();
+    h->d_slabs.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
+    h->d_dxp.release(); h->d_ctrl.release();
+    h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
+    h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
+    h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -956,6 +894,7 @@ int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
     prm.max_trials = h->opt.max_trials;
     prm.strategy = h->opt.strategy;
     prm.lambda_given = h->opt.lambda_init >= 0.0;
+    prm.gate_mode = h->opt.gate_mode;
     prm.huber_delta = h->opt.huber_delta;
     prm.stop_dchi2 = h->opt.stop_dchi2;
     prm.tau = h->opt.tau;
@@ -1063,6 +1002,42 @@ int lh_debug_event_floor(lh_handle* h, double* ms) {
     (void)hipEventDestroy(b);
     if (st == LH_OK) *ms = tot / 64.0;
     return st;
+}
+
+// k_lin's duration per trial: after a solve, clear the stop flag, replay the trial-mode k_lin
+// launch(es) `reps` times back to back between two events, raise the flag again.  Each replay reads
+// the committed buffers and rewrites the candidate ones: the same work as every trial of the solve.
+int lh_debug_time_lin(lh_handle* h, int reps, double* ms) {
+    if (!h || !ms || reps < 1) return LH_E_BADARG;
+    if (!h->uploaded) return LH_E_STATE;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    hipStream_t s = h->stream;
+    int* done = reinterpret_cast<int*>(reinterpret_cast<char*>(h->d_ctrl.p) + offsetof(lh_ctrl, done));
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return LH_E_HIP;
+    if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return LH_E_HIP; }
+    int st = LH_OK;
+    const int zero = 0, one = 1;
+    if (hipMemcpyAsync(done, &zero, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) st = LH_E_HIP;
+    if (st == LH_OK && launch_lin(h, 1) != LH_OK) st = LH_E_HIP;   // warm-up
+    if (st == LH_OK && hipEventRecord(a, s) != hipSuccess) st = LH_E_HIP;
+    for (int r = 0; r < reps && st == LH_OK; ++r)
+        if (launch_lin(h, 1) != LH_OK) st = LH_E_HIP;
+    if (st == LH_OK && hipEventRecord(b, s) != hipSuccess) st = LH_E_HIP;
+    if (hipMemcpyAsync(done, &one, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) st = LH_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) st = LH_E_HIP;
+    float e = 0.f;
+    if (st == LH_OK && hipEventElapsedTime(&e, a, b) != hipSuccess) st = LH_E_HIP;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (st == LH_OK) *ms = (double)e / reps;
+    return st;
+}
+
+int lh_debug_comm_count(lh_handle* h, int64_t* n) {
+    if (!h || !n) return LH_E_BADARG;
+    *n = h->n_coll;
+    return LH_OK;
 }
 
 int lh_debug_mfma_probe(const double* A, const double* B, double* D) {

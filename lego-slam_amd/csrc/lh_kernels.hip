@@ -267,7 +267,8 @@ __device__ __forceinline__ void edge_robust(EdgeEval& E, const lh_params& prm) {
             E.rho2 = -0.5 * E.rho1 / E.e2;
         }
         E.W00 = E.rho1; E.W01 = 0.0; E.W10 = 0.0; E.W11 = E.rho1;
-        if (E.rho1 + 2 * E.rho2 * E.e2 > 0.0) {
+        // gate_mode 1 (diagnostic): the analytically-zero residue of an outlier edge counts as 0
+        if (E.rho1 + 2 * E.rho2 * E.e2 > 0.0 && !(prm.gate_mode == 1 && E.e2 > d2)) {
             const double s2 = 2 * E.rho2;
             E.W00 += s2 * E.r0 * E.r0;
             E.W01 += s2 * E.r0 * E.r1;
@@ -630,11 +631,18 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         const double a22 = h[5] - l20 * l20 - l21 * l21;
         const double i22 = fast_rsq(a22);
         const bool pd = (h[0] > 0.0) && (a11 > 0.0) && (a22 > 0.0) && isfinite(i22) && isfinite(l21);
-        if (!pd) i00 = __builtin_nan("");   // poisons the step, like a singular LU inverse (problem.cpp:399)
+        // A landmark with one edge has a rank-2 H_ll: the reference's LU inverse (problem.cpp:399)
+        // returns inf or rounding garbage for it.  Such a landmark (or a non-PD H_ll) poisons the
+        // step like the inf does (guard 0: every trial is rejected, as the reference's solve is), or
+        // is held fixed (guard 1).  The NaN reciprocal is the record's marker in both modes.
+        const uint64_t vmask = __ballot(has);
+        const uint64_t gmask = (lg >= 6) ? ~0ull : (((1ull << (1 << lg)) - 1ull) << (lane & ~((1 << lg) - 1)));
+        const bool deg = !pd || __popcll(vmask & gmask) < 2;
+        if (deg) i00 = __builtin_nan("");
         const double w0 = h[6] * i00, w1 = (h[7] - l10 * w0) * i11, w2 = (h[8] - l20 * w0 - l21 * w1) * i22;
         if (lead) {
             maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
-            if (!pd) ndeg += 1.0;
+            if (deg) ndeg += 1.0;
             double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
             reinterpret_cast<double2*>(rw)[0] = double2{X[0], X[1]};
             reinterpret_cast<double2*>(rw)[1] = double2{X[2], i00};
@@ -651,7 +659,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         double G[18];
 #pragma unroll
         for (int i = 0; i < 18; ++i) G[i] = 0.0;
-        const bool gl = live && !(prm.guard && !pd);
+        const bool gl = live && !(prm.guard && deg);
         if (gl) {
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
@@ -1321,12 +1329,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const lh_rs_layout LY = lh_rs_make(P);
     STAMP_DECL
 
-    // host progress word: this trial's controller has started (its k_lin and k_reduce are done);
-    // the host keeps the queue filled from it instead of recording an event per trial
-    if (tid == 0 && host_done) host_done[1] = seq;
-
     // ---------------- 1. prefetch (one round trip); the controller's words first ----------------
-    double chi = 0.0, lam = 0.0, ni = 0.0, last = 0.0, spose = 0.0, chi0 = 0.0, tchi = 0.0, sl = 0.0;
+    double chi = 0.0, lam = 0.0, ni = 0.0, last = 0.0, spose = 0.0, chi0 = 0.0, tchi = 0.0, sl = 0.0, ndg = 0.0;
     int iter = 0, fc = 0, trials = 0, nacc = 0, done0 = 1, cur0 = 0, tl = 0;
     if (tid == 0) {
         chi = ctrl->chi; lam = ctrl->lambda; ni = ctrl->ni; last = ctrl->last_chi; spose = ctrl->spose;
@@ -1335,6 +1339,11 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         done0 = ctrl->done; cur0 = ctrl->cur; tl = ctrl->trace_len;
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+        ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
+        // host progress word: this live trial's controller has started (its k_lin and k_reduce are
+        // done).  The host keeps the queue filled from it; it never advances past the stop trial,
+        // which bounds how many trials (and all-reduces) any rank can have enqueued.
+        if (host_done && !done0) host_done[1] = seq;
     }
     double vs[NLD], vc[NLD];
     uint32_t mp[NLD];
@@ -1387,6 +1396,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                 }
                 last = 1e20;
                 iter = 0; fc = 0; trials = 0; nacc = 0; tl = 0;
+                ctrl->nonpd = (int)ndg;
                 cur = 1 - cur;           // the initial linearisation becomes the committed one
                 accept = 1;
                 if (prm.max_iters <= 0) done = 1;
@@ -1668,7 +1678,7 @@ __device__ __forceinline__ double po_rho0(double r0, double r1, double delta) {
 __device__ __forceinline__ void po_accumulate(double r0, double r1, const double J[12], double delta, double acc[FV]) {
     EdgeEval E;
     E.r0 = r0; E.r1 = r1;
-    lh_params pr;
+    lh_params pr{};
     pr.huber_delta = delta;
     edge_robust(E, pr);
     double JtW[12];
@@ -1997,22 +2007,21 @@ size_t lh_lin_smem(int T, int ncam) {
     }
 }
 
-// Raise the dynamic-LDS limit of every k_lin instantiation on the current device (lh_create), before any
-// launch or stream capture.
-hipError_t lh_prepare_lin() {
-    {
-        const void* fns[] = {reinterpret_cast<const void*>(&k_lin<1, false>), reinterpret_cast<const void*>(&k_lin<1, true>),
-                             reinterpret_cast<const void*>(&k_lin<2, false>), reinterpret_cast<const void*>(&k_lin<2, true>),
-                             reinterpret_cast<const void*>(&k_lin<3, false>), reinterpret_cast<const void*>(&k_lin<3, true>),
-                             reinterpret_cast<const void*>(&k_lin<4, false>), reinterpret_cast<const void*>(&k_lin<4, true>),
-                             reinterpret_cast<const void*>(&k_lin<5, false>), reinterpret_cast<const void*>(&k_lin<5, true>),
-                             reinterpret_cast<const void*>(&k_lin<6, false>), reinterpret_cast<const void*>(&k_lin<6, true>)};
-        for (const void* f : fns) {
-            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-        }
-        return hipSuccess;
+// Raise the dynamic-LDS limit of every k_lin instantiation on the current device (lh_create) to the
+// device's per-workgroup LDS (hipDeviceAttributeMaxSharedMemoryPerBlock, read once by the host, which
+// also rejects windows whose chunks would exceed it), before any launch.
+hipError_t lh_prepare_lin(int lds_limit) {
+    const void* fns[] = {reinterpret_cast<const void*>(&k_lin<1, false>), reinterpret_cast<const void*>(&k_lin<1, true>),
+                         reinterpret_cast<const void*>(&k_lin<2, false>), reinterpret_cast<const void*>(&k_lin<2, true>),
+                         reinterpret_cast<const void*>(&k_lin<3, false>), reinterpret_cast<const void*>(&k_lin<3, true>),
+                         reinterpret_cast<const void*>(&k_lin<4, false>), reinterpret_cast<const void*>(&k_lin<4, true>),
+                         reinterpret_cast<const void*>(&k_lin<5, false>), reinterpret_cast<const void*>(&k_lin<5, true>),
+                         reinterpret_cast<const void*>(&k_lin<6, false>), reinterpret_cast<const void*>(&k_lin<6, true>)};
+    for (const void* f : fns) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_limit);
+        if (e != hipSuccess) return e;
     }
+    return hipSuccess;
 }
 
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
@@ -2046,10 +2055,9 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     return hipGetLastError();
 }
 
-hipError_t lh_launch_reduce(hipStream_t st, const lh_chunk* chunks, const double* slabs, const uint32_t* pair_ptr,
-                            const uint32_t* items, const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage,
-                            double* maxd, lh_params prm, int n_chunks) {
-    (void)chunks;
+hipError_t lh_launch_reduce(hipStream_t st, const double* slabs, const uint32_t* pair_ptr, const uint32_t* items,
+                            const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
+                            lh_params prm, int n_chunks) {
     const int npairs = prm.P * (prm.P + 1) / 2;
     hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, slabs, pair_ptr, items, pair_pq, ctrl,
                        rs_stage, maxd, prm, n_chunks);
@@ -2068,13 +2076,29 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
     return hipGetLastError();
 }
 
-// ---- k_reset: restart a resident solve (one launch instead of five copies) ----
-__global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const double2* __restrict__ rec_init, long nrec2,
+// ---- k_reset: restart a resident solve from the uploaded window (one launch instead of five copies):
+//      committed landmark records = {X of the window landmark, zeros} (records are read as X only by the
+//      initial linearisation), poses and pose tables from their initial copies, controller zeroed ----
+__global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const int32_t* __restrict__ lm_perm,
+                                               const double* __restrict__ lm_in, int nrec,
                                                double* __restrict__ qt, const double* __restrict__ qt_init, int nqt,
                                                double* __restrict__ ptab, const double* __restrict__ ptab_init, int nptab,
                                                double* __restrict__ dxp, int ndxp, lh_ctrl* __restrict__ ctrl) {
+    // one thread per 16-B piece of a record (8 per record)
+    const long n2 = (long)nrec * (LH_REC / 2);
     const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
-    for (long i = i0; i < nrec2; i += st) rec[i] = rec_init[i];
+    for (long i = i0; i < n2; i += st) {
+        const int r = (int)(i >> 3), q = (int)(i & 7);
+        double2 v = {0.0, 0.0};
+        if (q < 2) {
+            const int l = lm_perm[r];
+            if (l >= 0) {
+                const double* X = lm_in + 3 * (size_t)l;
+                v = (q == 0) ? double2{X[0], X[1]} : double2{X[2], 0.0};
+            }
+        }
+        rec[i] = v;
+    }
     if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < nqt; i += 256) qt[i] = qt_init[i];
         for (int i = threadIdx.x; i < nptab; i += 256) ptab[i] = ptab_init[i];
@@ -2084,14 +2108,44 @@ __global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const 
     }
 }
 
-hipError_t lh_launch_reset(hipStream_t st, double* rec, const double* rec_init, long nrec_doubles, double* qt,
-                           const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab, double* dxp,
-                           int ndxp, lh_ctrl* ctrl) {
-    const long n2 = nrec_doubles / 2;
+hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
+                           double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
+                           double* dxp, int ndxp, lh_ctrl* ctrl) {
+    const long n2 = (long)nrec * (LH_REC / 2);
     const int blocks = (int)std::max(1L, std::min(2048L, (n2 + 255) / 256));
-    hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, st, reinterpret_cast<double2*>(rec),
-                       reinterpret_cast<const double2*>(rec_init), n2, qt, qt_init, nqt, ptab, ptab_init, nptab, dxp,
-                       ndxp, ctrl);
+    hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, st, reinterpret_cast<double2*>(rec), lm_perm, lm_in, nrec,
+                       qt, qt_init, nqt, ptab, ptab_init, nptab, dxp, ndxp, ctrl);
+    return hipGetLastError();
+}
+
+// ---- k_gather: results back into window order for the download: landmark positions from the
+//      committed records (into out_xyz, pre-filled with the input positions, so landmarks without an
+//      edge keep theirs), per-edge rho0 "as last evaluated" from the slots ----
+__global__ __launch_bounds__(256) void k_gather(const lh_ctrl* __restrict__ ctrl, const double* __restrict__ rec,
+                                                const int32_t* __restrict__ lm_perm, int nrec,
+                                                const double* __restrict__ rho, const int32_t* __restrict__ obs_perm,
+                                                long nslots, double* __restrict__ out_xyz, double* __restrict__ out_rho) {
+    const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
+    const double* rc = rec + (size_t)cur * nrec * LH_REC;
+    const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
+    for (long i = i0; i < nslots; i += st) {
+        const int o = obs_perm[i];
+        if (o >= 0) out_rho[o] = rho[i];
+    }
+    for (long i = i0; i < 3L * nrec; i += st) {
+        const int r = (int)(i / 3), a = (int)(i - 3L * r);
+        const int l = lm_perm[r];
+        if (l >= 0) out_xyz[3 * (size_t)l + a] = rc[(size_t)r * LH_REC + LH_REC_X + a];
+    }
+}
+
+hipError_t lh_launch_gather(hipStream_t st, const lh_ctrl* ctrl, const double* rec, const int32_t* lm_perm, int nrec,
+                            const double* rho, const int32_t* obs_perm, long nslots, double* out_xyz, double* out_rho) {
+    const long n = std::max(nslots, 3L * nrec);
+    if (n <= 0) return hipSuccess;
+    const int blocks = (int)std::max(1L, std::min(4096L, (n + 255) / 256));
+    hipLaunchKernelGGL(k_gather, dim3(blocks), dim3(256), 0, st, ctrl, rec, lm_perm, nrec, rho, obs_perm, nslots,
+                       out_xyz, out_rho);
     return hipGetLastError();
 }
 

@@ -1,0 +1,390 @@
+// lh_plan.cpp — window preprocessing (see lh_plan.h).  Pure C++17: no HIP, so the CPU test suite
+// builds it into a host-only library (liblego_plan.so) and checks the plan's invariants.
+#include "lh_plan.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace lh {
+
+// ---------------------------------------------------------------------------------------------
+// Pool
+// ---------------------------------------------------------------------------------------------
+Pool::Pool(int threads) {
+    for (int i = 1; i < threads; ++i) workers_.emplace_back([this] { loop(); });
+}
+
+Pool::~Pool() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+}
+
+void Pool::loop() {
+    uint64_t seen = 0;
+    for (;;) {
+        const std::function<void(int)>* job;
+        int n;
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            job = job_;
+            n = n_;
+            ++active_;
+        }
+        for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) (*job)(i);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (--active_ == 0) done_cv_.notify_all();
+        }
+    }
+}
+
+void Pool::run(int n, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    if (workers_.empty() || n == 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        job_ = &fn;
+        n_ = n;
+        next_.store(0);
+        ++gen_;
+    }
+    cv_.notify_all();
+    for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) fn(i);
+    std::unique_lock<std::mutex> g(mu_);
+    // every worker that picked this job up has drained the index range once active_ drops to 0;
+    // a worker that wakes late sees next_ >= n and does nothing
+    done_cv_.wait(g, [&] { return active_ == 0; });
+    job_ = nullptr;
+}
+
+namespace {
+
+// run fn(begin, end) over [0, n) in about 4 blocks per thread
+void parallel_range(Pool* pool, int64_t n, int64_t min_block, const std::function<void(int64_t, int64_t)>& fn) {
+    if (n <= 0) return;
+    const int threads = pool ? pool->size() : 1;
+    int64_t nb = std::max<int64_t>(1, std::min<int64_t>(4 * threads, (n + min_block - 1) / min_block));
+    const int64_t bs = (n + nb - 1) / nb;
+    nb = (n + bs - 1) / bs;
+    auto body = [&](int b) { fn((int64_t)b * bs, std::min<int64_t>(n, (int64_t)(b + 1) * bs)); };
+    if (pool) pool->run((int)nb, body);
+    else for (int b = 0; b < nb; ++b) body(b);
+}
+
+inline int popc(uint32_t m) { return __builtin_popcount(m); }
+inline int chunk_tiles(uint32_t mask) { return (6 * popc(mask) + 15) / 16; }
+inline int pow2log(int k) { int g = 1, lg = 0; while (g < k) { g <<= 1; ++lg; } return lg; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// plan_structure
+// ---------------------------------------------------------------------------------------------
+int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Plan& pl, Pool* pool) {
+    if (!w) return LH_E_BADARG;
+    if (w->n_poses < 0 || w->n_landmarks < 0 || w->n_obs < 0) return LH_E_BADARG;
+    if (w->n_poses > 0 && !w->pose_Tcw) return LH_E_BADARG;
+    if (w->n_landmarks > 0 && !w->lm_xyz) return LH_E_BADARG;
+    if (w->n_obs > 0 && (!w->obs_pose || !w->obs_lm || !w->obs_uv)) return LH_E_BADARG;
+    if (w->n_cams < 0 || w->n_cams > LH_MAX_CAMS || (w->n_cams > 0 && !w->cam_ext)) return LH_E_BADARG;
+    const int P = w->n_poses, L = w->n_landmarks;
+    const int64_t O = w->n_obs;
+    const int ncam = w->n_cams > 0 ? w->n_cams : 1;
+    pl.P = P; pl.L = L; pl.O = O; pl.ncam = ncam;
+
+    // ---- index checks and "already landmark-major" detection, one parallel pass ----
+    std::atomic<int> bad{0}, unsorted{0};
+    parallel_range(pool, O, 1 << 15, [&](int64_t b, int64_t e) {
+        uint32_t prev = b > 0 ? w->obs_lm[b - 1] : 0;
+        bool bd = false, us = false;
+        for (int64_t o = b; o < e; ++o) {
+            const uint32_t l = w->obs_lm[o];
+            bd |= w->obs_pose[o] >= (uint32_t)P || l >= (uint32_t)L || (w->obs_cam && w->obs_cam[o] >= ncam);
+            us |= l < prev;
+            prev = l;
+        }
+        if (bd) bad.store(1);
+        if (us) unsorted.store(1);
+    });
+    if (bad.load()) return LH_E_BADARG;
+    if (!allow_empty && (O == 0 || (P + L) == 0)) return LH_E_EMPTY;   // problem.cpp:157-161
+    if (P > LH_PMAX) return LH_E_UNSUPPORTED;
+    if (O >= (int64_t)1 << 30) return LH_E_UNSUPPORTED;                 // int32 slot indices
+    pl.fixed_mask = 0;
+    if (w->pose_fixed)
+        for (int p = 0; p < P; ++p)
+            if (w->pose_fixed[p]) pl.fixed_mask |= 1u << p;
+
+    // ---- landmark-major CSR ----
+    pl.lm_ptr.assign((size_t)L + 1, 0);
+    pl.csr.resize((size_t)O);
+    if (!unsorted.load()) {
+        // input already grouped by landmark (what Backend::Optimize's landmark loop produces)
+        parallel_range(pool, O, 1 << 15, [&](int64_t b, int64_t e) {
+            for (int64_t o = b; o < e; ++o) {
+                pl.csr[o] = o;
+                const int64_t lo = o > 0 ? (int64_t)w->obs_lm[o - 1] + 1 : 0;
+                for (int64_t l = lo; l <= (int64_t)w->obs_lm[o]; ++l) pl.lm_ptr[l] = o;
+            }
+        });
+        for (int64_t l = (O > 0 ? (int64_t)w->obs_lm[O - 1] + 1 : 0); l <= L; ++l) pl.lm_ptr[l] = O;
+    } else {
+        for (int64_t o = 0; o < O; ++o) pl.lm_ptr[w->obs_lm[o] + 1]++;
+        for (int l = 0; l < L; ++l) pl.lm_ptr[l + 1] += pl.lm_ptr[l];
+        std::vector<int64_t> pos(pl.lm_ptr.begin(), pl.lm_ptr.end() - 1);
+        for (int64_t o = 0; o < O; ++o) pl.csr[pos[w->obs_lm[o]]++] = o;
+    }
+
+    // ---- per landmark: ascending pose order, pose mask, envelope checks ----
+    pl.lm_mask.assign((size_t)L, 0u);
+    std::atomic<int> unsup{0};
+    parallel_range(pool, L, 4096, [&](int64_t b, int64_t e) {
+        bool us = false;
+        for (int64_t l = b; l < e; ++l) {
+            int64_t* s = pl.csr.data() + pl.lm_ptr[l];
+            const int64_t k = pl.lm_ptr[l + 1] - pl.lm_ptr[l];
+            if (k > LH_SB_OBS) { us = true; continue; }
+            for (int64_t i = 1; i < k; ++i) {   // insertion sort by (pose, window index)
+                const int64_t v = s[i];
+                const uint32_t pv = w->obs_pose[v];
+                int64_t j = i - 1;
+                while (j >= 0 && (w->obs_pose[s[j]] > pv || (w->obs_pose[s[j]] == pv && s[j] > v))) { s[j + 1] = s[j]; --j; }
+                s[j + 1] = v;
+            }
+            uint32_t m = 0;
+            for (int64_t i = 0; i < k; ++i) {
+                const uint32_t bit = 1u << w->obs_pose[s[i]];
+                if (m & bit) us = true;   // two edges landmark -> same pose (DESIGN.md "Limits")
+                m |= bit;
+            }
+            if (popc(m) > LH_UMAX) us = true;
+            pl.lm_mask[l] = m;
+        }
+        if (us) unsup.store(1);
+    });
+    if (unsup.load()) return LH_E_UNSUPPORTED;
+
+    // ---- landmark order by observation span (first pose, last pose, mask), stable ----
+    {
+        const int nb = std::max(P, 1) * std::max(P, 1);
+        std::vector<int32_t> bcnt((size_t)nb + 1, 0);
+        auto bucket = [&](int l) {
+            const uint32_t m = pl.lm_mask[l];
+            return __builtin_ctz(m) * P + (31 - __builtin_clz(m));
+        };
+        int Lact = 0;
+        for (int l = 0; l < L; ++l)
+            if (pl.lm_mask[l]) { bcnt[bucket(l) + 1]++; ++Lact; }   // edge-less landmarks are no vertex (backend_lego.cpp:126)
+        for (int b = 0; b < nb; ++b) bcnt[b + 1] += bcnt[b];
+        pl.order.resize((size_t)Lact);
+        {
+            std::vector<int32_t> cur(bcnt.begin(), bcnt.end() - 1);
+            for (int l = 0; l < L; ++l)
+                if (pl.lm_mask[l]) pl.order[cur[bucket(l)]++] = l;
+        }
+        for (int b = 0; b < nb; ++b) {
+            auto s = pl.order.begin() + bcnt[b], e = pl.order.begin() + bcnt[b + 1];
+            if (e - s < 2) continue;
+            const uint32_t m0 = pl.lm_mask[*s];
+            if (std::all_of(s, e, [&](int32_t l) { return pl.lm_mask[l] == m0; })) continue;
+            std::stable_sort(s, e, [&](int32_t a, int32_t c) { return pl.lm_mask[a] < pl.lm_mask[c]; });
+        }
+    }
+    const int Lact = (int)pl.order.size();
+
+    // ---- chunks: ~512 (2 workgroups per CU), multiples of 4 x 8 landmarks (equal work per wave) ----
+    int chunk_lm = (Lact + 511) / 512;
+    chunk_lm = ((chunk_lm + 4 * LH_SB_LM - 1) / (4 * LH_SB_LM)) * (4 * LH_SB_LM);
+    chunk_lm = std::max(32, std::min(256, chunk_lm));
+    if (cfg.chunk_lm > 0) chunk_lm = std::max(LH_SB_LM, std::min(512, cfg.chunk_lm));
+    pl.chunk_lm0.clear();
+    pl.chunk_mask.clear();
+    // a chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new chunk
+    // rather than let the union grow past the larger of the two tile counts
+    for (int i = 0; i < Lact; ++i) {
+        const uint32_t m = pl.lm_mask[pl.order[i]];
+        const bool fresh = pl.chunk_lm0.empty() || (i - pl.chunk_lm0.back()) >= chunk_lm ||
+                           popc(pl.chunk_mask.back() | m) > LH_UMAX ||
+                           chunk_tiles(pl.chunk_mask.back() | m) > std::max(chunk_tiles(pl.chunk_mask.back()), chunk_tiles(m));
+        if (fresh) {
+            pl.chunk_lm0.push_back(i);
+            pl.chunk_mask.push_back(0u);
+        }
+        pl.chunk_mask.back() |= m;
+    }
+    const int NC = (int)pl.chunk_mask.size();
+    pl.chunk_lm0.push_back(Lact);
+    pl.n_chunks = NC;
+
+    // launch order: grouped by T (one k_lin launch per tile count), stable
+    pl.corder.resize((size_t)NC);
+    {
+        int c = 0;
+        for (int T = 1; T <= LH_TMAX; ++T) {
+            pl.tgroup_begin[T] = c;
+            for (int i = 0; i < NC; ++i)
+                if (chunk_tiles(pl.chunk_mask[i]) == T) pl.corder[c++] = i;
+        }
+        pl.tgroup_begin[0] = 0;
+        pl.tgroup_begin[LH_TMAX + 1] = c;
+    }
+
+    // ---- sub-batches: landmark l owns the aligned lane group [l*G, l*G + k_l) of 64 slots ----
+    auto lm_k = [&](int pos) { const int l = pl.order[pos]; return (int)(pl.lm_ptr[l + 1] - pl.lm_ptr[l]); };
+    auto walk = [&](int c, const std::function<void(int, int, int)>& emit) {   // emit(first pos, n, lg)
+        const int b = pl.chunk_lm0[c], e = pl.chunk_lm0[c + 1];
+        int i = b;
+        while (i < e) {
+            int lg = 0, n = 0;
+            while (i + n < e && n < LH_SB_LM) {
+                const int lgn = std::max(lg, pow2log(lm_k(i + n)));
+                if ((n + 1) << lgn > LH_SB_OBS) break;
+                lg = lgn;
+                ++n;
+            }
+            emit(i, n, lg);
+            i += n;
+        }
+    };
+    std::vector<int32_t> nsb((size_t)NC, 0);
+    auto count_sb = [&](int c) { walk(c, [&](int, int, int) { nsb[c]++; }); };
+    if (pool) pool->run(NC, count_sb);
+    else for (int c = 0; c < NC; ++c) count_sb(c);
+    pl.chunk_sb0.assign((size_t)NC + 1, 0);
+    for (int ci = 0; ci < NC; ++ci) pl.chunk_sb0[ci + 1] = pl.chunk_sb0[ci] + nsb[pl.corder[ci]];   // by launch position
+    pl.n_sb = pl.chunk_sb0[NC];
+    pl.n_rec = pl.n_sb * LH_SB_LM;
+    pl.n_slots = (int64_t)pl.n_sb * LH_SB_OBS;
+    pl.sb_lm0.resize((size_t)pl.n_sb + 1);
+    pl.sb_lg.resize((size_t)pl.n_sb);
+    auto fill_sb = [&](int ci) {
+        int sb = pl.chunk_sb0[ci];
+        walk(pl.corder[ci], [&](int first, int, int lg) { pl.sb_lm0[sb] = first; pl.sb_lg[sb] = (uint8_t)lg; ++sb; });
+    };
+    if (pool) pool->run(NC, fill_sb);
+    else for (int ci = 0; ci < NC; ++ci) fill_sb(ci);
+    pl.sb_lm0[pl.n_sb] = Lact;   // never read as a start: the last sub-batch ends at its chunk's end
+
+    // ---- reduce plan sizes: per pose pair, the chunks touching it ----
+    pl.npairs = P * (P + 1) / 2;
+    pl.pair_ptr.assign((size_t)pl.npairs + 1, 0u);
+    for (int ci = 0; ci < NC; ++ci) {
+        const uint32_t m = pl.chunk_mask[pl.corder[ci]];
+        for (uint32_t a = m; a; a &= a - 1) {
+            const int p = __builtin_ctz(a);
+            for (uint32_t b = a; b; b &= b - 1) {
+                const int q = __builtin_ctz(b);
+                pl.pair_ptr[p * P - (p * (p - 1)) / 2 + (q - p) + 1]++;
+            }
+        }
+    }
+    for (int b = 0; b < pl.npairs; ++b) pl.pair_ptr[b + 1] += pl.pair_ptr[b];
+    pl.n_items = (int)pl.pair_ptr[pl.npairs];
+    return LH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// plan_fill
+// ---------------------------------------------------------------------------------------------
+void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool) {
+    const int P = pl.P, NC = pl.n_chunks;
+    // chunks and their sub-batches' observation slots, one task per chunk
+    auto chunk_task = [&](int ci) {
+        const int c = pl.corder[ci];
+        const uint32_t m = pl.chunk_mask[c];
+        lh_chunk ck;
+        std::memset(&ck, 0, sizeof(ck));
+        ck.U = (uint8_t)popc(m);
+        ck.T = (uint8_t)chunk_tiles(m);
+        int slot_of[32] = {0};
+        {
+            int s = 0;
+            for (uint32_t a = m; a; a &= a - 1) { const int p = __builtin_ctz(a); ck.pose[s] = (uint16_t)p; slot_of[p] = s++; }
+        }
+        ck.sb_begin = (uint32_t)pl.chunk_sb0[ci];
+        ck.sb_end = (uint32_t)pl.chunk_sb0[ci + 1];
+        out.chunks[ci] = ck;
+        const int lm_end = pl.chunk_lm0[c + 1];
+        for (int sb = pl.chunk_sb0[ci]; sb < pl.chunk_sb0[ci + 1]; ++sb) {
+            const int first = pl.sb_lm0[sb];
+            const int last = (sb + 1 < pl.chunk_sb0[ci + 1]) ? pl.sb_lm0[sb + 1] : lm_end;
+            const int n = last - first, lg = pl.sb_lg[sb];
+            lh_subbatch sbd;
+            std::memset(&sbd, 0, sizeof(sbd));
+            sbd.lm_begin = (uint32_t)sb * LH_SB_LM;
+            sbd.n_lm = (uint8_t)n;
+            sbd.lg = (uint8_t)lg;
+            out.sbs[sb] = sbd;
+            const int64_t base = (int64_t)sb * LH_SB_OBS;
+            auto pad = [&](int64_t s0, int64_t s1) {   // unused slots: a meta word without LH_META_VALID
+                for (int64_t s = s0; s < s1; ++s) {
+                    out.meta[s] = 0u;
+                    out.uv[2 * s] = 0.0;
+                    out.uv[2 * s + 1] = 0.0;
+                    out.obs_perm[s] = -1;
+                }
+            };
+            for (int q = 0; q < LH_SB_LM; ++q) out.lm_perm[sbd.lm_begin + q] = q < n ? pl.order[first + q] : -1;
+            for (int q = 0; q < n; ++q) {   // every slot is written once
+                const int l = pl.order[first + q];
+                int64_t slot = base + ((int64_t)q << lg);
+                for (int64_t r = pl.lm_ptr[l]; r < pl.lm_ptr[l + 1]; ++r, ++slot) {
+                    const int64_t o = pl.csr[r];
+                    const uint32_t p = w->obs_pose[o];
+                    const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
+                    out.meta[slot] = LH_META(p, cam, slot_of[p], q);
+                    out.uv[2 * slot] = w->obs_uv[2 * o];
+                    out.uv[2 * slot + 1] = w->obs_uv[2 * o + 1];
+                    out.obs_perm[slot] = (int32_t)o;
+                }
+                pad(slot, base + ((int64_t)(q + 1) << lg));
+            }
+            pad(base + ((int64_t)n << lg), base + LH_SB_OBS);
+        }
+    };
+    if (pool) pool->run(NC, chunk_task);
+    else for (int ci = 0; ci < NC; ++ci) chunk_task(ci);
+
+    // reduce plan items: (chunk launch position << 11) | (T << 8) | (slot p << 4) | slot q, per pair in
+    // launch order (k_reduce sums them in this order: a fixed, thread-count-independent order)
+    {
+        std::vector<uint32_t> cur(pl.pair_ptr.begin(), pl.pair_ptr.end() - 1);
+        for (int ci = 0; ci < NC; ++ci) {
+            const uint32_t m = pl.chunk_mask[pl.corder[ci]];
+            const int T = chunk_tiles(m);
+            int ps[32], U = 0;
+            for (uint32_t a = m; a; a &= a - 1) ps[U++] = __builtin_ctz(a);
+            for (int s = 0; s < U; ++s)
+                for (int t = s; t < U; ++t) {
+                    const int p = ps[s], q = ps[t];
+                    const int b = p * P - (p * (p - 1)) / 2 + (q - p);
+                    out.items[cur[b]++] = ((uint32_t)ci << 11) | ((uint32_t)T << 8) | ((uint32_t)s << 4) | (uint32_t)t;
+                }
+        }
+    }
+    for (int p = 0, b = 0; p < P; ++p)
+        for (int q = p; q < P; ++q, ++b) { out.pair_pq[2 * b] = (uint16_t)p; out.pair_pq[2 * b + 1] = (uint16_t)q; }
+    // reduced-system element map for k_ctrl's register scatter: S element of pose pair (pi, pj),
+    // pi <= pj, row a, col b -> global rows 6 pi + a, 6 pj + b, diagonal-block flag
+    for (int pi = 0, blk = 0; pi < P; ++pi)
+        for (int pj = pi; pj < P; ++pj, ++blk)
+            for (int a = 0; a < 6; ++a)
+                for (int b = 0; b < 6; ++b)
+                    out.rsmap[(size_t)blk * 36 + 6 * a + b] =
+                        (uint32_t)(6 * pi + a) | ((uint32_t)(6 * pj + b) << 8) | ((pi == pj ? 1u : 0u) << 16);
+    parallel_range(pool, 3 * (int64_t)pl.L, 1 << 16, [&](int64_t b, int64_t e) {
+        if (e > b) std::memcpy(out.lm_xyz + b, w->lm_xyz + b, (size_t)(e - b) * sizeof(double));
+    });
+}
+
+}  // namespace lh

@@ -1,0 +1,95 @@
+// lh_plan.h — window preprocessing for the device layout (host only, no HIP).
+//
+// One sliding window (include/lego_ba.h lh_window) becomes:
+//   * a landmark-major order of the observations, each landmark's observations in ascending pose
+//     order (the reference visits edges in unordered_map order, problem.cpp:285; any order is the
+//     same problem);
+//   * landmarks ordered by observation span and packed into chunks whose union of observing poses
+//     fits one MFMA window (<= LH_UMAX poses), chunks split into wave sub-batches (<= 8 landmarks,
+//     <= 64 observations, landmark l owning the aligned lane group [l*G, l*G + k_l));
+//   * the reduce plan: for every pose pair p <= q, the chunks whose slab holds a block of it.
+// Two phases so the bulk arrays are written once, straight into the caller's (pinned) staging:
+// plan_structure() sizes everything (O(O) scan + O(L) ordering), plan_fill() writes the arrays.
+// Both run on a small thread pool; the result does not depend on the thread count.
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/lego_ba.h"
+#include "lh_common.h"
+
+namespace lh {
+
+// Persistent worker pool: run(n, fn) calls fn(i) for i in [0, n) on the workers and the caller.
+class Pool {
+  public:
+    explicit Pool(int threads);
+    ~Pool();
+    int size() const { return (int)workers_.size() + 1; }
+    void run(int n, const std::function<void(int)>& fn);
+
+  private:
+    void loop();
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* job_ = nullptr;
+    int n_ = 0;
+    std::atomic<int> next_{0};
+    int active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+struct PlanCfg {
+    int chunk_lm = 0;      // landmarks per chunk; 0 = auto (~512 chunks, 2 workgroups per CU)
+};
+
+struct Plan {
+    // ---- sizes (plan_structure) ----
+    int P = 0, L = 0, ncam = 1;
+    int64_t O = 0;
+    int n_chunks = 0, n_sb = 0, n_items = 0, npairs = 0;
+    int n_rec = 0;                      // landmark records (8 per sub-batch)
+    int64_t n_slots = 0;                // observation slots (64 per sub-batch)
+    int tgroup_begin[LH_TMAX + 2] = {0};
+    uint32_t fixed_mask = 0;
+    // ---- internal (reused across windows) ----
+    std::vector<int64_t> lm_ptr;        // [L+1] CSR over landmarks
+    std::vector<int64_t> csr;           // [O] window obs, landmark-major, ascending pose
+    std::vector<uint32_t> lm_mask;      // [L] observing-pose mask
+    std::vector<int32_t> order;         // [L_act] landmarks with edges, span order
+    std::vector<int32_t> chunk_lm0;     // [n_chunks + 1] chunk c owns order[chunk_lm0[c] .. chunk_lm0[c+1])
+    std::vector<uint32_t> chunk_mask;   // [n_chunks] union pose mask
+    std::vector<int32_t> chunk_sb0;     // [n_chunks + 1] sub-batch prefix (chunks in T order)
+    std::vector<int32_t> corder;        // [n_chunks] launch order (grouped by T) -> chunk
+    std::vector<int32_t> sb_lm0;        // [n_sb + 1] sub-batch -> first position in order[]
+    std::vector<uint8_t> sb_lg;         // [n_sb]
+    std::vector<uint32_t> pair_ptr;     // [npairs + 1]
+};
+
+struct PlanOut {
+    lh_chunk* chunks;        // [n_chunks]
+    lh_subbatch* sbs;        // [n_sb]
+    uint32_t* meta;          // [n_slots]
+    double* uv;              // [2 n_slots]
+    int32_t* obs_perm;       // [n_slots] slot -> window obs (-1: padding)
+    int32_t* lm_perm;        // [n_rec] record -> window landmark (-1: padding)
+    uint32_t* items;         // [n_items]
+    uint16_t* pair_pq;       // [2 npairs]
+    uint32_t* rsmap;         // [npairs * 36]
+    double* lm_xyz;          // [3 L] copy of the window's positions
+};
+
+// lh_status.  LH_E_BADARG for out-of-range indices, LH_E_UNSUPPORTED outside the envelope
+// (DESIGN.md "Limits"), LH_E_EMPTY mirrors problem.cpp:157-161.
+int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Plan& pl, Pool* pool);
+void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool);
+
+}  // namespace lh

@@ -1,0 +1,81 @@
+// lh_plan_capi.cpp — C entry points of the window planner for the CPU test suite and the host-side
+// preprocessing timings (liblego_plan.so, built with g++ only: no HIP, no GPU).  Not part of the
+// solver ABI (include/lego_ba.h); the solver links lh_plan.cpp directly.
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "lh_plan.h"
+
+namespace {
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+extern "C" {
+
+// sizes[0..6] = n_chunks, n_sb, n_items, npairs, n_rec, n_slots, fixed_mask; tgroup[0..LH_TMAX+1]
+int lhp_plan_sizes(const lh_window* w, int chunk_lm, int threads, int64_t* sizes, int32_t* tgroup) {
+    lh::Pool pool(threads > 0 ? threads : 1);
+    lh::Plan pl;
+    lh::PlanCfg cfg;
+    cfg.chunk_lm = chunk_lm;
+    const int st = lh::plan_structure(w, cfg, false, pl, &pool);
+    if (st != LH_OK) return st;
+    const int64_t v[7] = {pl.n_chunks, pl.n_sb, pl.n_items, pl.npairs, pl.n_rec, pl.n_slots, (int64_t)pl.fixed_mask};
+    std::memcpy(sizes, v, sizeof(v));
+    for (int i = 0; i < LH_TMAX + 2; ++i) tgroup[i] = pl.tgroup_begin[i];
+    return LH_OK;
+}
+
+int lhp_plan_fill(const lh_window* w, int chunk_lm, int threads, lh_chunk* chunks, lh_subbatch* sbs, uint32_t* meta,
+                  double* uv, int32_t* obs_perm, int32_t* lm_perm, uint32_t* pair_ptr, uint32_t* items,
+                  uint16_t* pair_pq, uint32_t* rsmap, double* lm_xyz) {
+    lh::Pool pool(threads > 0 ? threads : 1);
+    lh::Plan pl;
+    lh::PlanCfg cfg;
+    cfg.chunk_lm = chunk_lm;
+    const int st = lh::plan_structure(w, cfg, false, pl, &pool);
+    if (st != LH_OK) return st;
+    lh::PlanOut po{chunks, sbs, meta, uv, obs_perm, lm_perm, items, pair_pq, rsmap, lm_xyz};
+    lh::plan_fill(w, pl, po, &pool);
+    std::memcpy(pair_ptr, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
+    return LH_OK;
+}
+
+// mean over reps plans (after one warm-up) on a persistent pool: ms of plan_structure and of
+// plan_fill into reused buffers, i.e. what lh_upload spends before its copies
+int lhp_plan_time(const lh_window* w, int chunk_lm, int threads, int reps, double* ms_structure, double* ms_fill) {
+    lh::Pool pool(threads > 0 ? threads : 1);
+    lh::Plan pl;
+    lh::PlanCfg cfg;
+    cfg.chunk_lm = chunk_lm;
+    std::vector<lh_chunk> chunks;
+    std::vector<lh_subbatch> sbs;
+    std::vector<uint32_t> meta, items, rsmap;
+    std::vector<double> uv, lm;
+    std::vector<int32_t> operm, lperm;
+    std::vector<uint16_t> pq;
+    double ts = 0.0, tf = 0.0;
+    for (int r = 0; r <= reps; ++r) {
+        const double t0 = now_ms();
+        const int st = lh::plan_structure(w, cfg, false, pl, &pool);
+        if (st != LH_OK) return st;
+        const double t1 = now_ms();
+        chunks.resize(pl.n_chunks); sbs.resize(pl.n_sb); meta.resize(pl.n_slots); uv.resize(2 * pl.n_slots);
+        operm.resize(pl.n_slots); lperm.resize(pl.n_rec); items.resize(pl.n_items); pq.resize(2 * (size_t)pl.npairs);
+        rsmap.resize((size_t)pl.npairs * 36); lm.resize(3 * (size_t)pl.L);
+        const double t2 = now_ms();
+        lh::PlanOut po{chunks.data(), sbs.data(), meta.data(), uv.data(), operm.data(), lperm.data(), items.data(),
+                       pq.data(), rsmap.data(), lm.data()};
+        lh::plan_fill(w, pl, po, &pool);
+        const double t3 = now_ms();
+        if (r > 0) { ts += t1 - t0; tf += t3 - t2; }
+    }
+    *ms_structure = ts / reps;
+    *ms_fill = tf / reps;
+    return LH_OK;
+}
+
+}  // extern "C"

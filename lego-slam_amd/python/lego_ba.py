@@ -119,8 +119,12 @@ def config_window(name, seed=0, **kw):
 # --------------------------------------------------------------------------
 
 LH_OK, LH_E_EMPTY, LH_E_BADARG, LH_E_HIP, LH_E_RCCL, LH_E_UNSUPPORTED, LH_E_STATE = range(7)
-LH_ABI_VERSION = 2
+LH_ABI_VERSION = 3
 LH_SOLVER_LDLT, LH_SOLVER_PCG = 0, 1
+LH_COMM_RCCL, LH_COMM_HOST = 0, 1
+
+# lh_allreduce_fn: int (*)(void* user, double* buf, int64_t count, int32_t op)   (op 0 sum, 1 max)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32)
 
 
 class LhOptions(C.Structure):
@@ -132,6 +136,8 @@ class LhOptions(C.Structure):
         ("world_size", C.c_int32), ("rank", C.c_int32), ("degenerate_guard", C.c_int32),
         ("trials_per_sync", C.c_int32), ("profile", C.c_int32), ("pcg_max_iters", C.c_int32),
         ("pcg_tol", C.c_double), ("comm_id", C.c_uint8 * 128),
+        ("gate_mode", C.c_int32), ("chunk_landmarks", C.c_int32), ("comm_mode", C.c_int32),
+        ("host_threads", C.c_int32), ("allreduce", C.c_void_p), ("allreduce_user", C.c_void_p),
     ]
 
 
@@ -152,6 +158,8 @@ class LhResult(C.Structure):
         ("trace_len", C.c_int32), ("iterations", C.c_int32), ("trials", C.c_int32),
         ("accepted", C.c_int32), ("chi2_initial", C.c_double), ("chi2_final", C.c_double),
         ("lambda_final", C.c_double), ("time_ms", C.c_double), ("pcg_iterations", C.c_int32),
+        ("degenerate", C.c_int32), ("time_prep_ms", C.c_double), ("time_upload_ms", C.c_double),
+        ("time_download_ms", C.c_double),
     ]
 
 
@@ -180,6 +188,7 @@ ABI_SYMBOLS = [
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
     "lh_estimate_pose",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
+    "lh_debug_time_lin", "lh_debug_comm_count",
 ]
 
 _balib = None
@@ -209,6 +218,9 @@ def ba_lib():
         lib.lh_estimate_pose.argtypes = [C.c_void_p, C.POINTER(LhFrames), C.POINTER(LhFramesResult)]
         lib.lh_classify_outliers.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.lh_debug_event_floor.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        lib.lh_debug_time_lin.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
+        lib.lh_debug_comm_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
         _balib = lib
     return _balib
 
@@ -270,9 +282,23 @@ class _WindowRef:
 class Solver:
     """One lh_handle (one GPU / one landmark shard)."""
 
-    def __init__(self, **opts):
+    def __init__(self, allreduce=None, **opts):
+        """allreduce: optional Python callable f(buf: np.ndarray, op: int) reducing buf in place over
+        the ranks (op 0 sum, 1 max), used with comm_mode=LH_COMM_HOST and world_size > 1."""
         lib = ba_lib()
+        self._cb = None
+        if allreduce is not None:
+            def _thunk(user, buf, count, op):
+                try:
+                    allreduce(np.ctypeslib.as_array(buf, shape=(count,)), int(op))
+                    return 0
+                except Exception:   # noqa: BLE001 - reported to the library as a failed exchange
+                    return 1
+            self._cb = ALLREDUCE_FN(_thunk)
+            opts.setdefault("comm_mode", LH_COMM_HOST)
         self.opts = default_options(**opts)
+        if self._cb is not None:
+            self.opts.allreduce = C.cast(self._cb, C.c_void_p)
         h = C.c_void_p()
         _check(lib.lh_create(C.byref(h), C.byref(self.opts)), "lh_create")
         self.h = h
@@ -309,7 +335,7 @@ class Solver:
         out["trace_chi2"] = out["trace_chi2"][:n]
         out["trace_lambda"] = out["trace_lambda"][:n]
         for f in ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "time_ms",
-                  "pcg_iterations"):
+                  "pcg_iterations", "degenerate", "time_prep_ms", "time_upload_ms", "time_download_ms"):
             out[f] = getattr(r, f)
         return out
 
@@ -368,10 +394,20 @@ class Solver:
     def event_floor_ms(self):
         """HIP-event bracket of an empty kernel on this solver's stream (lh_debug_event_floor)."""
         ms = C.c_double(0.0)
-        lib = ba_lib()
-        lib.lh_debug_event_floor.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
-        _check(lib.lh_debug_event_floor(self.h, C.byref(ms)), "lh_debug_event_floor")
+        _check(ba_lib().lh_debug_event_floor(self.h, C.byref(ms)), "lh_debug_event_floor")
         return ms.value
+
+    def time_lin_ms(self, reps=50):
+        """k_lin's duration per LM trial (lh_debug_time_lin): replayed back to back after a solve."""
+        ms = C.c_double(0.0)
+        _check(ba_lib().lh_debug_time_lin(self.h, reps, C.byref(ms)), "lh_debug_time_lin")
+        return ms.value
+
+    def comm_count(self):
+        """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""
+        n = C.c_int64(0)
+        _check(ba_lib().lh_debug_comm_count(self.h, C.byref(n)), "lh_debug_comm_count")
+        return n.value
 
 
 def debug_stamps(reset=True):
@@ -396,3 +432,58 @@ def classify_outliers(edge_rchi2, chi2_th=5.991):
     _check(ba_lib().lh_classify_outliers(_ptr(e), e.shape[0], chi2_th, _ptr(flags), C.byref(th),
                                          C.byref(ni), C.byref(no)), "lh_classify_outliers")
     return flags.astype(bool), th.value, ni.value, no.value
+
+
+# --------------------------------------------------------------------------
+# window planner (liblego_plan.so: lh_plan.cpp alone, host C++; CPU tests and timings)
+# --------------------------------------------------------------------------
+PLAN_LIB = os.path.join(LIB_DIR, "liblego_plan.so")
+LH_TMAX = 6
+
+# lh_chunk / lh_subbatch (lego-slam_amd/csrc/lh_common.h)
+CHUNK_DT = np.dtype([("sb_begin", "<u4"), ("sb_end", "<u4"), ("U", "u1"), ("T", "u1"), ("pad", "u1", 2),
+                     ("pose", "<u2", 16)])
+SUBBATCH_DT = np.dtype([("lm_begin", "<u4"), ("n_lm", "u1"), ("lg", "u1"), ("pad", "<u2")])
+
+_planlib = None
+
+
+def _pl():
+    global _planlib
+    if _planlib is None:
+        if not os.path.exists(PLAN_LIB):
+            raise RuntimeError(f"{PLAN_LIB} not built (run __graft_entry__.build())")
+        lib = C.CDLL(PLAN_LIB)
+        vp = C.c_void_p
+        lib.lhp_plan_sizes.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, vp, vp]
+        lib.lhp_plan_fill.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int] + [vp] * 11
+        lib.lhp_plan_time.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double)]
+        _planlib = lib
+    return _planlib
+
+
+def plan_window(w, chunk_lm=0, threads=1):
+    """The device layout lh_upload builds for window `w` (lh_plan.cpp), as numpy arrays."""
+    ref = _WindowRef(w)
+    sizes = np.zeros(7, np.int64)
+    tg = np.zeros(LH_TMAX + 2, np.int32)
+    _check(_pl().lhp_plan_sizes(C.byref(ref.s), chunk_lm, threads, _ptr(sizes), _ptr(tg)), "lhp_plan_sizes")
+    n_chunks, n_sb, n_items, npairs, n_rec, n_slots, fixed_mask = (int(x) for x in sizes)
+    out = dict(chunks=np.zeros(n_chunks, CHUNK_DT), sbs=np.zeros(n_sb, SUBBATCH_DT),
+               meta=np.zeros(n_slots, np.uint32), uv=np.zeros((n_slots, 2)), obs_perm=np.zeros(n_slots, np.int32),
+               lm_perm=np.zeros(n_rec, np.int32), pair_ptr=np.zeros(npairs + 1, np.uint32),
+               items=np.zeros(n_items, np.uint32), pair_pq=np.zeros((npairs, 2), np.uint16),
+               rsmap=np.zeros(npairs * 36, np.uint32), lm_xyz=np.zeros((ref.s.n_landmarks, 3)))
+    k = ("chunks", "sbs", "meta", "uv", "obs_perm", "lm_perm", "pair_ptr", "items", "pair_pq", "rsmap", "lm_xyz")
+    _check(_pl().lhp_plan_fill(C.byref(ref.s), chunk_lm, threads, *[_ptr(out[n]) for n in k]), "lhp_plan_fill")
+    out.update(tgroup_begin=tg, fixed_mask=fixed_mask)
+    return out
+
+
+def plan_time_ms(w, chunk_lm=0, threads=1, reps=5):
+    """Host preprocessing time of lh_upload for window `w`: (plan_structure ms, plan_fill ms)."""
+    ref = _WindowRef(w)
+    a, b = C.c_double(), C.c_double()
+    _check(_pl().lhp_plan_time(C.byref(ref.s), chunk_lm, threads, reps, C.byref(a), C.byref(b)), "lhp_plan_time")
+    return a.value, b.value

@@ -51,6 +51,11 @@ typedef struct orc_options {
     int32_t linear_solver; /* 0 Eigen LDLT (problem.cpp:420); 1 PCG (PCGSolver :584-614, fixed) */
     int32_t pcg_max_iters; /* <= 0: 2 * rows (problem.cpp:422) */
     double pcg_tol;        /* 1e-6 (problem.cpp:597) */
+    int32_t degenerate_guard; /* 0: reference (problem.cpp:396-400: the LU inverse of a rank-deficient
+                                 H_ll as it comes); 1: the solver's opt-in guard (include/lego_ba.h):
+                                 a landmark with < 2 edges or a non-PD H_ll is held fixed (no Schur
+                                 term, dx_l = 0) - restated here so the guard mode is checked too */
+    int32_t pad_;
 } orc_options;
 
 typedef struct orc_stats {
@@ -396,7 +401,21 @@ typedef struct {
     /* orc_reduced_system: capture the undamped reduced system instead of solving */
     double *S_out, *bs_out;
     int64_t pcg_iters;       /* PCG steps summed over the solve's trials */
+    int64_t *lm_cnt;         /* edges per landmark (degenerate_guard) */
 } prob_t;
+
+/* degenerate_guard 1: the solver's test (lh_kernels.hip k_lin): fewer than two edges, or a Cholesky
+   pivot of H_ll that is not positive */
+static int hll_degenerate(const prob_t *pb, int32_t l, const double *H) {
+    if (pb->lm_cnt[l] < 2) return 1;
+    if (!(H[0] > 0.0)) return 1;
+    const double l00 = sqrt(H[0]), l10 = H[1] / l00, l20 = H[2] / l00;
+    const double a11 = H[4] - l10 * l10;
+    if (!(a11 > 0.0)) return 1;
+    const double l21 = (H[5] - l20 * l10) / sqrt(a11);
+    const double a22 = H[8] - l20 * l20 - l21 * l21;
+    return !(a22 > 0.0) || !isfinite(a22);
+}
 
 /* ---- EdgeProjection arithmetic (include/legoslam/lego_types.h:200-254) ---- */
 
@@ -549,6 +568,8 @@ static void solve_dense(prob_t *pb) {
         for (int a = 0; a < 3; ++a)
             for (int c = 0; c < 3; ++c) blk[3 * a + c] = pb->H[(o + a) * n + o + c];
         lu_inverse3(blk, inv);
+        if (pb->opt.degenerate_guard && hll_degenerate(pb, l, blk))
+            for (int a = 0; a < 9; ++a) inv[a] = 0.0;   /* held fixed: no Schur term, dx_l = 0 */
         for (int a = 0; a < 3; ++a)
             for (int c = 0; c < 3; ++c) Hmm_inv[(3 * l + a) * nm + 3 * l + c] = inv[3 * a + c];
     }
@@ -675,6 +696,8 @@ static void solve_sparse(prob_t *pb) {
         for (int32_t l = 0; l < pb->L; ++l) {
             double *inv = Hinv + 9 * (size_t)l;
             lu_inverse3(pb->Hll + 9 * (size_t)l, inv);
+            if (pb->opt.degenerate_guard && hll_degenerate(pb, l, pb->Hll + 9 * (size_t)l))
+                for (int a = 0; a < 9; ++a) inv[a] = 0.0;   /* held fixed: no Schur term, dx_l = 0 */
             /* merge the landmark's edges per pose: H_pl block of the dense H */
             int nb = 0;
             for (int64_t q = pb->lm_ptr[l]; q < pb->lm_ptr[l + 1]; ++q) {
@@ -932,6 +955,8 @@ static int orc_run(int variant, int32_t P, const double *pose_in, const uint8_t 
     memcpy(pb.pose, pose_in, sizeof(double) * 12 * (size_t)P);
     memcpy(pb.lm, lm_in, sizeof(double) * 3 * (size_t)L);
     pb.res = (double *)calloc(2 * (size_t)O, sizeof(double));
+    pb.lm_cnt = (int64_t *)calloc((size_t)(L > 0 ? L : 1), sizeof(int64_t));
+    for (int64_t e = 0; e < O; ++e) pb.lm_cnt[ol[e]]++;
     pb.dx = (double *)calloc((size_t)pb.n, sizeof(double));
     pb.b = (double *)calloc((size_t)pb.n, sizeof(double));
     pb.hdiag = (double *)calloc((size_t)pb.n, sizeof(double));
@@ -963,7 +988,7 @@ static int orc_run(int variant, int32_t P, const double *pose_in, const uint8_t 
         free(pb.ext); free(pb.pose); free(pb.pose_bak); free(pb.lm); free(pb.lm_bak);
         free(pb.res); free(pb.dx); free(pb.b); free(pb.hdiag);
         free(pb.H); free(pb.Hpp); free(pb.bp); free(pb.Hll); free(pb.bl); free(pb.Hpl);
-        free(pb.lm_ptr); free(pb.lm_edges);
+        free(pb.lm_ptr); free(pb.lm_edges); free(pb.lm_cnt);
         return 0;
     }
     if (pb.opt.verbose) printf("==========LEGO OPTIMIZER==========\n");
@@ -1011,7 +1036,7 @@ static int orc_run(int variant, int32_t P, const double *pose_in, const uint8_t 
     free(pb.ext); free(pb.pose); free(pb.pose_bak); free(pb.lm); free(pb.lm_bak);
     free(pb.res); free(pb.dx); free(pb.b); free(pb.hdiag);
     free(pb.H); free(pb.Hpp); free(pb.bp); free(pb.Hll); free(pb.bl); free(pb.Hpl);
-    free(pb.lm_ptr); free(pb.lm_edges);
+    free(pb.lm_ptr); free(pb.lm_edges); free(pb.lm_cnt);
     return 0;
 }
 

@@ -21,6 +21,7 @@ class OrcOptions(C.Structure):
         ("huber_delta", C.c_double), ("stop_dchi2", C.c_double), ("tau", C.c_double),
         ("lambda_cap", C.c_double), ("lambda_init", C.c_double),
         ("linear_solver", C.c_int32), ("pcg_max_iters", C.c_int32), ("pcg_tol", C.c_double),
+        ("degenerate_guard", C.c_int32), ("pad_", C.c_int32),
     ]
 
 
@@ -33,16 +34,18 @@ class OrcStats(C.Structure):
     ]
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(ORACLE_LIB):
+def lib(path=None):
+    """The oracle library (default: oracle/liblego_oracle.so, the parity build); `path` loads another
+    build of the same source (bench.py's -O3 -march=native cpu_baseline build)."""
+    path = path or ORACLE_LIB
+    if path not in _libs:
+        if path == ORACLE_LIB and not os.path.exists(ORACLE_LIB):
             import subprocess
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
-        L = C.CDLL(ORACLE_LIB)
+        L = C.CDLL(path)
         vp = C.c_void_p
         L.orc_solve.argtypes = [C.c_int, C.c_int32, vp, vp, C.c_int32, vp, C.c_int64, vp, vp, vp, vp, vp,
                                 C.c_int32, vp, C.POINTER(OrcOptions), vp, vp, vp, vp, vp, C.c_int32,
@@ -59,8 +62,8 @@ def lib():
         L.orc_pcg_solve.argtypes = [vp, C.c_int, vp, vp, C.c_double, C.c_int]
         L.orc_pcg_solve.restype = C.c_int
         L.orc_edge_eval.argtypes = [vp] * 5 + [C.c_double] + [vp] * 6
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _p(a):
@@ -69,12 +72,12 @@ def _p(a):
 
 def options(max_iters=10, max_trials=10, strategy=0, huber_delta=5.991, stop_dchi2=1e-5, tau=1e-5,
             lambda_cap=5e10, lambda_init=-1.0, verbose=0, n_threads=0, gate_mode=0, linear_solver=0,
-            pcg_max_iters=0, pcg_tol=1e-6):
+            pcg_max_iters=0, pcg_tol=1e-6, degenerate_guard=0):
     return OrcOptions(max_iters, max_trials, strategy, verbose, n_threads, gate_mode, huber_delta, stop_dchi2,
-                      tau, lambda_cap, lambda_init, linear_solver, pcg_max_iters, pcg_tol)
+                      tau, lambda_cap, lambda_init, linear_solver, pcg_max_iters, pcg_tol, degenerate_guard, 0)
 
 
-def solve(w, variant=1, trace_cap=64, **opt):
+def solve(w, variant=1, trace_cap=64, lib_path=None, **opt):
     """Run the oracle on window dict `w` (lego_ba.generate_window layout)."""
     a = lambda k, dt: None if w.get(k) is None else np.ascontiguousarray(w[k], dtype=dt)
     pose, lm = a("pose_Tcw", np.float64), a("lm_xyz", np.float64)
@@ -86,7 +89,7 @@ def solve(w, variant=1, trace_cap=64, **opt):
                trace_chi2=np.zeros(trace_cap), trace_lambda=np.zeros(trace_cap))
     st = OrcStats()
     o = options(**opt)
-    rc = lib().orc_solve(variant, P, _p(pose), _p(fixed), L, _p(lm), O, _p(op), _p(ol), _p(oc), _p(uv), _p(K),
+    rc = lib(lib_path).orc_solve(variant, P, _p(pose), _p(fixed), L, _p(lm), O, _p(op), _p(ol), _p(oc), _p(uv), _p(K),
                          0 if ext is None else ext.shape[0], _p(ext), C.byref(o), _p(out["pose_Tcw"]),
                          _p(out["lm_xyz"]), _p(out["edge_robust_chi2"]), _p(out["trace_chi2"]),
                          _p(out["trace_lambda"]), trace_cap, C.byref(st))

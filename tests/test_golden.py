@@ -109,6 +109,7 @@ def test_gpu_matches_golden(path):
         assert g["iterations"] == int(z["out_iterations"]) and g["trials"] == int(z["out_trials"])
         assert rel(g["chi2_final"], float(z["out_chi2_final"])) < 1e-6
         assert np.allclose(g["pose_Tcw"], z["out_pose_Tcw"], atol=1e-6)
+        assert np.allclose(g["lm_xyz"], z["out_lm_xyz"], atol=1e-6)
         # per-edge rho0 "as last evaluated" (App. B4).  After an all-rejected exit that is a rejected
         # candidate whose landmark part is an undamped step (lambda only touches the pose diagonal,
         # problem.cpp:408-418) through H_ll built with the outlier gate (base_edge.cpp:55), whose

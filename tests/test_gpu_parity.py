@@ -136,6 +136,7 @@ def test_full_solve_parity_stable(solver, cfg, seed):
     assert rel(g["chi2_final"], o["chi2_final"]) < 1e-6
     assert rel(g["trace_chi2"][1], o["trace_chi2"][1]) < 1e-9      # after the first (bitwise-linearised) step
     assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-6)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-6)
 
 
 @pytest.mark.parametrize("cfg,seed", [("C1", 1), ("mini", 0), ("C2", 1), ("C2", 2)])
@@ -337,3 +338,114 @@ def test_landmark_seen_by_17_poses_is_unsupported():
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.Solver().solve(w)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
+
+
+# ---------------------------------------------------------------------------------------------
+# The reference's live configuration (survey-default family: free gauge, 2 % outliers, left image
+# only).  Most such windows are not reproducible even by the reference under a change of summation
+# order (tests/windows.py, DESIGN.md 4.2: the Huber gate's rounding residue, and landmarks that run
+# off to ~1e15 along their viewing rays).  These seeds are: the oracle's final chi2 moves < 1e-12
+# across OpenMP thread counts, with the reference gate (gate 0) or with the residue taken as 0
+# (gate 1, the diagnostic mode on both sides).  On them the full solve is held to the north-star bar.
+# ---------------------------------------------------------------------------------------------
+DEFAULT_REPRODUCIBLE = [("mini", 2, 0), ("mini", 6, 0), ("C1", 5, 1), ("C1", 6, 1), ("mini", 1, 1), ("mini", 4, 1),
+                        ("mini", 11, 1), ("C2", 0, 1), ("C2", 10, 1)]
+
+
+@pytest.mark.parametrize("cfg,seed,gate", DEFAULT_REPRODUCIBLE)
+def test_full_solve_parity_survey_default(cfg, seed, gate):
+    w = window(cfg, seed=seed)
+    assert w.get("pose_fixed") is None and not np.any(w["obs_cam"])   # gauge free, left image only
+    o, spread, its = oracle_envelope(w, threads=(1, 2, 8), gate_mode=gate)
+    assert spread < 1e-12, f"oracle not reproducible (spread {spread:.1e})"
+    g = lego_ba.Solver(gate_mode=gate).solve(w)
+    assert g["iterations"] in its and g["trials"] == o["trials"]
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-6
+    assert np.allclose(g["trace_chi2"], o["trace_chi2"], rtol=1e-6)
+    # the gauge is held only by lambda: states agree to the trajectory's own sensitivity
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-5)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], rtol=1e-5, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------------------------
+# Landmarks with a single edge: rank-2 H_ll.  In the live pipeline every freshly
+# triangulated landmark has one usable (left) observation.
+# ---------------------------------------------------------------------------------------------
+def k1_window(seed, family):
+    w = window("mini", seed=seed, family=family, pose_mode=1, k_min=1, k_max=8)
+    k = np.bincount(w["obs_lm"], minlength=len(w["lm_xyz"]))
+    assert np.sum(k == 1) > 20
+    return w, int(np.sum(k == 1))
+
+
+@pytest.mark.parametrize("seed,family", [(0, "stable_noout"), (1, "default"), (2, "stable")])
+def test_single_edge_landmarks_reference_semantics(seed, family):
+    """degenerate_guard 0: the reference inverts each rank-2 H_ll with PartialPivLU
+    (problem.cpp:396-400).  Some of those inverses are inf, which makes S and every step NaN: the
+    reference's solve rejects every trial (2 iterations x 10 trials, states and chi2 unchanged).  The
+    solver reproduces that outcome exactly (it poisons the step on any single-edge landmark)."""
+    w, nk1 = k1_window(seed, family)
+    o = ob.solve(w)
+    assert o["accepted"] == 0 and o["iterations"] == 2 and o["trials"] == 20   # the reference stalls
+    g = lego_ba.Solver().solve(w)
+    assert g["degenerate"] >= nk1
+    assert (g["iterations"], g["trials"], g["accepted"]) == (o["iterations"], o["trials"], o["accepted"])
+    assert g["chi2_final"] == g["chi2_initial"] and rel(g["chi2_final"], o["chi2_final"]) < 1e-13
+    assert np.array_equal(g["pose_Tcw"], w["pose_Tcw"]) and np.array_equal(g["lm_xyz"], w["lm_xyz"])
+    assert np.array_equal(g["edge_robust_chi2"], o["edge_robust_chi2"])
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_single_edge_landmarks_guard(seed):
+    """degenerate_guard 1 (opt-in deviation): single-edge landmarks are held fixed (no Schur term, no
+    update) and the solve proceeds; the oracle restates the same guard."""
+    w, nk1 = k1_window(seed, "stable_noout")
+    o, spread, its = oracle_envelope(w, threads=(1, 2, 8), degenerate_guard=1)
+    assert spread < 1e-12 and o["accepted"] > 0
+    g = lego_ba.Solver(degenerate_guard=1).solve(w)
+    assert g["degenerate"] == nk1
+    assert g["iterations"] in its and g["trials"] == o["trials"]
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-6
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-6)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-6)
+    k = np.bincount(w["obs_lm"], minlength=len(w["lm_xyz"]))
+    assert np.array_equal(g["lm_xyz"][k == 1], w["lm_xyz"][k == 1])   # held fixed
+    # one trial at the per-linearisation bar
+    g1 = lego_ba.Solver(degenerate_guard=1, max_iters=1, max_trials=1).solve(w)
+    o1 = ob.solve(w, degenerate_guard=1, max_iters=1, max_trials=1)
+    assert rel(g1["chi2_final"], o1["chi2_final"]) < 1e-9
+    assert np.allclose(g1["pose_Tcw"], o1["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g1["lm_xyz"], o1["lm_xyz"], atol=1e-7)
+
+
+# ---------------------------------------------------------------------------------------------
+# C4 (BASELINE configs[3]): 20 KF / 500 k landmarks / 4 M observations, the multi-GPU window, here
+# on one GPU against the oracle.
+# ---------------------------------------------------------------------------------------------
+def test_c4_window_one_gpu_parity():
+    w = window("C4", seed=0, family="stable_noout")
+    assert len(w["obs_pose"]) == 4_000_000
+    g = lego_ba.Solver().solve(w)
+    o, spread, its = oracle_envelope(w, threads=(8, 16))
+    assert g["iterations"] in its
+    assert rel(g["chi2_final"], o["chi2_final"]) < max(1e-6, 10 * spread)
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-6)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-6)
+    assert np.all(np.diff(g["trace_chi2"]) <= 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# The per-trial exchange must issue the same number of collectives on every rank: the stop trial is
+# decided by identical all-reduced data, and each rank tops up to min(stop trial + depth, cap).
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("depth", [1, 2, 5])
+def test_collective_count_is_a_function_of_the_stop_trial(monkeypatch, depth):
+    monkeypatch.setenv("LH_FORCE_RCCL", "1")
+    w = window("C2", seed=0, family="stable_noout")
+    s = lego_ba.Solver(trials_per_sync=depth)
+    counts = set()
+    for _ in range(3):
+        r = s.solve(w)
+        counts.add(s.comm_count())
+    assert counts == {1 + min(r["trials"] + depth, 100)}
+    s.close()

@@ -1,0 +1,144 @@
+"""CPU tests of the window planner (lego-slam_amd/csrc/lh_plan.cpp through liblego_plan.so): the
+host preprocessing lh_upload does before its copies.  The plan is the device layout every kernel
+trusts (DESIGN.md "Data layout"): each observation in exactly one slot of its landmark's aligned lane
+group, meta words consistent with the window, chunk windows within the MFMA envelope, and the reduce
+plan covering every (chunk, pose pair) block once, in launch order.  It must not depend on the
+thread count or on the order the caller lists observations in (the reference's is hash order,
+problem.cpp:285)."""
+import numpy as np
+import pytest
+
+import lego_ba
+from windows import window
+
+META_VALID = 1 << 23
+
+
+def check_plan(w, pl):
+    O = len(w["obs_pose"])
+    L = len(w["lm_xyz"])
+    P = w["n_poses"]
+    meta, perm = pl["meta"], pl["obs_perm"]
+    valid = (meta & META_VALID) != 0
+    # every observation in exactly one slot, padding slots marked invalid
+    assert np.array_equal(np.sort(perm[valid]), np.arange(O))
+    assert np.all(perm[~valid] == -1)
+    o = perm[valid]
+    m = meta[valid]
+    assert np.array_equal(m & 0xFFF, w["obs_pose"][o])
+    assert np.array_equal((m >> 12) & 0xF, w["obs_cam"][o])
+    assert np.array_equal(pl["uv"][valid], w["obs_uv"][o])
+    # landmark records: each landmark with an edge exactly once
+    lp = pl["lm_perm"]
+    has_edge = np.bincount(w["obs_lm"], minlength=L) > 0
+    assert np.array_equal(np.sort(lp[lp >= 0]), np.flatnonzero(has_edge))
+    # slot -> (sub-batch, landmark-in-sub-batch): the landmark's aligned lane group
+    slots = np.flatnonzero(valid)
+    sb = slots // 64
+    lms = (m >> 20) & 0x7
+    lg = pl["sbs"]["lg"][sb]
+    assert np.all((slots % 64) >> lg == lms)
+    assert np.array_equal(lp[sb * 8 + lms], w["obs_lm"][o])
+    assert np.all(lms < pl["sbs"]["n_lm"][sb])
+    # a landmark's observations in ascending pose order within its group
+    key = sb * 8 + lms
+    same = key[1:] == key[:-1]
+    assert np.all(w["obs_pose"][o][1:][same] > w["obs_pose"][o][:-1][same])
+    # chunks: window poses, T = ceil(6U / 16), grouped by T in launch order
+    ch = pl["chunks"]
+    assert np.all(ch["U"] <= 16) and np.all(ch["T"] == (6 * ch["U"].astype(int) + 15) // 16)
+    assert np.all(np.diff(ch["T"].astype(int)) >= 0)
+    tg = pl["tgroup_begin"]
+    for T in range(1, 7):
+        assert np.all(ch["T"][tg[T]:tg[T + 1]] == T)
+    chunk_of_sb = np.repeat(np.arange(len(ch)), ch["sb_end"] - ch["sb_begin"])
+    assert np.array_equal(ch["sb_begin"][1:], ch["sb_end"][:-1]) and ch["sb_end"][-1] == len(pl["sbs"])
+    c = chunk_of_sb[sb]
+    window_slot = (m >> 16) & 0xF
+    assert np.array_equal(ch["pose"][c, window_slot], w["obs_pose"][o])
+    # reduce plan: one item per (chunk, pose pair of its window), per pair in launch order
+    items, ptr, pq = pl["items"].astype(np.int64), pl["pair_ptr"].astype(np.int64), pl["pair_pq"]
+    assert len(pq) == P * (P + 1) // 2 and ptr[-1] == len(items)
+    expect = sum(int(u) * (int(u) + 1) // 2 for u in ch["U"])
+    assert len(items) == expect
+    for b in range(len(pq)):
+        it = items[ptr[b]:ptr[b + 1]]
+        ci, s, t = it >> 11, (it >> 4) & 15, it & 15
+        assert np.all(np.diff(ci) > 0)
+        assert np.all(ch["pose"][ci, s] == pq[b, 0]) and np.all(ch["pose"][ci, t] == pq[b, 1])
+    assert np.array_equal(pl["lm_xyz"], w["lm_xyz"])
+
+
+@pytest.mark.parametrize("cfg,seed,kw", [("C1", 0, {}), ("mini", 1, {}), ("C2", 2, {}),
+                                         ("C2", 3, dict(pose_mode=1, k_min=2, k_max=10)),
+                                         ("mini", 4, dict(pose_mode=1, k_min=1, k_max=16))])
+def test_plan_invariants(cfg, seed, kw):
+    w = window(cfg, seed=seed, **kw)
+    pl = lego_ba.plan_window(w, threads=3)
+    check_plan(w, pl)
+
+
+def test_plan_independent_of_threads_and_observation_order():
+    w = window("C2", seed=1, pose_mode=1, k_min=2, k_max=12)
+    a = lego_ba.plan_window(w, threads=1)
+    b = lego_ba.plan_window(w, threads=6)
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+    perm = np.random.default_rng(3).permutation(len(w["obs_pose"]))
+    w2 = dict(w)
+    for k in ("obs_pose", "obs_lm", "obs_cam", "obs_uv"):
+        w2[k] = w[k][perm]
+    c = lego_ba.plan_window(w2, threads=4)
+    check_plan(w2, c)
+    # identical layout; the slot -> observation map goes through the permutation
+    for k in ("chunks", "sbs", "meta", "uv", "lm_perm", "items", "pair_ptr"):
+        assert np.array_equal(a[k], c[k]), k
+    v = a["obs_perm"] >= 0
+    assert np.array_equal(perm[c["obs_perm"][v]], a["obs_perm"][v])
+
+
+@pytest.mark.parametrize("chunk_lm", [8, 24, 64, 200])
+def test_plan_chunk_size_option(chunk_lm):
+    w = window("mini", seed=2)
+    pl = lego_ba.plan_window(w, chunk_lm=chunk_lm, threads=2)
+    check_plan(w, pl)
+    per_chunk = [int((pl["sbs"]["n_lm"][s:e]).sum()) for s, e in zip(pl["chunks"]["sb_begin"], pl["chunks"]["sb_end"])]
+    assert max(per_chunk) <= chunk_lm
+
+
+def test_plan_envelope_and_errors():
+    w = window("C1", seed=0)
+    dup = dict(w)
+    for k in ("obs_pose", "obs_lm", "obs_cam", "obs_uv"):
+        dup[k] = np.concatenate([w[k], w[k][:1]])
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(dup)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # two edges landmark -> same pose
+    bad = dict(w, obs_lm=w["obs_lm"].copy())
+    bad["obs_lm"][3] = len(w["lm_xyz"])
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(bad)
+    assert e.value.status == lego_ba.LH_E_BADARG
+    empty = dict(w)
+    for k in ("obs_pose", "obs_lm", "obs_cam", "obs_uv"):
+        empty[k] = w[k][:0]
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(empty)
+    assert e.value.status == lego_ba.LH_E_EMPTY                 # problem.cpp:157-161
+    wide = lego_ba.generate_window(P=20, L=50, k=17, seed=1, pose_mode=1)
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(wide)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > 16 poses per landmark
+    p22 = lego_ba.generate_window(P=22, L=50, k=8, seed=1)
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(p22)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > LH_PMAX poses
+
+
+def test_plan_unobserved_landmarks_and_fixed_mask():
+    w = window("C1", seed=1, family="stable")
+    w["lm_xyz"] = np.vstack([w["lm_xyz"], [[1.0, 2.0, 3.0]], w["lm_xyz"][:2]])
+    pl = lego_ba.plan_window(w)
+    check_plan(w, pl)
+    assert pl["fixed_mask"] == 1
+    assert np.all(np.isin(np.arange(len(w["lm_xyz"]) - 3, len(w["lm_xyz"])), pl["lm_perm"], invert=True))
