@@ -36,6 +36,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFS = 78.6       # MI355X FP64 spec (vector = matrix); measured on the box:
                            # v_mfma_f64_16x16x4 72.0 TF, v_fma_f64 60.5 TF (lego-slam_amd/tools/ubench_fp64_peak.hip)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_k_lin.json")
+ROCPROF_K_LIN = os.path.join(ROOT, "profiles", "r02_rocprof_k_lin.json")
 WORKLOADS = {"C3": dict(P=20, L=50_000, k=8), "C4": dict(P=20, L=500_000, k=8)}
 
 
@@ -64,8 +65,34 @@ def pmc_traffic(cfg_key):
     return d.get("bytes_per_launch") if d.get("workload") == cfg_key else None
 
 
+def cgroup_cpus():
+    """CPUs this process may actually use per the cgroup CPU quota (cpu.max: "quota period"), or
+    None without a quota.  A GPU box exposes every core of the host in its affinity mask (256)
+    but grants the job a share of them through the quota."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, -(-int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_info():
-    """The host the CPU baseline ran on: core counts and CPU model."""
+    """The host the CPU baseline ran on: core counts and CPU model, and the
+    thread count the baseline uses: every CPU this process may use (affinity mask capped by the
+    cgroup quota; without a quota, by OMP_NUM_THREADS when the job sets one)."""
     model = platform.processor() or ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -79,7 +106,15 @@ def host_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return {"nproc": os.cpu_count(), "cpus_available": avail, "cpu_model": model}
+    quota = cgroup_cpus()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    usable = avail
+    if quota is not None:
+        usable = min(usable, quota)
+    elif omp and omp.isdigit() and int(omp) > 0:
+        usable = min(usable, int(omp))
+    return {"nproc": os.cpu_count(), "cpus_in_affinity_mask": avail, "cgroup_cpu_quota": quota,
+            "omp_num_threads_env": omp, "cpus_usable": usable, "cpu_model": model}
 
 
 def native_oracle():
@@ -131,6 +166,17 @@ def time_solves(solver, steps, barrier):
     return time.perf_counter() - t0, it, tr, res
 
 
+def rocprof_k_lin(cfg_key):
+    """k_lin durations from the committed rocprofv3 kernel trace of this bench (scripts/rocprof_k_lin.py):
+    the same back-to-back replays the live timing uses, and the launches inside the timed solves."""
+    try:
+        with open(ROCPROF_K_LIN) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return d if d.get("workload") == cfg_key else None
+
+
 def roofline(solver, n_obs, n_lm, k, cfg_key, reps=50):
     """k_lin (the dominant kernel; one launch = one LM trial's linearise / back-substitute / chi2 pass)
     against the FP64 peak: SURVEY 8(d) flops per iteration / k_lin's duration, the latter measured by
@@ -142,11 +188,19 @@ def roofline(solver, n_obs, n_lm, k, cfg_key, reps=50):
     tfs = flops / (ms * 1e-3) / 1e12
     gbs = nbytes / (ms * 1e-3) / 1e9
     traffic = pmc_traffic(cfg_key)
-    return ({"bound": "mfma", "achieved": round(tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-             "frac": round(tfs / FP64_PEAK_TFS, 4), "traffic": traffic, "kernel": "k_lin",
-             "avg_launch_ms": round(ms, 5), "timing": f"{reps} back-to-back replays between HIP events",
-             "flops_per_launch": flops,
-             "peak_note": "FP64 spec (vector = matrix); measured here 72.0 TF MFMA, 60.5 TF VALU"},
+    rl = {"bound": "mfma", "achieved": round(tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+          "frac": round(tfs / FP64_PEAK_TFS, 4), "traffic": traffic, "kernel": "k_lin",
+          "avg_launch_ms": round(ms, 5), "timing": f"{reps} back-to-back replays between HIP events on the solver's stream",
+          "flops_per_launch": flops,
+          "peak_note": "FP64 spec (vector = matrix); measured here 72.0 TF MFMA, 60.5 TF VALU"}
+    rp = rocprof_k_lin(cfg_key)
+    if rp:
+        # the committed kernel trace of the same command: its replay launches (must agree with
+        # avg_launch_ms) and the k_lin launches inside the solves (after k_ctrl, a few us slower)
+        rl["rocprof_replay_avg_ms"] = round(rp["replay_avg_us"] * 1e-3, 5)
+        rl["rocprof_in_solve_avg_ms"] = round(rp["in_solve_avg_us"] * 1e-3, 5)
+        rl["frac_in_solve_rocprof"] = round(flops / (rp["in_solve_avg_us"] * 1e-6) / 1e12 / FP64_PEAK_TFS, 4)
+    return (rl,
             {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes, "traffic": traffic})
 
@@ -333,7 +387,7 @@ def main():
         import oracle_bind
         lib_path, flags = native_oracle()
         hi = host_info()
-        threads = hi["cpus_available"]
+        threads = hi["cpus_usable"]
         o = oracle_bind.solve(w, n_threads=threads, lib_path=lib_path)   # warm-up
         t0 = time.perf_counter()
         its = nsolve = 0
@@ -347,7 +401,8 @@ def main():
         out["cpu_baseline"] = {"value": round(its / ct, 4), "unit": "LM iterations/s", "cores": threads, "kind": "port",
                                "sample": f"{nsolve} full solve(10)s of the same C3 window by the block-sparse oracle "
                                          f"(oracle/lego_oracle.c ref_sparse, gcc {flags}, OpenMP {threads} threads = "
-                                         f"every CPU available to this process), {ct:.1f} s, {its} iterations",
+                                         f"every CPU this process may use: affinity mask capped by the cgroup "
+                                         f"quota), {ct:.1f} s, {its} iterations",
                                "host": hi}
         out["chi2_rel_vs_oracle"] = abs(last["chi2_final"] - o["chi2_final"]) / o["chi2_final"]
         op = oracle_bind.solve(w, n_threads=threads)

@@ -26,18 +26,17 @@ Pool::~Pool() {
 void Pool::loop() {
     uint64_t seen = 0;
     for (;;) {
-        const std::function<void(int)>* job;
-        int n;
+        Job* job;
         {
             std::unique_lock<std::mutex> g(mu_);
             cv_.wait(g, [&] { return stop_ || gen_ != seen; });
             if (stop_) return;
             seen = gen_;
             job = job_;
-            n = n_;
+            if (!job) continue;   // woke after run() retired this generation's job
             ++active_;
         }
-        for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) (*job)(i);
+        for (int i = job->next.fetch_add(1); i < job->n; i = job->next.fetch_add(1)) (*job->fn)(i);
         {
             std::lock_guard<std::mutex> g(mu_);
             if (--active_ == 0) done_cv_.notify_all();
@@ -51,20 +50,22 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
         for (int i = 0; i < n; ++i) fn(i);
         return;
     }
+    Job job;
+    job.fn = &fn;
+    job.n = n;
     {
         std::lock_guard<std::mutex> g(mu_);
-        job_ = &fn;
-        n_ = n;
-        next_.store(0);
+        job_ = &job;
         ++gen_;
     }
     cv_.notify_all();
-    for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) fn(i);
+    for (int i = job.next.fetch_add(1); i < n; i = job.next.fetch_add(1)) fn(i);
     std::unique_lock<std::mutex> g(mu_);
-    // every worker that picked this job up has drained the index range once active_ drops to 0;
-    // a worker that wakes late sees next_ >= n and does nothing
-    done_cv_.wait(g, [&] { return active_ == 0; });
+    // Retire the job under the lock first: a worker joins only while job_ is set (and counts itself
+    // in active_ under the same lock), so once active_ drops to 0 no thread can still touch `job`,
+    // which lives on this stack frame.  A worker that wakes late sees job_ == nullptr.
     job_ = nullptr;
+    done_cv_.wait(g, [&] { return active_ == 0; });
 }
 
 namespace {

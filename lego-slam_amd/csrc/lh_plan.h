@@ -35,13 +35,16 @@ class Pool {
     void run(int n, const std::function<void(int)>& fn);
 
   private:
+    struct Job {
+        const std::function<void(int)>* fn = nullptr;
+        int n = 0;
+        std::atomic<int> next{0};
+    };
     void loop();
     std::vector<std::thread> workers_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    const std::function<void(int)>* job_ = nullptr;
-    int n_ = 0;
-    std::atomic<int> next_{0};
+    Job* job_ = nullptr;   // the live job of generation gen_, nullptr once run() retires it
     int active_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;

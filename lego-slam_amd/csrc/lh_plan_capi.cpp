@@ -79,3 +79,14 @@ int lhp_plan_time(const lh_window* w, int chunk_lm, int threads, int reps, doubl
 }
 
 }  // extern "C"
+
+extern "C" {
+// Pool stress for the CPU suite: `runs` back-to-back small jobs on one persistent pool (late-waking
+// workers must never touch a retired job).  Returns the sum of all indices visited.
+int64_t lhp_pool_stress(int threads, int runs, int n) {
+    lh::Pool pool(threads > 0 ? threads : 1);
+    std::atomic<int64_t> s{0};
+    for (int r = 0; r < runs; ++r) pool.run(n, [&](int i) { s += i; });
+    return s.load();
+}
+}  // extern "C"

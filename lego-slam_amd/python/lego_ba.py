@@ -459,6 +459,8 @@ def _pl():
         lib.lhp_plan_fill.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int] + [vp] * 11
         lib.lhp_plan_time.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]
+        lib.lhp_pool_stress.argtypes = [C.c_int, C.c_int, C.c_int]
+        lib.lhp_pool_stress.restype = C.c_int64
         _planlib = lib
     return _planlib
 
@@ -479,6 +481,11 @@ def plan_window(w, chunk_lm=0, threads=1):
     _check(_pl().lhp_plan_fill(C.byref(ref.s), chunk_lm, threads, *[_ptr(out[n]) for n in k]), "lhp_plan_fill")
     out.update(tgroup_begin=tg, fixed_mask=fixed_mask)
     return out
+
+
+def pool_stress(threads, runs, n):
+    """Sum of every index the planner's worker pool visits over `runs` back-to-back jobs of size n."""
+    return int(_pl().lhp_pool_stress(threads, runs, n))
 
 
 def plan_time_ms(w, chunk_lm=0, threads=1, reps=5):

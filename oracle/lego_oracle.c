@@ -283,22 +283,33 @@ static void ldlt_solve(double *A, int n, const double *b, double *x) {
         if (rs > 0 && valid)
             for (int i = k + 1; i < n; ++i) A_(i, k) /= akk;
     }
-    /* solve */
+    (void)all_zero;   /* Eigen records it (ret = false) but LDLT::_solve_impl still runs both solves */
+    /* LDLT::_solve_impl: dst = P b; L^-1; pseudo-inverse of D; L^-T; P^T.  The triangular solves
+       follow Eigen's triangular_solve_vector in NaN/Inf semantics (for finite data the operations
+       below are bitwise those of a plain column-oriented solve, since x - L*0 == x):
+       - L (unit lower, column-major storage): panels of 8 rows; inside a panel a column whose x
+         is exactly 0 is skipped (not_equal_strict(rhs[i], 0)); rows below the panel take the
+         whole panel by GEMV, zero entries included (0 * NaN = NaN there);
+       - L^T (unit upper, row-major view): dot products, nothing skipped.
+       After an all-NaN S (an inf PartialPivLU inverse makes every S entry NaN through the dense
+       GEMMs, problem.cpp:399-404) this leaves a NaN step, not the zero step a shortcut would. */
     for (int i = 0; i < n; ++i) x[i] = b[i];
     for (int k = 0; k < n; ++k) { int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
-    if (!all_zero) {
-        for (int k = 0; k < n; ++k)
-            for (int i = k + 1; i < n; ++i) x[i] -= A_(i, k) * x[k];
+    for (int p0 = 0; p0 < n; p0 += 8) {
+        const int p1 = p0 + 8 < n ? p0 + 8 : n;
+        for (int k = p0; k < p1; ++k) {
+            if (x[k] != 0.0)
+                for (int i = k + 1; i < p1; ++i) x[i] -= A_(i, k) * x[k];
+            for (int i = p1; i < n; ++i) x[i] -= A_(i, k) * x[k];
+        }
     }
     const double tol = 2.2250738585072014e-308; /* numeric_limits<double>::min() */
     for (int i = 0; i < n; ++i) {
         double d = A_(i, i);
         if (fabs(d) > tol) x[i] /= d; else x[i] = 0.0;
     }
-    if (!all_zero) {
-        for (int k = n - 1; k >= 0; --k)
-            for (int i = 0; i < k; ++i) x[i] -= A_(k, i) * x[k];
-    }
+    for (int k = n - 1; k >= 0; --k)
+        for (int i = 0; i < k; ++i) x[i] -= A_(k, i) * x[k];
     for (int k = n - 1; k >= 0; --k) { int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
 #undef A_
     free(tr);

@@ -96,10 +96,18 @@ def test_two_rank_sharded_solve_matches_one_rank(cfg, seed, family):
     assert a["iterations"] == one["iterations"] and a["trials"] == one["trials"]
     assert rel(a["chi2_initial"], one["chi2_initial"]) < 1e-12
     assert rel(a["chi2_final"], one["chi2_final"]) < 1e-9
-    assert np.allclose(a["pose_Tcw"], one["pose_Tcw"], atol=1e-9)
     L = len(w["lm_xyz"])
     lm = np.vstack([a["lm_xyz"], b["lm_xyz"]])
     assert lm.shape == (L, 3)
-    assert np.allclose(lm, one["lm_xyz"], atol=1e-7)
+    if family.startswith("stable"):
+        assert np.allclose(a["pose_Tcw"], one["pose_Tcw"], atol=1e-9)
+        assert np.allclose(lm, one["lm_xyz"], atol=1e-7)
+    else:
+        # survey-default windows (gauge free, reference Huber gate): summation order moves the
+        # states by as much as the oracle's own reorderings do (tests/align.py)
+        from align import oracle_state_spread
+        _, lm_sp, pose_sp = oracle_state_spread(w, threads=(1, 2, 8))
+        assert np.abs(a["pose_Tcw"] - one["pose_Tcw"]).max() <= max(1e-5, 10 * pose_sp)
+        assert np.abs(lm - one["lm_xyz"]).max() <= max(1e-5, 10 * lm_sp)
     rho = np.concatenate([a["edge_robust_chi2"], b["edge_robust_chi2"]])
     assert rel(rho.sum(), one["edge_robust_chi2"].sum()) < 1e-9

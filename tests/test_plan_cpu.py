@@ -142,3 +142,13 @@ def test_plan_unobserved_landmarks_and_fixed_mask():
     check_plan(w, pl)
     assert pl["fixed_mask"] == 1
     assert np.all(np.isin(np.arange(len(w["lm_xyz"]) - 3, len(w["lm_xyz"])), pl["lm_perm"], invert=True))
+
+
+def test_pool_back_to_back_jobs():
+    """The planner's persistent worker pool runs several jobs per upload back to back.  A worker
+    that wakes after run() has retired a job must never touch it (round-2 GPU segfault: a late
+    worker called through the cleared job pointer with the next job's index counter)."""
+    import lego_ba
+    for n in (2, 3, 17):
+        runs = 20000
+        assert lego_ba.pool_stress(8, runs, n) == runs * n * (n - 1) // 2
