@@ -42,10 +42,22 @@ __device__ unsigned long long lh_stamps[64];
             for (int i_ = 0; i_ < (cnt); ++i_)                                     \
                 if (sacc_[((base) + i_) % 24]) atomicAdd(&lh_stamps[(base) + i_], sacc_[((base) + i_) % 24]); \
     } while (0)
+// k_ctrl wall-clock stamps: thread 0 (wave 0, the critical chain) adds s_memtime at each
+// barrier-aligned phase boundary of every live launch into lh_stamps[32 + i]; consecutive sums
+// difference to per-phase latency.  [61] live launches, [62]/[63] s_memrealtime at start / end.
+#define CSTAMP(i)                                                                  \
+    do {                                                                           \
+        if (threadIdx.x == 0) {                                                    \
+            __builtin_amdgcn_sched_barrier(0);                                     \
+            atomicAdd(&lh_stamps[32 + (i)], (unsigned long long)__builtin_amdgcn_s_memtime()); \
+            __builtin_amdgcn_sched_barrier(0);                                     \
+        }                                                                          \
+    } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_FLUSH(base, cnt)
+#define CSTAMP(i)
 #endif
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -906,9 +918,9 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
 #define CT 1024
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
 #define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
-#define NBLK (LH_NPAD / 8)
 #define RS_MAX (LH_PMAX * (LH_PMAX + 1) / 2 * 36 + 18 * LH_PMAX + 8)
 #define NLD ((RS_MAX + CT - 1) / CT)
+#define NBLK (LH_NPAD / 8)
 
 // Per-block products of the 8x8 diagonal-block factor (LDS, shared by all waves).
 struct LdltBlockLds {
@@ -1142,14 +1154,11 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
     __shared__ __attribute__((aligned(16))) LdltBlockLds F;
-#ifdef LH_STAMPS
-    unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_, sacc_[24] = {0};
-#endif
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     if (wv == 0) factor_block8(A, F.N[0], F.ND[0], 0, lane);
     lds_barrier();
-    STAMP(18);
+    CSTAMP(5);
     for (int k0 = 0; k0 < nb; k0 += 8) {
         const int t = k0 >> 3, par = t & 1, m0 = k0 + 8;
         const double* N = F.N[par];
@@ -1168,7 +1177,6 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 ldlt_tile_row(A, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
                 wave_sync();
                 factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
-                STAMP(12);
             }
             const int gl = (NE >> 4) - 1, R = gl - tg + 1;
             const int u = wave_unit(wv);
@@ -1182,8 +1190,8 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
             }
         }
         lds_barrier();
-        STAMP(16);
     }
+    CSTAMP(6);
 
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
     if (wv == 0) {
@@ -1208,11 +1216,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         if (lane + 64 < NE) xsol[lane + 64] = y1;
     }
     lds_barrier();
-    STAMP(13);
-
-#ifdef LH_STAMPS
-    STAMP_FLUSH(10, 14);
-#endif
+    CSTAMP(7);
 }
 
 // Phases 3-4 of k_ctrl, PCG variant (lh_options.linear_solver = LH_SOLVER_PCG): Jacobi-preconditioned
@@ -1327,7 +1331,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
     const lh_rs_layout LY = lh_rs_make(P);
-    STAMP_DECL
+#ifdef LH_STAMPS
+    const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---------------- 1. prefetch (one round trip); the controller's words first ----------------
     double chi = 0.0, lam = 0.0, ni = 0.0, last = 0.0, spose = 0.0, chi0 = 0.0, tchi = 0.0, sl = 0.0, ndg = 0.0;
@@ -1461,7 +1467,14 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
     if (done) return;
     const double lambda = s_lam;
-    STAMP(17);
+#ifdef LH_STAMPS
+    if (tid == 0) {
+        atomicAdd(&lh_stamps[32], ct_start);
+        atomicAdd(&lh_stamps[61], 1ull);
+        atomicAdd(&lh_stamps[62], rt_start);
+    }
+#endif
+    CSTAMP(1);
 
     // ---------------- 2. commit, diag + lambda, pivot order, scatter into LDS ----------------
 #pragma unroll
@@ -1483,7 +1496,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     if (tid >= n && tid < NP) dg[tid] = __builtin_nan("");   // key -1 at an index above every real row: never counted
     lds_barrier();
-    STAMP(19);
+    CSTAMP(2);
     {
         // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation.
         // Eight threads per row, each counting over 16 of the 128 keys (dg[n..NP) are NaN).
@@ -1512,7 +1525,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
     }
     lds_barrier();
-    STAMP(21);
+    CSTAMP(3);
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
         const int i = u * CT + tid;
@@ -1531,10 +1544,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         if (c < r) A[r * AS + c] = 0.0;
     }
     lds_barrier();
-    STAMP(11);
+    CSTAMP(4);
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
-    STAMP_FLUSH(10, 14);
     if constexpr (SOLVER == 1) {
         const int its = lds_pcg_solve(A, yv, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
         if (tid == 0) ctrl->pcg_iters += its;
@@ -1543,11 +1555,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
     lds_barrier();
-#ifdef LH_STAMPS
-    st0_ = __builtin_amdgcn_s_memtime();
-    for (int i_ = 0; i_ < 24; ++i_) sacc_[i_] = 0;
-#endif
-    STAMP(10);
+    CSTAMP(8);
 
     // ---------------- pose part of the gain denominator; candidate poses ----------------
     double sp = 0.0;
@@ -1584,6 +1592,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         d_q_from_R(Rc, s_qT[lane]);
     }
     lds_barrier();
+    CSTAMP(9);
     if (wave == 0 && lane < P) {
         const int pidx = lane;
         double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
@@ -1602,6 +1611,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
     }
     lds_barrier();
+    CSTAMP(10);
     if (tid < 12 * P) pose_mat[(size_t)cand * P * 12 + tid] = s_pm[cand][tid];
     if (tid >= 64 && tid < 64 + P * prm.ncam) {
         const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
@@ -1611,13 +1621,16 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
     }
     lds_barrier();
+    CSTAMP(11);
     if (tid == 0) {
         double s2 = 0.0;
         for (int w = 0; w < CT / 64; ++w) s2 += s_red[w];
         ctrl->spose = s2;
     }
-    STAMP(14);
-    STAMP_FLUSH(10, 14);
+    CSTAMP(12);
+#ifdef LH_STAMPS
+    if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // ============================================================================

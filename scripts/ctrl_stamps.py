@@ -1,0 +1,36 @@
+"""Diagnostic: k_ctrl latency by phase (thread 0's wall clock at the barrier-aligned phase
+boundaries) from the -DLH_STAMPS build: LH_LIB=lego-slam_amd/lib/liblego_ba_stamps.so.
+The stamps' atomics perturb the kernel a little; shares and orders of magnitude only."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "lego-slam_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import lego_ba  # noqa: E402
+from windows import window  # noqa: E402
+
+NAMES = ["start", "prefetch + LM logic", "commit + diag", "pivot rank", "scatter into LDS", "block 0 factor",
+         "LDLT steps", "back substitution", "dx scatter", "trig / q_T", "pose compose", "pose / table stores", "tail"]
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+w = window(cfg, seed=0, family="stable_noout")
+s = lego_ba.Solver(device=0)
+s.upload(w)
+s.solve_resident()
+lego_ba.debug_stamps(reset=True)
+for _ in range(5):
+    s.solve_resident()
+st = [int(x) for x in lego_ba.debug_stamps(reset=True)]
+n = st[61]
+cyc = [st[32 + i] for i in range(len(NAMES))]
+tot_cyc = (cyc[-1] - cyc[0]) / n
+tot_ns = (st[63] - st[62]) / n * 10.0
+print(f"{cfg}: {n} live k_ctrl launches, {tot_cyc:.0f} cycles = {tot_ns / 1000:.2f} us start-to-end "
+      f"(clock {tot_cyc / tot_ns:.2f} GHz)")
+for i in range(1, len(NAMES)):
+    d = (cyc[i] - cyc[i - 1]) / n
+    print(f"  {NAMES[i]:22s} {d:9.0f} cycles {d / tot_cyc * 100:5.1f}%  {d / (tot_cyc / tot_ns) / 1000:6.2f} us")
+for b, nm in ((49, "steps 0-3"), (45, "steps 4+")):
+    k = max(st[b + 3], 1)
+    print(f"  LDLT {nm}: {k // max(n, 1)} per launch; per step: wave 0 chain {st[b] / k:.0f}, slowest other wave "
+          f"{st[b + 1] / k:.0f}, barrier to barrier {st[b + 2] / k:.0f} cycles")
