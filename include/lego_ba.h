@@ -19,6 +19,7 @@
  *     vertex->getEstimate()        base_vertex.h:34 lh_result.pose_Tcw / lm_xyz
  *     outlier threshold loop       backend_lego.cpp:163-194 lh_classify_outliers
  *     Frontend::EstimateCurrentPose frontend_lego.cpp:157-250 lh_estimate_pose (batched)
+ *     LKOpticalFlow4Layer / 1Layer  algorithm.cpp:11-206      lh_lk_track
  *     ~Problem                     problem.cpp:32 lh_destroy
  *
  * Plain C types only (no torch, Eigen or Sophus in any signature).  No C++
@@ -216,6 +217,40 @@ typedef struct lh_frames_result {
 } lh_frames_result;
 
 int lh_estimate_pose(lh_handle *h, const lh_frames *in, lh_frames_result *out);
+
+/*
+ * Gauss-Newton pyramidal LK optical flow, replacing
+ *   void LKOpticalFlow4Layer(const cv::Mat &img1, const cv::Mat &img2,
+ *                            const std::vector<cv::KeyPoint> &kp1, std::vector<cv::KeyPoint> &kp2,
+ *                            std::vector<bool> &success, bool inverse, bool has_initial)
+ *                                                                      (src/algorithm.cpp:128-206)
+ * (levels = 4) and LKOpticalFlow1Layer (algorithm.cpp:11-31, levels = 1), as the frontend's
+ * *LKOpticalFlow4LayerSelf trackers call them (frontend_lego.cpp:466-556).  Images are 8-bit gray
+ * (CV_8UC1 layout: rows of `step` bytes); keypoints are cv::KeyPoint::pt.  The pyramid is built as
+ * cv::resize(INTER_LINEAR, 0.5) does (exactly for even-sized levels; see oracle/lk_oracle.c).
+ * Semantics as written, including inverse mode's single J variable (from iteration 1 on every
+ * patch pixel uses the last pixel's J, algorithm.cpp:73-78).  kp2 and success are overwritten;
+ * with has_initial, kp2 holds the initial guess on entry.
+ */
+typedef struct lh_lk_input {
+    int32_t cols, rows;         /* level-0 image size                                                */
+    int64_t step;               /* bytes per image row (>= cols)                                      */
+    const uint8_t *img1;        /* [rows][step] previous / left image                                 */
+    const uint8_t *img2;        /* [rows][step] current / right image                                 */
+    int32_t n_points;
+    const float *kp1;           /* [n_points][2] keypoints in img1                                    */
+    int32_t inverse;            /* 0: forward (the frontend's mode), 1: inverse                       */
+    int32_t has_initial;        /* kp2 on entry is the initial guess                                  */
+    int32_t levels;             /* 4 (LKOpticalFlow4Layer) or 1 (LKOpticalFlow1Layer)                  */
+} lh_lk_input;
+
+typedef struct lh_lk_result {
+    float *kp2;                 /* [n_points][2] in: initial guess (has_initial); out: tracked points */
+    uint8_t *success;           /* [n_points] out                                                     */
+    double time_ms;             /* device time: pyramid + tracking (copies excluded)                  */
+} lh_lk_result;
+
+int lh_lk_track(lh_handle *h, const lh_lk_input *in, lh_lk_result *out);
 
 /* ---- test hooks (not part of the reference interface) ---- */
 /* f64 MFMA accumulator-layout probe: D(16x16) = A(16x4) * B(4x16), device pointers, row-major */

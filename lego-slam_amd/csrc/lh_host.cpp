@@ -22,6 +22,7 @@
 
 #include "../../include/lego_ba.h"
 #include "lh_common.h"
+#include "lh_lk.h"
 #include "lh_plan.h"
 
 extern "C" {
@@ -47,6 +48,11 @@ hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double*
                                 int* iters);
 hipError_t lh_launch_mfma_probe(const double* A, const double* B, double* D);
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset);
+hipError_t lh_launch_lk_pyr(hipStream_t st, const uint8_t* src, int sw, int sh, int64_t sstep, uint8_t* dst, int dw,
+                            int dh);
+hipError_t lh_launch_lk_track(hipStream_t st, const lh_lk_levels* L1, const lh_lk_levels* L2, int levels, int n,
+                              const float* kp1, const float* kp2_in, float* kp2_out, uint8_t* success, int inverse,
+                              int has_initial);
 hipError_t lh_launch_frames(hipStream_t st, int n_frames, const int64_t* obs_ptr, const double* pose_in,
                             const double* pts, const double* uv, const uint8_t* flag_in, lh_params prm, double* res,
                             double* pose_out, uint8_t* flag_out, double* rchi2_out, int32_t* iters_out,
@@ -238,6 +244,9 @@ struct lh_handle {
     DevBuf<double> f_pose_in, f_pts, f_uv, f_res, f_pose_out, f_rchi2;
     DevBuf<uint8_t> f_flag_in, f_flag_out;
     DevBuf<int32_t> f_iters, f_inl;
+    // LK optical flow (lh_lk_track): both images' pyramids, keypoints
+    DevBuf<uint8_t> k_img[2], k_succ;
+    DevBuf<float> k_kp1, k_kp2;
     lh_ctrl* h_ctrl = nullptr;   // pinned
     int* h_done = nullptr;       // pinned, mapped: [0] k_ctrl raises it when the LM loop stops, [1] progress
     int* d_done = nullptr;       // device alias of h_done
@@ -794,6 +803,7 @@ void lh_destroy(lh_handle* h) {
     h->f_ptr.release(); h->f_pose_in.release(); h->f_pts.release(); h->f_uv.release(); h->f_res.release();
     h->f_pose_out.release(); h->f_rchi2.release(); h->f_flag_in.release(); h->f_flag_out.release();
     h->f_iters.release(); h->f_inl.release();
+    h->k_img[0].release(); h->k_img[1].release(); h->k_succ.release(); h->k_kp1.release(); h->k_kp2.release();
     h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release(); h->d_obs_perm.release(); h->d_lm_perm.release();
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
@@ -914,6 +924,75 @@ int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
     if (out->edge_chi2 && O > 0) HIPCHK(down(out->edge_chi2, h->f_rchi2.p, sizeof(double) * (size_t)O));
     if (out->n_inliers) HIPCHK(down(out->n_inliers, h->f_inl.p, sizeof(int32_t) * (size_t)F));
     if (out->iterations) HIPCHK(down(out->iterations, h->f_iters.p, sizeof(int32_t) * (size_t)F));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    out->time_ms = ms;
+    h->event_next = 0;
+    return LH_OK;
+}
+
+// LKOpticalFlow4Layer / LKOpticalFlow1Layer (algorithm.cpp:11-206): upload both images, build the
+// pyramids (k_lk_pyr per level and image), track every keypoint (k_lk_track), download.
+int lh_lk_track(lh_handle* h, const lh_lk_input* in, lh_lk_result* out) {
+    if (!h || !in || !out) return LH_E_BADARG;
+    if (in->levels != 1 && in->levels != LH_LK_MAX_LEVELS) return LH_E_BADARG;
+    if (in->cols < 1 || in->rows < 1 || in->step < in->cols || in->n_points < 0) return LH_E_BADARG;
+    if (!in->img1 || !in->img2) return LH_E_BADARG;
+    const int n = in->n_points;
+    if (n > 0 && (!in->kp1 || !out->kp2 || !out->success)) return LH_E_BADARG;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    // level sizes: cv::Size(cols * 0.5, rows * 0.5) truncated (algorithm.cpp:146-153)
+    int cols[LH_LK_MAX_LEVELS], rows[LH_LK_MAX_LEVELS];
+    int64_t step[LH_LK_MAX_LEVELS], off[LH_LK_MAX_LEVELS];
+    cols[0] = in->cols; rows[0] = in->rows; step[0] = in->step; off[0] = 0;
+    int64_t total = (int64_t)in->rows * in->step;
+    for (int l = 1; l < in->levels; ++l) {
+        cols[l] = (int)(cols[l - 1] * 0.5);
+        rows[l] = (int)(rows[l - 1] * 0.5);
+        if (cols[l] < 1 || rows[l] < 1) return LH_E_BADARG;
+        step[l] = cols[l];
+        off[l] = total;
+        total += (int64_t)cols[l] * rows[l];
+    }
+    hipStream_t s = h->stream;
+    HIPCHK(h->k_img[0].ensure((size_t)total));
+    HIPCHK(h->k_img[1].ensure((size_t)total));
+    HIPCHK(h->k_kp1.ensure(2 * (size_t)std::max(n, 1)));
+    HIPCHK(h->k_kp2.ensure(2 * (size_t)std::max(n, 1)));
+    HIPCHK(h->k_succ.ensure((size_t)std::max(n, 1)));
+    const size_t img_bytes = (size_t)in->rows * (size_t)in->step;
+    HIPCHK(hipMemcpyAsync(h->k_img[0].p, in->img1, img_bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->k_img[1].p, in->img2, img_bytes, hipMemcpyHostToDevice, s));
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(h->k_kp1.p, in->kp1, 2 * sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
+        // without an initial guess kp2 is scaled but never read (dx = dy = 0 at the top level)
+        if (in->has_initial) HIPCHK(hipMemcpyAsync(h->k_kp2.p, out->kp2, 2 * sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
+        else HIPCHK(hipMemsetAsync(h->k_kp2.p, 0, 2 * sizeof(float) * (size_t)n, s));
+    }
+    lh_lk_levels L[2];
+    for (int im = 0; im < 2; ++im)
+        for (int l = 0; l < LH_LK_MAX_LEVELS; ++l) {
+            const int ll = l < in->levels ? l : 0;
+            L[im].data[l] = h->k_img[im].p + off[ll];
+            L[im].cols[l] = cols[ll];
+            L[im].rows[l] = rows[ll];
+            L[im].step[l] = step[ll];
+        }
+    hipEvent_t e0 = next_event(h), e1 = next_event(h);
+    if (!e0 || !e1) return LH_E_HIP;
+    HIPCHK(hipEventRecord(e0, s));
+    for (int l = 1; l < in->levels; ++l)
+        for (int im = 0; im < 2; ++im)
+            HIPCHK(lh_launch_lk_pyr(s, L[im].data[l - 1], cols[l - 1], rows[l - 1], step[l - 1],
+                                    h->k_img[im].p + off[l], cols[l], rows[l]));
+    HIPCHK(lh_launch_lk_track(s, &L[0], &L[1], in->levels, n, h->k_kp1.p, h->k_kp2.p, h->k_kp2.p, h->k_succ.p,
+                              in->inverse ? 1 : 0, in->has_initial ? 1 : 0));
+    HIPCHK(hipEventRecord(e1, s));
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(out->kp2, h->k_kp2.p, 2 * sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(out->success, h->k_succ.p, (size_t)n, hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));

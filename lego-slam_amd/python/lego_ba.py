@@ -177,6 +177,18 @@ class LhFramesResult(C.Structure):
     ]
 
 
+class LhLkInput(C.Structure):
+    _fields_ = [
+        ("cols", C.c_int32), ("rows", C.c_int32), ("step", C.c_int64), ("img1", C.c_void_p), ("img2", C.c_void_p),
+        ("n_points", C.c_int32), ("kp1", C.c_void_p), ("inverse", C.c_int32), ("has_initial", C.c_int32),
+        ("levels", C.c_int32),
+    ]
+
+
+class LhLkResult(C.Structure):
+    _fields_ = [("kp2", C.c_void_p), ("success", C.c_void_p), ("time_ms", C.c_double)]
+
+
 class LhKernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64 * 8), ("total_ms", C.c_double * 8)]
 
@@ -186,7 +198,7 @@ ABI_SYMBOLS = [
     "lh_strerror", "lh_default_options", "lh_kernel_name", "lh_comm_unique_id",
     "lh_create", "lh_destroy", "lh_solve", "lh_upload", "lh_solve_resident",
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
-    "lh_estimate_pose",
+    "lh_estimate_pose", "lh_lk_track",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
     "lh_debug_time_lin", "lh_debug_comm_count",
 ]
@@ -216,6 +228,7 @@ def ba_lib():
         lib.lh_kernel_stats_reset.argtypes = [C.c_void_p]
         lib.lh_set_profiling.argtypes = [C.c_void_p, C.c_int]
         lib.lh_estimate_pose.argtypes = [C.c_void_p, C.POINTER(LhFrames), C.POINTER(LhFramesResult)]
+        lib.lh_lk_track.argtypes = [C.c_void_p, C.POINTER(LhLkInput), C.POINTER(LhLkResult)]
         lib.lh_classify_outliers.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p, C.c_void_p]
         lib.lh_debug_event_floor.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
@@ -354,6 +367,30 @@ class Solver:
         r, out = self._result(s.n_poses, s.n_landmarks, s.n_obs, trace_cap, want_states, want_edges)
         _check(ba_lib().lh_solve_resident(self.h, C.byref(r)), "lh_solve_resident")
         return self._finish(r, out)
+
+    def lk_track(self, img1, img2, kp1, kp2_init=None, inverse=False, levels=4):
+        """LKOpticalFlow4Layer (levels=4) / LKOpticalFlow1Layer (levels=1) of algorithm.cpp on 8-bit
+        images (2-D uint8 arrays, rows contiguous).  Returns kp2 [n, 2] float32, success [n] bool and
+        the device time."""
+        i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+        i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+        if i1.shape != i2.shape or i1.ndim != 2:
+            raise ValueError("images must be 2-D uint8 arrays of one shape")
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32).reshape(-1, 2)
+        n = k1.shape[0]
+        k2 = (np.zeros((n, 2), np.float32) if kp2_init is None
+              else np.array(kp2_init, dtype=np.float32, copy=True).reshape(-1, 2))
+        ok = np.zeros(n, np.uint8)
+        a = LhLkInput()
+        a.rows, a.cols = i1.shape
+        a.step = i1.strides[0]
+        a.img1, a.img2 = _ptr(i1), _ptr(i2)
+        a.n_points, a.kp1 = n, _ptr(k1)
+        a.inverse, a.has_initial, a.levels = int(bool(inverse)), int(kp2_init is not None), int(levels)
+        r = LhLkResult()
+        r.kp2, r.success = _ptr(k2), _ptr(ok)
+        _check(ba_lib().lh_lk_track(self.h, C.byref(a), C.byref(r)), "lh_lk_track")
+        return dict(kp2=k2, success=ok.astype(bool), time_ms=r.time_ms)
 
     def estimate_pose(self, fb, is_outlier_in=None):
         """Frontend::EstimateCurrentPose on every frame of batch `fb` (obs_ptr CSR, pose_Tcw, pts,

@@ -207,3 +207,33 @@ def edge_eval(T12, X, uv, K, ext12=None, huber_delta=5.991):
     lib().orc_edge_eval(f(T12), f(X), f(uv), f(K), f(ext12), huber_delta, _p(r), _p(Jp), _p(Jl), _p(W),
                         C.byref(drho), C.byref(rc))
     return dict(r=r, Jp=Jp.reshape(2, 6), Jl=Jl.reshape(2, 3), W=W.reshape(2, 2), drho=drho.value, rchi2=rc.value)
+
+
+def lk_track(img1, img2, kp1, kp2_init=None, inverse=False, levels=4):
+    """orc_lk_track: the restated LKOpticalFlow4Layer / 1Layer (oracle/lk_oracle.c)."""
+    L = lib()
+    L.orc_lk_track.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
+                               C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+    L.orc_lk_track.restype = C.c_int
+    i1 = np.ascontiguousarray(img1, dtype=np.uint8)
+    i2 = np.ascontiguousarray(img2, dtype=np.uint8)
+    k1 = np.ascontiguousarray(kp1, dtype=np.float32).reshape(-1, 2)
+    n = k1.shape[0]
+    k2 = (np.zeros((n, 2), np.float32) if kp2_init is None
+          else np.array(kp2_init, dtype=np.float32, copy=True).reshape(-1, 2))
+    ok = np.zeros(n, np.uint8)
+    rows, cols = i1.shape
+    rc = L.orc_lk_track(i1.ctypes.data, i2.ctypes.data, cols, rows, i1.strides[0], n, k1.ctypes.data, k2.ctypes.data,
+                        ok.ctypes.data, int(bool(inverse)), int(kp2_init is not None), int(levels))
+    if rc != 0:
+        raise ValueError(f"orc_lk_track: {rc}")
+    return dict(kp2=k2, success=ok.astype(bool))
+
+
+def lk_pyr_down(src, dw, dh):
+    L = lib()
+    L.orc_lk_pyr_down.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_int32, C.c_int32]
+    s = np.ascontiguousarray(src, dtype=np.uint8)
+    d = np.zeros((dh, dw), np.uint8)
+    L.orc_lk_pyr_down(s.ctypes.data, s.shape[1], s.shape[0], s.strides[0], d.ctypes.data, dw, dh)
+    return d
