@@ -121,11 +121,11 @@ def native_oracle():
     """The timed CPU baseline build: the oracle at -O3 -march=native, compiled
     here for this host's CPU (the parity build in oracle/ is portable).  -ffp-contract=off keeps the
     reference's roundings (no FMA), so it computes the same numbers.  Falls back to the parity build."""
-    src = os.path.join(ROOT, "oracle", "lego_oracle.c")
+    src = [os.path.join(ROOT, "oracle", "lego_oracle.c"), os.path.join(ROOT, "oracle", "lk_oracle.c")]
     out = os.path.join(tempfile.gettempdir(), f"liblego_oracle_native_{os.getpid()}.so")
     flags = ["-O3", "-march=native", "-fPIC", "-std=gnu11", "-ffp-contract=off", "-fopenmp", "-shared"]
     try:
-        subprocess.run(["gcc", *flags, "-o", out, src, "-lm"], check=True, timeout=120, capture_output=True)
+        subprocess.run(["gcc", *flags, "-o", out, *src, "-lm"], check=True, timeout=120, capture_output=True)
         return out, " ".join(flags)
     except (OSError, subprocess.SubprocessError):
         return None, "-O3 -ffp-contract=off -fopenmp (parity build; native build failed)"
@@ -218,6 +218,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="only the timed line (no side measurements)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="length of the cpu_baseline sample")
     ap.add_argument("--trials-per-sync", type=int, default=0)
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="per-trial exchange with N > 1: RCCL over xGMI (the product path), or the ABI's "
+                         "host transport over gloo (a rehearsal of the N-rank flow on fewer GPUs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -232,16 +235,26 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    ndev = max(1, torch.cuda.device_count())
+    if world > 1 and args.comm == "rccl" and ndev < world:
+        raise SystemExit(f"{world} ranks need {world} GPUs for RCCL (found {ndev}); --comm host rehearses on fewer")
+    local = local % ndev
     torch.cuda.set_device(local)
 
     w = make_window(name, args.family, args.seed, rank, world)
     comm_id = bytes(128)
-    if world > 1:
+    extra = {}
+    if world > 1 and args.comm == "rccl":
         obj = [lego_ba.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
+    elif world > 1:
+        def allreduce(buf, op):
+            t = torch.from_numpy(buf)   # the library's pinned exchange buffer
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
+        extra = dict(allreduce=allreduce)
     solver = lego_ba.Solver(device=local, world_size=world, rank=rank, comm_id=comm_id,
-                            trials_per_sync=args.trials_per_sync)
+                            trials_per_sync=args.trials_per_sync, **extra)
     solver.upload(w)
 
     def barrier():
@@ -291,7 +304,9 @@ def main():
         "config": {"workload": f"{name}: sliding-window BA solve(10), {c['P']} KF / {c['L']} landmarks / "
                                f"{c['L'] * c['k']} obs" + (f", landmark-sharded over {world} GPUs" if world > 1 else ""),
                    "keyframes": c["P"], "landmarks": c["L"], "landmarks_per_gpu": c["L"] // world,
-                   "obs_this_rank": n_obs, "parallelism": f"landmark-shard x{world}"},
+                   "obs_this_rank": n_obs, "parallelism": f"landmark-shard x{world}",
+                   "exchange": ("none" if world == 1 else ("RCCL all-reduce" if args.comm == "rccl"
+                                                          else "host transport over gloo (rehearsal)"))},
         "iterations_per_solve": iters / args.steps,
         "trials_per_solve": trials / args.steps,
         "trials_per_s": round(trials / dt, 3),
@@ -383,6 +398,24 @@ def main():
                             "note": "single frame: host-to-host lh_estimate_pose call (4 rounds of solve(10)); "
                                     "batch: device time of one launch"}
     sf.close()
+    # pyramidal LK optical flow (LKOpticalFlow4Layer): a KITTI-sized pair
+    # (1241 x 376), 2000 keypoints, forward mode with an initial guess (the frontend's call)
+    import images
+    li1, li2 = images.pair(376, 1241, shift=(3.1, 0.4), seed=11)
+    lk1 = images.keypoints(376, 1241, 2000, seed=11, border=False)
+    lki = lk1 + np.float32([2.0, 0.0])
+    sl = lego_ba.Solver(device=local)
+    sl.lk_track(li1, li2, lk1, kp2_init=lki)
+    lt = sorted(sl.lk_track(li1, li2, lk1, kp2_init=lki)["time_ms"] for _ in range(5))
+    t0 = time.perf_counter()
+    lr = sl.lk_track(li1, li2, lk1, kp2_init=lki)
+    lh_ms = (time.perf_counter() - t0) * 1e3
+    sl.close()
+    out["lk_optical_flow"] = {"image": "1241x376 u8", "keypoints": len(lk1), "levels": 4,
+                              "device_ms": round(lt[2], 4), "keypoints_per_s": round(len(lk1) / (lt[2] * 1e-3), 1),
+                              "host_call_ms": round(lh_ms, 3), "tracked": int(lr["success"].sum()),
+                              "note": "device_ms: pyramids of both images + tracking, median of 5; host_call_ms "
+                                      "includes the image and keypoint copies"}
     if not args.no_cpu:
         import oracle_bind
         lib_path, flags = native_oracle()
@@ -411,6 +444,12 @@ def main():
         od = oracle_bind.solve(wd, n_threads=threads, gate_mode=1, lib_path=lib_path)
         out["survey_default_c3"]["chi2_rel_vs_oracle"] = abs(ld["chi2_final"] - od["chi2_final"]) / od["chi2_final"]
         out["survey_default_c3"]["oracle_iterations"] = od["iterations"]
+        t0 = time.perf_counter()
+        ol = oracle_bind.lk_track(li1, li2, lk1, kp2_init=lki, lib_path=lib_path)
+        out["lk_optical_flow"]["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        out["lk_optical_flow"]["cpu_oracle_threads"] = 1
+        out["lk_optical_flow"]["bitwise_equal_to_oracle"] = bool(np.array_equal(ol["kp2"], lr["kp2"]) and
+                                                                  np.array_equal(ol["success"], lr["success"]))
         if lib_path:
             try:
                 os.unlink(lib_path)

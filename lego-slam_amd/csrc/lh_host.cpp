@@ -195,11 +195,22 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Planner threads: the CPUs this process may use (affinity mask, capped by a cgroup v2 CPU quota:
+// a GPU box exposes every host core but grants a share of them), at most 16.
 int auto_host_threads() {
     cpu_set_t set;
     int n = 8;
     if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
-    return std::max(1, std::min(8, n));
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long per = 0;
+        if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+            const long quota = std::atol(q);
+            if (quota > 0) n = std::min<long>(n, (quota + per - 1) / per);
+        }
+        std::fclose(f);
+    }
+    return std::max(1, std::min(16, n));
 }
 
 }  // namespace
@@ -229,6 +240,7 @@ struct lh_handle {
     HostBuf<uint16_t> s_pair_pq;
     HostBuf<int32_t> s_obs_perm, s_lm_perm;
     HostBuf<double> s_uv, s_lm, s_qt, s_ptab, s_ext, s_rs;   // s_rs: the host-exchange buffer
+    HostBuf<double> s_out;                                   // pinned staging of the download
 
     // device buffers
     DevBuf<lh_chunk> d_chunks;
@@ -550,27 +562,43 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     return LH_OK;
 }
 
+// Results into the caller's buffers: device -> pinned staging in one stream (poses, landmark
+// positions gathered into window order, per-edge rho0), then the staging is copied out on the
+// planner's threads (a pageable device-to-host copy runs at a fraction of the link).
 int download(lh_handle* h, lh_result* out, int cur) {
     hipStream_t s = h->stream;
     const int P = h->P;
     const double t0 = now_ms();
-    if (out->pose_Tcw && P)   // estimate_ of every VertexPose (backend_lego.cpp:198-213)
-        HIPCHK(hipMemcpyAsync(out->pose_Tcw, h->d_qt.p + 12 * (size_t)cur * P, 12 * (size_t)P * sizeof(double),
-                              hipMemcpyDeviceToHost, s));
-    if (out->lm_xyz || out->edge_robust_chi2) {
+    const size_t np = out->pose_Tcw ? 12 * (size_t)P : 0;
+    const size_t nl = (out->lm_xyz && h->L) ? 3 * (size_t)h->L : 0;
+    const size_t ne = (out->edge_robust_chi2 && h->O) ? (size_t)h->O : 0;
+    HIPCHK(h->s_out.ensure(np + nl + ne));
+    double* st = h->s_out.p;
+    if (np)   // estimate_ of every VertexPose (backend_lego.cpp:198-213)
+        HIPCHK(hipMemcpyAsync(st, h->d_qt.p + 12 * (size_t)cur * P, np * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (nl || ne) {
         // landmarks without an edge are not vertices (backend_lego.cpp:126): they keep their input
-        if (out->lm_xyz && h->L)
-            HIPCHK(hipMemcpyAsync(h->d_out_xyz.p, h->d_lm_in.p, 3 * (size_t)h->L * sizeof(double), hipMemcpyDeviceToDevice, s));
-        HIPCHK(lh_launch_gather(s, h->d_ctrl.p, h->d_rec.p, h->d_lm_perm.p, out->lm_xyz ? h->n_rec : 0, h->d_rho.p,
-                                h->d_obs_perm.p, out->edge_robust_chi2 ? (long)h->n_slots : 0L, h->d_out_xyz.p,
-                                h->d_out_rho.p));
-        if (out->lm_xyz && h->L)
-            HIPCHK(hipMemcpyAsync(out->lm_xyz, h->d_out_xyz.p, 3 * (size_t)h->L * sizeof(double), hipMemcpyDeviceToHost, s));
-        if (out->edge_robust_chi2 && h->O)
-            HIPCHK(hipMemcpyAsync(out->edge_robust_chi2, h->d_out_rho.p, (size_t)h->O * sizeof(double),
-                                  hipMemcpyDeviceToHost, s));
+        if (nl) HIPCHK(hipMemcpyAsync(h->d_out_xyz.p, h->d_lm_in.p, nl * sizeof(double), hipMemcpyDeviceToDevice, s));
+        HIPCHK(lh_launch_gather(s, h->d_ctrl.p, h->d_rec.p, h->d_lm_perm.p, nl ? h->n_rec : 0, h->d_rho.p,
+                                h->d_obs_perm.p, ne ? (long)h->n_slots : 0L, h->d_out_xyz.p, h->d_out_rho.p));
+        if (nl) HIPCHK(hipMemcpyAsync(st + np, h->d_out_xyz.p, nl * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (ne) HIPCHK(hipMemcpyAsync(st + np + nl, h->d_out_rho.p, ne * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
+    // copy-out in blocks of ~256 KB over the three destinations
+    struct Seg { double* dst; const double* src; size_t n; };
+    const Seg seg[3] = {{out->pose_Tcw, st, np}, {out->lm_xyz, st + np, nl}, {out->edge_robust_chi2, st + np + nl, ne}};
+    const size_t blk = 32768;
+    std::vector<std::pair<int, size_t>> jobs;
+    for (int k = 0; k < 3; ++k)
+        for (size_t o = 0; o < seg[k].n; o += blk) jobs.emplace_back(k, o);
+    auto job = [&](int j) {
+        const Seg& g = seg[jobs[j].first];
+        const size_t o = jobs[j].second, c = std::min(blk, g.n - o);
+        std::memcpy(g.dst + o, g.src + o, c * sizeof(double));
+    };
+    if (h->pool) h->pool->run((int)jobs.size(), job);
+    else for (int j = 0; j < (int)jobs.size(); ++j) job(j);
     out->time_download_ms = now_ms() - t0;
     return LH_OK;
 }
@@ -813,6 +841,7 @@ void lh_destroy(lh_handle* h) {
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
+    h->s_out.release();
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);
     if (h->stream) (void)hipStreamDestroy(h->stream);

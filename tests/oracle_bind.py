@@ -209,9 +209,9 @@ def edge_eval(T12, X, uv, K, ext12=None, huber_delta=5.991):
     return dict(r=r, Jp=Jp.reshape(2, 6), Jl=Jl.reshape(2, 3), W=W.reshape(2, 2), drho=drho.value, rchi2=rc.value)
 
 
-def lk_track(img1, img2, kp1, kp2_init=None, inverse=False, levels=4):
+def lk_track(img1, img2, kp1, kp2_init=None, inverse=False, levels=4, lib_path=None):
     """orc_lk_track: the restated LKOpticalFlow4Layer / 1Layer (oracle/lk_oracle.c)."""
-    L = lib()
+    L = lib(lib_path)
     L.orc_lk_track.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
     L.orc_lk_track.restype = C.c_int
