@@ -10,7 +10,8 @@
 #endif
 
 // ---- envelope ---------------------------------------------------------------
-#define LH_PMAX 21            // poses per window (reduced system n = 6P <= 126 fits LDS)
+#define LH_PMAX 21            // poses per window solved in LDS (reduced system n = 6P <= 126, k_ctrl)
+#define LH_PMAX_WIN 64        // pose masks (planner, k_lin's fixed-pose mask) are 64-bit
 #define LH_UMAX 16            // distinct poses in one chunk window (6U <= 96 rows); the reference window is
                               // 15 keyframes (map.h:82), so any landmark of it fits one chunk window
 #define LH_TMAX 6             // 16-row MFMA tiles per window side
@@ -56,6 +57,12 @@
 #define LH_PT_TET 11
 #define LH_PT_RT 14
 #define LH_EXT 16
+
+// reduced-system element map (k_ctrl scatter): row | col << 9 | diagonal-block flag << 18
+#define LH_RSMAP(r, c, d) ((uint32_t)(r) | ((uint32_t)(c) << 9) | ((d) ? (1u << 18) : 0u))
+#define LH_RSMAP_ROW(m) ((m) & 0x1FFu)
+#define LH_RSMAP_COL(m) (((m) >> 9) & 0x1FFu)
+#define LH_RSMAP_DIAG(m) ((m) >> 18)
 
 // obs meta packing
 #define LH_META(pose, cam, slot, lms) ((uint32_t)(pose) | ((uint32_t)(cam) << 12) | ((uint32_t)(slot) << 16) | ((uint32_t)(lms) << 20) | LH_META_VALID)

@@ -32,7 +32,7 @@ hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
-                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint32_t fixed_mask);
+                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint64_t fixed_mask);
 hipError_t lh_launch_reduce(hipStream_t st, const double* slabs, const uint32_t* pair_ptr, const uint32_t* items,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks);

@@ -420,7 +420,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
     const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
-    double* __restrict__ edge_rho, double* __restrict__ slabs, lh_params prm, int nrec, uint32_t fixed_mask,
+    double* __restrict__ edge_rho, double* __restrict__ slabs, lh_params prm, int nrec, uint64_t fixed_mask,
     int chunk_base) {
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 
         const bool has = (meta & LH_META_VALID) != 0u;
         const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta);
-        const bool pfixed = (fixed_mask >> p) & 1u;
+        const bool pfixed = (fixed_mask >> p) & 1ull;
         const bool live = has && !pfixed;
         const double* e = wext + cam * LH_EXT;
         const bool ext_id = (prm.ext_identity >> cam) & 1;
@@ -1484,7 +1484,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         vs[u] = v;
         if (accept && i < LY.total) rs_commit[i] = v;
         if (i < LY.off_bs) {
-            const int gi = mp[u] & 0xff, gj = (mp[u] >> 8) & 0xff;
+            const int gi = LH_RSMAP_ROW(mp[u]), gj = LH_RSMAP_COL(mp[u]);
             if (gi == gj) dg[gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
         } else if (i < LY.off_bp) {
             bsv[i - LY.off_bs] = v;
@@ -1530,8 +1530,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     for (int u = 0; u < NLD; ++u) {
         const int i = u * CT + tid;
         if (i < LY.off_bs) {
-            const int ri = iperm[mp[u] & 0xff], rj = iperm[(mp[u] >> 8) & 0xff];
-            if (!(mp[u] >> 16)) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
+            const int ri = iperm[LH_RSMAP_ROW(mp[u])], rj = iperm[LH_RSMAP_COL(mp[u])];
+            if (!LH_RSMAP_DIAG(mp[u])) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
             else if (ri > rj) A[ri * AS + rj] = vs[u];
         }
     }
@@ -2040,7 +2040,7 @@ hipError_t lh_prepare_lin(int lds_limit) {
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
-                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint32_t fixed_mask) {
+                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint64_t fixed_mask) {
     if (nchunks <= 0) return hipSuccess;
     dim3 g(nchunks), b(256);
 #define LH_LIN(TT, TR)                                                                                             \

@@ -82,8 +82,8 @@ void parallel_range(Pool* pool, int64_t n, int64_t min_block, const std::functio
     else for (int b = 0; b < nb; ++b) body(b);
 }
 
-inline int popc(uint32_t m) { return __builtin_popcount(m); }
-inline int chunk_tiles(uint32_t mask) { return (6 * popc(mask) + 15) / 16; }
+inline int popc(uint64_t m) { return __builtin_popcountll(m); }
+inline int chunk_tiles(uint64_t mask) { return (6 * popc(mask) + 15) / 16; }
 inline int pow2log(int k) { int g = 1, lg = 0; while (g < k) { g <<= 1; ++lg; } return lg; }
 
 }  // namespace
@@ -119,12 +119,12 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     });
     if (bad.load()) return LH_E_BADARG;
     if (!allow_empty && (O == 0 || (P + L) == 0)) return LH_E_EMPTY;   // problem.cpp:157-161
-    if (P > LH_PMAX) return LH_E_UNSUPPORTED;
+    if (P > LH_PMAX) return LH_E_UNSUPPORTED;   // the reduced pose system is solved in one CU's LDS
     if (O >= (int64_t)1 << 30) return LH_E_UNSUPPORTED;                 // int32 slot indices
     pl.fixed_mask = 0;
     if (w->pose_fixed)
         for (int p = 0; p < P; ++p)
-            if (w->pose_fixed[p]) pl.fixed_mask |= 1u << p;
+            if (w->pose_fixed[p]) pl.fixed_mask |= 1ull << p;
 
     // ---- landmark-major CSR ----
     pl.lm_ptr.assign((size_t)L + 1, 0);
@@ -147,7 +147,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     }
 
     // ---- per landmark: ascending pose order, pose mask, envelope checks ----
-    pl.lm_mask.assign((size_t)L, 0u);
+    pl.lm_mask.assign((size_t)L, 0ull);
     std::atomic<int> unsup{0};
     parallel_range(pool, L, 4096, [&](int64_t b, int64_t e) {
         bool us = false;
@@ -162,9 +162,9 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
                 while (j >= 0 && (w->obs_pose[s[j]] > pv || (w->obs_pose[s[j]] == pv && s[j] > v))) { s[j + 1] = s[j]; --j; }
                 s[j + 1] = v;
             }
-            uint32_t m = 0;
+            uint64_t m = 0;
             for (int64_t i = 0; i < k; ++i) {
-                const uint32_t bit = 1u << w->obs_pose[s[i]];
+                const uint64_t bit = 1ull << w->obs_pose[s[i]];
                 if (m & bit) us = true;   // two edges landmark -> same pose (DESIGN.md "Limits")
                 m |= bit;
             }
@@ -180,8 +180,8 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         const int nb = std::max(P, 1) * std::max(P, 1);
         std::vector<int32_t> bcnt((size_t)nb + 1, 0);
         auto bucket = [&](int l) {
-            const uint32_t m = pl.lm_mask[l];
-            return __builtin_ctz(m) * P + (31 - __builtin_clz(m));
+            const uint64_t m = pl.lm_mask[l];
+            return __builtin_ctzll(m) * P + (63 - __builtin_clzll(m));
         };
         int Lact = 0;
         for (int l = 0; l < L; ++l)
@@ -196,7 +196,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         for (int b = 0; b < nb; ++b) {
             auto s = pl.order.begin() + bcnt[b], e = pl.order.begin() + bcnt[b + 1];
             if (e - s < 2) continue;
-            const uint32_t m0 = pl.lm_mask[*s];
+            const uint64_t m0 = pl.lm_mask[*s];
             if (std::all_of(s, e, [&](int32_t l) { return pl.lm_mask[l] == m0; })) continue;
             std::stable_sort(s, e, [&](int32_t a, int32_t c) { return pl.lm_mask[a] < pl.lm_mask[c]; });
         }
@@ -213,13 +213,13 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     // a chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new chunk
     // rather than let the union grow past the larger of the two tile counts
     for (int i = 0; i < Lact; ++i) {
-        const uint32_t m = pl.lm_mask[pl.order[i]];
+        const uint64_t m = pl.lm_mask[pl.order[i]];
         const bool fresh = pl.chunk_lm0.empty() || (i - pl.chunk_lm0.back()) >= chunk_lm ||
                            popc(pl.chunk_mask.back() | m) > LH_UMAX ||
                            chunk_tiles(pl.chunk_mask.back() | m) > std::max(chunk_tiles(pl.chunk_mask.back()), chunk_tiles(m));
         if (fresh) {
             pl.chunk_lm0.push_back(i);
-            pl.chunk_mask.push_back(0u);
+            pl.chunk_mask.push_back(0ull);
         }
         pl.chunk_mask.back() |= m;
     }
@@ -280,11 +280,11 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     pl.npairs = P * (P + 1) / 2;
     pl.pair_ptr.assign((size_t)pl.npairs + 1, 0u);
     for (int ci = 0; ci < NC; ++ci) {
-        const uint32_t m = pl.chunk_mask[pl.corder[ci]];
-        for (uint32_t a = m; a; a &= a - 1) {
-            const int p = __builtin_ctz(a);
-            for (uint32_t b = a; b; b &= b - 1) {
-                const int q = __builtin_ctz(b);
+        const uint64_t m = pl.chunk_mask[pl.corder[ci]];
+        for (uint64_t a = m; a; a &= a - 1) {
+            const int p = __builtin_ctzll(a);
+            for (uint64_t b = a; b; b &= b - 1) {
+                const int q = __builtin_ctzll(b);
                 pl.pair_ptr[p * P - (p * (p - 1)) / 2 + (q - p) + 1]++;
             }
         }
@@ -302,15 +302,15 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
     // chunks and their sub-batches' observation slots, one task per chunk
     auto chunk_task = [&](int ci) {
         const int c = pl.corder[ci];
-        const uint32_t m = pl.chunk_mask[c];
+        const uint64_t m = pl.chunk_mask[c];
         lh_chunk ck;
         std::memset(&ck, 0, sizeof(ck));
         ck.U = (uint8_t)popc(m);
         ck.T = (uint8_t)chunk_tiles(m);
-        int slot_of[32] = {0};
+        int slot_of[64] = {0};
         {
             int s = 0;
-            for (uint32_t a = m; a; a &= a - 1) { const int p = __builtin_ctz(a); ck.pose[s] = (uint16_t)p; slot_of[p] = s++; }
+            for (uint64_t a = m; a; a &= a - 1) { const int p = __builtin_ctzll(a); ck.pose[s] = (uint16_t)p; slot_of[p] = s++; }
         }
         ck.sb_begin = (uint32_t)pl.chunk_sb0[ci];
         ck.sb_end = (uint32_t)pl.chunk_sb0[ci + 1];
@@ -361,10 +361,10 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
     {
         std::vector<uint32_t> cur(pl.pair_ptr.begin(), pl.pair_ptr.end() - 1);
         for (int ci = 0; ci < NC; ++ci) {
-            const uint32_t m = pl.chunk_mask[pl.corder[ci]];
+            const uint64_t m = pl.chunk_mask[pl.corder[ci]];
             const int T = chunk_tiles(m);
-            int ps[32], U = 0;
-            for (uint32_t a = m; a; a &= a - 1) ps[U++] = __builtin_ctz(a);
+            int ps[64], U = 0;
+            for (uint64_t a = m; a; a &= a - 1) ps[U++] = __builtin_ctzll(a);
             for (int s = 0; s < U; ++s)
                 for (int t = s; t < U; ++t) {
                     const int p = ps[s], q = ps[t];
@@ -376,13 +376,13 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
     for (int p = 0, b = 0; p < P; ++p)
         for (int q = p; q < P; ++q, ++b) { out.pair_pq[2 * b] = (uint16_t)p; out.pair_pq[2 * b + 1] = (uint16_t)q; }
     // reduced-system element map for k_ctrl's register scatter: S element of pose pair (pi, pj),
-    // pi <= pj, row a, col b -> global rows 6 pi + a, 6 pj + b, diagonal-block flag
+    // pi <= pj, row a, col b -> global rows 6 pi + a, 6 pj + b (9 bits each), diagonal-block flag
     for (int pi = 0, blk = 0; pi < P; ++pi)
         for (int pj = pi; pj < P; ++pj, ++blk)
             for (int a = 0; a < 6; ++a)
                 for (int b = 0; b < 6; ++b)
                     out.rsmap[(size_t)blk * 36 + 6 * a + b] =
-                        (uint32_t)(6 * pi + a) | ((uint32_t)(6 * pj + b) << 8) | ((pi == pj ? 1u : 0u) << 16);
+                        LH_RSMAP(6 * pi + a, 6 * pj + b, pi == pj);
     parallel_range(pool, 3 * (int64_t)pl.L, 1 << 16, [&](int64_t b, int64_t e) {
         if (e > b) std::memcpy(out.lm_xyz + b, w->lm_xyz + b, (size_t)(e - b) * sizeof(double));
     });
