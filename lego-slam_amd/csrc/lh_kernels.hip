@@ -300,6 +300,8 @@ __device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, co
     d_q_rotate(pt + LH_PT_QET, X, Pc);
 #pragma unroll
     for (int i = 0; i < 3; ++i) Pc[i] = Pc[i] + pt[LH_PT_TET + i];
+    {
+#pragma clang fp contract(fast)   // the Jacobians are not on the bitwise-mirrored path (the residual is)
     const double fx = prm.K[0], fy = prm.K[1];
     const double x = Pc[0], y = Pc[1], z = Pc[2];
     const double zi = 1.0 / (z + 1e-18);
@@ -329,6 +331,7 @@ __device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, co
 #pragma unroll
         for (int j = 0; j < 3; ++j)
             Jl[3 * i + j] = A[3 * i] * Rt[j] + A[3 * i + 1] * Rt[3 + j] + A[3 * i + 2] * Rt[6 + j];
+    }
 }
 
 #pragma clang fp contract(fast)
@@ -420,8 +423,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
     const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
-    double* __restrict__ edge_rho, double* __restrict__ slabs, lh_params prm, int nrec, uint64_t fixed_mask,
-    int chunk_base) {
+    double* __restrict__ edge_rho, double* __restrict__ slabs, uint8_t* __restrict__ wflag, long nslots,
+    lh_params prm, int nrec, uint64_t fixed_mask, int chunk_base) {
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
 
@@ -475,15 +478,21 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // flight with counted vmcnt waits across the iteration.
     const int sb_last = (int)sb_end - 1;
     int sb = (int)sb_begin + wave;
+    // wflag[buffer][slot]: 1 where the linearisation that produced that buffer's state found the edge
+    // an inlier (e2 <= delta^2, or no robust kernel), i.e. its robust weight W is exactly I
+    const uint8_t* __restrict__ wf_c = wflag + (size_t)cur * nslots;
+    uint8_t* __restrict__ wf_n = wflag + (size_t)cand * nslots;
     uint32_t meta_n;
     double u_n, v_n;
     double2 r_n;
+    int wfl_n = 0;
     lh_subbatch S_n;
     {
         const int sbc = min(sb, sb_last);
         const int o = sbc * 64 + lane;
         S_n = sbs[sbc];
         meta_n = obs_meta[o];
+        if (TRIAL) wfl_n = wf_c[o];
         u_n = obs_uv[2 * (size_t)o];
         v_n = obs_uv[2 * (size_t)o + 1];
         r_n = rc2[(size_t)sbc * 64 + lane];
@@ -499,12 +508,14 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         const uint32_t meta = meta_n;
         const double u = u_n, v = v_n;
         const double2 rr = r_n;
+        const int wfl = wfl_n;
         const int o = sb * 64 + lane;
         {
             const int sbn = min(sb + LH_WAVES, sb_last);
             const int on = sbn * 64 + lane;
             S_n = sbs[sbn];
             meta_n = obs_meta[on];
+            if (TRIAL) wfl_n = wf_c[on];
             u_n = obs_uv[2 * (size_t)on];
             v_n = obs_uv[2 * (size_t)on + 1];
             r_n = rc2[(size_t)sbn * 64 + lane];
@@ -544,8 +555,12 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (live) {
                 const double* pt = wt_c + (slot * ncam + cam) * LH_PT;
                 EdgeEval E;
-                edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
-                edge_robust(E, prm);
+                if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
+                    E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+                } else {
+                    edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
+                    edge_robust(E, prm);
+                }
                 edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
                 const double* d = wdx + 6 * slot;
                 double jd0 = 0.0, jd1 = 0.0;
@@ -594,6 +609,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
             edge_rho[o] = E.rho0;
             chi_acc += E.rho0;
+            wf_n[o] = (prm.huber_delta <= 0.0 || E.e2 <= prm.huber_delta * prm.huber_delta) ? 1 : 0;
             const double dr = (prm.huber_delta > 0.0) ? E.rho1 : 1.0;
             double WJl[6];
 #pragma unroll
@@ -2040,14 +2056,15 @@ hipError_t lh_prepare_lin(int lds_limit) {
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
-                         double* edge_rho, double* slabs, lh_params prm, int nrec, uint64_t fixed_mask) {
+                         double* edge_rho, double* slabs, uint8_t* wflag, long nslots, lh_params prm, int nrec,
+                         uint64_t fixed_mask) {
     if (nchunks <= 0) return hipSuccess;
     dim3 g(nchunks), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
         const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
         hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
-                           edge_rho, slabs, prm, nrec, fixed_mask, chunk_base);                                    \
+                           edge_rho, slabs, wflag, nslots, prm, nrec, fixed_mask, chunk_base);                     \
     } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
