@@ -383,16 +383,18 @@ def main():
     sf = lego_ba.Solver(device=local)
     one = frames.batch(args.seed, 1, n_obs=150)
     sf.estimate_pose(one)
-    lat = []
+    lat, lat_dev = [], []
     for _ in range(20):
         t0 = time.perf_counter()
-        sf.estimate_pose(one)
+        r1 = sf.estimate_pose(one)
         lat.append((time.perf_counter() - t0) * 1e3)
+        lat_dev.append(r1["time_ms"])
     nf = 2048
     fb = frames.batch(args.seed, nf, n_obs=150)
     sf.estimate_pose(fb)
     tms = [sf.estimate_pose(fb)["time_ms"] for _ in range(3)]
-    out["estimate_pose"] = {"single_frame_ms": round(float(np.median(lat)), 4), "obs_per_frame": 150,
+    out["estimate_pose"] = {"single_frame_ms": round(float(np.median(lat)), 4),
+                            "single_frame_kernel_ms": round(float(np.median(lat_dev)), 4), "obs_per_frame": 150,
                             "batch_frames": nf, "batch_ms": round(min(tms), 4),
                             "batch_frames_per_s": round(nf / (min(tms) * 1e-3), 1),
                             "note": "single frame: host-to-host lh_estimate_pose call (4 rounds of solve(10)); "

@@ -254,10 +254,11 @@ struct lh_handle {
     DevBuf<lh_ctrl> d_ctrl;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
     // frontend pose-only batch (lh_estimate_pose)
-    DevBuf<int64_t> f_ptr;
-    DevBuf<double> f_pose_in, f_pts, f_uv, f_res, f_pose_out, f_rchi2;
-    DevBuf<uint8_t> f_flag_in, f_flag_out;
-    DevBuf<int32_t> f_iters, f_inl;
+    // inputs and outputs each packed into one arena, so a call is one upload and one download
+    // through pinned staging (a single frame is latency-bound: every extra copy costs ~10 us)
+    DevBuf<uint8_t> f_in, f_out;
+    DevBuf<double> f_res;
+    HostBuf<uint8_t> s_fin, s_fout;
     // LK optical flow (lh_lk_track): both images' pyramids, keypoints
     DevBuf<uint8_t> k_img[2], k_succ;
     DevBuf<float> k_kp1, k_kp2;
@@ -568,6 +569,30 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
 // Results into the caller's buffers: device -> pinned staging in one stream (poses, landmark
 // positions gathered into window order, per-edge rho0), then the staging is copied out on the
 // planner's threads (a pageable device-to-host copy runs at a fraction of the link).
+// host copies between caller memory and pinned staging, in ~256 KB blocks over the planner's pool
+struct ByteSeg { void* dst; const void* src; size_t n; };
+void par_copy(lh_handle* h, const ByteSeg* seg, int nseg) {
+    const size_t blk = 262144;
+    size_t total = 0;
+    for (int k = 0; k < nseg; ++k) total += (seg[k].dst && seg[k].src) ? seg[k].n : 0;
+    if (total < 4 * blk) {   // waking the pool costs more than copying a small call's bytes
+        for (int k = 0; k < nseg; ++k)
+            if (seg[k].dst && seg[k].src && seg[k].n) std::memcpy(seg[k].dst, seg[k].src, seg[k].n);
+        return;
+    }
+    std::vector<std::pair<int, size_t>> jobs;
+    for (int k = 0; k < nseg; ++k)
+        if (seg[k].dst && seg[k].src)
+            for (size_t o = 0; o < seg[k].n; o += blk) jobs.emplace_back(k, o);
+    auto job = [&](int j) {
+        const ByteSeg& g = seg[jobs[j].first];
+        const size_t o = jobs[j].second, c = std::min(blk, g.n - o);
+        std::memcpy((uint8_t*)g.dst + o, (const uint8_t*)g.src + o, c);
+    };
+    if (h->pool && jobs.size() > 1) h->pool->run((int)jobs.size(), job);
+    else for (int j = 0; j < (int)jobs.size(); ++j) job(j);
+}
+
 int download(lh_handle* h, lh_result* out, int cur) {
     hipStream_t s = h->stream;
     const int P = h->P;
@@ -588,20 +613,10 @@ int download(lh_handle* h, lh_result* out, int cur) {
         if (ne) HIPCHK(hipMemcpyAsync(st + np + nl, h->d_out_rho.p, ne * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
-    // copy-out in blocks of ~256 KB over the three destinations
-    struct Seg { double* dst; const double* src; size_t n; };
-    const Seg seg[3] = {{out->pose_Tcw, st, np}, {out->lm_xyz, st + np, nl}, {out->edge_robust_chi2, st + np + nl, ne}};
-    const size_t blk = 32768;
-    std::vector<std::pair<int, size_t>> jobs;
-    for (int k = 0; k < 3; ++k)
-        for (size_t o = 0; o < seg[k].n; o += blk) jobs.emplace_back(k, o);
-    auto job = [&](int j) {
-        const Seg& g = seg[jobs[j].first];
-        const size_t o = jobs[j].second, c = std::min(blk, g.n - o);
-        std::memcpy(g.dst + o, g.src + o, c * sizeof(double));
-    };
-    if (h->pool) h->pool->run((int)jobs.size(), job);
-    else for (int j = 0; j < (int)jobs.size(); ++j) job(j);
+    const ByteSeg seg[3] = {{out->pose_Tcw, st, np * sizeof(double)},
+                            {out->lm_xyz, st + np, nl * sizeof(double)},
+                            {out->edge_robust_chi2, st + np + nl, ne * sizeof(double)}};
+    par_copy(h, seg, 3);
     out->time_download_ms = now_ms() - t0;
     return LH_OK;
 }
@@ -831,9 +846,7 @@ void lh_destroy(lh_handle* h) {
     if (h->comm) ncclCommDestroy(h->comm);
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     delete h->pool;
-    h->f_ptr.release(); h->f_pose_in.release(); h->f_pts.release(); h->f_uv.release(); h->f_res.release();
-    h->f_pose_out.release(); h->f_rchi2.release(); h->f_flag_in.release(); h->f_flag_out.release();
-    h->f_iters.release(); h->f_inl.release();
+    h->f_in.release(); h->f_out.release(); h->f_res.release(); h->s_fin.release(); h->s_fout.release();
     h->k_img[0].release(); h->k_img[1].release(); h->k_succ.release(); h->k_kp1.release(); h->k_kp2.release();
     h->d_chunks.release(); h->d_sbs.release(); h->d_meta.release(); h->d_obs_perm.release(); h->d_lm_perm.release();
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
@@ -912,25 +925,32 @@ int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
     if (!out->pose_Tcw) return LH_E_BADARG;
     if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
     hipStream_t s = h->stream;
-    HIPCHK(h->f_ptr.ensure(F + 1));
-    HIPCHK(h->f_pose_in.ensure(12 * (size_t)F));
-    HIPCHK(h->f_pose_out.ensure(12 * (size_t)F));
-    HIPCHK(h->f_pts.ensure(3 * (size_t)O));
-    HIPCHK(h->f_uv.ensure(2 * (size_t)O));
+    // arena layouts (16-byte aligned segments)
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const bool has_flag = in->is_outlier && O > 0;
+    const size_t i_ptr = 0, i_pose = al(sizeof(int64_t) * (F + 1)), i_pts = i_pose + al(sizeof(double) * 12 * (size_t)F),
+                 i_uv = i_pts + al(sizeof(double) * 3 * (size_t)O), i_flag = i_uv + al(sizeof(double) * 2 * (size_t)O),
+                 i_end = i_flag + (has_flag ? al((size_t)O) : 0);
+    const size_t o_pose = 0, o_rchi2 = al(sizeof(double) * 12 * (size_t)F), o_iters = o_rchi2 + al(sizeof(double) * (size_t)O),
+                 o_inl = o_iters + al(sizeof(int32_t) * (size_t)F), o_flag = o_inl + al(sizeof(int32_t) * (size_t)F),
+                 o_end = o_flag + al((size_t)O);
+    HIPCHK(h->f_in.ensure(i_end));
+    HIPCHK(h->f_out.ensure(o_end));
     HIPCHK(h->f_res.ensure(2 * (size_t)O));
-    HIPCHK(h->f_rchi2.ensure((size_t)O));
-    HIPCHK(h->f_flag_in.ensure((size_t)O));
-    HIPCHK(h->f_flag_out.ensure((size_t)O));
-    HIPCHK(h->f_iters.ensure((size_t)F));
-    HIPCHK(h->f_inl.ensure((size_t)F));
-    auto up = [&](void* d, const void* src, size_t bytes) { return hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, s); };
-    HIPCHK(up(h->f_ptr.p, in->obs_ptr, sizeof(int64_t) * (F + 1)));
-    HIPCHK(up(h->f_pose_in.p, in->pose_Tcw, sizeof(double) * 12 * (size_t)F));
-    if (O > 0) {
-        HIPCHK(up(h->f_pts.p, in->pts_w, sizeof(double) * 3 * (size_t)O));
-        HIPCHK(up(h->f_uv.p, in->obs_uv, sizeof(double) * 2 * (size_t)O));
-        if (in->is_outlier) HIPCHK(up(h->f_flag_in.p, in->is_outlier, (size_t)O));
+    HIPCHK(h->s_fin.ensure(i_end));
+    HIPCHK(h->s_fout.ensure(o_end));
+    {
+        uint8_t* st = h->s_fin.p;
+        const ByteSeg seg[5] = {{st + i_ptr, in->obs_ptr, sizeof(int64_t) * (F + 1)},
+                                {st + i_pose, in->pose_Tcw, sizeof(double) * 12 * (size_t)F},
+                                {st + i_pts, in->pts_w, sizeof(double) * 3 * (size_t)O},
+                                {st + i_uv, in->obs_uv, sizeof(double) * 2 * (size_t)O},
+                                {st + i_flag, in->is_outlier, has_flag ? (size_t)O : 0}};
+        par_copy(h, seg, 5);
     }
+    HIPCHK(hipMemcpyAsync(h->f_in.p, h->s_fin.p, i_end, hipMemcpyHostToDevice, s));
+    uint8_t* fi = h->f_in.p;
+    uint8_t* fo = h->f_out.p;
     lh_params prm{};
     prm.max_iters = h->opt.max_iters;
     prm.max_trials = h->opt.max_trials;
@@ -946,17 +966,28 @@ int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
     hipEvent_t e0 = next_event(h), e1 = next_event(h);
     if (!e0 || !e1) return LH_E_HIP;
     HIPCHK(hipEventRecord(e0, s));
-    HIPCHK(lh_launch_frames(s, F, h->f_ptr.p, h->f_pose_in.p, h->f_pts.p, h->f_uv.p,
-                            in->is_outlier ? h->f_flag_in.p : nullptr, prm, h->f_res.p, h->f_pose_out.p,
-                            h->f_flag_out.p, h->f_rchi2.p, h->f_iters.p, h->f_inl.p));
+    HIPCHK(lh_launch_frames(s, F, (const int64_t*)(fi + i_ptr), (const double*)(fi + i_pose),
+                            (const double*)(fi + i_pts), (const double*)(fi + i_uv), has_flag ? fi + i_flag : nullptr,
+                            prm, h->f_res.p, (double*)(fo + o_pose), fo + o_flag, (double*)(fo + o_rchi2),
+                            (int32_t*)(fo + o_iters), (int32_t*)(fo + o_inl)));
     HIPCHK(hipEventRecord(e1, s));
-    auto down = [&](void* dst, const void* d, size_t bytes) { return hipMemcpyAsync(dst, d, bytes, hipMemcpyDeviceToHost, s); };
-    HIPCHK(down(out->pose_Tcw, h->f_pose_out.p, sizeof(double) * 12 * (size_t)F));
-    if (out->is_outlier && O > 0) HIPCHK(down(out->is_outlier, h->f_flag_out.p, (size_t)O));
-    if (out->edge_chi2 && O > 0) HIPCHK(down(out->edge_chi2, h->f_rchi2.p, sizeof(double) * (size_t)O));
-    if (out->n_inliers) HIPCHK(down(out->n_inliers, h->f_inl.p, sizeof(int32_t) * (size_t)F));
-    if (out->iterations) HIPCHK(down(out->iterations, h->f_iters.p, sizeof(int32_t) * (size_t)F));
+    // one download of what the caller asked for: the pose block always, the rest up to the last wanted
+    const size_t want = out->is_outlier && O > 0 ? o_end
+                        : out->n_inliers         ? o_flag
+                        : out->iterations        ? o_inl
+                        : out->edge_chi2 && O > 0 ? o_iters
+                                                 : o_rchi2;
+    HIPCHK(hipMemcpyAsync(h->s_fout.p, fo, want, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    {
+        const uint8_t* st = h->s_fout.p;
+        const ByteSeg seg[5] = {{out->pose_Tcw, st + o_pose, sizeof(double) * 12 * (size_t)F},
+                                {out->edge_chi2, st + o_rchi2, out->edge_chi2 ? sizeof(double) * (size_t)O : 0},
+                                {out->iterations, st + o_iters, out->iterations ? sizeof(int32_t) * (size_t)F : 0},
+                                {out->n_inliers, st + o_inl, out->n_inliers ? sizeof(int32_t) * (size_t)F : 0},
+                                {out->is_outlier, st + o_flag, out->is_outlier ? (size_t)O : 0}};
+        par_copy(h, seg, 5);
+    }
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     out->time_ms = ms;

@@ -1657,8 +1657,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 // from the frame's pose, then the outlier flags (:205-226); the edges lose the
 // Huber cost after round three (:223-225).  Edges are never removed (the
 // reference's setLevel is commented out).  n = 6: the Schur complement is H_pp
-// itself (problem.cpp:380-430 with no landmark vertex), solved by thread 0 with
-// Eigen's pivoted LDLT.  Per-edge arithmetic is the bitwise mirror of
+// itself (problem.cpp:380-430 with no landmark vertex), solved by wave 0 in
+// registers with Eigen's pivoted LDLT (po_ldlt6_wave).  Per-edge arithmetic is the bitwise mirror of
 // oracle/lego_oracle.c (po_residual / po_jacobian); sums have a fixed order
 // (thread-strided, then a fixed tree), so a batch is bitwise reproducible.
 // ============================================================================
@@ -1726,56 +1726,89 @@ __device__ __forceinline__ void po_accumulate(double r0, double r1, const double
     acc[27] += E.rho0;
 }
 
-// Eigen LDLT<Lower> (diagonal pivoting) + solve on a 6x6 (the oracle's ldlt_solve, n = 6).
-// A, x, tr, temp live in LDS: the pivot swaps index dynamically (registers would go to scratch).
-__device__ void po_ldlt6(double* A, const double* b, double* x, int* tr, double* temp) {
-    int all_zero = 0;
+// swap x[k] and x[j] of a 6-register array, j wave-uniform (an SGPR): scalar branches over
+// static registers (an indexed select chain is lowered to a scratch array)
+__device__ __forceinline__ void po_swap6(double x[6], int k, int j) {
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+        if (m > k && m == j) { const double t = x[k]; x[k] = x[m]; x[m] = t; }
+}
+
+// The same LDLT + solve as the oracle's ldlt_solve (n = 6: one 8-row panel) on one wave, in
+// registers: lane r < 6 holds row r of the full symmetric A (lanes >= 6 mirror row 5 and are
+// never read).  Eigen's in-place swaps on the lower triangle are a row exchange of lanes k and
+// idx plus a column exchange in every lane: the unfactored block stays full-symmetric, so the
+// upper entries the column exchange reads equal the lower ones Eigen swaps in.  Every element
+// sees the oracle's operations in the oracle's order (contraction off): bitwise the same x.
+// All 64 lanes of the wave call it; every lane returns x.
+__device__ void po_ldlt6_wave(double a[6], const double b[6], double x[6], int lane) {
+    double dd[6];
+    int tr[6];
+    bool all_zero = false;
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
+        if (all_zero) continue;   // (no break: the loop must unroll, a[k] stays a register)
         int idx = k;
-        double big = fabs(A[7 * k]);
-        for (int i = k + 1; i < 6; ++i)
-            if (fabs(A[7 * i]) > big) { big = fabs(A[7 * i]); idx = i; }
+        double big = fabs(__shfl(a[k], k));
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double di = fabs(__shfl(a[i], i));
+            if (di > big) { big = di; idx = i; }
+        }
+        idx = __builtin_amdgcn_readfirstlane(idx);   // uniform: every lane scanned the same values
         tr[k] = idx;
-        if (k != idx) {
-            for (int j = 0; j < k; ++j) { double t = A[6 * k + j]; A[6 * k + j] = A[6 * idx + j]; A[6 * idx + j] = t; }
-            for (int i = idx + 1; i < 6; ++i) { double t = A[6 * i + k]; A[6 * i + k] = A[6 * i + idx]; A[6 * i + idx] = t; }
-            { double t = A[7 * k]; A[7 * k] = A[7 * idx]; A[7 * idx] = t; }
-            for (int i = k + 1; i < idx; ++i) { double t = A[6 * i + k]; A[6 * i + k] = A[6 * idx + i]; A[6 * idx + i] = t; }
+        if (idx != k) {
+            const int partner = lane == k ? idx : (lane == idx ? k : lane);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) a[j] = __shfl(a[j], partner);
+            po_swap6(a, k, idx);
         }
         if (k > 0) {
-            for (int j = 0; j < k; ++j) temp[j] = A[7 * j] * A[6 * k + j];
-            double s = 0.0;
-            for (int j = 0; j < k; ++j) s += A[6 * k + j] * temp[j];
-            A[7 * k] -= s;
-            for (int i = k + 1; i < 6; ++i) {
-                double si = 0.0;
-                for (int j = 0; j < k; ++j) si += A[6 * i + j] * temp[j];
-                A[6 * i + k] -= si;
-            }
+            double temp[6];
+#pragma unroll
+            for (int j = 0; j < k; ++j) temp[j] = dd[j] * __shfl(a[j], k);
+            double si = 0.0;
+#pragma unroll
+            for (int j = 0; j < k; ++j) si += a[j] * temp[j];
+            if (lane >= k) a[k] -= si;
         }
-        const double akk = A[7 * k];
+        const double akk = __shfl(a[k], k);
+        dd[k] = akk;
         const bool valid = fabs(akk) > 0.0;
-        if (k == 0 && !valid) {
+        if (k == 0 && !valid) {   // Eigen: identity transpositions, A left as it is
+#pragma unroll
             for (int j = 0; j < 6; ++j) tr[j] = j;
-            all_zero = 1;
-            break;
+            all_zero = true;
+            continue;
         }
-        if (k < 5 && valid)
-            for (int i = k + 1; i < 6; ++i) A[6 * i + k] /= akk;
+        if (k < 5 && valid && lane > k) a[k] /= akk;
     }
+    (void)all_zero;   // the solves run regardless (LDLT::_solve_impl)
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = b[i];
-    for (int k = 0; k < 6; ++k) { const int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
-    if (!all_zero)
-        for (int k = 0; k < 6; ++k)
-            for (int i = k + 1; i < 6; ++i) x[i] -= A[6 * i + k] * x[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) po_swap6(x, k, tr[k]);
+    double L[6][6];   // L[i][k] = A(i, k), i > k: every lane's copy of the factor
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int i = k; i < 6; ++i) L[i][k] = __shfl(a[k], i);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (x[k] != 0.0)
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) x[i] -= L[i][k] * x[k];
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
-        const double d = A[7 * i];
+        const double d = L[i][i];
         x[i] = (fabs(d) > 2.2250738585072014e-308) ? x[i] / d : 0.0;
     }
-    if (!all_zero)
-        for (int k = 5; k >= 0; --k)
-            for (int i = 0; i < k; ++i) x[i] -= A[6 * k + i] * x[k];
-    for (int k = 5; k >= 0; --k) { const int j = tr[k]; if (j != k) { double t = x[k]; x[k] = x[j]; x[j] = t; } }
+#pragma unroll
+    for (int k = 5; k >= 0; --k)
+#pragma unroll
+        for (int i = 0; i < k; ++i) x[i] -= L[k][i] * x[k];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) po_swap6(x, k, tr[k]);
 }
 
 // VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91)
@@ -1807,8 +1840,7 @@ __device__ void po_pose_add(const double d_in[6], const double* T12, double* out
 
 struct PoShared {
     double pose[12], cand[12], q[4], t[3], K[4];
-    double H[36], b[6], dx[6], A[36], tmp[6];
-    int tr[6];
+    double H[36], b[6], dx[6];
     double red[FT / 64][FV];
     double sum[FV];
     double chi, lam, ni, last, delta;
@@ -1816,15 +1848,12 @@ struct PoShared {
 };
 
 // all FT threads: the workgroup's fixed-order sum of acc[FV] into S.sum
-__device__ __forceinline__ void po_reduce(double acc[FV], PoShared& S, int tid) {
+__device__ __forceinline__ void po_reduce(double (&acc)[FV], PoShared& S, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
+    group_sum(acc, 6);   // DPP within rows, ds_bpermute across them; every lane gets the totals
+    if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < FV; ++k) {
-        double v = acc[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) S.red[wave][k] = v;
-    }
+        for (int k = 0; k < FV; ++k) S.red[wave][k] = acc[k];
     lds_barrier();
     if (tid < FV) {
         double s = 0.0;
@@ -1916,12 +1945,23 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
                 if (tid == 0) { S.flags[0] = 1; S.flags[2] = 0; }   // trial loop, false_cnt
                 lds_barrier();
                 while (S.flags[0]) {
-                    if (tid == 0) {
-                        for (int i = 0; i < 36; ++i) S.A[i] = S.H[i];
-                        for (int i = 0; i < 6; ++i) S.A[7 * i] += (prm.strategy == 0) ? S.lam : S.lam * S.A[7 * i];
-                        po_ldlt6(S.A, S.b, S.dx, S.tr, S.tmp);
-                        po_pose_add(S.dx, S.pose, S.cand);
-                        po_table(S, S.cand);
+                    if (tid < 64) {   // wave 0: H + lambda, the 6x6 solve in registers; lane 0: the update
+                        const int r = tid < 6 ? tid : 5;
+                        double a[6], bb[6], x[6];
+                        const double lam = S.lam;
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) {
+                            a[j] = S.H[6 * r + j];
+                            bb[j] = S.b[j];
+                            if (j == r) a[j] += (prm.strategy == 0) ? lam : lam * a[j];
+                        }
+                        po_ldlt6_wave(a, bb, x, tid);
+                        if (tid == 0) {
+#pragma unroll
+                            for (int j = 0; j < 6; ++j) S.dx[j] = x[j];
+                            po_pose_add(S.dx, S.pose, S.cand);
+                            po_table(S, S.cand);
+                        }
                     }
                     lds_barrier();
                     linearise();   // isGoodStepInLM's residuals (:524) and, if accepted, buildHessian's
