@@ -357,6 +357,13 @@ __device__ __forceinline__ double fast_rsq(double a) {
     return y;
 }
 
+// LDS strides of k_lin's window pose tables and landmark-record stage, padded off the global
+// ones so the entries lanes read at once fall in distinct bank groups: 26 doubles = 52 dwords puts
+// 16 (slot, camera) entries on 16 distinct 4-bank groups (24 gave 4), 18 = 36 dwords puts the 8
+// records of a sub-batch on 8 (16 gave 2).  Both keep 16-byte alignment for b128 loads.
+#define LH_PT_LDS 26
+#define LH_REC_LDS 18
+
 template <int T>
 struct LinCfg {
     static constexpr int NT = T * (T + 1) / 2;          // upper MFMA tiles of the window
@@ -367,7 +374,7 @@ struct LinCfg {
     // the global slab at LH_SLAB_* offsets)
     static constexpr int LS_TASK = NT * 256, LS_SC = LS_TASK + UMAX * LH_TASKS, LS = LS_SC + 8;
     // per-wave LDS scratch: pose-sum image [slot][landmark][33], G image [24][GS], the record
-    // stage (128), and (over the 4 waves) the two combine slabs
+    // stage (8 x LH_REC_LDS), and (over the 4 waves) the two combine slabs
     static constexpr int A_ = UMAX * LH_SB_LM * LH_TASKS, B_ = 3 * LH_SB_LM * GS, C_ = (2 * LS + 3) / 4;
     static constexpr int SCR = ((A_ > B_ ? (A_ > C_ ? A_ : C_) : (B_ > C_ ? B_ : C_)) + 1) & ~1;
 };
@@ -445,16 +452,17 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // the chunk's window, LDS-resident: committed and candidate pose tables per (slot, camera),
     // the pending pose step per slot, the camera extrinsics
     double* wt_c = dsm + LH_WAVES * Cfg::SCR;
-    double* wt_n = wt_c + Cfg::UMAX * ncam * LH_PT;     // a chunk of T tiles has U <= UMAX poses
-    double* wdx = wt_n + Cfg::UMAX * ncam * LH_PT;
+    double* wt_n = wt_c + Cfg::UMAX * ncam * LH_PT_LDS;     // a chunk of T tiles has U <= UMAX poses
+    double* wdx = wt_n + Cfg::UMAX * ncam * LH_PT_LDS;
     double* wext = wdx + Cfg::UMAX * 6;
     {
         const int per = ncam * LH_PT, ne = U * per;
         for (int i = tid; i < ne; i += 256) {
-            const int sl = i / per;
-            const size_t g = (size_t)cpose[sl] * per + (i - sl * per);
-            wt_c[i] = pose_tab[(size_t)cur * PT + g];
-            wt_n[i] = pose_tab[(size_t)cand * PT + g];
+            const int sl = i / per, r = i - sl * per, ent = r / LH_PT;
+            const size_t g = (size_t)cpose[sl] * per + r;
+            const int l = (sl * ncam + ent) * LH_PT_LDS + (r - ent * LH_PT);
+            wt_c[l] = pose_tab[(size_t)cur * PT + g];
+            wt_n[l] = pose_tab[(size_t)cand * PT + g];
         }
         if (TRIAL)
             for (int i = tid; i < 6 * U; i += 256) wdx[i] = dxp[6 * cpose[i / 6] + (i - 6 * (i / 6))];
@@ -520,10 +528,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             v_n = obs_uv[2 * (size_t)on + 1];
             r_n = rc2[(size_t)sbn * 64 + lane];
         }
-        // landmark records through LDS: lane -> its landmark's record
-        reinterpret_cast<double2*>(scr)[lane] = rr;
+        // landmark records through LDS: lane -> its landmark's record (records LH_REC_LDS apart)
+        reinterpret_cast<double2*>(scr)[(lane >> 3) * (LH_REC_LDS / 2) + (lane & 7)] = rr;
         wave_sync();
-        const double* myrec = scr + (ls & 7) * LH_REC;
+        const double* myrec = scr + (ls & 7) * LH_REC_LDS;
         double X[3] = {myrec[LH_REC_X], myrec[LH_REC_X + 1], myrec[LH_REC_X + 2]};
         double cl[12];
         if (TRIAL) {
@@ -553,7 +561,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         if (TRIAL) {
             double v3[3] = {0.0, 0.0, 0.0};
             if (live) {
-                const double* pt = wt_c + (slot * ncam + cam) * LH_PT;
+                const double* pt = wt_c + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
                 if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
                     E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
@@ -602,7 +610,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         // [landmark][slot][33]: unique writer; a wave's 16-lane store group covers distinct cells
         double* trow = scr + ((ls & 7) * Cfg::UMAX + slot) * LH_TASKS;
         if (has) {
-            const double* pt = wt_n + (slot * ncam + cam) * LH_PT;
+            const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
             EdgeEval E;
             edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
             edge_robust(E, prm);
@@ -2053,7 +2061,7 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
 template <int T>
 static size_t lin_smem_bytes(int ncam) {
     using Cfg = LinCfg<T>;
-    return sizeof(double) * ((size_t)LH_WAVES * Cfg::SCR + 2 * (size_t)Cfg::UMAX * ncam * LH_PT + Cfg::UMAX * 6 +
+    return sizeof(double) * ((size_t)LH_WAVES * Cfg::SCR + 2 * (size_t)Cfg::UMAX * ncam * LH_PT_LDS + Cfg::UMAX * 6 +
                              (size_t)ncam * LH_EXT);
 }
 
