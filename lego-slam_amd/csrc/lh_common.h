@@ -23,10 +23,8 @@
 #define LH_TRACE 64
 #define LH_NPAD 128           // reduced system padded size (LDS LDLT)
 
-#define LH_SLAB_TILES (LH_TMAX * (LH_TMAX + 1) / 2)
-#define LH_SLAB_TASK_OFF (LH_SLAB_TILES * 256)
-#define LH_SLAB_SC_OFF (LH_SLAB_TASK_OFF + LH_UMAX * LH_TASKS)
-#define LH_SLAB_STRIDE (LH_SLAB_SC_OFF + 8)
+// pair row (k_lin -> k_reduce): S block landmark part (36) | the pose's 33 sums (diagonal pairs) | pad
+#define LH_ROW 72
 
 // slab scalars
 #define LH_SC_CHI2 0          // sum rho0 (not halved)
@@ -76,6 +74,7 @@ struct lh_chunk {
     uint32_t sb_begin, sb_end;   // sub-batch range
     uint8_t U, T, pad0, pad1;
     uint16_t pose[LH_UMAX];      // window slot -> pose
+    uint32_t item_base;          // the chunk's U(U+1)/2 entries of the row map (items[])
 };
 
 // A sub-batch is one wave's unit of work: n_lm landmarks, landmark l owning the

@@ -32,9 +32,9 @@ hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
-                         double* edge_rho, double* slabs, uint8_t* wflag, long nslots, lh_params prm, int nrec,
-                         uint64_t fixed_mask);
-hipError_t lh_launch_reduce(hipStream_t st, const double* slabs, const uint32_t* pair_ptr, const uint32_t* items,
+                         double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag,
+                         long nslots, lh_params prm, int nrec, uint64_t fixed_mask);
+hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
@@ -249,7 +249,7 @@ struct lh_handle {
     DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
     DevBuf<uint16_t> d_pair_pq;
     DevBuf<int32_t> d_obs_perm, d_lm_perm;
-    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_slabs, d_rs_stage,
+    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_rs_stage,
         d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
@@ -451,7 +451,8 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->d_ext.ensure(LH_EXT * (size_t)ncam));
     HIPCHK(h->d_rho.ensure(pl.n_slots));
     HIPCHK(h->d_wflag.ensure(2 * (size_t)pl.n_slots));
-    HIPCHK(h->d_slabs.ensure((size_t)pl.n_chunks * LH_SLAB_STRIDE));
+    HIPCHK(h->d_rows.ensure((size_t)pl.n_items * LH_ROW));
+    HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
     HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
@@ -504,8 +505,9 @@ int launch_lin(lh_handle* h, int trial) {
     for (int T = 1; T <= LH_TMAX; ++T) {
         const int c0 = h->plan.tgroup_begin[T], c1 = h->plan.tgroup_begin[T + 1];
         HIPCHK(lh_launch_lin(T, trial, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p, h->d_meta.p, h->d_rec.p,
-                             h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p, h->d_rho.p, h->d_slabs.p,
-                             h->d_wflag.p, (long)h->n_slots, h->prm, h->n_rec, h->plan.fixed_mask));
+                             h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p, h->d_rho.p, h->d_rows.p,
+                             h->d_csc.p, h->d_items.p, h->d_wflag.p, (long)h->n_slots, h->prm, h->n_rec,
+                             h->plan.fixed_mask));
         DBGSYNC("k_lin");
     }
     return LH_OK;
@@ -539,7 +541,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     }
     {
         Prof pr(h, KC_REDUCE);
-        HIPCHK(lh_launch_reduce(s, h->d_slabs.p, h->d_pair_ptr.p, h->d_items.p, h->d_pair_pq.p, h->d_ctrl.p,
+        HIPCHK(lh_launch_reduce(s, h->d_rows.p, h->d_csc.p, h->d_pair_ptr.p, h->d_pair_pq.p, h->d_ctrl.p,
                                 h->d_rs_stage.p, h->d_maxd.p, h->prm, h->plan.n_chunks));
         DBGSYNC("k_reduce");
     }
@@ -852,7 +854,7 @@ void lh_destroy(lh_handle* h) {
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
-    h->d_slabs.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
+    h->d_rows.release(); h->d_csc.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
     h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();

@@ -6,7 +6,7 @@
 //             there (residual, SE(3)/point Jacobians, Huber weights, H_pp, H_pl,
 //             H_ll, b), eliminate the landmarks (Schur) — the landmark part as
 //             an f64 MFMA SYRK over a chunk window — and emit one slab per chunk.
-//   k_reduce  fixed-order sum of the slabs into the reduced pose system.
+//   k_reduce  fixed-order sum of the pair rows into the reduced pose system.
 //   k_ctrl    one workgroup: LM accept/reject and lambda schedule
 //             (isGoodStepInLM, problem.cpp:520-581), LDLT of S + lambda
 //             (problem.cpp:406-420), candidate poses T' = exp(dx) T
@@ -370,8 +370,8 @@ struct LinCfg {
     // G row stride: >= 16T and = 16 mod 32 doubles (conflict-free b64 fragment loads)
     static constexpr int GS = (T == 1) ? 16 : (T <= 3 ? 48 : (T <= 5 ? 80 : 112));
     static constexpr int UMAX = (16 * T) / 6;           // window poses that fit 16T rows
-    // the chunk slab as combined in LDS: NT tiles | UMAX x 33 per-pose sums | 4 scalars (written to
-    // the global slab at LH_SLAB_* offsets)
+    // the chunk slab as combined in LDS: NT tiles | UMAX x 33 per-pose sums | 4 scalars (written out
+    // as pair rows and the chunk scalars)
     static constexpr int LS_TASK = NT * 256, LS_SC = LS_TASK + UMAX * LH_TASKS, LS = LS_SC + 8;
     // per-wave LDS scratch: pose-sum image [slot][landmark][33], G image [24][GS], the record
     // stage (8 x LH_REC_LDS), and (over the 4 waves) the two combine slabs
@@ -430,7 +430,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
     const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
-    double* __restrict__ edge_rho, double* __restrict__ slabs, uint8_t* __restrict__ wflag, long nslots,
+    double* __restrict__ edge_rho, double* __restrict__ rows, double* __restrict__ csc,
+    const uint32_t* __restrict__ crow, uint8_t* __restrict__ wflag, long nslots,
     lh_params prm, int nrec, uint64_t fixed_mask, int chunk_base) {
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
@@ -446,6 +447,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const int PT = prm.P * ncam * LH_PT;
     const int U = chunks[chunk].U;
     const uint32_t sb_begin = chunks[chunk].sb_begin, sb_end = chunks[chunk].sb_end;
+    const uint32_t item_base = chunks[chunk].item_base;
     const uint16_t* __restrict__ cpose = chunks[chunk].pose;
 
     double* scr = dsm + wave * Cfg::SCR;
@@ -467,6 +469,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         if (TRIAL)
             for (int i = tid; i < 6 * U; i += 256) wdx[i] = dxp[6 * cpose[i / 6] + (i - 6 * (i / 6))];
         for (int i = tid; i < ncam * LH_EXT; i += 256) wext[i] = ext[i];
+        // the chunk's pair rows (written by the epilogue)
+        uint32_t* wrow = reinterpret_cast<uint32_t*>(wext + ncam * LH_EXT);
+        for (int i = tid; i < U * (U + 1) / 2; i += 256) wrow[i] = crow[item_base + i];
     }
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
@@ -775,8 +780,6 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     lds_barrier();
     STAMP(8);
     double* smem = dsm;
-    const int ntile = Cfg::NT * 256;
-    const int ntask = U * LH_TASKS;
     for (int phase = 0; phase < 2; ++phase) {
         if ((wave >> 1) == phase) {
             double* sl = smem + (wave & 1) * Cfg::LS;
@@ -806,13 +809,33 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         lds_barrier();
     }
     STAMP(9);
+    // the chunk's contribution to each pose pair of its window, one pair row each (pair-major,
+    // rows of one pair contiguous: k_reduce's loads need no index word).  Row: [0, 36) the
+    // landmark part of S block (p, q), row-major; diagonal pairs also [36, 69) the pose's 33 sums.
     const double* s0 = smem;
     const double* s1 = smem + Cfg::LS;
-    double* gs = slabs + (size_t)chunk * LH_SLAB_STRIDE;
-    for (int i = tid; i < ntile; i += 256) gs[i] = s0[i] + s1[i];
-    for (int i = tid; i < ntask; i += 256) gs[LH_SLAB_TASK_OFF + i] = s0[Cfg::LS_TASK + i] + s1[Cfg::LS_TASK + i];
-    if (tid < 3) gs[LH_SLAB_SC_OFF + tid] = s0[Cfg::LS_SC + tid] + s1[Cfg::LS_SC + tid];
-    if (tid == 3) gs[LH_SLAB_SC_OFF + 3] = fmax(s0[Cfg::LS_SC + 3], s1[Cfg::LS_SC + 3]);
+    const uint32_t* wrow = reinterpret_cast<const uint32_t*>(wext + ncam * LH_EXT);
+    {
+        const int a = lane / 6, bb = lane - 6 * (lane / 6);
+        int lp = 0;
+        for (int s = 0; s < U; ++s)
+            for (int t = s; t < U; ++t, ++lp) {
+                if ((lp & (LH_WAVES - 1)) != wave) continue;
+                double* row = rows + (size_t)wrow[lp] * LH_ROW;
+                if (lane < 36) {
+                    int ra = 6 * s + a, rc = 6 * t + bb;
+                    if ((ra >> 4) > (rc >> 4)) { const int x = ra; ra = rc; rc = x; }
+                    const int R = ra >> 4, Cc = rc >> 4;
+                    const int idx = (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15);
+                    row[lane] = s0[idx] + s1[idx];
+                }
+                if (s == t && lane < LH_TASKS)
+                    row[36 + lane] = s0[Cfg::LS_TASK + s * LH_TASKS + lane] + s1[Cfg::LS_TASK + s * LH_TASKS + lane];
+            }
+    }
+    double* gs = csc + (size_t)chunk * 4;
+    if (tid < 3) gs[tid] = s0[Cfg::LS_SC + tid] + s1[Cfg::LS_SC + tid];
+    if (tid == 3) gs[3] = fmax(s0[Cfg::LS_SC + 3], s1[Cfg::LS_SC + 3]);
     STAMP(10);
     STAMP_FLUSH(0, 11);
 }
@@ -828,8 +851,8 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
 #define RT 1024
 #define RW (RT / 64)
 
-__global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs, const uint32_t* __restrict__ pair_ptr,
-                                               const uint32_t* __restrict__ items, const uint16_t* __restrict__ pair_pq,
+__global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, const double* __restrict__ csc,
+                                               const uint32_t* __restrict__ pair_ptr, const uint16_t* __restrict__ pair_pq,
                                                const lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
                                                double* __restrict__ maxd_out, lh_params prm, int n_chunks) {
     STAMP_DECL
@@ -845,7 +868,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
     if (b == LY.npairs) {
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
         for (int c = tid; c < n_chunks; c += RT) {
-            const double* sc = slabs + (size_t)c * LH_SLAB_STRIDE + LH_SLAB_SC_OFF;
+            const double* sc = csc + (size_t)c * 4;
             s0 += sc[0]; s1 += sc[1]; s2 += sc[2]; mx = fmax(mx, sc[3]);
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -869,22 +892,12 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
     const int a = lane / 6, bb = lane - 6 * (lane / 6);
     // lanes 0..35: S entry (a, bb) [+ H_pp entry on the diagonal]; 36..41: b_p; 42..47: bsd
     int off_h = 0;
-    if (lane < 36) off_h = LH_SLAB_TASK_OFF + (diag ? ((a < bb ? a : bb) * 6 - ((a < bb ? a : bb) * ((a < bb ? a : bb) - 1)) / 2 + ((a < bb ? bb : a) - (a < bb ? a : bb))) : 0);
-    else if (lane < 42) off_h = LH_SLAB_TASK_OFF + 21 + (lane - 36);
-    else if (lane < 48) off_h = LH_SLAB_TASK_OFF + 27 + (lane - 42);
+    if (lane < 36) off_h = 36 + (diag ? hpp_index(a < bb ? a : bb, a < bb ? bb : a) : 0);
+    else if (lane < 42) off_h = 36 + 21 + (lane - 36);
+    else if (lane < 48) off_h = 36 + 27 + (lane - 42);
     const bool act_s = lane < 36, act_h = (lane < 36 && diag) || (lane >= 36 && lane < 48 && diag);
-    auto slab_off = [&](uint32_t item, int& off_s, const double*& sl) {
-        const int ch = item >> 11, T = (item >> 8) & 7, sp = (item >> 4) & 15, sq = item & 15;
-        sl = slabs + (size_t)ch * LH_SLAB_STRIDE;
-        int ra = 6 * sp + a, rc = 6 * sq + bb;
-        if ((ra >> 4) > (rc >> 4)) { const int t = ra; ra = rc; rc = t; }
-        const int R = ra >> 4, Cc = rc >> 4;
-        off_s = act_s ? (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15) : 0;
-        return sp;
-    };
-    // Each wave walks its items (wave, wave + RW, ...) in order, eight at a time: the item words are
-    // wave-uniform (scalar loads straight from global, no LDS staging or barrier) and all eight
-    // items' slab loads are in flight together.  Same per-wave order as one item at a time.
+    // Each wave walks its rows (wave, wave + RW, ...) in order, eight at a time; the addresses
+    // follow from the pair's row range alone, so every load of the pair is in flight together.
     double vs = 0.0, vh = 0.0;
     const int w_u = __builtin_amdgcn_readfirstlane(wave);
     for (int base = ib + w_u; base < ie; base += 8 * RW) {
@@ -893,11 +906,9 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ slabs,
         for (int u = 0; u < 8; ++u) {
             const int it = base + u * RW;
             const bool in = it < ie;
-            const uint32_t item = items[in ? it : ib];
-            int off_s; const double* sl;
-            const int sp = slab_off(item, off_s, sl);
-            x[u] = (in && act_s) ? sl[off_s] : 0.0;
-            y[u] = (in && act_h) ? sl[off_h + sp * LH_TASKS] : 0.0;
+            const double* row = rows + (size_t)(in ? it : ib) * LH_ROW;
+            x[u] = (in && act_s) ? row[lane] : 0.0;
+            y[u] = (in && act_h) ? row[off_h] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) { vs += x[u]; vh += y[u]; }
@@ -2062,7 +2073,7 @@ template <int T>
 static size_t lin_smem_bytes(int ncam) {
     using Cfg = LinCfg<T>;
     return sizeof(double) * ((size_t)LH_WAVES * Cfg::SCR + 2 * (size_t)Cfg::UMAX * ncam * LH_PT_LDS + Cfg::UMAX * 6 +
-                             (size_t)ncam * LH_EXT);
+                             (size_t)ncam * LH_EXT + (Cfg::UMAX * (Cfg::UMAX + 1) / 2 + 1) / 2);
 }
 
 // ============================================================================
@@ -2104,7 +2115,8 @@ hipError_t lh_prepare_lin(int lds_limit) {
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
-                         double* edge_rho, double* slabs, uint8_t* wflag, long nslots, lh_params prm, int nrec,
+                         double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag, long nslots,
+                         lh_params prm, int nrec,
                          uint64_t fixed_mask) {
     if (nchunks <= 0) return hipSuccess;
     dim3 g(nchunks), b(256);
@@ -2112,7 +2124,7 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     do {                                                                                                           \
         const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
         hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
-                           edge_rho, slabs, wflag, nslots, prm, nrec, fixed_mask, chunk_base);                     \
+                           edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_mask, chunk_base);             \
     } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
@@ -2133,11 +2145,11 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     return hipGetLastError();
 }
 
-hipError_t lh_launch_reduce(hipStream_t st, const double* slabs, const uint32_t* pair_ptr, const uint32_t* items,
+hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks) {
     const int npairs = prm.P * (prm.P + 1) / 2;
-    hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, slabs, pair_ptr, items, pair_pq, ctrl,
+    hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, rows, csc, pair_ptr, pair_pq, ctrl,
                        rs_stage, maxd, prm, n_chunks);
     return hipGetLastError();
 }

@@ -203,9 +203,14 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     }
     const int Lact = (int)pl.order.size();
 
-    // ---- chunks: ~512 (2 workgroups per CU), multiples of 4 x 8 landmarks (equal work per wave) ----
+    // ---- chunks: at most ~512 (2 workgroups per CU, all resident at once), whole sub-batches of 8
+    //      landmarks.  Rounding up to 8 rather than to 4 x 8 (equal sub-batches per wave) keeps the
+    //      count near 512 (C3: 104 landmarks, 488 chunks of 13 sub-batches, so one wave in four runs
+    //      a fourth sub-batch).  Rounding to 32 gives 128 (398 chunks: 142 CUs run two chunks of
+    //      4 sub-batches per wave, 114 run one), and 96 gives 528 chunks (16 wait for a free slot).
+    //      Measured on C3: k_lin 41.2 us at 104, 44.0 at 128, 51.6 at 96. ----
     int chunk_lm = (Lact + 511) / 512;
-    chunk_lm = ((chunk_lm + 4 * LH_SB_LM - 1) / (4 * LH_SB_LM)) * (4 * LH_SB_LM);
+    chunk_lm = ((chunk_lm + LH_SB_LM - 1) / LH_SB_LM) * LH_SB_LM;
     chunk_lm = std::max(32, std::min(256, chunk_lm));
     if (cfg.chunk_lm > 0) chunk_lm = std::max(LH_SB_LM, std::min(512, cfg.chunk_lm));
     pl.chunk_lm0.clear();
@@ -291,6 +296,11 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     }
     for (int b = 0; b < pl.npairs; ++b) pl.pair_ptr[b + 1] += pl.pair_ptr[b];
     pl.n_items = (int)pl.pair_ptr[pl.npairs];
+    pl.chunk_ib.assign((size_t)NC + 1, 0u);
+    for (int ci = 0; ci < NC; ++ci) {
+        const uint32_t u = (uint32_t)popc(pl.chunk_mask[pl.corder[ci]]);
+        pl.chunk_ib[ci + 1] = pl.chunk_ib[ci] + u * (u + 1) / 2;
+    }
     return LH_OK;
 }
 
@@ -314,6 +324,7 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
         }
         ck.sb_begin = (uint32_t)pl.chunk_sb0[ci];
         ck.sb_end = (uint32_t)pl.chunk_sb0[ci + 1];
+        ck.item_base = pl.chunk_ib[ci];
         out.chunks[ci] = ck;
         const int lm_end = pl.chunk_lm0[c + 1];
         for (int sb = pl.chunk_sb0[ci]; sb < pl.chunk_sb0[ci + 1]; ++sb) {
@@ -356,20 +367,22 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
     if (pool) pool->run(NC, chunk_task);
     else for (int ci = 0; ci < NC; ++ci) chunk_task(ci);
 
-    // reduce plan items: (chunk launch position << 11) | (T << 8) | (slot p << 4) | slot q, per pair in
-    // launch order (k_reduce sums them in this order: a fixed, thread-count-independent order)
+    // reduce plan: pose pair b owns the pair rows pair_ptr[b] .. pair_ptr[b+1], one per chunk whose
+    // window holds both poses, in launch order (k_reduce sums them in this order: a fixed,
+    // thread-count-independent order).  items[] maps each chunk's slot pairs (s <= t, row-major
+    // over its U slots, from chunk_ib) to the row k_lin writes that pair's block into.
     {
         std::vector<uint32_t> cur(pl.pair_ptr.begin(), pl.pair_ptr.end() - 1);
         for (int ci = 0; ci < NC; ++ci) {
             const uint64_t m = pl.chunk_mask[pl.corder[ci]];
-            const int T = chunk_tiles(m);
             int ps[64], U = 0;
             for (uint64_t a = m; a; a &= a - 1) ps[U++] = __builtin_ctzll(a);
+            uint32_t k = pl.chunk_ib[ci];
             for (int s = 0; s < U; ++s)
                 for (int t = s; t < U; ++t) {
                     const int p = ps[s], q = ps[t];
                     const int b = p * P - (p * (p - 1)) / 2 + (q - p);
-                    out.items[cur[b]++] = ((uint32_t)ci << 11) | ((uint32_t)T << 8) | ((uint32_t)s << 4) | (uint32_t)t;
+                    out.items[k++] = cur[b]++;
                 }
         }
     }

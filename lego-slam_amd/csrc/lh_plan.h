@@ -75,6 +75,7 @@ struct Plan {
     std::vector<int32_t> sb_lm0;        // [n_sb + 1] sub-batch -> first position in order[]
     std::vector<uint8_t> sb_lg;         // [n_sb]
     std::vector<uint32_t> pair_ptr;     // [npairs + 1]
+    std::vector<uint32_t> chunk_ib;     // [n_chunks + 1] first item of each chunk (launch order)
 };
 
 struct PlanOut {
@@ -84,7 +85,7 @@ struct PlanOut {
     double* uv;              // [2 n_slots]
     int32_t* obs_perm;       // [n_slots] slot -> window obs (-1: padding)
     int32_t* lm_perm;        // [n_rec] record -> window landmark (-1: padding)
-    uint32_t* items;         // [n_items]
+    uint32_t* items;         // [n_items] per chunk (launch order), per slot pair (s <= t): its pair row
     uint16_t* pair_pq;       // [2 npairs]
     uint32_t* rsmap;         // [npairs * 36]
     double* lm_xyz;          // [3 L] copy of the window's positions

@@ -479,7 +479,7 @@ LH_TMAX = 6
 
 # lh_chunk / lh_subbatch (lego-slam_amd/csrc/lh_common.h)
 CHUNK_DT = np.dtype([("sb_begin", "<u4"), ("sb_end", "<u4"), ("U", "u1"), ("T", "u1"), ("pad", "u1", 2),
-                     ("pose", "<u2", 16)])
+                     ("pose", "<u2", 16), ("item_base", "<u4")])
 SUBBATCH_DT = np.dtype([("lm_begin", "<u4"), ("n_lm", "u1"), ("lg", "u1"), ("pad", "<u2")])
 
 _planlib = None

@@ -56,16 +56,29 @@ def check_plan(w, pl):
     c = chunk_of_sb[sb]
     window_slot = (m >> 16) & 0xF
     assert np.array_equal(ch["pose"][c, window_slot], w["obs_pose"][o])
-    # reduce plan: one item per (chunk, pose pair of its window), per pair in launch order
+    # reduce plan: one pair row per (chunk, slot pair of its window); pair b owns rows
+    # ptr[b] .. ptr[b+1], in launch order; items[] maps each chunk's slot pairs to their rows
     items, ptr, pq = pl["items"].astype(np.int64), pl["pair_ptr"].astype(np.int64), pl["pair_pq"]
     assert len(pq) == P * (P + 1) // 2 and ptr[-1] == len(items)
-    expect = sum(int(u) * (int(u) + 1) // 2 for u in ch["U"])
-    assert len(items) == expect
+    U = ch["U"].astype(np.int64)
+    expect = U * (U + 1) // 2
+    assert len(items) == expect.sum()
+    assert np.array_equal(ch["item_base"].astype(np.int64), np.concatenate([[0], np.cumsum(expect)[:-1]]))
+    assert np.array_equal(np.sort(items), np.arange(len(items)))       # every row written once
+    pair_of = np.zeros(len(items), np.int64)
+    chunk_of_row = np.zeros(len(items), np.int64)
+    for ci in range(len(ch)):
+        k = int(ch["item_base"][ci])
+        for s in range(U[ci]):
+            for t in range(s, U[ci]):
+                p, q = int(ch["pose"][ci, s]), int(ch["pose"][ci, t])
+                b = p * P - p * (p - 1) // 2 + (q - p)
+                r = items[k]
+                assert ptr[b] <= r < ptr[b + 1] and tuple(pq[b]) == (p, q)
+                chunk_of_row[r] = ci
+                k += 1
     for b in range(len(pq)):
-        it = items[ptr[b]:ptr[b + 1]]
-        ci, s, t = it >> 11, (it >> 4) & 15, it & 15
-        assert np.all(np.diff(ci) > 0)
-        assert np.all(ch["pose"][ci, s] == pq[b, 0]) and np.all(ch["pose"][ci, t] == pq[b, 1])
+        assert np.all(np.diff(chunk_of_row[ptr[b]:ptr[b + 1]]) > 0)     # launch order within a pair
     assert np.array_equal(pl["lm_xyz"], w["lm_xyz"])
 
 
