@@ -37,9 +37,10 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks);
+hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
-                          lh_params prm, int mode, int* host_done, int seq);
+                          lh_params prm, int mode, int* host_done, int seq, double* gA);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
                            double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
                            double* dxp, int ndxp, lh_ctrl* ctrl);
@@ -249,7 +250,7 @@ struct lh_handle {
     DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
     DevBuf<uint16_t> d_pair_pq;
     DevBuf<int32_t> d_obs_perm, d_lm_perm;
-    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_rs_stage,
+    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_rs_stage,
         d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
@@ -352,6 +353,8 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     lh::Plan& pl = h->plan;
     int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
     if (st != LH_OK) return st;
+    // past LH_PMAX poses the reduced system is solved in global memory (k_ctrl_g): LDL^T only
+    if (pl.P > LH_PMAX && h->opt.linear_solver != LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
     // a chunk window must fit one CU's LDS
     for (int T = 1; T <= LH_TMAX; ++T)
         if (pl.tgroup_begin[T + 1] > pl.tgroup_begin[T] && lh_lin_smem(T, pl.ncam) > (size_t)h->lds_limit)
@@ -455,6 +458,12 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
+    if (P > LH_PMAX) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once (its unused upper triangle)
+        const size_t ng = (size_t)((6 * P + 31) & ~31);
+        const bool fresh = h->d_gA.n < ng * ng;
+        HIPCHK(h->d_gA.ensure(ng * ng));
+        if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
+    }
     HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
     HIPCHK(h->d_maxd.ensure(1));
     HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
@@ -562,7 +571,8 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     {
         Prof pr(h, KC_CTRL);
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p,
-                              h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial));
+                              h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial,
+                              h->d_gA.p));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -854,7 +864,7 @@ void lh_destroy(lh_handle* h) {
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
-    h->d_rows.release(); h->d_csc.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
+    h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
     h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
@@ -1100,10 +1110,21 @@ int lh_debug_stamps(unsigned long long* out, int n, int reset) {
 }
 
 // test hook: k_ctrl's reduced-system solve on a dense symmetric S, device pointers
+// (n > LH_NPAD: k_ctrl_g's global-memory solve, the windows past LH_PMAX poses)
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x) {
     if (!S || !b || !x) return LH_E_BADARG;
-    if (n < 1 || n > LH_NPAD) return LH_E_UNSUPPORTED;
-    HIPCHK(lh_launch_ldlt_probe(S, b, n, x, 0, 0.0, 0, nullptr));
+    if (n < 1 || n > 6 * LH_PMAX_WIN) return LH_E_UNSUPPORTED;
+    if (n <= LH_NPAD) {
+        HIPCHK(lh_launch_ldlt_probe(S, b, n, x, 0, 0.0, 0, nullptr));
+    } else {
+        const size_t ng = (size_t)((n + 31) & ~31);
+        double* gA = nullptr;
+        HIPCHK(hipMalloc(&gA, ng * ng * sizeof(double)));
+        hipError_t e = lh_launch_ldlt_g_probe(S, b, n, x, gA);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        (void)hipFree(gA);
+        if (e != hipSuccess) return LH_E_HIP;
+    }
     HIPCHK(hipDeviceSynchronize());
     return LH_OK;
 }

@@ -1346,6 +1346,193 @@ __device__ __forceinline__ int lds_pcg_solve(const double* __restrict__ A, doubl
     return it;
 }
 
+// Problem::solve's LM bookkeeping for one trial (thread 0 of either controller): computeLambdaInitLM
+// on the initial linearisation (mode 0, problem.cpp:470-504), else isGoodStepInLM (:520-581), the
+// lambda / nu update, commit or rollback (a buffer index flip), the stop rule and the trace.  mdiag:
+// max |diag| of H_pp and H_ll (mode 0).  Returns the controller's state through done/accept/cur/lam.
+struct CtrlWords {
+    double chi, lam, ni, last, spose, chi0;
+    int iter, fc, trials, nacc, done, cur, tl;
+};
+__device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl) {
+    CtrlWords w;
+    w.chi = ctrl->chi; w.lam = ctrl->lambda; w.ni = ctrl->ni; w.last = ctrl->last_chi; w.spose = ctrl->spose;
+    w.chi0 = ctrl->chi2_initial;
+    w.iter = ctrl->iter; w.fc = ctrl->false_cnt; w.trials = ctrl->trials; w.nacc = ctrl->accepted;
+    w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
+    return w;
+}
+__device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
+                                             int mode, double mdiag, double tchi, double sl, double ndg,
+                                             volatile int* __restrict__ host_done, int& done_o, int& accept_o,
+                                             int& cur_o, double& lam_o) {
+    double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
+    int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
+    int done = w.done, cur = w.cur;
+    int accept = 0, trace = 0;
+    if (!done) {
+        if (mode == 0) {
+            // computeLambdaInitLM (problem.cpp:470-504)
+            ni = 2.0;
+            chi = tchi;
+            chi0 = tchi;
+            if (prm.strategy == 0) {
+                if (!prm.lambda_given) {
+                    double m = fmin(prm.lambda_cap, mdiag);
+                    lam = prm.tau * m;
+                } else {
+                    lam = prm.lambda_init;
+                }
+            } else {
+                lam = 1e-5;
+            }
+            last = 1e20;
+            iter = 0; fc = 0; trials = 0; nacc = 0; tl = 0;
+            ctrl->nonpd = (int)ndg;
+            cur = 1 - cur;           // the initial linearisation becomes the committed one
+            accept = 1;
+            if (prm.max_iters <= 0) done = 1;
+            else trace = 1;
+        } else {
+            // isGoodStepInLM (problem.cpp:520-581)
+            double scale = 0.5 * (spose + sl);
+            scale += 1e-10;
+            const double rho = (chi - tchi) / scale;
+            const bool ok = rho > 0 && isfinite(tchi);
+            if (prm.strategy == 0) {
+                if (ok) {
+                    const double m = 2 * rho - 1;
+                    double alpha = 1.0 - m * m * m;   // std::pow(2 rho - 1, 3), problem.cpp:541 (within an ulp)
+                    alpha = fmin(alpha, 2.0 / 3.0);
+                    lam *= fmax(1.0 / 3.0, alpha);
+                    ni = 2;
+                    chi = tchi;
+                } else {
+                    lam *= ni;
+                    ni *= 2;
+                }
+            } else {
+                if (ok) { lam = fmax(lam / 9.0, 1e-7); chi = tchi; }
+                else lam = fmin(lam * 11.0, 1e7);
+            }
+            trials += 1;
+            bool inner_end;
+            if (ok) {
+                nacc += 1;
+                cur = 1 - cur;       // commit candidate landmarks, caches and poses
+                accept = 1;
+                fc = 0;
+                inner_end = true;
+            } else {
+                fc += 1;             // rollbackStates: the committed buffers are untouched
+                inner_end = fc >= prm.max_trials;
+            }
+            if (inner_end) {
+                iter += 1;
+                if (last - chi < prm.stop_dchi2) done = 1;
+                last = chi;
+                if (!done && iter >= prm.max_iters) done = 1;
+                if (!done) { fc = 0; trace = 1; }
+            }
+        }
+        if (trace) {
+            if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
+            tl += 1;
+        }
+        ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
+        ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
+        ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+        if (done && host_done) *host_done = 1;
+    }
+    done_o = done;
+    accept_o = accept;
+    cur_o = cur;
+    lam_o = lam;
+}
+
+// The controller's tail, shared by both controllers (xs: the pose step in pose order, in LDS):
+// the pose part of the gain denominator (isGoodStepInLM's scale, problem.cpp:528-533, summed into
+// ctrl->spose), the candidate poses (VertexPose::add) and their pose tables.  All CT threads.
+template <int PM>
+__device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
+                                               int cur, const double* xs, const double* bpv, const double* hdv,
+                                               double* s_red, double (*s_pm)[PM * 12], double (*s_trig)[4],
+                                               double (*s_qT)[4], double* __restrict__ pose_mat,
+                                               double* __restrict__ ptab, const double* __restrict__ ext) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = prm.P;
+    // ---------------- pose part of the gain denominator; candidate poses ----------------
+    double sp = 0.0;
+    if (tid < n) {
+        const double d = xs[tid], b = bpv[tid];
+        sp = (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[tid] * d + b);
+    }
+    for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
+    if (lane == 0) s_red[wave] = sp;
+    const int cand = 1 - cur;
+    // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix(), one pose per
+    // lane in three steps: (1) wave 0 sin/cos(theta/2), wave 1 sin/cos(theta), wave 2 the current
+    // quaternion; (2) wave 0 composes; (3) one lane per (pose, camera) builds the pose table
+    auto pose_step = [&](int pidx, double up[6]) {
+        bool bad = false;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
+        if (bad) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
+        }
+    };
+    if (wave < 2 && lane < P) {
+        double up[6];
+        pose_step(lane, up);
+        const double th = d_twist_theta(up);
+        double sn, cs;
+        sincos(wave == 0 ? 0.5 * th : th, &sn, &cs);
+        s_trig[lane][2 * wave] = sn;
+        s_trig[lane][2 * wave + 1] = cs;
+    } else if (wave == 2 && lane < P) {
+        const double* Tc = &s_pm[cur][lane * 12];
+        const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
+        d_q_from_R(Rc, s_qT[lane]);
+    }
+    lds_barrier();
+    CSTAMP(9);
+    if (wave == 0 && lane < P) {
+        const int pidx = lane;
+        double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
+        pose_step(pidx, up);
+        d_se3_exp_trig(up, s_trig[pidx][0], s_trig[pidx][1], s_trig[pidx][2], s_trig[pidx][3], qe, te);
+        const double* Tc = &s_pm[cur][pidx * 12];
+        const double tc[3] = {Tc[3], Tc[7], Tc[11]};
+        d_q_mul(qe, s_qT[pidx], qn);
+        d_q_rotate(qe, tc, tr);
+        d_R_from_q(qn, Rn);
+        double* To = &s_pm[cand][pidx * 12];   // the candidate buffer's LDS copy is free after the solve
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
+            To[4 * i + 3] = te[i] + tr[i];
+        }
+    }
+    lds_barrier();
+    CSTAMP(10);
+    if (tid < 12 * P) pose_mat[(size_t)cand * P * 12 + tid] = s_pm[cand][tid];
+    if (tid >= 64 && tid < 64 + P * prm.ncam) {
+        const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
+        double To[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pidx * 12 + i];
+        d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
+    }
+    lds_barrier();
+    CSTAMP(11);
+    if (tid == 0) {
+        double s2 = 0.0;
+        for (int w = 0; w < CT / 64; ++w) s2 += s_red[w];
+        ctrl->spose = s2;
+    }
+}
+
 template <int SOLVER>
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
@@ -1371,20 +1558,17 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #endif
 
     // ---------------- 1. prefetch (one round trip); the controller's words first ----------------
-    double chi = 0.0, lam = 0.0, ni = 0.0, last = 0.0, spose = 0.0, chi0 = 0.0, tchi = 0.0, sl = 0.0, ndg = 0.0;
-    int iter = 0, fc = 0, trials = 0, nacc = 0, done0 = 1, cur0 = 0, tl = 0;
+    double tchi = 0.0, sl = 0.0, ndg = 0.0;
+    CtrlWords cw{};
     if (tid == 0) {
-        chi = ctrl->chi; lam = ctrl->lambda; ni = ctrl->ni; last = ctrl->last_chi; spose = ctrl->spose;
-        chi0 = ctrl->chi2_initial;
-        iter = ctrl->iter; fc = ctrl->false_cnt; trials = ctrl->trials; nacc = ctrl->accepted;
-        done0 = ctrl->done; cur0 = ctrl->cur; tl = ctrl->trace_len;
+        cw = ctrl_load(ctrl);
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
         // host progress word: this live trial's controller has started (its k_lin and k_reduce are
         // done).  The host keeps the queue filled from it; it never advances past the stop trial,
         // which bounds how many trials (and all-reduces) any rank can have enqueued.
-        if (host_done && !done0) host_done[1] = seq;
+        if (host_done && !cw.done) host_done[1] = seq;
     }
     double vs[NLD], vc[NLD];
     uint32_t mp[NLD];
@@ -1414,89 +1598,18 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 
     // ---------------- LM bookkeeping (thread 0) ----------------
     if (tid == 0) {
-        int done = done0, cur = cur0;
-        int accept = 0, trace = 0;
-        if (!done) {
-            if (mode == 0) {
-                // computeLambdaInitLM (problem.cpp:470-504)
-                ni = 2.0;
-                chi = tchi;
-                chi0 = tchi;
-                if (prm.strategy == 0) {
-                    if (!prm.lambda_given) {
-                        double m = 0.0;
-                        for (int w = 0; w < CT / 64; ++w) m = fmax(m, s_red[w]);
-                        m = fmax(*maxd_in, m);
-                        m = fmin(prm.lambda_cap, m);
-                        lam = prm.tau * m;
-                    } else {
-                        lam = prm.lambda_init;
-                    }
-                } else {
-                    lam = 1e-5;
-                }
-                last = 1e20;
-                iter = 0; fc = 0; trials = 0; nacc = 0; tl = 0;
-                ctrl->nonpd = (int)ndg;
-                cur = 1 - cur;           // the initial linearisation becomes the committed one
-                accept = 1;
-                if (prm.max_iters <= 0) done = 1;
-                else trace = 1;
-            } else {
-                // isGoodStepInLM (problem.cpp:520-581)
-                double scale = 0.5 * (spose + sl);
-                scale += 1e-10;
-                const double rho = (chi - tchi) / scale;
-                const bool ok = rho > 0 && isfinite(tchi);
-                if (prm.strategy == 0) {
-                    if (ok) {
-                        const double m = 2 * rho - 1;
-                        double alpha = 1.0 - m * m * m;   // std::pow(2 rho - 1, 3), problem.cpp:541 (within an ulp)
-                        alpha = fmin(alpha, 2.0 / 3.0);
-                        lam *= fmax(1.0 / 3.0, alpha);
-                        ni = 2;
-                        chi = tchi;
-                    } else {
-                        lam *= ni;
-                        ni *= 2;
-                    }
-                } else {
-                    if (ok) { lam = fmax(lam / 9.0, 1e-7); chi = tchi; }
-                    else lam = fmin(lam * 11.0, 1e7);
-                }
-                trials += 1;
-                bool inner_end;
-                if (ok) {
-                    nacc += 1;
-                    cur = 1 - cur;       // commit candidate landmarks, caches and poses
-                    accept = 1;
-                    fc = 0;
-                    inner_end = true;
-                } else {
-                    fc += 1;             // rollbackStates: the committed buffers are untouched
-                    inner_end = fc >= prm.max_trials;
-                }
-                if (inner_end) {
-                    iter += 1;
-                    if (last - chi < prm.stop_dchi2) done = 1;
-                    last = chi;
-                    if (!done && iter >= prm.max_iters) done = 1;
-                    if (!done) { fc = 0; trace = 1; }
-                }
-            }
-            if (trace) {
-                if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
-                tl += 1;
-            }
-            ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
-            ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
-            ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
-            if (done && host_done) *host_done = 1;
+        double mdiag = 0.0;
+        if (mode == 0) {
+            for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
+            mdiag = fmax(*maxd_in, mdiag);
         }
+        int done, accept, cur;
+        double lam_n;
+        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, done, accept, cur, lam_n);
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
-        s_lam = lam;
+        s_lam = lam_n;
     }
     lds_barrier();
     const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
@@ -1592,80 +1705,299 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     lds_barrier();
     CSTAMP(8);
 
-    // ---------------- pose part of the gain denominator; candidate poses ----------------
-    double sp = 0.0;
-    if (tid < n) {
-        const double d = xs[tid], b = bpv[tid];
-        sp = (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[tid] * d + b);
-    }
-    for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
-    if (lane == 0) s_red[wave] = sp;
-    const int cand = 1 - cur;
-    // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix(), one pose per
-    // lane in three steps: (1) wave 0 sin/cos(theta/2), wave 1 sin/cos(theta), wave 2 the current
-    // quaternion; (2) wave 0 composes; (3) one lane per (pose, camera) builds the pose table
-    auto pose_step = [&](int pidx, double up[6]) {
-        bool bad = false;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
-        if (bad) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
-        }
-    };
-    if (wave < 2 && lane < P) {
-        double up[6];
-        pose_step(lane, up);
-        const double th = d_twist_theta(up);
-        double sn, cs;
-        sincos(wave == 0 ? 0.5 * th : th, &sn, &cs);
-        s_trig[lane][2 * wave] = sn;
-        s_trig[lane][2 * wave + 1] = cs;
-    } else if (wave == 2 && lane < P) {
-        const double* Tc = &s_pm[cur][lane * 12];
-        const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
-        d_q_from_R(Rc, s_qT[lane]);
-    }
-    lds_barrier();
-    CSTAMP(9);
-    if (wave == 0 && lane < P) {
-        const int pidx = lane;
-        double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
-        pose_step(pidx, up);
-        d_se3_exp_trig(up, s_trig[pidx][0], s_trig[pidx][1], s_trig[pidx][2], s_trig[pidx][3], qe, te);
-        const double* Tc = &s_pm[cur][pidx * 12];
-        const double tc[3] = {Tc[3], Tc[7], Tc[11]};
-        d_q_mul(qe, s_qT[pidx], qn);
-        d_q_rotate(qe, tc, tr);
-        d_R_from_q(qn, Rn);
-        double* To = &s_pm[cand][pidx * 12];   // the candidate buffer's LDS copy is free after the solve
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
-            To[4 * i + 3] = te[i] + tr[i];
-        }
-    }
-    lds_barrier();
-    CSTAMP(10);
-    if (tid < 12 * P) pose_mat[(size_t)cand * P * 12 + tid] = s_pm[cand][tid];
-    if (tid >= 64 && tid < 64 + P * prm.ncam) {
-        const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
-        double To[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pidx * 12 + i];
-        d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
-    }
-    lds_barrier();
-    CSTAMP(11);
-    if (tid == 0) {
-        double s2 = 0.0;
-        for (int w = 0; w < CT / 64; ++w) s2 += s_red[w];
-        ctrl->spose = s2;
-    }
+    ctrl_pose_tail<LH_PMAX>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
+}
+
+// ============================================================================
+// k_ctrl_g: the controller for windows past LH_PMAX poses (21 < P <= LH_PMAX_WIN, 6P <= 384 rows).
+// Same LM bookkeeping and pose tail as k_ctrl; the reduced system lives in global memory (gA,
+// row-major, stride NG = ceil32(6P), L2-resident: <= 1.2 MB) instead of one CU's LDS.  Eigen's
+// pivot order is the same static sort of |diag(S + lambda D)|.  The factorisation is a blocked
+// right-looking LDL^T over 32-column panels:
+//   (a) the panel (rows K.., columns K..K+31) into LDS;
+//   (b) its 32x32 diagonal block by wave 0 in registers (lane r = row r; pivots and column
+//       entries by lane broadcast);
+//   (c) the panel rows below: one thread per row, 32 columns in registers;
+//   (d) L and D back to gA;
+//   (e) the trailing block, A_ij -= sum_k L_ik (D_k L_jk), as 16x16 f64 MFMA tiles (one wave per
+//       tile, 8 MFMAs over the panel).
+// Eigen semantics kept: a zero pivot skips the division (pivot_is_valid); if the largest |diag| is
+// 0 there is no factorisation and the solves run on the raw matrix with identity transpositions.
+// The triangular solves visit each row's terms in the oracle's order (ldlt_solve: ascending
+// columns, 8-row panels whose zero entries skip in-panel updates; descending in L^T), so they
+// are bitwise the oracle's solve of the same factor.  The factor's rounding differs from Eigen's
+// left-looking dot products (parity to tolerance).
+// ============================================================================
+#define GNB 32                          // panel width
+#define GNMAX (6 * LH_PMAX_WIN)         // largest reduced system
+#define GPS (GNB + 1)                   // LDS panel row stride (conflict-free column reads)
+
+// k_ctrl_g's reduced-system solve (shared with the probe): gA holds the permuted system's lower
+// triangle (stride NG, identity padding to NG), yv the permuted right-hand side (LDS, n entries);
+// on return yv holds the solution in pivot order and gA the factor.  All CT threads.
+__device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, int n, bool all_zero, double* yv,
+                                             double* pnl) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ double ginv[GNB];   // 1/D of the current block's pivots (1 where the pivot is invalid)
+    // ---------------- blocked right-looking LDL^T ----------------
+    if (!all_zero) {
+        for (int K = 0; K < NG; K += GNB) {
+            const int m = NG - K;
+            // (a) the panel into LDS (lower part of the diagonal block, all of the rows below)
+            for (int x = tid; x < m * GNB; x += CT) {
+                const int r = x / GNB, c = x - GNB * (x / GNB);
+                pnl[r * GPS + c] = (r >= c) ? gA[(size_t)(K + r) * NG + K + c] : 0.0;
+            }
+            lds_barrier();
+            // (b) the diagonal block: wave 0, lane r updates row r in place (LDS accesses of one wave
+            //     are in order: the L column written for step k is what the updates read)
+            if (wave == 0) {
+                const int r = lane;
+                for (int k = 0; k < GNB; ++k) {
+                    const double d = pnl[k * GPS + k];
+                    const double id = (fabs(d) > 0.0) ? fast_rcp(d) : 1.0;   // pivot_is_valid: no division
+                    if (lane == k) ginv[k] = id;
+                    double l = 0.0;
+                    if (r > k && r < GNB) {
+                        l = pnl[r * GPS + k] * id;
+                        pnl[r * GPS + k] = l;
+                    }
+                    wave_sync();
+                    if (r > k && r < GNB)
+                        for (int j = k + 1; j <= r; ++j) pnl[r * GPS + j] -= l * (d * pnl[j * GPS + k]);
+                    wave_sync();
+                }
+            }
+            lds_barrier();
+            // (c) the panel rows below the block.  W = D_j L(k, j) (k > j) into the diagonal block's
+            //     free upper triangle; then per row, column k takes the updates of columns j < k in
+            //     ascending j (the right-looking order and roundings) and its pivot reciprocal.
+            if (wave == 0 && lane < GNB)
+                for (int k = lane + 1; k < GNB; ++k) pnl[lane * GPS + k] = pnl[lane * GPS + lane] * pnl[k * GPS + lane];
+            lds_barrier();
+            for (int r = GNB + tid; r < m; r += CT) {
+                double* row = pnl + r * GPS;
+                for (int k = 0; k < GNB; ++k) {
+                    double a = row[k];
+#pragma unroll 4
+                    for (int j = 0; j < k; ++j) a -= row[j] * pnl[j * GPS + k];
+                    row[k] = a * ginv[k];
+                }
+            }
+            lds_barrier();
+            // (d) L and D of the panel back to gA
+            for (int x = tid; x < m * GNB; x += CT) {
+                const int r = x / GNB, c = x - GNB * (x / GNB);
+                if (r >= c) gA[(size_t)(K + r) * NG + K + c] = pnl[r * GPS + c];
+            }
+            // (e) trailing block: 16x16 tiles (I >= J), one wave each
+            const int mt = (m - GNB) >> 4;
+            const int ntiles = mt * (mt + 1) / 2;
+            for (int t = wave; t < ntiles; t += CT / 64) {
+                int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+                while ((I + 1) * (I + 2) / 2 <= t) ++I;
+                while (I * (I + 1) / 2 > t) --I;
+                const int J = t - I * (I + 1) / 2;
+                const int r0 = K + GNB + 16 * I, c0 = K + GNB + 16 * J;
+                v4d acc;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[v] = gA[(size_t)(r0 + (lane >> 4) + 4 * v) * NG + c0 + (lane & 15)];
+#pragma unroll
+                for (int kk = 0; kk < GNB; kk += 4) {
+                    const int k = kk + (lane >> 4);
+                    const double av = -pnl[(GNB + 16 * I + (lane & 15)) * GPS + k];
+                    const double bv = pnl[k * GPS + k] * pnl[(GNB + 16 * J + (lane & 15)) * GPS + k];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) gA[(size_t)(r0 + (lane >> 4) + 4 * v) * NG + c0 + (lane & 15)] = acc[v];
+            }
+            __syncthreads();
+        }
+    }
+
+    // ---------------- forward substitution (unit L), the oracle's order ----------------
+    for (int K = 0; K < n; K += GNB) {
+        const int kb = min(GNB, n - K);
+        if (wave == 0) {
+            const int r = lane & (GNB - 1);
+            double x = yv[K + r];
+            double Lr[GNB];
+#pragma unroll
+            for (int k = 0; k < GNB; ++k) Lr[k] = (r > k && K + r < n) ? gA[(size_t)(K + r) * NG + K + k] : 0.0;
+#pragma unroll
+            for (int k = 0; k < GNB; ++k) {
+                const double xk = __shfl(x, k);
+                if (k < kb && r > k && r < kb) {
+                    const bool same_panel = (r >> 3) == (k >> 3);
+                    if (!same_panel || xk != 0.0) x -= Lr[k] * xk;
+                }
+            }
+            if (lane < kb) yv[K + lane] = x;
+        }
+        lds_barrier();
+        for (int i = K + kb + tid; i < n; i += CT) {
+            double x = yv[i];
+            for (int k = 0; k < kb; ++k) x -= gA[(size_t)i * NG + K + k] * yv[K + k];
+            yv[i] = x;
+        }
+        lds_barrier();
+    }
+    // D^+ (tolerance: numeric_limits<double>::min())
+    for (int i = tid; i < n; i += CT) {
+        const double d = gA[(size_t)i * NG + i];
+        yv[i] = (fabs(d) > 2.2250738585072014e-308) ? yv[i] / d : 0.0;
+    }
+    lds_barrier();
+    // ---------------- back substitution (L^T), descending ----------------
+    for (int K = ((n - 1) / GNB) * GNB; K >= 0; K -= GNB) {
+        const int kb = min(GNB, n - K);
+        if (wave == 0) {
+            const int r = lane & (GNB - 1);
+            double x = yv[K + r];
+            double Lc[GNB];
+#pragma unroll
+            for (int k = 0; k < GNB; ++k) Lc[k] = (k > r && k < kb) ? gA[(size_t)(K + k) * NG + K + r] : 0.0;
+#pragma unroll
+            for (int k = GNB - 1; k >= 0; --k) {
+                const double xk = __shfl(x, k);
+                if (k < kb && r < k) x -= Lc[k] * xk;
+            }
+            if (lane < kb) yv[K + lane] = x;
+        }
+        lds_barrier();
+        for (int i = tid; i < K; i += CT) {
+            double x = yv[i];
+            for (int k = kb - 1; k >= 0; --k) x -= gA[(size_t)(K + k) * NG + i] * yv[K + k];
+            yv[i] = x;
+        }
+        lds_barrier();
+    }
+}
+
+__global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
+                                               const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
+                                               const uint32_t* __restrict__ rsmap, double* __restrict__ pose_mat,
+                                               double* __restrict__ ptab, const double* __restrict__ ext,
+                                               double* __restrict__ dxp, lh_params prm, int mode,
+                                               volatile int* __restrict__ host_done, int seq, double* __restrict__ gA) {
+    __shared__ double pnl[GNMAX * GPS];
+    __shared__ double dg[GNMAX], bsv[GNMAX], bpv[GNMAX], hdv[GNMAX], xs[GNMAX], yv[GNMAX];
+    __shared__ int perm[GNMAX], iperm[GNMAX];
+    __shared__ int s_flags[4];
+    __shared__ double s_red[CT / 64], s_lam;
+    __shared__ double s_pm[2][LH_PMAX_WIN * 12];
+    __shared__ double s_trig[LH_PMAX_WIN][4], s_qT[LH_PMAX_WIN][4];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = prm.P, n = 6 * P, NG = (n + GNB - 1) & ~(GNB - 1);
+    const lh_rs_layout LY = lh_rs_make(P);
+
+    // ---------------- controller words, pose matrices, max |diag| (mode 0) ----------------
+    double tchi = 0.0, sl = 0.0, ndg = 0.0;
+    CtrlWords cw{};
+    if (tid == 0) {
+        cw = ctrl_load(ctrl);
+        tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
+        sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+        ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
+        if (host_done && !cw.done) host_done[1] = seq;
+    }
+    for (int i = tid; i < 24 * P; i += CT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
+    {
+        double mx = 0.0;
+        if (mode == 0)
+            for (int i = tid; i < n; i += CT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
+        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+        if (lane == 0) s_red[wave] = mx;
+    }
+    lds_barrier();
+    if (tid == 0) {
+        double mdiag = 0.0;
+        if (mode == 0) {
+            for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
+            mdiag = fmax(*maxd_in, mdiag);
+        }
+        int done, accept, cur;
+        double lam_n;
+        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, done, accept, cur, lam_n);
+        s_flags[0] = done;
+        s_flags[1] = accept;
+        s_flags[2] = cur;
+        s_lam = lam_n;
+    }
+    lds_barrier();
+    const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
+    if (done) return;
+    const double lambda = s_lam;
+
+    // ---------------- commit; diagonal + lambda; right-hand sides ----------------
+    const double* __restrict__ src = accept ? rs_stage : rs_commit;
+    for (int i = tid; i < LY.total; i += CT) {
+        const double v = src[i];
+        if (accept) rs_commit[i] = v;
+        if (i < LY.off_bs) {
+            const uint32_t m = rsmap[i];
+            const int gi = LH_RSMAP_ROW(m), gj = LH_RSMAP_COL(m);
+            if (gi == gj) dg[gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
+        } else if (i < LY.off_bp) {
+            bsv[i - LY.off_bs] = v;
+        } else if (i < LY.off_hd) {
+            bpv[i - LY.off_bp] = v;
+        } else if (i < LY.off_hd + n) {
+            hdv[i - LY.off_hd] = v;
+        }
+    }
+    lds_barrier();
+
+    // ---------------- pivot order: |diag| descending, ties by index, NaN last (as k_ctrl) ----------------
+    for (int row = tid; row < n; row += CT) {
+        double di = fabs(dg[row]);
+        if (!(di == di)) di = -1.0;
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            double d = fabs(dg[j]);
+            if (!(d == d)) d = -1.0;
+            r += (d > di) || (d == di && j < row);
+        }
+        perm[r] = row;
+        iperm[row] = r;
+    }
+    lds_barrier();
+    // Eigen's k = 0 test: the largest |diag| is not > 0 -> identity transpositions, no factorisation
+    const bool all_zero = !(fabs(dg[perm[0]]) > 0.0);
+    lds_barrier();
+    if (all_zero)
+        for (int i = tid; i < n; i += CT) { perm[i] = i; iperm[i] = i; }
+    lds_barrier();
+
+    // ---------------- the permuted system into gA (lower triangle), identity padding ----------------
+    for (int i = tid; i < LY.off_bs; i += CT) {
+        const uint32_t m = rsmap[i];
+        const int ri = iperm[LH_RSMAP_ROW(m)], rj = iperm[LH_RSMAP_COL(m)];
+        const double v = src[i];
+        if (!LH_RSMAP_DIAG(m)) gA[(size_t)max(ri, rj) * NG + min(ri, rj)] = v;
+        else if (ri > rj) gA[(size_t)ri * NG + rj] = v;
+    }
+    for (int i = tid; i < NG; i += CT) {
+        gA[(size_t)i * NG + i] = i < n ? dg[perm[i]] : 1.0;
+        yv[i] = i < n ? bsv[perm[i]] : 0.0;
+    }
+    for (int x = tid; x < (NG - n) * NG; x += CT) {
+        const int r = n + x / NG, c = x - NG * (x / NG);
+        if (c < r) gA[(size_t)r * NG + c] = 0.0;
+    }
+    __syncthreads();   // global stores before the panel loads
+
+    g_ldlt_solve(gA, NG, n, all_zero, yv, pnl);
+    if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
+    for (int i = CT + tid; i < n; i += CT) { xs[perm[i]] = yv[i]; dxp[perm[i]] = yv[i]; }
+    lds_barrier();
+    ctrl_pose_tail<LH_PMAX_WIN>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
 }
 
 // ============================================================================
@@ -2156,8 +2488,11 @@ hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* cs
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
-                          int* host_done, int seq) {
-    if (prm.solver == 1)
+                          int* host_done, int seq, double* gA) {
+    if (prm.P > LH_PMAX)
+        hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
+                           dxp, prm, mode, (volatile int*)host_done, seq, gA);
+    else if (prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     else
@@ -2280,6 +2615,52 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     }
     lds_barrier();
     if (tid < n) x[perm[tid]] = xsol[tid];
+}
+
+// ---- the same probe through k_ctrl_g's global-memory solve (LH_NPAD < n <= 6 LH_PMAX_WIN):
+//      gA: scratch of ceil32(n)^2 doubles ----
+__global__ __launch_bounds__(CT) void k_ldlt_g_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
+                                                     double* __restrict__ x, double* __restrict__ gA) {
+    __shared__ double pnl[GNMAX * GPS];
+    __shared__ double dg[GNMAX], yv[GNMAX];
+    __shared__ int perm[GNMAX], iperm[GNMAX];
+    const int tid = threadIdx.x, NG = (n + GNB - 1) & ~(GNB - 1);
+    for (int i = tid; i < n; i += CT) dg[i] = S[(size_t)i * n + i];
+    lds_barrier();
+    for (int row = tid; row < n; row += CT) {
+        double di = fabs(dg[row]);
+        if (!(di == di)) di = -1.0;
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            double d = fabs(dg[j]);
+            if (!(d == d)) d = -1.0;
+            r += (d > di) || (d == di && j < row);
+        }
+        perm[r] = row;
+        iperm[row] = r;
+    }
+    lds_barrier();
+    const bool all_zero = !(fabs(dg[perm[0]]) > 0.0);
+    lds_barrier();
+    if (all_zero)
+        for (int i = tid; i < n; i += CT) { perm[i] = i; iperm[i] = i; }
+    lds_barrier();
+    for (int x2 = tid; x2 < NG * NG; x2 += CT) {
+        const int r = x2 / NG, c = x2 - NG * (x2 / NG);
+        double v = 0.0;
+        if (r < n && c < n) v = (c <= r) ? S[(size_t)perm[r] * n + perm[c]] : 0.0;
+        else if (r == c) v = 1.0;
+        gA[x2] = v;
+    }
+    for (int i = tid; i < NG; i += CT) yv[i] = i < n ? b[perm[i]] : 0.0;
+    __syncthreads();
+    g_ldlt_solve(gA, NG, n, all_zero, yv, pnl);
+    for (int i = tid; i < n; i += CT) x[perm[i]] = yv[i];
+}
+
+hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA) {
+    hipLaunchKernelGGL(k_ldlt_g_probe, dim3(1), dim3(CT), 0, 0, S, b, n, x, gA);
+    return hipGetLastError();
 }
 
 hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x, int solver, double tol, int max_it,

@@ -119,7 +119,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     });
     if (bad.load()) return LH_E_BADARG;
     if (!allow_empty && (O == 0 || (P + L) == 0)) return LH_E_EMPTY;   // problem.cpp:157-161
-    if (P > LH_PMAX) return LH_E_UNSUPPORTED;   // the reduced pose system is solved in one CU's LDS
+    if (P > LH_PMAX_WIN) return LH_E_UNSUPPORTED;   // 64-bit pose masks (P > LH_PMAX: k_ctrl_g, global memory)
     if (O >= (int64_t)1 << 30) return LH_E_UNSUPPORTED;                 // int32 slot indices
     pl.fixed_mask = 0;
     if (w->pose_fixed)

@@ -57,10 +57,11 @@ def _ldlt_probe(S, b):
     return xt.cpu().numpy()
 
 
-@pytest.mark.parametrize("n", [6, 12, 60, 96, 114, 120, 126])
+@pytest.mark.parametrize("n", [6, 12, 60, 96, 114, 120, 126, 132, 186, 258, 384])
 def test_reduced_solve_spd(n):
     """k_ctrl's blocked LDL^T + solve (through the test hook) against numpy on SPD systems
-    shaped like S + lambda I (problem.cpp:404-420): block-banded, wide diagonal spread."""
+    shaped like S + lambda I (problem.cpp:404-420): block-banded, wide diagonal spread.  Past 128
+    rows (windows past 21 poses) the hook runs k_ctrl_g's global-memory solve."""
     rng = np.random.default_rng(n)
     P = n // 6
     S = np.zeros((n, n))
@@ -75,11 +76,11 @@ def test_reduced_solve_spd(n):
     assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
 
 
-def test_reduced_solve_zero_rows():
+@pytest.mark.parametrize("n", [60, 222])
+def test_reduced_solve_zero_rows(n):
     """STRATEGY1 with a fixed pose: exactly-zero rows and columns (diag 0 + lambda*0); Eigen's
     LDLT pivots them last, skips the invalid pivots and returns 0 there (LDLT::_solve_impl)."""
     rng = np.random.default_rng(7)
-    n = 60
     M = rng.standard_normal((n, n))
     S = M @ M.T + n * np.eye(n)
     S[:6, :] = 0.0
@@ -90,6 +91,19 @@ def test_reduced_solve_zero_rows():
     assert np.all(x[:6] == 0.0)
     xr = np.linalg.solve(S[6:, 6:], b[6:])
     assert np.allclose(x[6:], xr, rtol=1e-11, atol=1e-13)
+
+
+@pytest.mark.parametrize("n", [138, 240, 384])
+def test_reduced_solve_global_vs_oracle(n):
+    """k_ctrl_g's solve against the oracle's restatement of Eigen's LDLT (ldlt_solve: the same
+    pivot order, the same triangular-solve order); only the factor's rounding differs."""
+    rng = np.random.default_rng(100 + n)
+    M = rng.standard_normal((n, n))
+    S = M @ M.T + np.diag(10.0 ** rng.uniform(0, 6, n))
+    b = rng.standard_normal(n)
+    x = _ldlt_probe(S, b)
+    xo = ob.ldlt_solve(S, b)
+    assert np.linalg.norm(x - xo) <= 1e-11 * np.linalg.norm(xo)
 
 
 @pytest.mark.parametrize("cfg,seed,family", [("C1", 0, "default"), ("C1", 1, "stable"), ("mini", 0, "default"),
@@ -304,8 +318,9 @@ def test_random_pose_subsets_all_tile_counts(kmin, kmax):
     assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
 
 
-def test_largest_supported_window_p21():
-    """P = 21 keyframes: the 126 x 126 reduced system (two identity padding rows in LDS)."""
+def test_largest_lds_window_p21():
+    """P = 21 keyframes: the largest reduced system k_ctrl factors in LDS (126 x 126, two
+    identity padding rows)."""
     w = lego_ba.generate_window(P=21, L=3000, k=8, seed=4, **dict(__import__("windows").STABLE, outlier_frac=0.0))
     f = np.zeros(21, np.uint8)
     f[0] = 1
@@ -314,9 +329,56 @@ def test_largest_supported_window_p21():
     o, spread, its = oracle_envelope(w, threads=(1, 2, 8))
     assert g["iterations"] in its
     assert rel(g["chi2_final"], o["chi2_final"]) < max(1e-6, 10 * spread)
-    with pytest.raises(lego_ba.LhError) as e:     # one keyframe more is outside the envelope
-        w22 = lego_ba.generate_window(P=22, L=500, k=8, seed=4)
-        lego_ba.Solver().solve(w22)
+
+
+def _stable_window(P, L, seed, **kw):
+    w = lego_ba.generate_window(P=P, L=L, k=8, seed=seed, **dict(__import__("windows").STABLE, outlier_frac=0.0), **kw)
+    f = np.zeros(P, np.uint8)
+    f[0] = 1
+    w["pose_fixed"] = f
+    return w
+
+
+@pytest.mark.parametrize("P,L,seed,mode", [(22, 3000, 4, 0), (32, 4000, 1, 0), (40, 3000, 3, 1), (64, 6000, 2, 0)])
+def test_large_windows_global_memory_solve(P, L, seed, mode):
+    """Windows past 21 keyframes (the reference solver takes any number, problem.cpp:277-279):
+    the reduced system (6P up to 384 rows) is solved in global memory by k_ctrl_g.  One trial at
+    the single-trial bar, then the full solve at the north-star bar (chi2 1e-6, poses and
+    landmarks 1e-6) against the oracle on reproducible windows.  mode 1: landmarks seen by random
+    keyframe subsets (chunk windows of several tile counts, a dense reduced system)."""
+    kw = dict(pose_mode=1, k_min=2, k_max=8) if mode else {}
+    w = _stable_window(P, L, seed, **kw)
+    g = lego_ba.Solver(max_iters=1, max_trials=1).solve(w)
+    o = ob.solve(w, max_iters=1, max_trials=1)
+    assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-12
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-7)
+    gf = lego_ba.Solver().solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 2, 8))
+    assert gf["iterations"] in its
+    assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+    assert np.allclose(gf["pose_Tcw"], of["pose_Tcw"], atol=1e-6)
+    assert np.allclose(gf["lm_xyz"], of["lm_xyz"], atol=1e-6)
+
+
+def test_large_window_default_family_gate1():
+    """A survey-default (gauge-free, outliers, left-only) window of 30 keyframes in the diagnostic
+    gate mode: inside the oracle's own reorder envelope."""
+    w = lego_ba.generate_window(P=30, L=3000, k=8, seed=5)
+    g = lego_ba.Solver(gate_mode=1).solve(w)
+    o, spread, _ = oracle_envelope(w, threads=(1, 2, 8), gate_mode=1)
+    assert rel(g["chi2_final"], o["chi2_final"]) <= max(1e-6, 10 * spread)
+    assert g["chi2_final"] < g["chi2_initial"]
+
+
+def test_window_envelope_edges():
+    """65 keyframes is past the 64-bit pose masks; PCG past 21 keyframes is not offered."""
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.Solver().solve(lego_ba.generate_window(P=65, L=500, k=8, seed=4))
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.Solver(linear_solver=lego_ba.LH_SOLVER_PCG).solve(lego_ba.generate_window(P=22, L=500, k=8, seed=4))
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
 
 

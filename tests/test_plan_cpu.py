@@ -142,10 +142,12 @@ def test_plan_envelope_and_errors():
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.plan_window(wide)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > 16 poses per landmark
-    p22 = lego_ba.generate_window(P=22, L=50, k=8, seed=1)
+    check_plan(lego_ba.generate_window(P=64, L=300, k=8, seed=1), lego_ba.plan_window(
+        lego_ba.generate_window(P=64, L=300, k=8, seed=1), threads=2))   # 64 poses: 64-bit masks
+    p65 = lego_ba.generate_window(P=65, L=50, k=8, seed=1)
     with pytest.raises(lego_ba.LhError) as e:
-        lego_ba.plan_window(p22)
-    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > LH_PMAX poses
+        lego_ba.plan_window(p65)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > LH_PMAX_WIN poses
 
 
 def test_plan_unobserved_landmarks_and_fixed_mask():
