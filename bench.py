@@ -377,6 +377,28 @@ def main():
                   "iterations_per_solve": ip / npcg, "pcg_steps_per_solve": rp["pcg_iterations"],
                   "chi2_rel_vs_ldlt": abs(rp["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
     sp.close()
+    # a 64-keyframe window of C3's size (windows past 21 keyframes, the reduced
+    # system of 384 rows solved in global memory by k_ctrl_g), against the oracle's final chi2
+    from windows import STABLE
+    w64 = lego_ba.generate_window(P=64, L=50000, k=8, seed=args.seed, **dict(STABLE, outlier_frac=0.0))
+    f64 = np.zeros(64, np.uint8)
+    f64[0] = 1
+    w64["pose_fixed"] = f64
+    s64 = lego_ba.Solver(device=local)
+    s64.upload(w64)
+    s64.solve_resident()
+    d64, i64, t64, l64 = time_solves(s64, 5, barrier)
+    s64.set_profiling(True)
+    s64.kernel_stats_reset()
+    time_solves(s64, 2, barrier)
+    k64 = s64.kernel_stats()
+    s64.set_profiling(False)
+    s64.close()
+    out["p64_window"] = {"keyframes": 64, "landmarks": 50000, "obs": len(w64["obs_pose"]),
+                         "iterations_per_s": round(i64 / d64, 3), "ms_per_solve": round(d64 / 5 * 1e3, 3),
+                         "iterations_per_solve": i64 / 5, "trials_per_solve": t64 / 5,
+                         "k_ctrl_g_ms_per_trial": round(k64["k_ctrl"][1] / max(1, k64["k_ctrl"][0]), 4),
+                         "kernels_ms_per_solve_event_bracketed": {k: round(v[1] / 2, 4) for k, v in k64.items()}}
     # the frontend's pose-only LM (Frontend::EstimateCurrentPose): one frame the way
     # the reference calls it (frontend_lego.cpp:157, once per frame), and a batch of frames
     import frames
@@ -446,6 +468,13 @@ def main():
         od = oracle_bind.solve(wd, n_threads=threads, gate_mode=1, lib_path=lib_path)
         out["survey_default_c3"]["chi2_rel_vs_oracle"] = abs(ld["chi2_final"] - od["chi2_final"]) / od["chi2_final"]
         out["survey_default_c3"]["oracle_iterations"] = od["iterations"]
+        t0 = time.perf_counter()
+        o64 = oracle_bind.solve(w64, n_threads=threads, lib_path=lib_path)
+        c64 = time.perf_counter() - t0
+        out["p64_window"]["chi2_rel_vs_oracle"] = abs(l64["chi2_final"] - o64["chi2_final"]) / o64["chi2_final"]
+        out["p64_window"]["oracle_iterations"] = o64["iterations"]
+        out["p64_window"]["cpu_oracle_iterations_per_s"] = round(o64["iterations"] / c64, 3)
+        out["p64_window"]["cpu_oracle_threads"] = threads
         t0 = time.perf_counter()
         ol = oracle_bind.lk_track(li1, li2, lk1, kp2_init=lki, lib_path=lib_path)
         out["lk_optical_flow"]["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 3)

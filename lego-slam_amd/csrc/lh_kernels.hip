@@ -1453,7 +1453,7 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
 // The controller's tail, shared by both controllers (xs: the pose step in pose order, in LDS):
 // the pose part of the gain denominator (isGoodStepInLM's scale, problem.cpp:528-533, summed into
 // ctrl->spose), the candidate poses (VertexPose::add) and their pose tables.  All CT threads.
-template <int PM>
+template <int PM, int NT>
 __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
                                                int cur, const double* xs, const double* bpv, const double* hdv,
                                                double* s_red, double (*s_pm)[PM * 12], double (*s_trig)[4],
@@ -1463,9 +1463,9 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
     const int P = prm.P;
     // ---------------- pose part of the gain denominator; candidate poses ----------------
     double sp = 0.0;
-    if (tid < n) {
-        const double d = xs[tid], b = bpv[tid];
-        sp = (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[tid] * d + b);
+    for (int i = tid; i < n; i += NT) {
+        const double d = xs[i], b = bpv[i];
+        sp += (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[i] * d + b);
     }
     for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
     if (lane == 0) s_red[wave] = sp;
@@ -1516,7 +1516,7 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
     }
     lds_barrier();
     CSTAMP(10);
-    if (tid < 12 * P) pose_mat[(size_t)cand * P * 12 + tid] = s_pm[cand][tid];
+    for (int i = tid; i < 12 * P; i += NT) pose_mat[(size_t)cand * P * 12 + i] = s_pm[cand][i];
     if (tid >= 64 && tid < 64 + P * prm.ncam) {
         const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
         double To[12];
@@ -1528,7 +1528,7 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
     CSTAMP(11);
     if (tid == 0) {
         double s2 = 0.0;
-        for (int w = 0; w < CT / 64; ++w) s2 += s_red[w];
+        for (int w = 0; w < NT / 64; ++w) s2 += s_red[w];
         ctrl->spose = s2;
     }
 }
@@ -1705,7 +1705,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     lds_barrier();
     CSTAMP(8);
 
-    ctrl_pose_tail<LH_PMAX>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
+    ctrl_pose_tail<LH_PMAX, CT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1735,6 +1735,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #define GNB 32                          // panel width
 #define GNMAX (6 * LH_PMAX_WIN)         // largest reduced system
 #define GPS (GNB + 1)                   // LDS panel row stride (conflict-free column reads)
+#define GT 512                          // k_ctrl_g threads: 8 waves, 256 VGPRs (register rows in the factor)
 
 // k_ctrl_g's reduced-system solve (shared with the probe): gA holds the permuted system's lower
 // triangle (stride NG, identity padding to NG), yv the permuted right-hand side (LDS, n entries);
@@ -1743,83 +1744,129 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
                                              double* pnl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ double ginv[GNB];   // 1/D of the current block's pivots (1 where the pivot is invalid)
+    CSTAMP(5);
     // ---------------- blocked right-looking LDL^T ----------------
     if (!all_zero) {
         for (int K = 0; K < NG; K += GNB) {
             const int m = NG - K;
             // (a) the panel into LDS (lower part of the diagonal block, all of the rows below)
-            for (int x = tid; x < m * GNB; x += CT) {
+            for (int x = tid; x < m * GNB; x += GT) {
                 const int r = x / GNB, c = x - GNB * (x / GNB);
                 pnl[r * GPS + c] = (r >= c) ? gA[(size_t)(K + r) * NG + K + c] : 0.0;
             }
             lds_barrier();
-            // (b) the diagonal block: wave 0, lane r updates row r in place (LDS accesses of one wave
-            //     are in order: the L column written for step k is what the updates read)
+            CSTAMP(13);
+            // (b) the diagonal block: wave 0, lane j holds column j of the full symmetric block in
+            //     registers (c[i] = A(i, j)).  Step k: D_k and the column k entries come from lane k
+            //     by readlane (uniform values); lane j's own L(j, k) is its register c[k] (the
+            //     symmetric copy), so nothing is indexed per lane and nothing goes through memory.
             if (wave == 0) {
-                const int r = lane;
+                const int j = lane & (GNB - 1);
+                double c[GNB];
+#pragma unroll
+                for (int i = 0; i < GNB; ++i) c[i] = (i >= j) ? pnl[i * GPS + j] : pnl[j * GPS + i];
+#pragma unroll
                 for (int k = 0; k < GNB; ++k) {
-                    const double d = pnl[k * GPS + k];
+                    const double d = readlane_d(c[k], k);
                     const double id = (fabs(d) > 0.0) ? fast_rcp(d) : 1.0;   // pivot_is_valid: no division
-                    if (lane == k) ginv[k] = id;
-                    double l = 0.0;
-                    if (r > k && r < GNB) {
-                        l = pnl[r * GPS + k] * id;
-                        pnl[r * GPS + k] = l;
+                    const double wj = d * (c[k] * id);                        // D_k L(j, k)
+#pragma unroll
+                    for (int i = k + 1; i < GNB; ++i) {
+                        const double lik = readlane_d(c[i], k) * id;          // L(i, k), uniform
+                        c[i] -= lik * wj;
                     }
-                    wave_sync();
-                    if (r > k && r < GNB)
-                        for (int j = k + 1; j <= r; ++j) pnl[r * GPS + j] -= l * (d * pnl[j * GPS + k]);
-                    wave_sync();
+                    if (j > k) c[k] *= id;       // row j of column k becomes L(j, k)
+                    if (lane == k) ginv[k] = id;
+                }
+                // lane j ends with row j of the factor: c[i] = L(j, i) for i < j (its symmetric copies,
+                // scaled at step i), c[j] = D_j; its entries below the diagonal are spent
+                if (lane < GNB) {
+#pragma unroll
+                    for (int i = 0; i < GNB; ++i)
+                        if (i <= j) pnl[j * GPS + i] = c[i];
                 }
             }
             lds_barrier();
-            // (c) the panel rows below the block.  W = D_j L(k, j) (k > j) into the diagonal block's
-            //     free upper triangle; then per row, column k takes the updates of columns j < k in
-            //     ascending j (the right-looking order and roundings) and its pivot reciprocal.
+            CSTAMP(14);
+            // (c) the panel rows below the block.  W = D_k L(j, k) (j > k) into the diagonal block's
+            //     free upper triangle; each row in registers, right-looking: the same operations and
+            //     roundings as the diagonal block's rows.
             if (wave == 0 && lane < GNB)
-                for (int k = lane + 1; k < GNB; ++k) pnl[lane * GPS + k] = pnl[lane * GPS + lane] * pnl[k * GPS + lane];
+                for (int j = lane + 1; j < GNB; ++j) pnl[lane * GPS + j] = pnl[lane * GPS + lane] * pnl[j * GPS + lane];
             lds_barrier();
-            for (int r = GNB + tid; r < m; r += CT) {
-                double* row = pnl + r * GPS;
+            for (int r = GNB + tid; r < m; r += GT) {
+                double a[GNB];
+#pragma unroll
+                for (int c = 0; c < GNB; ++c) a[c] = pnl[r * GPS + c];
+#pragma unroll
                 for (int k = 0; k < GNB; ++k) {
-                    double a = row[k];
-#pragma unroll 4
-                    for (int j = 0; j < k; ++j) a -= row[j] * pnl[j * GPS + k];
-                    row[k] = a * ginv[k];
+                    const double l = a[k] * ginv[k];
+                    a[k] = l;
+#pragma unroll
+                    for (int j = k + 1; j < GNB; ++j) a[j] -= l * pnl[k * GPS + j];
+                    __builtin_amdgcn_sched_barrier(0);   // one step's loads at a time (register budget)
                 }
+#pragma unroll
+                for (int c = 0; c < GNB; ++c) pnl[r * GPS + c] = a[c];
             }
             lds_barrier();
+            CSTAMP(15);
             // (d) L and D of the panel back to gA
-            for (int x = tid; x < m * GNB; x += CT) {
+            for (int x = tid; x < m * GNB; x += GT) {
                 const int r = x / GNB, c = x - GNB * (x / GNB);
                 if (r >= c) gA[(size_t)(K + r) * NG + K + c] = pnl[r * GPS + c];
             }
-            // (e) trailing block: 16x16 tiles (I >= J), one wave each
+            // (e) trailing block: 16x16 tiles (I >= J), four per wave at a time (their loads in flight
+            //     together), 8 f64 MFMAs per tile over the panel
             const int mt = (m - GNB) >> 4;
             const int ntiles = mt * (mt + 1) / 2;
-            for (int t = wave; t < ntiles; t += CT / 64) {
-                int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-                while ((I + 1) * (I + 2) / 2 <= t) ++I;
-                while (I * (I + 1) / 2 > t) --I;
-                const int J = t - I * (I + 1) / 2;
-                const int r0 = K + GNB + 16 * I, c0 = K + GNB + 16 * J;
-                v4d acc;
+            for (int t0 = 4 * wave; t0 < ntiles; t0 += 4 * (GT / 64)) {
+                int I[4], J[4];
+                v4d acc[4];
 #pragma unroll
-                for (int v = 0; v < 4; ++v) acc[v] = gA[(size_t)(r0 + (lane >> 4) + 4 * v) * NG + c0 + (lane & 15)];
+                for (int u = 0; u < 4; ++u) {
+                    const int t = min(t0 + u, ntiles - 1);
+                    int ii = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+                    while ((ii + 1) * (ii + 2) / 2 <= t) ++ii;
+                    while (ii * (ii + 1) / 2 > t) --ii;
+                    I[u] = ii;
+                    J[u] = t - ii * (ii + 1) / 2;
+                    const int r0 = K + GNB + 16 * I[u], c0 = K + GNB + 16 * J[u];
 #pragma unroll
-                for (int kk = 0; kk < GNB; kk += 4) {
-                    const int k = kk + (lane >> 4);
-                    const double av = -pnl[(GNB + 16 * I + (lane & 15)) * GPS + k];
-                    const double bv = pnl[k * GPS + k] * pnl[(GNB + 16 * J + (lane & 15)) * GPS + k];
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                    for (int v = 0; v < 4; ++v) acc[u][v] = gA[(size_t)(r0 + (lane >> 4) + 4 * v) * NG + c0 + (lane & 15)];
                 }
 #pragma unroll
-                for (int v = 0; v < 4; ++v) gA[(size_t)(r0 + (lane >> 4) + 4 * v) * NG + c0 + (lane & 15)] = acc[v];
+                for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                    for (int kk = 0; kk < GNB; kk += 4) {
+                        const int k = kk + (lane >> 4);
+                        const double av = -pnl[(GNB + 16 * I[u] + (lane & 15)) * GPS + k];
+                        const double bv = pnl[k * GPS + k] * pnl[(GNB + 16 * J[u] + (lane & 15)) * GPS + k];
+                        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (t0 + u >= ntiles) break;
+                    const int r0 = K + GNB + 16 * I[u], c0 = K + GNB + 16 * J[u];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) gA[(size_t)(r0 + (lane >> 4) + 4 * v) * NG + c0 + (lane & 15)] = acc[u][v];
+                }
             }
             __syncthreads();
+            CSTAMP(16);
         }
     }
 
+    CSTAMP(6);
+    // the factor's diagonal blocks into LDS (the panel buffer is free now): block b's rows at
+    // pnl[(32 b + r) * GPS + c], one round trip for all of them
+    for (int x = tid; x < n * GNB; x += GT) {
+        const int r = x / GNB, c = x - GNB * (x / GNB);
+        const int K = r & ~(GNB - 1);
+        pnl[r * GPS + c] = (K + c < n) ? gA[(size_t)r * NG + K + c] : 0.0;
+    }
+    lds_barrier();
     // ---------------- forward substitution (unit L), the oracle's order ----------------
     for (int K = 0; K < n; K += GNB) {
         const int kb = min(GNB, n - K);
@@ -1828,7 +1875,7 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             double x = yv[K + r];
             double Lr[GNB];
 #pragma unroll
-            for (int k = 0; k < GNB; ++k) Lr[k] = (r > k && K + r < n) ? gA[(size_t)(K + r) * NG + K + k] : 0.0;
+            for (int k = 0; k < GNB; ++k) Lr[k] = (r > k && K + r < n) ? pnl[(K + r) * GPS + k] : 0.0;
 #pragma unroll
             for (int k = 0; k < GNB; ++k) {
                 const double xk = __shfl(x, k);
@@ -1840,16 +1887,21 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             if (lane < kb) yv[K + lane] = x;
         }
         lds_barrier();
-        for (int i = K + kb + tid; i < n; i += CT) {
+        for (int i = K + kb + tid; i < n; i += GT) {   // the block's columns, ascending; loads all in flight
+            double Lr[GNB];
+#pragma unroll
+            for (int k = 0; k < GNB; ++k) Lr[k] = k < kb ? gA[(size_t)i * NG + K + k] : 0.0;
             double x = yv[i];
-            for (int k = 0; k < kb; ++k) x -= gA[(size_t)i * NG + K + k] * yv[K + k];
+#pragma unroll
+            for (int k = 0; k < GNB; ++k)
+                if (k < kb) x -= Lr[k] * yv[K + k];
             yv[i] = x;
         }
         lds_barrier();
     }
     // D^+ (tolerance: numeric_limits<double>::min())
-    for (int i = tid; i < n; i += CT) {
-        const double d = gA[(size_t)i * NG + i];
+    for (int i = tid; i < n; i += GT) {
+        const double d = pnl[i * GPS + (i & (GNB - 1))];
         yv[i] = (fabs(d) > 2.2250738585072014e-308) ? yv[i] / d : 0.0;
     }
     lds_barrier();
@@ -1861,7 +1913,7 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             double x = yv[K + r];
             double Lc[GNB];
 #pragma unroll
-            for (int k = 0; k < GNB; ++k) Lc[k] = (k > r && k < kb) ? gA[(size_t)(K + k) * NG + K + r] : 0.0;
+            for (int k = 0; k < GNB; ++k) Lc[k] = (k > r && k < kb) ? pnl[(K + k) * GPS + r] : 0.0;
 #pragma unroll
             for (int k = GNB - 1; k >= 0; --k) {
                 const double xk = __shfl(x, k);
@@ -1870,16 +1922,22 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             if (lane < kb) yv[K + lane] = x;
         }
         lds_barrier();
-        for (int i = tid; i < K; i += CT) {
+        for (int i = tid; i < K; i += GT) {   // the block's rows, descending; loads all in flight
+            double Lc[GNB];
+#pragma unroll
+            for (int k = 0; k < GNB; ++k) Lc[k] = k < kb ? gA[(size_t)(K + k) * NG + i] : 0.0;
             double x = yv[i];
-            for (int k = kb - 1; k >= 0; --k) x -= gA[(size_t)(K + k) * NG + i] * yv[K + k];
+#pragma unroll
+            for (int k = GNB - 1; k >= 0; --k)
+                if (k < kb) x -= Lc[k] * yv[K + k];
             yv[i] = x;
         }
         lds_barrier();
     }
+    CSTAMP(7);
 }
 
-__global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
+__global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                                const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                                const uint32_t* __restrict__ rsmap, double* __restrict__ pose_mat,
                                                double* __restrict__ ptab, const double* __restrict__ ext,
@@ -1889,13 +1947,16 @@ __global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     __shared__ double dg[GNMAX], bsv[GNMAX], bpv[GNMAX], hdv[GNMAX], xs[GNMAX], yv[GNMAX];
     __shared__ int perm[GNMAX], iperm[GNMAX];
     __shared__ int s_flags[4];
-    __shared__ double s_red[CT / 64], s_lam;
+    __shared__ double s_red[GT / 64], s_lam;
     __shared__ double s_pm[2][LH_PMAX_WIN * 12];
     __shared__ double s_trig[LH_PMAX_WIN][4], s_qT[LH_PMAX_WIN][4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NG = (n + GNB - 1) & ~(GNB - 1);
     const lh_rs_layout LY = lh_rs_make(P);
+#ifdef LH_STAMPS
+    const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---------------- controller words, pose matrices, max |diag| (mode 0) ----------------
     double tchi = 0.0, sl = 0.0, ndg = 0.0;
@@ -1907,11 +1968,11 @@ __global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
         if (host_done && !cw.done) host_done[1] = seq;
     }
-    for (int i = tid; i < 24 * P; i += CT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
+    for (int i = tid; i < 24 * P; i += GT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
     {
         double mx = 0.0;
         if (mode == 0)
-            for (int i = tid; i < n; i += CT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
+            for (int i = tid; i < n; i += GT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
         for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
         if (lane == 0) s_red[wave] = mx;
     }
@@ -1919,7 +1980,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     if (tid == 0) {
         double mdiag = 0.0;
         if (mode == 0) {
-            for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
+            for (int w = 0; w < GT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
             mdiag = fmax(*maxd_in, mdiag);
         }
         int done, accept, cur;
@@ -1935,27 +1996,30 @@ __global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     if (done) return;
     const double lambda = s_lam;
 
-    // ---------------- commit; diagonal + lambda; right-hand sides ----------------
+#ifdef LH_STAMPS
+    if (tid == 0) {
+        atomicAdd(&lh_stamps[32], ct_start);
+        atomicAdd(&lh_stamps[61], 1ull);
+        atomicAdd(&lh_stamps[62], rt_start);
+    }
+#endif
+    CSTAMP(1);
+
+    // ---------------- diagonal + lambda and right-hand sides (one round trip) ----------------
     const double* __restrict__ src = accept ? rs_stage : rs_commit;
-    for (int i = tid; i < LY.total; i += CT) {
-        const double v = src[i];
-        if (accept) rs_commit[i] = v;
-        if (i < LY.off_bs) {
-            const uint32_t m = rsmap[i];
-            const int gi = LH_RSMAP_ROW(m), gj = LH_RSMAP_COL(m);
-            if (gi == gj) dg[gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
-        } else if (i < LY.off_bp) {
-            bsv[i - LY.off_bs] = v;
-        } else if (i < LY.off_hd) {
-            bpv[i - LY.off_bp] = v;
-        } else if (i < LY.off_hd + n) {
-            hdv[i - LY.off_hd] = v;
-        }
+    for (int i = tid; i < n; i += GT) {
+        const int p = i / 6, a = i - 6 * (i / 6);
+        const double v = src[LY.off_S + (p * P - (p * (p - 1)) / 2) * 36 + 7 * a];   // S block (p, p), entry (a, a)
+        dg[i] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
+        bsv[i] = src[LY.off_bs + i];
+        bpv[i] = src[LY.off_bp + i];
+        hdv[i] = src[LY.off_hd + i];
     }
     lds_barrier();
+    CSTAMP(2);
 
     // ---------------- pivot order: |diag| descending, ties by index, NaN last (as k_ctrl) ----------------
-    for (int row = tid; row < n; row += CT) {
+    for (int row = tid; row < n; row += GT) {
         double di = fabs(dg[row]);
         if (!(di == di)) di = -1.0;
         int r = 0;
@@ -1972,32 +2036,50 @@ __global__ __launch_bounds__(CT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     const bool all_zero = !(fabs(dg[perm[0]]) > 0.0);
     lds_barrier();
     if (all_zero)
-        for (int i = tid; i < n; i += CT) { perm[i] = i; iperm[i] = i; }
+        for (int i = tid; i < n; i += GT) { perm[i] = i; iperm[i] = i; }
     lds_barrier();
+    CSTAMP(3);
 
-    // ---------------- the permuted system into gA (lower triangle), identity padding ----------------
-    for (int i = tid; i < LY.off_bs; i += CT) {
-        const uint32_t m = rsmap[i];
-        const int ri = iperm[LH_RSMAP_ROW(m)], rj = iperm[LH_RSMAP_COL(m)];
-        const double v = src[i];
-        if (!LH_RSMAP_DIAG(m)) gA[(size_t)max(ri, rj) * NG + min(ri, rj)] = v;
-        else if (ri > rj) gA[(size_t)ri * NG + rj] = v;
+    // ---------------- one pass over the system: commit, scatter into gA (permuted lower triangle) ----------------
+    for (int base = tid; base < LY.total; base += 16 * GT) {
+        double v[16];
+        uint32_t mp[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = base + u * GT;
+            v[u] = i < LY.total ? src[i] : 0.0;
+            mp[u] = i < LY.off_bs ? rsmap[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = base + u * GT;
+            if (accept && i < LY.total) rs_commit[i] = v[u];
+            if (i < LY.off_bs) {
+                const int ri = iperm[LH_RSMAP_ROW(mp[u])], rj = iperm[LH_RSMAP_COL(mp[u])];
+                if (!LH_RSMAP_DIAG(mp[u])) gA[(size_t)max(ri, rj) * NG + min(ri, rj)] = v[u];
+                else if (ri > rj) gA[(size_t)ri * NG + rj] = v[u];
+            }
+        }
     }
-    for (int i = tid; i < NG; i += CT) {
+    for (int i = tid; i < NG; i += GT) {
         gA[(size_t)i * NG + i] = i < n ? dg[perm[i]] : 1.0;
         yv[i] = i < n ? bsv[perm[i]] : 0.0;
     }
-    for (int x = tid; x < (NG - n) * NG; x += CT) {
+    for (int x = tid; x < (NG - n) * NG; x += GT) {
         const int r = n + x / NG, c = x - NG * (x / NG);
         if (c < r) gA[(size_t)r * NG + c] = 0.0;
     }
     __syncthreads();   // global stores before the panel loads
-
+    CSTAMP(4);
     g_ldlt_solve(gA, NG, n, all_zero, yv, pnl);
-    if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
-    for (int i = CT + tid; i < n; i += CT) { xs[perm[i]] = yv[i]; dxp[perm[i]] = yv[i]; }
+    for (int i = tid; i < n; i += GT) { xs[perm[i]] = yv[i]; dxp[perm[i]] = yv[i]; }
     lds_barrier();
-    ctrl_pose_tail<LH_PMAX_WIN>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
+    CSTAMP(8);
+    ctrl_pose_tail<LH_PMAX_WIN, GT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
+    CSTAMP(12);
+#ifdef LH_STAMPS
+    if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // ============================================================================
@@ -2490,7 +2572,7 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA) {
     if (prm.P > LH_PMAX)
-        hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
+        hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA);
     else if (prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
@@ -2619,15 +2701,15 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
 
 // ---- the same probe through k_ctrl_g's global-memory solve (LH_NPAD < n <= 6 LH_PMAX_WIN):
 //      gA: scratch of ceil32(n)^2 doubles ----
-__global__ __launch_bounds__(CT) void k_ldlt_g_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
+__global__ __launch_bounds__(GT) void k_ldlt_g_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
                                                      double* __restrict__ x, double* __restrict__ gA) {
     __shared__ double pnl[GNMAX * GPS];
     __shared__ double dg[GNMAX], yv[GNMAX];
     __shared__ int perm[GNMAX], iperm[GNMAX];
     const int tid = threadIdx.x, NG = (n + GNB - 1) & ~(GNB - 1);
-    for (int i = tid; i < n; i += CT) dg[i] = S[(size_t)i * n + i];
+    for (int i = tid; i < n; i += GT) dg[i] = S[(size_t)i * n + i];
     lds_barrier();
-    for (int row = tid; row < n; row += CT) {
+    for (int row = tid; row < n; row += GT) {
         double di = fabs(dg[row]);
         if (!(di == di)) di = -1.0;
         int r = 0;
@@ -2643,23 +2725,23 @@ __global__ __launch_bounds__(CT) void k_ldlt_g_probe(const double* __restrict__ 
     const bool all_zero = !(fabs(dg[perm[0]]) > 0.0);
     lds_barrier();
     if (all_zero)
-        for (int i = tid; i < n; i += CT) { perm[i] = i; iperm[i] = i; }
+        for (int i = tid; i < n; i += GT) { perm[i] = i; iperm[i] = i; }
     lds_barrier();
-    for (int x2 = tid; x2 < NG * NG; x2 += CT) {
+    for (int x2 = tid; x2 < NG * NG; x2 += GT) {
         const int r = x2 / NG, c = x2 - NG * (x2 / NG);
         double v = 0.0;
         if (r < n && c < n) v = (c <= r) ? S[(size_t)perm[r] * n + perm[c]] : 0.0;
         else if (r == c) v = 1.0;
         gA[x2] = v;
     }
-    for (int i = tid; i < NG; i += CT) yv[i] = i < n ? b[perm[i]] : 0.0;
+    for (int i = tid; i < NG; i += GT) yv[i] = i < n ? b[perm[i]] : 0.0;
     __syncthreads();
     g_ldlt_solve(gA, NG, n, all_zero, yv, pnl);
-    for (int i = tid; i < n; i += CT) x[perm[i]] = yv[i];
+    for (int i = tid; i < n; i += GT) x[perm[i]] = yv[i];
 }
 
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA) {
-    hipLaunchKernelGGL(k_ldlt_g_probe, dim3(1), dim3(CT), 0, 0, S, b, n, x, gA);
+    hipLaunchKernelGGL(k_ldlt_g_probe, dim3(1), dim3(GT), 0, 0, S, b, n, x, gA);
     return hipGetLastError();
 }
 

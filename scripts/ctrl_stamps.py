@@ -13,7 +13,14 @@ from windows import window  # noqa: E402
 NAMES = ["start", "prefetch + LM logic", "commit + diag", "pivot rank", "scatter into LDS", "block 0 factor",
          "LDLT steps", "back substitution", "dx scatter", "trig / q_T", "pose compose", "pose / table stores", "tail"]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
-w = window(cfg, seed=0, family="stable_noout")
+if cfg.startswith("P"):   # P<n>: an n-keyframe window of C3's size (n > 21: k_ctrl_g; its phase 5 is unused)
+    from windows import STABLE
+    import numpy as np
+    P = int(cfg[1:])
+    w = lego_ba.generate_window(P=P, L=50000, k=8, seed=0, **dict(STABLE, outlier_frac=0.0))
+    w["pose_fixed"] = np.eye(1, P, dtype=np.uint8)[0]
+else:
+    w = window(cfg, seed=0, family="stable_noout")
 s = lego_ba.Solver(device=0)
 s.upload(w)
 s.solve_resident()
@@ -30,6 +37,14 @@ print(f"{cfg}: {n} live k_ctrl launches, {tot_cyc:.0f} cycles = {tot_ns / 1000:.
 for i in range(1, len(NAMES)):
     d = (cyc[i] - cyc[i - 1]) / n
     print(f"  {NAMES[i]:22s} {d:9.0f} cycles {d / tot_cyc * 100:5.1f}%  {d / (tot_cyc / tot_ns) / 1000:6.2f} us")
+if cfg.startswith("P"):   # k_ctrl_g's panel sub-phases, summed over the panels: (a) load, (b) diagonal
+    # block, (c) rows below, (d)+(e) write-back and trailing tiles (stamps 13-16 follow stamp 5)
+    sub = [st[32 + 5]] + [st[32 + i] for i in (13, 14, 15, 16)]
+    for nm, i in (("(a) panel load", 1), ("(b) diagonal block", 2), ("(c) rows below", 3), ("(d)+(e) trailing", 4)):
+        k = st[32 + 13] and n
+        d = (sub[i] - sub[i - 1]) / n if i > 1 else None
+        if d is not None:
+            print(f"    {nm:20s} {d:9.0f} cycles  {d / (tot_cyc / tot_ns) / 1000:6.2f} us")
 for b, nm in ((49, "steps 0-3"), (45, "steps 4+")):
     k = max(st[b + 3], 1)
     print(f"  LDLT {nm}: {k // max(n, 1)} per launch; per step: wave 0 chain {st[b] / k:.0f}, slowest other wave "
