@@ -256,7 +256,8 @@ int lh_lk_track(lh_handle *h, const lh_lk_input *in, lh_lk_result *out);
 /* f64 MFMA accumulator-layout probe: D(16x16) = A(16x4) * B(4x16), device pointers, row-major */
 int lh_debug_mfma_probe(const double *A, const double *B, double *D);
 /* k_ctrl's reduced-system solve (Eigen-LDLT pivot order, blocked LDL^T, back substitution) on a
-   dense symmetric n x n S (row-major), n <= 128: x = S^-1 b.  Device pointers. */
+   dense symmetric n x n S (row-major), n <= 384: x = S^-1 b.  Device pointers.  n > 128 runs k_ctrl_g's
+   global-memory solve (the windows of 22..64 keyframes). */
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x);
 /* k_ctrl's PCG solve (same LDS layout and pivot order) on a dense symmetric n x n S, n <= 128:
    x ~= S^-1 b to ||r|| <= tol ||b|| within max_iters (<= 0: 2n).  Device pointers; *iters host. */
