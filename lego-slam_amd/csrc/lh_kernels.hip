@@ -1517,8 +1517,9 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
     lds_barrier();
     CSTAMP(10);
     for (int i = tid; i < 12 * P; i += NT) pose_mat[(size_t)cand * P * 12 + i] = s_pm[cand][i];
-    if (tid >= 64 && tid < 64 + P * prm.ncam) {
-        const int pc = tid - 64, pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
+    for (int pc = tid - 64; pc < P * prm.ncam; pc += NT - 64) {   // threads 64.. (wave 0 stores pose_mat)
+        if (pc < 0) break;
+        const int pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
         double To[12];
 #pragma unroll
         for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pidx * 12 + i];
@@ -1744,6 +1745,7 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
                                              double* pnl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ double ginv[GNB];   // 1/D of the current block's pivots (1 where the pivot is invalid)
+    __shared__ double gdia[GNB];   // D of the current block's pivots
     CSTAMP(5);
     // ---------------- blocked right-looking LDL^T ----------------
     if (!all_zero) {
@@ -1775,16 +1777,20 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
                         const double lik = readlane_d(c[i], k) * id;          // L(i, k), uniform
                         c[i] -= lik * wj;
                     }
-                    if (j > k) c[k] *= id;       // row j of column k becomes L(j, k)
-                    if (lane == k) ginv[k] = id;
+                    // row j of column k becomes L(j, k) for j > k; lanes j <= k scale entries they never
+                    // read again (the diagonal D_k is kept in gdia), so no lane masks are needed
+                    c[k] *= id;
+                    if (lane == 0) { ginv[k] = id; gdia[k] = d; }
                 }
                 // lane j ends with row j of the factor: c[i] = L(j, i) for i < j (its symmetric copies,
-                // scaled at step i), c[j] = D_j; its entries below the diagonal are spent
+                // scaled at step i); the rest of its row is written too (the upper part is overwritten
+                // by (c), the diagonal below)
                 if (lane < GNB) {
 #pragma unroll
-                    for (int i = 0; i < GNB; ++i)
-                        if (i <= j) pnl[j * GPS + i] = c[i];
+                    for (int i = 0; i < GNB; ++i) pnl[j * GPS + i] = c[i];
                 }
+                wave_sync();
+                if (lane < GNB) pnl[lane * GPS + lane] = gdia[lane];
             }
             lds_barrier();
             CSTAMP(14);
