@@ -1261,95 +1261,81 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
 // the reference never adds the first step alpha*p to x (:595-596); here every step is applied.
 // A zero diagonal entry (STRATEGY1 with a fixed pose: 0 + lambda*0) preconditions with 0 instead of
 // Eigen's inf (which would turn the whole step into NaN).
-// Layout: eight threads per row (row = tid >> 3), each holding 16 entries of its row in registers and
-// summing those columns of A p; every thread of a row keeps that row's x, r, p, 1/d.  Three barriers per iteration (A p | p.q | r.r and r.z, p).
+// Layout: one wave runs the whole iteration, with no workgroup barrier inside the loop.  The
+// system is first mirrored to full storage in LDS (the upper triangle is free in this variant).
+// Lane l owns rows l and l + 64: x, r, p and 1/d in registers; A p reads those rows from LDS and p
+// by broadcast; the three dots per step (p.q, r.z, r.r) are a fixed DPP/ds_bpermute butterfly over
+// the wave.  Round 1 ran eight threads per row over 16 waves with three barriers per step
+// (~3 us per step; this is ~0.6 us).
 // At most max_it steps (callers pass the reference cap + 1: its first step precedes its loop).
 // Returns the iteration count.  Must be called by all CT threads; xsol[r] = x in pivot order.
-__device__ __forceinline__ int lds_pcg_solve(const double* __restrict__ A, double* __restrict__ xsol, double* __restrict__ pv,
+__device__ __forceinline__ int lds_pcg_solve(double* __restrict__ A, double* __restrict__ xsol, double* __restrict__ pv,
                              double* __restrict__ s_red2, int n, int tid, double tol_rel, int max_it) {
-    const int row = tid >> 3, part = tid & 7, lane = tid & 63, wave = tid >> 6;
-    const bool live = row < n;
-    auto Aij = [&](int i, int j) { return i >= j ? A[i * AS + j] : A[j * AS + i]; };
-    // this thread's 16 entries of its row, kept in registers for the whole solve (zero outside n x n)
-    double arow[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int c = part * 16 + u;
-        arow[u] = (live && c < n) ? Aij(row, c) : 0.0;
-    }
-    const double d = live ? Aij(row, row) : 0.0;
-    const double dinv = (d != 0.0) ? 1.0 / d : 0.0;
-    double r = live ? A[NP * AS + row] : 0.0;
-    double x = 0.0;
-    double z = r * dinv;
-    double p = z;
-    // wave partial of a per-row value (counted once per row: part 0), then the 16 waves in order
-    auto wsum = [&](double v) {
-        v = (part == 0) ? v : 0.0;
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        return v;
-    };
-    auto total = [&](int slot) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < CT / 64; ++w) t += s_red2[slot * 16 + w];
-        return t;
-    };
-    {
-        const double a = wsum(r * z), c = wsum(r * r);
-        if (lane == 0) { s_red2[wave] = a; s_red2[16 + wave] = c; }
-        if (part == 0 && row < NP) pv[row] = live ? p : 0.0;   // rows n..NP-1 stay 0
+    const int lane = tid & 63, wave = tid >> 6;
+    // full symmetric storage of the n x n system (rows and columns past n are never read)
+    for (int x = tid; x < n * n; x += CT) {
+        const int i = x / n, j = x - n * (x / n);
+        if (j > i) A[i * AS + j] = A[j * AS + i];
     }
     lds_barrier();
-    double rz = total(0);
-    const double bnorm = sqrt(total(1));
-    const double thr = tol_rel * bnorm;
-    int it = 0;
-    if (bnorm > 0.0) {
+    if (wave == 0) {
+        const int r0 = lane, r1 = lane + 64;
+        const bool v0 = r0 < n, v1 = r1 < n;
+        const double d0 = v0 ? A[r0 * AS + r0] : 0.0, d1 = v1 ? A[r1 * AS + r1] : 0.0;
+        const double i0 = (d0 != 0.0) ? 1.0 / d0 : 0.0, i1 = (d1 != 0.0) ? 1.0 / d1 : 0.0;
+        double rr0 = v0 ? A[NP * AS + r0] : 0.0, rr1 = v1 ? A[NP * AS + r1] : 0.0;
+        double x0 = 0.0, x1 = 0.0;
+        double z0 = rr0 * i0, z1 = rr1 * i1;
+        double p0 = z0, p1 = z1;
+        double t[2] = {rr0 * z0 + rr1 * z1, rr0 * rr0 + rr1 * rr1};
+        group_sum(t, 6);
+        double rz = t[0];
+        const double bnorm = sqrt(t[1]);
+        const double thr = tol_rel * bnorm;
+        int it = 0;
+        if (bnorm > 0.0) {
 #pragma clang loop unroll(disable)
-        while (it < max_it) {
-            // q = A p over this thread's 16 columns, then across the row's 8 threads
-            double q = 0.0;
-#pragma unroll
-            for (int u = 0; u < 16; ++u) q += arow[u] * pv[part * 16 + u];
-            q += __shfl_xor(q, 1);
-            q += __shfl_xor(q, 2);
-            q += __shfl_xor(q, 4);
-            {
-                const double a = wsum(p * q);
-                if (lane == 0) s_red2[32 + wave] = a;
+            while (it < max_it) {
+                pv[r0] = p0;
+                if (r1 < NP) pv[r1] = p1;
+                wave_sync();
+                // q = A p over the two rows, columns in order
+                double q0 = 0.0, q1 = 0.0;
+                const double* a0 = A + r0 * AS;
+                const double* a1 = A + (v1 ? r1 : r0) * AS;
+#pragma unroll 8
+                for (int c = 0; c < n; ++c) {
+                    const double pc = pv[c];
+                    q0 += a0[c] * pc;
+                    q1 += a1[c] * pc;
+                }
+                if (!v0) q0 = 0.0;
+                if (!v1) q1 = 0.0;
+                double pq[1] = {p0 * q0 + p1 * q1};
+                group_sum(pq, 6);
+                const double alpha = rz / pq[0];
+                x0 += alpha * p0; x1 += alpha * p1;
+                rr0 -= alpha * q0; rr1 -= alpha * q1;
+                z0 = rr0 * i0; z1 = rr1 * i1;
+                double u[2] = {rr0 * z0 + rr1 * z1, rr0 * rr0 + rr1 * rr1};
+                group_sum(u, 6);
+                ++it;
+                if (!(sqrt(u[1]) > thr)) break;       // also stops on NaN
+                const double beta = u[0] / rz;
+                rz = u[0];
+                p0 = z0 + beta * p0;
+                p1 = z1 + beta * p1;
+                wave_sync();                          // every lane's reads of pv before the next writes
             }
-            lds_barrier();
-            const double alpha = rz / total(2);
-            x += alpha * p;
-            r -= alpha * q;
-            z = r * dinv;
-            {
-                const double a = wsum(r * z), c = wsum(r * r);
-                if (lane == 0) { s_red2[wave] = a; s_red2[16 + wave] = c; }
-            }
-            ++it;
-            lds_barrier();
-            const double rzn = total(0), rr = total(1);
-            if (!(sqrt(rr) > thr)) break;       // also stops on NaN
-            const double beta = rzn / rz;
-            rz = rzn;
-            p = z + beta * p;
-            if (part == 0 && live) pv[row] = p;
-            lds_barrier();
         }
+        if (v0) xsol[r0] = x0;
+        if (v1) xsol[r1] = x1;
+        if (lane == 0) s_red2[0] = (double)it;
     }
-    if (part == 0 && live) xsol[row] = x;
     lds_barrier();
-    return it;
+    return (int)s_red2[0];
 }
 
-// Problem::solve's LM bookkeeping for one trial (thread 0 of either controller): computeLambdaInitLM
-// on the initial linearisation (mode 0, problem.cpp:470-504), else isGoodStepInLM (:520-581), the
-// lambda / nu update, commit or rollback (a buffer index flip), the stop rule and the trace.  mdiag:
-// max |diag| of H_pp and H_ll (mode 0).  Returns the controller's state through done/accept/cur/lam.
 struct CtrlWords {
     double chi, lam, ni, last, spose, chi0;
     int iter, fc, trials, nacc, done, cur, tl;
