@@ -208,7 +208,8 @@ def roofline(solver, n_obs, n_lm, k, cfg_key, reps=50):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 1000 C3 solves is ~1.1 s of GPU work: long enough for the driver's utilisation sampling to see it
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="auto", choices=["auto", "C3", "C4"],
                     help="auto: C3 on one GPU, C4 sharded over N > 1")
@@ -272,7 +273,7 @@ def main():
     # the same solves with a HIP event pair around every kernel: per-kernel ms per solve
     solver.set_profiling(True)
     solver.kernel_stats_reset()
-    time_solves(solver, max(2, args.steps // 4), barrier)
+    time_solves(solver, max(2, min(20, args.steps // 4)), barrier)
     ks = solver.kernel_stats()
     solver.set_profiling(False)
     n_obs, n_lm = len(w["obs_pose"]), len(w["lm_xyz"])
@@ -287,7 +288,7 @@ def main():
         return
 
     value = iters / dt
-    nprof = max(2, args.steps // 4)
+    nprof = max(2, min(20, args.steps // 4))
     out = {
         "metric": "LM iterations/sec + ms/solve, 20KF/50k-pts/400k-obs window; final chi2 vs ref",
         "value": round(value, 3),
@@ -371,8 +372,8 @@ def main():
     sp = lego_ba.Solver(device=local, linear_solver=lego_ba.LH_SOLVER_PCG)
     sp.upload(w)
     sp.solve_resident()
-    dp, ip, _, rp = time_solves(sp, max(3, args.steps // 4), barrier)
-    npcg = max(3, args.steps // 4)
+    npcg = max(3, min(20, args.steps // 4))
+    dp, ip, _, rp = time_solves(sp, npcg, barrier)
     out["pcg"] = {"ms_per_solve": round(dp / npcg * 1e3, 4), "iterations_per_s": round(ip / dp, 3),
                   "iterations_per_solve": ip / npcg, "pcg_steps_per_solve": rp["pcg_iterations"],
                   "chi2_rel_vs_ldlt": abs(rp["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
