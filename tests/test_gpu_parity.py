@@ -362,6 +362,19 @@ def test_large_windows_global_memory_solve(P, L, seed, mode):
     assert np.allclose(gf["lm_xyz"], of["lm_xyz"], atol=1e-6)
 
 
+def test_large_window_strategy1():
+    """STRATEGY1 (lambda scaled by the diagonal, problem.cpp:420) on a 32-keyframe window: one trial
+    at the single-trial bar, the full solve inside the oracle's envelope."""
+    w = window("W32", seed=2, family="stable_noout")
+    g = lego_ba.Solver(strategy=1, max_iters=1, max_trials=1).solve(w)
+    o = ob.solve(w, strategy=1, max_iters=1, max_trials=1)
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    gf = lego_ba.Solver(strategy=1).solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 2, 8), strategy=1)
+    assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+
+
 def test_large_window_default_family_gate1():
     """A survey-default (gauge-free, outliers, left-only) window of 30 keyframes in the diagnostic
     gate mode: inside the oracle's own reorder envelope."""

@@ -80,7 +80,7 @@ def rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
 
 
-@pytest.mark.parametrize("cfg,seed,family", [("C2", 0, "stable_noout"), ("mini", 2, "default")])
+@pytest.mark.parametrize("cfg,seed,family", [("C2", 0, "stable_noout"), ("mini", 2, "default"), ("W32", 1, "stable_noout")])
 def test_two_rank_sharded_solve_matches_one_rank(cfg, seed, family):
     import lego_ba
     from windows import window
