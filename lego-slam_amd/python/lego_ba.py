@@ -68,6 +68,7 @@ CONFIGS = {
     "C3": dict(P=20, L=50000, k=8),     # bench workload (metric window)
     "C4": dict(P=20, L=500000, k=8),    # 8-GPU window
     "W32": dict(P=32, L=3000, k=8),     # past 21 keyframes: the reduced system in global memory (k_ctrl_g)
+    "W24s": dict(P=24, L=500, k=8),     # a small window past 21 keyframes (golden fixture)
 }
 
 

@@ -51,6 +51,7 @@ CASES = [
     ("c1_fixed_first_default_s5", "C1", "default", 5, {}, dict(fix_first=True)),
     ("c1_right_edges_s6", "C1", "stable_noout", 6, {}, dict(right_frac=0.5)),
     ("mini_stable_noout_s0", "mini", "stable_noout", 0, {}, {}),
+    ("w24s_stable_noout_s1", "W24s", "stable_noout", 1, {}, {}),
 ]
 
 
@@ -128,5 +129,7 @@ def make(name, cfg, fam, seed, opt, over):
 
 
 if __name__ == "__main__":
+    only = set(sys.argv[1:])   # optional: names of the cases to (re)generate
     for case in CASES:
-        make(*case[:4], dict(case[4]), dict(case[5]))
+        if not only or case[0] in only:
+            make(*case[:4], dict(case[4]), dict(case[5]))
