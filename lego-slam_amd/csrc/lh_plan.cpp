@@ -3,6 +3,7 @@
 #include "lh_plan.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 namespace lh {
@@ -102,6 +103,10 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     const int64_t O = w->n_obs;
     const int ncam = w->n_cams > 0 ? w->n_cams : 1;
     pl.P = P; pl.L = L; pl.O = O; pl.ncam = ncam;
+    const auto t_0 = std::chrono::steady_clock::now();
+    auto stage = [&](int i) {
+        pl.t_stage[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_0).count();
+    };
 
     // ---- index checks and "already landmark-major" detection, one parallel pass ----
     std::atomic<int> bad{0}, unsorted{0};
@@ -126,6 +131,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         for (int p = 0; p < P; ++p)
             if (w->pose_fixed[p]) pl.fixed_mask |= 1ull << p;
 
+    stage(0);
     // ---- landmark-major CSR ----
     pl.lm_ptr.assign((size_t)L + 1, 0);
     pl.csr.resize((size_t)O);
@@ -146,6 +152,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         for (int64_t o = 0; o < O; ++o) pl.csr[pos[w->obs_lm[o]]++] = o;
     }
 
+    stage(1);
     // ---- per landmark: ascending pose order, pose mask, envelope checks ----
     pl.lm_mask.assign((size_t)L, 0ull);
     std::atomic<int> unsup{0};
@@ -175,33 +182,62 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     });
     if (unsup.load()) return LH_E_UNSUPPORTED;
 
-    // ---- landmark order by observation span (first pose, last pose, mask), stable ----
+    stage(2);
+    // ---- landmark order by observation span (first pose, last pose, mask), stable: a parallel
+    //      counting sort (per-block histograms, prefix in bucket-major / block-minor order, so each
+    //      bucket keeps landmark order), then a stable sort by mask inside the buckets that mix masks ----
     {
         const int nb = std::max(P, 1) * std::max(P, 1);
-        std::vector<int32_t> bcnt((size_t)nb + 1, 0);
         auto bucket = [&](int l) {
             const uint64_t m = pl.lm_mask[l];
             return __builtin_ctzll(m) * P + (63 - __builtin_clzll(m));
         };
-        int Lact = 0;
-        for (int l = 0; l < L; ++l)
-            if (pl.lm_mask[l]) { bcnt[bucket(l) + 1]++; ++Lact; }   // edge-less landmarks are no vertex (backend_lego.cpp:126)
-        for (int b = 0; b < nb; ++b) bcnt[b + 1] += bcnt[b];
-        pl.order.resize((size_t)Lact);
-        {
-            std::vector<int32_t> cur(bcnt.begin(), bcnt.end() - 1);
-            for (int l = 0; l < L; ++l)
-                if (pl.lm_mask[l]) pl.order[cur[bucket(l)]++] = l;
-        }
-        for (int b = 0; b < nb; ++b) {
-            auto s = pl.order.begin() + bcnt[b], e = pl.order.begin() + bcnt[b + 1];
-            if (e - s < 2) continue;
+        const int threads = pool ? pool->size() : 1;
+        const int nblk = std::max(1, std::min(4 * threads, (L + 8191) / 8192));
+        const int bsz = (L + nblk - 1) / std::max(nblk, 1);
+        std::vector<int32_t> hist((size_t)nblk * (nb + 1), 0);
+        auto count_blk = [&](int k) {
+            int32_t* h = hist.data() + (size_t)k * (nb + 1);
+            const int l0 = k * bsz, l1 = std::min(L, l0 + bsz);
+            for (int l = l0; l < l1; ++l)
+                if (pl.lm_mask[l]) h[bucket(l)]++;   // edge-less landmarks are no vertex (backend_lego.cpp:126)
+        };
+        if (pool) pool->run(nblk, count_blk);
+        else for (int k = 0; k < nblk; ++k) count_blk(k);
+        int32_t run = 0;
+        for (int bk = 0; bk < nb; ++bk)
+            for (int k = 0; k < nblk; ++k) {
+                int32_t& h = hist[(size_t)k * (nb + 1) + bk];
+                const int32_t c = h;
+                h = run;
+                run += c;
+            }
+        const int Lact0 = run;
+        pl.order.resize((size_t)Lact0);
+        auto scatter_blk = [&](int k) {
+            int32_t* h = hist.data() + (size_t)k * (nb + 1);
+            const int l0 = k * bsz, l1 = std::min(L, l0 + bsz);
+            for (int l = l0; l < l1; ++l)
+                if (pl.lm_mask[l]) pl.order[h[bucket(l)]++] = l;
+        };
+        if (pool) pool->run(nblk, scatter_blk);
+        else for (int k = 0; k < nblk; ++k) scatter_blk(k);
+        // bucket bounds: after the scatter, block nblk-1's cursor of bucket bk is the bucket's end
+        std::vector<int32_t> bend((size_t)nb);
+        for (int bk = 0; bk < nb; ++bk) bend[bk] = hist[(size_t)(nblk - 1) * (nb + 1) + bk];
+        auto sort_bucket = [&](int bk) {
+            const int32_t e0 = bend[bk], s0 = bk > 0 ? bend[bk - 1] : 0;
+            auto s = pl.order.begin() + s0, e = pl.order.begin() + e0;
+            if (e - s < 2) return;
             const uint64_t m0 = pl.lm_mask[*s];
-            if (std::all_of(s, e, [&](int32_t l) { return pl.lm_mask[l] == m0; })) continue;
-            std::stable_sort(s, e, [&](int32_t a, int32_t c) { return pl.lm_mask[a] < pl.lm_mask[c]; });
-        }
+            if (std::all_of(s, e, [&](int32_t l) { return pl.lm_mask[l] == m0; })) return;
+            std::stable_sort(s, e, [&](int32_t x, int32_t y) { return pl.lm_mask[x] < pl.lm_mask[y]; });
+        };
+        if (pool) pool->run(nb, sort_bucket);
+        else for (int bk = 0; bk < nb; ++bk) sort_bucket(bk);
     }
     const int Lact = (int)pl.order.size();
+    stage(3);
 
     // ---- chunks: at most ~512 (2 workgroups per CU, all resident at once), whole sub-batches of 8
     //      landmarks.  Rounding up to 8 rather than to 4 x 8 (equal sub-batches per wave) keeps the
@@ -213,23 +249,60 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     chunk_lm = ((chunk_lm + LH_SB_LM - 1) / LH_SB_LM) * LH_SB_LM;
     chunk_lm = std::max(32, std::min(256, chunk_lm));
     if (cfg.chunk_lm > 0) chunk_lm = std::max(LH_SB_LM, std::min(512, cfg.chunk_lm));
+    // One serial pass over the span order cuts the chunks and packs their sub-batches (the masks and
+    // lane-group logs gathered first, in parallel, so the pass reads them sequentially).
+    // A chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new chunk
+    // rather than let the union grow past the larger of the two tile counts.  A sub-batch takes
+    // landmarks while it holds < 8 and (n + 1) << lg <= 64 (landmark l owns the aligned lane group
+    // [l*G, l*G + k_l) of its 64 slots, G = 2^lg the largest pow2ceil(k) in the sub-batch).
+    std::vector<uint64_t> om((size_t)Lact);
+    std::vector<uint8_t> olg((size_t)Lact);
+    parallel_range(pool, Lact, 4096, [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+            const int l = pl.order[i];
+            om[i] = pl.lm_mask[l];
+            olg[i] = (uint8_t)pow2log((int)(pl.lm_ptr[l + 1] - pl.lm_ptr[l]));
+        }
+    });
     pl.chunk_lm0.clear();
     pl.chunk_mask.clear();
-    // a chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new chunk
-    // rather than let the union grow past the larger of the two tile counts
+    std::vector<int32_t> c_sb0;              // per chunk (creation order): its first sub-batch
+    std::vector<int32_t> t_first;            // sub-batches in creation order: first position
+    std::vector<uint8_t> t_lg;
+    t_first.reserve((size_t)Lact / 4 + 16);
+    t_lg.reserve((size_t)Lact / 4 + 16);
+    int sb_start = 0, sb_n = 0, sb_lg = 0;
+    auto close_sb = [&]() {
+        if (sb_n > 0) { t_first.push_back(sb_start); t_lg.push_back((uint8_t)sb_lg); }
+        sb_n = 0;
+    };
     for (int i = 0; i < Lact; ++i) {
-        const uint64_t m = pl.lm_mask[pl.order[i]];
+        const uint64_t m = om[i];
         const bool fresh = pl.chunk_lm0.empty() || (i - pl.chunk_lm0.back()) >= chunk_lm ||
                            popc(pl.chunk_mask.back() | m) > LH_UMAX ||
                            chunk_tiles(pl.chunk_mask.back() | m) > std::max(chunk_tiles(pl.chunk_mask.back()), chunk_tiles(m));
         if (fresh) {
+            close_sb();
             pl.chunk_lm0.push_back(i);
             pl.chunk_mask.push_back(0ull);
+            c_sb0.push_back((int32_t)t_first.size());
         }
         pl.chunk_mask.back() |= m;
+        const int lgn = std::max(sb_lg, (int)olg[i]);
+        if (sb_n > 0 && sb_n < LH_SB_LM && ((sb_n + 1) << lgn) <= LH_SB_OBS) {
+            ++sb_n;
+            sb_lg = lgn;
+        } else {
+            close_sb();
+            sb_start = i;
+            sb_n = 1;
+            sb_lg = olg[i];
+        }
     }
+    close_sb();
     const int NC = (int)pl.chunk_mask.size();
     pl.chunk_lm0.push_back(Lact);
+    c_sb0.push_back((int32_t)t_first.size());
     pl.n_chunks = NC;
 
     // launch order: grouped by T (one k_lin launch per tile count), stable
@@ -244,43 +317,27 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         pl.tgroup_begin[0] = 0;
         pl.tgroup_begin[LH_TMAX + 1] = c;
     }
+    stage(4);
 
-    // ---- sub-batches: landmark l owns the aligned lane group [l*G, l*G + k_l) of 64 slots ----
-    auto lm_k = [&](int pos) { const int l = pl.order[pos]; return (int)(pl.lm_ptr[l + 1] - pl.lm_ptr[l]); };
-    auto walk = [&](int c, const std::function<void(int, int, int)>& emit) {   // emit(first pos, n, lg)
-        const int b = pl.chunk_lm0[c], e = pl.chunk_lm0[c + 1];
-        int i = b;
-        while (i < e) {
-            int lg = 0, n = 0;
-            while (i + n < e && n < LH_SB_LM) {
-                const int lgn = std::max(lg, pow2log(lm_k(i + n)));
-                if ((n + 1) << lgn > LH_SB_OBS) break;
-                lg = lgn;
-                ++n;
-            }
-            emit(i, n, lg);
-            i += n;
-        }
-    };
-    std::vector<int32_t> nsb((size_t)NC, 0);
-    auto count_sb = [&](int c) { walk(c, [&](int, int, int) { nsb[c]++; }); };
-    if (pool) pool->run(NC, count_sb);
-    else for (int c = 0; c < NC; ++c) count_sb(c);
+    // ---- sub-batches in launch order ----
     pl.chunk_sb0.assign((size_t)NC + 1, 0);
-    for (int ci = 0; ci < NC; ++ci) pl.chunk_sb0[ci + 1] = pl.chunk_sb0[ci] + nsb[pl.corder[ci]];   // by launch position
+    for (int ci = 0; ci < NC; ++ci) {
+        const int c = pl.corder[ci];
+        pl.chunk_sb0[ci + 1] = pl.chunk_sb0[ci] + (c_sb0[c + 1] - c_sb0[c]);   // by launch position
+    }
     pl.n_sb = pl.chunk_sb0[NC];
     pl.n_rec = pl.n_sb * LH_SB_LM;
     pl.n_slots = (int64_t)pl.n_sb * LH_SB_OBS;
     pl.sb_lm0.resize((size_t)pl.n_sb + 1);
     pl.sb_lg.resize((size_t)pl.n_sb);
-    auto fill_sb = [&](int ci) {
-        int sb = pl.chunk_sb0[ci];
-        walk(pl.corder[ci], [&](int first, int, int lg) { pl.sb_lm0[sb] = first; pl.sb_lg[sb] = (uint8_t)lg; ++sb; });
-    };
-    if (pool) pool->run(NC, fill_sb);
-    else for (int ci = 0; ci < NC; ++ci) fill_sb(ci);
+    for (int ci = 0; ci < NC; ++ci) {
+        const int c = pl.corder[ci], n = c_sb0[c + 1] - c_sb0[c];
+        std::memcpy(pl.sb_lm0.data() + pl.chunk_sb0[ci], t_first.data() + c_sb0[c], (size_t)n * sizeof(int32_t));
+        std::memcpy(pl.sb_lg.data() + pl.chunk_sb0[ci], t_lg.data() + c_sb0[c], (size_t)n);
+    }
     pl.sb_lm0[pl.n_sb] = Lact;   // never read as a start: the last sub-batch ends at its chunk's end
 
+    stage(5);
     // ---- reduce plan sizes: per pose pair, the chunks touching it ----
     pl.npairs = P * (P + 1) / 2;
     pl.pair_ptr.assign((size_t)pl.npairs + 1, 0u);
@@ -301,6 +358,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         const uint32_t u = (uint32_t)popc(pl.chunk_mask[pl.corder[ci]]);
         pl.chunk_ib[ci + 1] = pl.chunk_ib[ci] + u * (u + 1) / 2;
     }
+    stage(6);
     return LH_OK;
 }
 

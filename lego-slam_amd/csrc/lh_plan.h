@@ -76,6 +76,7 @@ struct Plan {
     std::vector<uint8_t> sb_lg;         // [n_sb]
     std::vector<uint32_t> pair_ptr;     // [npairs + 1]
     std::vector<uint32_t> chunk_ib;     // [n_chunks + 1] first item of each chunk (launch order)
+    double t_stage[8] = {0};            // diagnostic: ms at plan_structure's stage ends (lhp_plan_stages)
 };
 
 struct PlanOut {

@@ -46,6 +46,20 @@ int lhp_plan_fill(const lh_window* w, int chunk_lm, int threads, lh_chunk* chunk
 
 // mean over reps plans (after one warm-up) on a persistent pool: ms of plan_structure and of
 // plan_fill into reused buffers, i.e. what lh_upload spends before its copies
+// diagnostic: plan_structure's stage end times (ms from its start): index checks, CSR, per-landmark
+// sort + masks, span order, chunking, sub-batches, reduce-plan sizes; the last run of reps
+int lhp_plan_stages(const lh_window* w, int threads, int reps, double* out7) {
+    lh::Pool pool(threads > 0 ? threads : 1);
+    lh::Plan pl;
+    lh::PlanCfg cfg;
+    for (int r = 0; r <= reps; ++r) {
+        const int st = lh::plan_structure(w, cfg, false, pl, &pool);
+        if (st != LH_OK) return st;
+    }
+    for (int i = 0; i < 7; ++i) out7[i] = pl.t_stage[i];
+    return LH_OK;
+}
+
 int lhp_plan_time(const lh_window* w, int chunk_lm, int threads, int reps, double* ms_structure, double* ms_fill) {
     lh::Pool pool(threads > 0 ? threads : 1);
     lh::Plan pl;

@@ -498,6 +498,8 @@ def _pl():
         lib.lhp_plan_fill.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int] + [vp] * 11
         lib.lhp_plan_time.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]
+        if hasattr(lib, "lhp_plan_stages"):   # diagnostic entry point
+            lib.lhp_plan_stages.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, vp]
         lib.lhp_pool_stress.argtypes = [C.c_int, C.c_int, C.c_int]
         lib.lhp_pool_stress.restype = C.c_int64
         _planlib = lib
@@ -525,6 +527,15 @@ def plan_window(w, chunk_lm=0, threads=1):
 def pool_stress(threads, runs, n):
     """Sum of every index the planner's worker pool visits over `runs` back-to-back jobs of size n."""
     return int(_pl().lhp_pool_stress(threads, runs, n))
+
+
+def plan_stages_ms(w, threads=1, reps=3):
+    """Diagnostic: plan_structure's stage end times in ms (index checks, CSR, per-landmark sort and
+    masks, span order, chunking, sub-batches, reduce-plan sizes)."""
+    ref = _WindowRef(w)
+    out = np.zeros(7)
+    _check(_pl().lhp_plan_stages(C.byref(ref.s), threads, reps, _ptr(out)), "lhp_plan_stages")
+    return out
 
 
 def plan_time_ms(w, chunk_lm=0, threads=1, reps=5):
