@@ -95,7 +95,8 @@ typedef struct lh_options {
                                  as 0 (the oracle's gate_mode 1; parity tests only)            */
     int32_t chunk_landmarks;  /* landmarks per k_lin chunk; 0 = auto (~2 workgroups per CU)     */
     int32_t comm_mode;        /* lh_comm_mode (world_size > 1)                                  */
-    int32_t host_threads;     /* window-preprocessing threads; 0 = auto (<= 8)                   */
+    int32_t host_threads;     /* window-preprocessing threads; 0 = auto (the CPUs this process may
+                                 use: affinity mask capped by the cgroup CPU quota, <= 16)       */
     lh_allreduce_fn allreduce;  /* LH_COMM_HOST: the exchange                                    */
     void *allreduce_user;       /* its first argument                                            */
 } lh_options;
