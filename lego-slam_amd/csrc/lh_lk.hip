@@ -44,6 +44,38 @@ __device__ __forceinline__ float lk_pixel(const Img& im, float x, float y) {
                    (1 - xx) * yy * lk_byte(im, o + im.step) + xx * yy * lk_byte(im, o + im.step + 1));
 }
 
+// The same sample with its four bytes read from an LDS copy of the image when the taps fall inside it.
+// The window holds win[r][c] = lk_byte(im, (wy0 + r) * step + wx0 + c): bytes by linear index, so
+// tap o + 1 is column c + 1 even where it wraps into the next image row (as the reference's does)
+// and out-of-buffer taps are the same zeros.  Taps outside it read global memory.
+#define LK_WW 32
+#define LK_WH 24
+__device__ __forceinline__ float lk_pixel_w(const Img& im, const uint8_t* win, int wx0, int wy0, float x, float y) {
+    if (x < 0) x = 0;
+    if (y < 0) y = 0;
+    if (x >= im.cols) x = im.cols - 1;
+    if (y >= im.rows) y = im.rows - 1;
+    const int xi = (int)x, yi = (int)y;
+    const float xx = x - floorf(x);
+    const float yy = y - floorf(y);
+    const int c = xi - wx0, r = yi - wy0;
+    int b00, b01, b10, b11;
+    if ((unsigned)c < LK_WW - 1 && (unsigned)r < LK_WH - 1) {
+        const uint8_t* q = win + r * LK_WW + c;
+        b00 = q[0];
+        b01 = q[1];
+        b10 = q[LK_WW];
+        b11 = q[LK_WW + 1];
+    } else {
+        const int64_t o = (int64_t)yi * im.step + xi;
+        b00 = lk_byte(im, o);
+        b01 = lk_byte(im, o + 1);
+        b10 = lk_byte(im, o + im.step);
+        b11 = lk_byte(im, o + im.step + 1);
+    }
+    return (float)((1 - xx) * (1 - yy) * b00 + xx * (1 - yy) * b01 + (1 - xx) * yy * b10 + xx * yy * b11);
+}
+
 // Eigen Matrix2d::ldlt().solve(b): the oracle's ldlt_solve (Eigen ldlt_inplace with diagonal
 // pivoting + LDLT::_solve_impl) for n = 2, operation for operation
 __device__ __forceinline__ void ldlt2_solve(const double H[4], const double b[2], double x[2]) {
@@ -120,18 +152,29 @@ __global__ __launch_bounds__(256) void k_lk_pyr(const uint8_t* __restrict__ src,
 
 // ---- LKOpticalFlow{4,1}Layer, one wave per keypoint ----
 #define LKW 4   // keypoints (waves) per workgroup
+#define LK_TROW 66
+
+__device__ __forceinline__ double lk_readlane(double v, int l) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
 __global__ __launch_bounds__(64 * LKW) void k_lk_track(lh_lk_levels L1, lh_lk_levels L2, int levels, int n,
                                                        const float* __restrict__ kp1, const float* __restrict__ kp2_in,
                                                        float* __restrict__ kp2_out, uint8_t* __restrict__ success,
                                                        int inverse, int has_initial) {
-    __shared__ double terms[LKW][6][64];
+    // row stride 66 doubles: 16-byte aligned rows, and the six summing lanes (one row each) hit
+    // banks 4 apart
+    __shared__ double terms[LKW][6][LK_TROW];
+    __shared__ uint8_t window[LKW][LK_WH * LK_WW];   // the second image around this level's guess
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = blockIdx.x * LKW + w;
     if (i >= n) return;   // wave-uniform: no barrier below spans waves
     const int px = lane / 7 - 3, py = lane - 7 * (lane / 7) - 3;
     const bool act = lane < 49;
-    double (*T)[64] = terms[w];
+    double (*T)[LK_TROW] = terms[w];
+    uint8_t* win = window[w];
 
     const double scale_top = levels == 4 ? 0.125 : 1.0;
     float k1x = (float)(kp1[2 * i] * scale_top), k1y = (float)(kp1[2 * i + 1] * scale_top);
@@ -152,15 +195,28 @@ __global__ __launch_bounds__(64 * LKW) void k_lk_track(lh_lk_levels L1, lh_lk_le
         double H[4] = {0, 0, 0, 0};
         double Jlast0 = 0, Jlast1 = 0;   // inverse mode: the J variable after iteration 0 (last pixel's)
         const float ax = k1x + px, ay = k1y + py;
+        const float v1 = act ? lk_pixel(i1, ax, ay) : 0.f;   // the template sample is loop-invariant
+        // stage i2 around the initial guess: the iterations' taps stay inside while |dx - dx0| <= 11
+        // and |dy - dy0| <= 7 pixels (placement only decides which taps come from LDS, not values)
+        const int wx0 = (int)floorf(fminf(fmaxf((float)(k1x + dx), -1e6f), 1e6f)) - 15;
+        const int wy0 = (int)floorf(fminf(fmaxf((float)(k1y + dy), -1e6f), 1e6f)) - 11;
+#pragma unroll
+        for (int k = 0; k < LK_WH * LK_WW / 64; ++k) {
+            const int idx = k * 64 + lane;
+            win[idx] = (uint8_t)lk_byte(i2, (int64_t)(wy0 + idx / LK_WW) * i2.step + wx0 + idx % LK_WW);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (int iter = 0; iter < 10; ++iter) {
             double e = 0, J0 = 0, J1 = 0;
             if (act) {
-                e = lk_pixel(i1, ax, ay) - lk_pixel(i2, (float)(ax + dx), (float)(ay + dy));
+                e = v1 - lk_pixel_w(i2, win, wx0, wy0, (float)(ax + dx), (float)(ay + dy));
                 if (!inverse) {
-                    const double gx = 0.5 * (lk_pixel(i2, (float)(ax + dx + 1), (float)(ay + dy)) -
-                                             lk_pixel(i2, (float)(ax + dx - 1), (float)(ay + dy)));
-                    const double gy = 0.5 * (lk_pixel(i2, (float)(ax + dx), (float)(ay + dy + 1)) -
-                                             lk_pixel(i2, (float)(ax + dx), (float)(ay + dy - 1)));
+                    const double gx = 0.5 * (lk_pixel_w(i2, win, wx0, wy0, (float)(ax + dx + 1), (float)(ay + dy)) -
+                                             lk_pixel_w(i2, win, wx0, wy0, (float)(ax + dx - 1), (float)(ay + dy)));
+                    const double gy = 0.5 * (lk_pixel_w(i2, win, wx0, wy0, (float)(ax + dx), (float)(ay + dy + 1)) -
+                                             lk_pixel_w(i2, win, wx0, wy0, (float)(ax + dx), (float)(ay + dy - 1)));
                     J0 = -1.0 * gx;
                     J1 = -1.0 * gy;
                 } else if (iter == 0) {
@@ -187,25 +243,24 @@ __global__ __launch_bounds__(64 * LKW) void k_lk_track(lh_lk_levels L1, lh_lk_le
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // the patch loop's sums, in pixel order
-            double b0 = 0, b1 = 0, c = 0;
-            // forward mode resets H every iteration; inverse mode keeps it and adds only at iteration 0
-            double h00 = inverse ? H[0] : 0.0, h01 = inverse ? H[1] : 0.0, h11 = inverse ? H[3] : 0.0;
-            for (int p = 0; p < 49; ++p) {
-                b0 += T[0][p];
-                b1 += T[1][p];
-                c += T[2][p];
-                if (hterm) {
-                    h00 += T[3][p];
-                    h01 += T[4][p];
-                    h11 += T[5][p];
-                }
+            // the patch loop's sums, in pixel order: lane k < 6 runs sum k sequentially from 0.0
+            // (b0, b1, cost, H00, H01, H11).  H starts at 0.0 in each level, so inverse mode's
+            // "H += ..." at iteration 0 is this same sum, and later iterations keep H.
+            double acc = 0.0;
+            if (lane < 6) {
+                const double* row = T[lane];
+#pragma unroll
+                for (int p = 0; p < 49; ++p) acc += row[p];
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            cost = c;
-            H[0] = h00; H[1] = h01; H[2] = h01; H[3] = h11;   // J1 * J0 == J0 * J1 bitwise
+            const double b0 = lk_readlane(acc, 0), b1 = lk_readlane(acc, 1);
+            cost = lk_readlane(acc, 2);
+            if (hterm) {
+                const double h00 = lk_readlane(acc, 3), h01 = lk_readlane(acc, 4), h11 = lk_readlane(acc, 5);
+                H[0] = h00; H[1] = h01; H[2] = h01; H[3] = h11;   // J1 * J0 == J0 * J1 bitwise
+            }
             const double bb[2] = {b0, b1};
             double u[2];
             ldlt2_solve(H, bb, u);

@@ -2,7 +2,7 @@
 (exit 1) if any kernel uses scratch (a register spill): DESIGN.md states every solver kernel is
 spill-free, and the Makefile runs this on every build.
 
-usage: python3 scripts/resource_check.py lego-slam_amd/lib/lh_kernels.resource.txt
+usage: python3 scripts/resource_check.py lego-slam_amd/lib/lh_kernels.resource.txt [lh_lk.resource.txt ...]
 """
 import re
 import subprocess
@@ -42,7 +42,7 @@ SPILL_ALLOWED = {"k_ctrl_g": 64, "k_ldlt_g_probe": 64}
 
 
 def main():
-    kernels = parse(sys.argv[1])
+    kernels = [k for path in sys.argv[1:] for k in parse(path)]
     if not kernels:
         print("resource_check: no kernel-resource-usage remarks found", file=sys.stderr)
         return 1

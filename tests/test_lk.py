@@ -117,6 +117,27 @@ def test_gpu_lk_bitwise_vs_oracle(rows, cols, shift, inverse, levels, initial):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inverse,levels,init_off", [(False, 1, None), (True, 1, None), (False, 4, (90.0, -70.0))])
+def test_gpu_lk_taps_outside_the_staged_window(inverse, levels, init_off):
+    """k_lk_track reads the second image from an LDS window placed at each level's initial guess
+    (32 x 24 bytes); a large motion tracked on one level, or a far-off initial guess, drives the
+    taps out of it onto the global-memory path, which must give the same bits."""
+    import lego_ba
+    rows, cols, shift = 200, 300, (13.5, -9.2)
+    i1, i2 = images.pair(rows, cols, shift=shift, seed=5)
+    k1 = images.keypoints(rows, cols, 400, seed=6)
+    init = None if init_off is None else k1 + np.float32(init_off)
+    s = lego_ba.Solver(device=0)
+    g = s.lk_track(i1, i2, k1, kp2_init=init, inverse=inverse, levels=levels)
+    o = ob.lk_track(i1, i2, k1, kp2_init=init, inverse=inverse, levels=levels)
+    s.close()
+    assert np.array_equal(g["success"], o["success"])
+    assert np.array_equal(g["kp2"], o["kp2"])
+    moved = np.abs(o["kp2"] - (k1 if init is None else init)).max(axis=1)
+    assert (moved > 11).any()   # some keypoints did leave the window
+
+
+@pytest.mark.gpu
 def test_gpu_lk_empty_and_errors():
     import lego_ba
     s = lego_ba.Solver(device=0)
