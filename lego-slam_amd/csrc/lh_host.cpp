@@ -666,15 +666,18 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         // word; the host keeps `depth` trials enqueued past it until the device raises done.
         // hipStreamQuery every few thousand polls turns a device fault into an error return.
         unsigned spin = 0;
+        const bool query_often = getenv("LH_QUERY_OFTEN") != nullptr;   // diagnostic A/B switch
+        double t_query = now_ms();
         while (!hd[0] && enq < max_total) {
             if (enq - hd[1] < depth) {
                 if ((st = enqueue_trial(h, 1, &stopped)) != LH_OK) return st;
                 ++enq;
                 continue;
             }
-            if ((++spin & 4095) == 0) {
+            if ((++spin & 4095) == 0 && (query_often || now_ms() - t_query > 50.0)) {
                 const hipError_t q = hipStreamQuery(s);
                 if (q != hipSuccess && q != hipErrorNotReady) return LH_E_HIP;
+                t_query = now_ms();
             }
             __builtin_ia32_pause();
         }
