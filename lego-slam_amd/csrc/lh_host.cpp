@@ -265,6 +265,7 @@ struct lh_handle {
     DevBuf<float> k_kp1, k_kp2;
     lh_ctrl* h_ctrl = nullptr;   // pinned
     int* h_done = nullptr;       // pinned, mapped: [0] k_ctrl raises it when the LM loop stops, [1] progress
+                                 // word 2 * (last live trial) + (one iteration from max_iters)
     int* d_done = nullptr;       // device alias of h_done
 
     // per-solve bookkeeping
@@ -640,7 +641,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     const size_t PT = (size_t)P * h->ncam * LH_PT;
     hipEvent_t e0 = next_event(h), e1 = next_event(h);
     if (!e0 || !e1) return LH_E_HIP;
-    volatile int* hd = h->h_done;   // [0] done, [1] last trial whose k_ctrl started live
+    volatile int* hd = h->h_done;   // [0] done, [1] progress word (ctrl_lm_step)
     hd[0] = 0;
     hd[1] = -1;
     h->n_coll = 0;
@@ -662,14 +663,17 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
             if (!stopped) ++enq;
         }
     } else {
-        // k_ctrl writes the trial it starts (when the loop is still live) into the mapped progress
-        // word; the host keeps `depth` trials enqueued past it until the device raises done.
-        // hipStreamQuery every few thousand polls turns a device fault into an error return.
+        // k_ctrl writes each live trial it has decided into the mapped progress word; the host
+        // keeps `depth` trials enqueued past it (one when the next completed iteration reaches
+        // max_iters) until the device raises done.  hipStreamQuery at most every 50 ms turns a
+        // device fault into an error return (each query delays the next launch by ~6 us).
         unsigned spin = 0;
         const bool query_often = getenv("LH_QUERY_OFTEN") != nullptr;   // diagnostic A/B switch
         double t_query = now_ms();
         while (!hd[0] && enq < max_total) {
-            if (enq - hd[1] < depth) {
+            const int pw = hd[1];   // 2 * (last live trial) + near, or -1 before the first
+            const int last = pw < 0 ? -1 : (pw >> 1);
+            if (enq - last < ((pw >= 0 && (pw & 1)) ? 1 : depth)) {
                 if ((st = enqueue_trial(h, 1, &stopped)) != LH_OK) return st;
                 ++enq;
                 continue;

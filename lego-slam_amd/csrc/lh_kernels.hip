@@ -1350,7 +1350,7 @@ __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl)
 }
 __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
-                                             volatile int* __restrict__ host_done, int& done_o, int& accept_o,
+                                             volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
                                              int& cur_o, double& lam_o) {
     double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
     int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
@@ -1428,7 +1428,16 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
         ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
         ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
-        if (done && host_done) *host_done = 1;
+        // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
+        // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
+        // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
+        // trial ahead when near, so a stop by max_iters leaves nothing enqueued past it); it never
+        // advances past the stop trial, which bounds how many trials (and all-reduces) any rank
+        // can have enqueued.  One 32-bit store: the host never sees a torn pair.
+        if (host_done) {
+            if (done) host_done[0] = 1;
+            else host_done[1] = 2 * seq + ((prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0);
+        }
     }
     done_o = done;
     accept_o = accept;
@@ -1552,10 +1561,6 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
-        // host progress word: this live trial's controller has started (its k_lin and k_reduce are
-        // done).  The host keeps the queue filled from it; it never advances past the stop trial,
-        // which bounds how many trials (and all-reduces) any rank can have enqueued.
-        if (host_done && !cw.done) host_done[1] = seq;
     }
     double vs[NLD], vc[NLD];
     uint32_t mp[NLD];
@@ -1592,7 +1597,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
         int done, accept, cur;
         double lam_n;
-        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, done, accept, cur, lam_n);
+        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
@@ -1958,7 +1963,6 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
-        if (host_done && !cw.done) host_done[1] = seq;
     }
     for (int i = tid; i < 24 * P; i += GT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
     {
@@ -1977,7 +1981,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         }
         int done, accept, cur;
         double lam_n;
-        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, done, accept, cur, lam_n);
+        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
