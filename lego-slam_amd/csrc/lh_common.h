@@ -108,7 +108,8 @@ struct lh_ctrl {
     double chi, lambda, ni, last_chi, spose, chi2_initial;
     int32_t iter, false_cnt, trials, accepted, done, cur, trace_len;
     int32_t nonpd;             // rank-deficient H_ll landmarks at the initial linearisation
-    int32_t pcg_iters, pad_;   // PCG iterations summed over the solve's trials
+    int32_t pcg_iters;         // PCG iterations summed over the solve's trials
+    int32_t evo;               // the next trial is in the final LM iteration: k_lin evaluates only
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
 };
 
@@ -117,7 +118,7 @@ struct lh_params {
     int32_t ext_identity;   // bit c: camera c's extrinsic is exactly the identity
     int32_t solver;         // 0 LDL^T (Eigen LDLT, problem.cpp:420), 1 PCG (problem.cpp:422, :584-614)
     int32_t gate_mode;      // 0 reference Huber gate (base_edge.cpp:55); 1 diagnostic (residue taken as 0)
-    int32_t pad0_;
+    int32_t no_evo;         // 1: every trial linearises in full (diagnostic A/B of ctrl.evo; env LH_NO_EVO)
     double huber_delta, stop_dchi2, tau, lambda_cap, lambda_init;
     double pcg_tol;         // PCG stop: ||r|| <= pcg_tol ||b|| (reference 1e-6, problem.cpp:597)
     int32_t pcg_max_it;     // PCG cap (<= 0: 2 * rows, problem.cpp:422)

@@ -432,6 +432,7 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     prm.solver = h->opt.linear_solver;
     prm.pcg_tol = h->opt.pcg_tol;
     prm.pcg_max_it = h->opt.pcg_max_iters;
+    prm.no_evo = getenv("LH_NO_EVO") != nullptr;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     const double t1 = now_ms();
 
@@ -1185,12 +1186,16 @@ int lh_debug_time_lin(lh_handle* h, int reps, double* ms) {
     if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
     hipStream_t s = h->stream;
     int* done = reinterpret_cast<int*>(reinterpret_cast<char*>(h->d_ctrl.p) + offsetof(lh_ctrl, done));
+    int* evo = reinterpret_cast<int*>(reinterpret_cast<char*>(h->d_ctrl.p) + offsetof(lh_ctrl, evo));
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess) return LH_E_HIP;
     if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return LH_E_HIP; }
     int st = LH_OK;
     const int zero = 0, one = 1;
-    if (hipMemcpyAsync(done, &zero, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) st = LH_E_HIP;
+    int evo_saved = 0;   // a solve stopped by max_iters leaves evo set: replay the full linearisation
+    if (hipMemcpyAsync(&evo_saved, evo, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess) st = LH_E_HIP;
+    if (st == LH_OK && hipMemcpyAsync(evo, &zero, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) st = LH_E_HIP;
+    if (st == LH_OK && hipMemcpyAsync(done, &zero, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) st = LH_E_HIP;
     if (st == LH_OK && launch_lin(h, 1) != LH_OK) st = LH_E_HIP;   // warm-up
     if (st == LH_OK && hipEventRecord(a, s) != hipSuccess) st = LH_E_HIP;
     for (int r = 0; r < reps && st == LH_OK; ++r)
@@ -1198,6 +1203,7 @@ int lh_debug_time_lin(lh_handle* h, int reps, double* ms) {
     if (st == LH_OK && hipEventRecord(b, s) != hipSuccess) st = LH_E_HIP;
     if (hipMemcpyAsync(done, &one, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) st = LH_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) st = LH_E_HIP;
+    if (hipMemcpy(evo, &evo_saved, sizeof(int), hipMemcpyHostToDevice) != hipSuccess) st = LH_E_HIP;
     float e = 0.f;
     if (st == LH_OK && hipEventElapsedTime(&e, a, b) != hipSuccess) st = LH_E_HIP;
     (void)hipEventDestroy(a);

@@ -438,6 +438,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 
     if (__builtin_amdgcn_readfirstlane(ctrl->done)) return;
     const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
+    // a trial of the final LM iteration (ctrl->evo, ctrl_lm_step): back substitution and the
+    // candidate's evaluation only (landmark positions, rho0 per edge, chi2 and the gain scale)
+    const bool evo = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->evo) != 0;
     const int cand = 1 - cur;
     const double lambda = ctrl->lambda;
     const int chunk = chunk_base + blockIdx.x;
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             for (int i = 0; i < 12; ++i) cl[i] = myrec[LH_REC_L + i];
         }
         wave_sync();
-        {
+        if (!evo) {
             // the pose-sum image [landmark][slot][33] starts at zero: cells without a live
             // observation then add exact zeros, and the per-slot sums need no masks or branches
             double2* z = reinterpret_cast<double2*>(scr);
@@ -605,6 +608,23 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             }
         }
         STAMP(0);
+
+        if (evo) {   // the same evaluation as below, without the linearisation
+            if (has) {
+                const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
+                EdgeEval E;
+                edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
+                edge_robust(E, prm);
+                edge_rho[o] = E.rho0;
+                chi_acc += E.rho0;
+            }
+            if (lead) {
+                double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
+                reinterpret_cast<double2*>(rw)[0] = double2{X[0], X[1]};
+                rw[2] = X[2];
+            }
+            continue;
+        }
 
         // ---- evaluate and linearise at the candidate (problem.cpp:285-331, :523-526) ----
         // H_pp and b_p go straight to this lane's row of the pose-sum transpose
@@ -780,6 +800,20 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     lds_barrier();
     STAMP(8);
     double* smem = dsm;
+    if (evo) {   // the chunk's scalars only, combined in the same order as below
+        for (int phase = 0; phase < 2; ++phase) {
+            if ((wave >> 1) == phase && lane == 0) {
+                double* sc = smem + (wave & 1) * 2;
+                if (phase == 0) { sc[0] = chi_acc; sc[1] = scale_acc; }
+                else { sc[0] += chi_acc; sc[1] += scale_acc; }
+            }
+            lds_barrier();
+        }
+        double* gs = csc + (size_t)chunk * 4;
+        if (tid < 2) gs[tid] = smem[tid] + smem[2 + tid];
+        if (tid == 2 || tid == 3) gs[tid] = 0.0;
+        return;
+    }
     for (int phase = 0; phase < 2; ++phase) {
         if ((wave >> 1) == phase) {
             double* sl = smem + (wave & 1) * Cfg::LS;
@@ -861,10 +895,11 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // the stop flag and this block's pair words are independent loads: one round trip for all
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
+    const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_lin wrote the chunk scalars only
     const int bq = b < LY.npairs ? b : 0;
     const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
     const int ib = pair_ptr[bq], ie = pair_ptr[bq + 1];
-    if (done) return;
+    if (done || (evo && b < LY.npairs)) return;
     if (b == LY.npairs) {
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
         for (int c = tid; c < n_chunks; c += RT) {
@@ -1428,6 +1463,11 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
         ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
         ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+        // The next trial is in the final iteration when one more completed iteration reaches max_iters.
+        // Its decision then either stops the loop (accept, or the last rejection) or leads to another
+        // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).
+        const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
+        ctrl->evo = (done || prm.no_evo) ? 0 : near;
         // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
         // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
         // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
@@ -1436,7 +1476,7 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         // can have enqueued.  One 32-bit store: the host never sees a torn pair.
         if (host_done) {
             if (done) host_done[0] = 1;
-            else host_done[1] = 2 * seq + ((prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0);
+            else host_done[1] = 2 * seq + near;
         }
     }
     done_o = done;

@@ -564,3 +564,30 @@ def test_collective_count_is_a_function_of_the_stop_trial(monkeypatch, depth):
         counts.add(s.comm_count())
     assert counts == {1 + min(r["trials"] + depth, 100)}
     s.close()
+
+
+# A trial of the final LM iteration only evaluates the candidate (ctrl.evo): its linearisation could
+# never be used.  LH_NO_EVO=1 (read when a window is uploaded) linearises every trial in full; both
+# runs must agree bit for bit, including runs that reject in the final iteration.
+@pytest.mark.parametrize("cfg,family,kw", [
+    ("C2", "stable", {}),
+    ("C2", "default", {}),
+    ("C1", "default", dict(max_iters=3, max_trials=3)),
+    ("C2", "default", dict(strategy=1, max_iters=4)),
+    ("C1", "stable", dict(max_iters=1, max_trials=1)),
+    ("W24s", "stable_noout", dict(max_iters=3)),
+])
+def test_final_iteration_trials_evaluate_only(cfg, family, kw, monkeypatch):
+    w = window(cfg, seed=4, family=family)
+    monkeypatch.setenv("LH_NO_EVO", "1")
+    s = lego_ba.Solver(**kw)
+    full = s.solve(w)
+    s.close()
+    monkeypatch.delenv("LH_NO_EVO")
+    s = lego_ba.Solver(**kw)
+    evo = s.solve(w)
+    s.close()
+    for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final"):
+        assert full[k] == evo[k], k
+    for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
+        assert np.array_equal(full[k], evo[k]), k
