@@ -93,7 +93,7 @@ __device__ __forceinline__ void lds_barrier() {
 #pragma clang fp contract(off)
 
 // Eigen Quaternion(Matrix3): q = {w, x, y, z}, R row-major
-__device__ inline void d_q_from_R(const double* R, double q[4]) {
+__device__ __forceinline__ void d_q_from_R(const double* R, double q[4]) {
     double t = R[0] + R[4] + R[8];
     double w, x, y, z;     // scalars, not an indexed array: keeps the pose code out of scratch
     if (t > 0.0) {
@@ -132,7 +132,7 @@ __device__ inline void d_q_from_R(const double* R, double q[4]) {
 }
 
 // Eigen QuaternionBase::toRotationMatrix
-__device__ inline void d_R_from_q(const double q[4], double R[9]) {
+__device__ __forceinline__ void d_R_from_q(const double q[4], double R[9]) {
     const double w = q[0], x = q[1], y = q[2], z = q[3];
     const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
     const double twx = tx * w, twy = ty * w, twz = tz * w;
@@ -159,7 +159,7 @@ __device__ __forceinline__ void d_q_rotate(const double* q, const double v[3], d
 }
 
 // Eigen quaternion product + Sophus SO3Base::operator*= renormalisation
-__device__ inline void d_q_mul(const double* a, const double* b, double o[4]) {
+__device__ __forceinline__ void d_q_mul(const double* a, const double* b, double o[4]) {
     double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
     double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
     double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
@@ -173,13 +173,13 @@ __device__ inline void d_q_mul(const double* a, const double* b, double o[4]) {
 }
 
 // rotation angle of a twist (upsilon, omega): theta = |omega|
-__device__ inline double d_twist_theta(const double a[6]) {
+__device__ __forceinline__ double d_twist_theta(const double a[6]) {
     return sqrt(a[3] * a[3] + a[4] * a[4] + a[5] * a[5]);
 }
 
 // Sophus SE3::exp, twist (upsilon, omega) -> (q, t)   (Sophus 1.0 se3.hpp), with the
 // transcendentals given: sh, ch = sin, cos(theta / 2) and st, ct = sin, cos(theta)
-__device__ inline void d_se3_exp_trig(const double a[6], double sh, double ch, double st, double ct, double q[4],
+__device__ __forceinline__ void d_se3_exp_trig(const double a[6], double sh, double ch, double st, double ct, double q[4],
                                       double t[3]) {
     const double eps = 1e-10;
     const double* w = a + 3;
@@ -2203,45 +2203,51 @@ __device__ __forceinline__ void po_swap6(double x[6], int k, int j) {
         if (m > k && m == j) { const double t = x[k]; x[k] = x[m]; x[m] = t; }
 }
 
-// The same LDLT + solve as the oracle's ldlt_solve (n = 6: one 8-row panel) on one wave, in
-// registers: lane r < 6 holds row r of the full symmetric A (lanes >= 6 mirror row 5 and are
-// never read).  Eigen's in-place swaps on the lower triangle are a row exchange of lanes k and
-// idx plus a column exchange in every lane: the unfactored block stays full-symmetric, so the
-// upper entries the column exchange reads equal the lower ones Eigen swaps in.  Every element
-// sees the oracle's operations in the oracle's order (contraction off): bitwise the same x.
-// All 64 lanes of the wave call it; every lane returns x.
-__device__ void po_ldlt6_wave(double a[6], const double b[6], double x[6], int lane) {
+// The oracle's ldlt_solve (Eigen ldlt_inplace with diagonal pivoting + LDLT::_solve_impl) for n = 6
+// in registers: every lane holds the whole symmetric A and runs the same operations in the oracle's
+// order (contraction off), so x is bitwise the oracle's and no value crosses lanes.  Eigen's
+// in-place swaps on the lower triangle are a row and a column exchange of the full symmetric
+// storage: the unfactored block stays symmetric, so the upper entries the column exchange reads
+// equal the lower ones Eigen swaps in.  The pivot index is made wave-uniform (readfirstlane) so
+// the swaps are scalar branches over static registers.
+__device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b)[6], double (&x)[6]) {
     double dd[6];
     int tr[6];
     bool all_zero = false;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        if (all_zero) continue;   // (no break: the loop must unroll, a[k] stays a register)
+        if (all_zero) continue;   // (no break: the loop must unroll, A stays in registers)
         int idx = k;
-        double big = fabs(__shfl(a[k], k));
+        double big = fabs(A[k][k]);
 #pragma unroll
         for (int i = k + 1; i < 6; ++i) {
-            const double di = fabs(__shfl(a[i], i));
+            const double di = fabs(A[i][i]);
             if (di > big) { big = di; idx = i; }
         }
         idx = __builtin_amdgcn_readfirstlane(idx);   // uniform: every lane scanned the same values
         tr[k] = idx;
-        if (idx != k) {
-            const int partner = lane == k ? idx : (lane == idx ? k : lane);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) a[j] = __shfl(a[j], partner);
-            po_swap6(a, k, idx);
+        for (int m = k + 1; m < 6; ++m) {
+            if (m == idx) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) { const double t = A[k][j]; A[k][j] = A[m][j]; A[m][j] = t; }
+#pragma unroll
+                for (int i = 0; i < 6; ++i) { const double t = A[i][k]; A[i][k] = A[i][m]; A[i][m] = t; }
+            }
         }
         if (k > 0) {
             double temp[6];
 #pragma unroll
-            for (int j = 0; j < k; ++j) temp[j] = dd[j] * __shfl(a[j], k);
-            double si = 0.0;
+            for (int j = 0; j < k; ++j) temp[j] = dd[j] * A[k][j];
 #pragma unroll
-            for (int j = 0; j < k; ++j) si += a[j] * temp[j];
-            if (lane >= k) a[k] -= si;
+            for (int r = k; r < 6; ++r) {
+                double si = 0.0;
+#pragma unroll
+                for (int j = 0; j < k; ++j) si += A[r][j] * temp[j];
+                A[r][k] -= si;
+            }
         }
-        const double akk = __shfl(a[k], k);
+        const double akk = A[k][k];
         dd[k] = akk;
         const bool valid = fabs(akk) > 0.0;
         if (k == 0 && !valid) {   // Eigen: identity transpositions, A left as it is
@@ -2250,96 +2256,110 @@ __device__ void po_ldlt6_wave(double a[6], const double b[6], double x[6], int l
             all_zero = true;
             continue;
         }
-        if (k < 5 && valid && lane > k) a[k] /= akk;
+        if (k < 5 && valid) {
+#pragma unroll
+            for (int r = k + 1; r < 6; ++r) A[r][k] /= akk;
+        }
     }
     (void)all_zero;   // the solves run regardless (LDLT::_solve_impl)
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = b[i];
 #pragma unroll
     for (int k = 0; k < 6; ++k) po_swap6(x, k, tr[k]);
-    double L[6][6];   // L[i][k] = A(i, k), i > k: every lane's copy of the factor
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-#pragma unroll
-        for (int i = k; i < 6; ++i) L[i][k] = __shfl(a[k], i);
 #pragma unroll
     for (int k = 0; k < 6; ++k)
         if (x[k] != 0.0)
 #pragma unroll
-            for (int i = k + 1; i < 6; ++i) x[i] -= L[i][k] * x[k];
+            for (int i = k + 1; i < 6; ++i) x[i] -= A[i][k] * x[k];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        const double d = L[i][i];
+        const double d = A[i][i];
         x[i] = (fabs(d) > 2.2250738585072014e-308) ? x[i] / d : 0.0;
     }
 #pragma unroll
     for (int k = 5; k >= 0; --k)
 #pragma unroll
-        for (int i = 0; i < k; ++i) x[i] -= L[k][i] * x[k];
+        for (int i = 0; i < k; ++i) x[i] -= A[k][i] * x[k];
 #pragma unroll
     for (int k = 5; k >= 0; --k) po_swap6(x, k, tr[k]);
 }
 
-// VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91)
-__device__ void po_pose_add(const double d_in[6], const double* T12, double* out12) {
+// VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91),
+// on one wave: every lane computes the same result, except that lane 0 takes sin/cos(theta/2) and
+// lane 1 sin/cos(theta) in one sincos pass.  qT = the quaternion of SE3(T12) (d_q_from_R of its
+// rotation), cached by the caller.  out12: the new pose matrix (every lane), q/t: its SE3 table.
+__device__ __forceinline__ void po_pose_add_wave(const double (&d_in)[6], const double* T12, const double* qT,
+                                                 double (&out12)[12], double (&qo)[4], double (&to)[3], int lane) {
     double d[6];
     bool bad = false;
+#pragma unroll
     for (int a = 0; a < 6; ++a) { d[a] = d_in[a]; bad |= !isfinite(d[a]); }
-    if (bad)
+    if (bad) {
+#pragma unroll
         for (int a = 0; a < 6; ++a) d[a] = 0.0;
+    }
     const double th = d_twist_theta(d);
-    double sh, ch, st, ct;
-    sincos(0.5 * th, &sh, &ch);
-    sincos(th, &st, &ct);
-    double qe[4], te[3], qT[4], qn[4], tr[3], Rn[9];
+    double sn, cs;
+    sincos(lane == 1 ? th : 0.5 * th, &sn, &cs);
+    const double sh = readlane_d(sn, 0), ch = readlane_d(cs, 0), st = readlane_d(sn, 1), ct = readlane_d(cs, 1);
+    double qe[4], te[3], qn[4], tr[3], Rn[9];
     d_se3_exp_trig(d, sh, ch, st, ct, qe, te);
-    const double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
-    d_q_from_R(R, qT);
+    const double qTr[4] = {qT[0], qT[1], qT[2], qT[3]};
     const double tc[3] = {T12[3], T12[7], T12[11]};
-    d_q_mul(qe, qT, qn);
+    d_q_mul(qe, qTr, qn);
     d_q_rotate(qe, tc, tr);
     d_R_from_q(qn, Rn);
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
         out12[4 * i] = Rn[3 * i]; out12[4 * i + 1] = Rn[3 * i + 1]; out12[4 * i + 2] = Rn[3 * i + 2];
         out12[4 * i + 3] = te[i] + tr[i];
     }
+    // SE3(estimate_) of the new matrix, as the next linearisation reads it
+    const double R[9] = {out12[0], out12[1], out12[2], out12[4], out12[5], out12[6], out12[8], out12[9], out12[10]};
+    d_q_from_R(R, qo);
+    to[0] = out12[3]; to[1] = out12[7]; to[2] = out12[11];
 }
 
 #pragma clang fp contract(fast)
 
 struct PoShared {
-    double pose[12], cand[12], q[4], t[3], K[4];
+    double pose[12], cand[12], q[4], t[3], qp[4], K[4];   // q/t: the table being linearised; qp: SE3(pose)'s q
     double H[36], b[6], dx[6];
-    double red[FT / 64][FV];
+    double part[FT / 64][FV];
     double sum[FV];
+    double rows[FT][FV + 1];   // one thread's per-edge sums per row (odd stride: column reads spread over banks)
     double chi, lam, ni, last, delta;
-    int flags[4];              // 0: trial loop running, 1: iteration loop running
+    int iter, fc, cont;        // completed iterations, rejected trials in the iteration, another trial follows
 };
 
-// all FT threads: the workgroup's fixed-order sum of acc[FV] into S.sum
-__device__ __forceinline__ void po_reduce(double (&acc)[FV], PoShared& S, int tid) {
+// all FT threads: each thread's acc[FV] through LDS rows; per wave, lane 2k + h (k < FV) sums column k
+// over the wave's rows of parity h, in row order, and the two halves are added: S.part[wave].
+// The caller's barrier follows.  Fixed order: a batch is bitwise reproducible.
+__device__ __forceinline__ void po_rows_to_parts(const double (&acc)[FV], PoShared& S, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
-    group_sum(acc, 6);   // DPP within rows, ds_bpermute across them; every lane gets the totals
-    if (lane == 0)
 #pragma unroll
-        for (int k = 0; k < FV; ++k) S.red[wave][k] = acc[k];
-    lds_barrier();
-    if (tid < FV) {
+    for (int k = 0; k < FV; ++k) S.rows[tid][k] = acc[k];
+    wave_sync();
+    if (lane < 2 * FV) {
+        const int k = lane >> 1, h = lane & 1;
         double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < FT / 64; ++w) s += S.red[w][tid];
-        S.sum[tid] = s;
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) s += S.rows[64 * wave + 2 * i + h][k];
+        s += dpp_d<0xB1>(s);   // quad_perm [1,0,3,2]: the other parity's half
+        if (h == 0) S.part[wave][k] = s;
     }
-    lds_barrier();
 }
 
-// SE3(estimate_) of S.cand (or S.pose) into S.q / S.t (one thread)
-__device__ __forceinline__ void po_table(PoShared& S, const double* T12) {
+// SE3(estimate_) of T12 into q / t (d_q_from_R of its rotation)
+__device__ __forceinline__ void po_table_regs(const double* T12, double (&q)[4], double (&t)[3]) {
     const double R[9] = {T12[0], T12[1], T12[2], T12[4], T12[5], T12[6], T12[8], T12[9], T12[10]};
-    d_q_from_R(R, S.q);
-    S.t[0] = T12[3]; S.t[1] = T12[7]; S.t[2] = T12[11];
+    d_q_from_R(R, q);
+    t[0] = T12[3]; t[1] = T12[7]; t[2] = T12[11];
 }
 
+// One workgroup per frame.  Per LM trial there are two barriers: after the linearisation's per-wave
+// sums, and after wave 0 has finished the sums, taken the LM decision (lane 0) and, when another
+// trial follows, solved the 6x6 step and composed the candidate pose (all of wave 0).
 __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_ptr, const double* __restrict__ pose_in,
                                                const double* __restrict__ pts, const double* __restrict__ uv,
                                                const uint8_t* __restrict__ flag_in, lh_params prm,
@@ -2347,7 +2367,8 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
                                                uint8_t* __restrict__ flag_out, double* __restrict__ rchi2_out,
                                                int32_t* __restrict__ iters_out, int32_t* __restrict__ inliers_out) {
     __shared__ PoShared S;
-    const int f = blockIdx.x, tid = threadIdx.x;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t o0 = obs_ptr[f];
     const int O = (int)(obs_ptr[f + 1] - o0);
     const double* X = pts + 3 * o0;
@@ -2359,8 +2380,8 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
     if (tid == 0) S.delta = prm.huber_delta;
     int its = 0;
 
-    // linearise at T12 (S.q / S.t already its table): residuals -> R, H, b, sum rho0 -> S.sum
-    auto linearise = [&]() {
+    // linearise at the table S.q / S.t: residuals -> R, per-wave sums -> S.part (then a barrier)
+    auto linearise = [&]() __attribute__((always_inline)) {
         double acc[FV];
 #pragma unroll
         for (int k = 0; k < FV; ++k) acc[k] = 0.0;
@@ -2373,68 +2394,90 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
             R[2 * e + 1] = r1;
             po_accumulate(r0, r1, J, delta, acc);
         }
-        po_reduce(acc, S, tid);
+        po_rows_to_parts(acc, S, tid);
+        lds_barrier();
     };
-    auto load_system = [&]() {   // thread 0: S.sum -> H (full symmetric), b
+    // wave 0: the four waves' parts -> S.sum (lane k < FV)
+    auto finish_sums = [&]() __attribute__((always_inline)) {
+        if (lane < FV) S.sum[lane] = ((S.part[0][lane] + S.part[1][lane]) + S.part[2][lane]) + S.part[3][lane];
+        wave_sync();
+    };
+    auto load_system = [&]() __attribute__((always_inline)) {   // lane 0: S.sum -> H (full symmetric), b
         int k = 0;
         for (int a = 0; a < 6; ++a)
             for (int c = a; c < 6; ++c) { S.H[6 * a + c] = S.sum[k]; S.H[6 * c + a] = S.sum[k]; ++k; }
         for (int a = 0; a < 6; ++a) S.b[a] = S.sum[21 + a];
+    };
+    // wave 0: (H + lambda D) dx = b, then the candidate pose and its table
+    auto solve_step = [&]() __attribute__((always_inline)) {
+        double A[6][6], bb[6], x[6];
+        const double lam = S.lam;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) A[r][j] = S.H[6 * r + j];
+            bb[r] = S.b[r];
+            A[r][r] += (prm.strategy == 0) ? lam : lam * A[r][r];
+        }
+        po_ldlt6_reg(A, bb, x);
+        double cand[12], q[4], t[3];
+        po_pose_add_wave(x, S.pose, S.qp, cand, q, t, lane);
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) S.dx[j] = x[j];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) S.cand[i] = cand[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) S.q[i] = q[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) S.t[i] = t[i];
+        }
     };
 
     for (int round = 0; round < 4; ++round) {
         if (tid < 12) S.pose[tid] = pose_in[12 * (size_t)f + tid];   // setEstimate(current_frame_->Pose()) :201
         lds_barrier();
         if (O > 0) {   // Problem::solve returns false with no edge (problem.cpp:157-161)
-            if (tid == 0) po_table(S, S.pose);
-            lds_barrier();
-            linearise();
             if (tid == 0) {
-                load_system();
-                // computeLambdaInitLM (problem.cpp:470-504)
-                S.ni = 2.0;
-                S.chi = 0.5 * S.sum[27];
-                if (prm.strategy == 0) {
-                    if (prm.lambda_given) {
-                        S.lam = prm.lambda_init;
-                    } else {
-                        double m = 0.0;
-                        for (int i = 0; i < 6; ++i) m = fmax(fabs(S.H[7 * i]), m);
-                        S.lam = prm.tau * fmin(prm.lambda_cap, m);
-                    }
-                } else {
-                    S.lam = 1e-5;
-                }
-                S.last = 1e20;
-                S.flags[1] = prm.max_iters > 0;
+                double q[4], t[3];
+                po_table_regs(S.pose, q, t);
+                for (int i = 0; i < 4; ++i) { S.q[i] = q[i]; S.qp[i] = q[i]; }
+                for (int i = 0; i < 3; ++i) S.t[i] = t[i];
             }
             lds_barrier();
-            int iter = 0;
-            while (S.flags[1]) {
-                if (tid == 0) { S.flags[0] = 1; S.flags[2] = 0; }   // trial loop, false_cnt
-                lds_barrier();
-                while (S.flags[0]) {
-                    if (tid < 64) {   // wave 0: H + lambda, the 6x6 solve in registers; lane 0: the update
-                        const int r = tid < 6 ? tid : 5;
-                        double a[6], bb[6], x[6];
-                        const double lam = S.lam;
-#pragma unroll
-                        for (int j = 0; j < 6; ++j) {
-                            a[j] = S.H[6 * r + j];
-                            bb[j] = S.b[j];
-                            if (j == r) a[j] += (prm.strategy == 0) ? lam : lam * a[j];
+            linearise();
+            if (wave == 0) {
+                finish_sums();
+                if (lane == 0) {
+                    load_system();
+                    // computeLambdaInitLM (problem.cpp:470-504)
+                    S.ni = 2.0;
+                    S.chi = 0.5 * S.sum[27];
+                    if (prm.strategy == 0) {
+                        if (prm.lambda_given) {
+                            S.lam = prm.lambda_init;
+                        } else {
+                            double m = 0.0;
+                            for (int i = 0; i < 6; ++i) m = fmax(fabs(S.H[7 * i]), m);
+                            S.lam = prm.tau * fmin(prm.lambda_cap, m);
                         }
-                        po_ldlt6_wave(a, bb, x, tid);
-                        if (tid == 0) {
-#pragma unroll
-                            for (int j = 0; j < 6; ++j) S.dx[j] = x[j];
-                            po_pose_add(S.dx, S.pose, S.cand);
-                            po_table(S, S.cand);
-                        }
+                    } else {
+                        S.lam = 1e-5;
                     }
-                    lds_barrier();
-                    linearise();   // isGoodStepInLM's residuals (:524) and, if accepted, buildHessian's
-                    if (tid == 0) {
+                    S.last = 1e20;
+                    S.iter = 0;
+                    S.fc = 0;
+                    S.cont = prm.max_iters > 0;
+                }
+                wave_sync();
+                if (S.cont) solve_step();
+            }
+            lds_barrier();
+            while (S.cont) {
+                linearise();   // isGoodStepInLM's residuals (:524) and, if accepted, buildHessian's
+                if (wave == 0) {
+                    finish_sums();
+                    if (lane == 0) {
                         const double tchi = 0.5 * S.sum[27];
                         double scale = 0.0;
                         for (int i = 0; i < 6; ++i)
@@ -2460,29 +2503,40 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
                             if (ok) { S.lam = fmax(S.lam / 9.0, 1e-7); S.chi = tchi; }
                             else S.lam = fmin(S.lam * 11.0, 1e7);
                         }
+                        bool inner_end;
                         if (ok) {
                             for (int i = 0; i < 12; ++i) S.pose[i] = S.cand[i];
+                            for (int i = 0; i < 4; ++i) S.qp[i] = S.q[i];   // the candidate's table is SE3(pose)'s
                             load_system();
-                            S.flags[0] = 0;
+                            inner_end = true;
                         } else {
-                            S.flags[2] += 1;                   // rollbackStates: S.pose untouched
-                            if (S.flags[2] >= prm.max_trials) S.flags[0] = 0;
+                            S.fc += 1;                         // rollbackStates: S.pose untouched
+                            inner_end = S.fc >= prm.max_trials;
                         }
+                        int cont = 1;
+                        if (inner_end) {
+                            S.iter += 1;
+                            if (S.last - S.chi < prm.stop_dchi2 || S.iter >= prm.max_iters) cont = 0;
+                            S.last = S.chi;
+                            S.fc = 0;
+                        }
+                        S.cont = cont;
                     }
-                    lds_barrier();
-                }
-                ++iter;
-                if (tid == 0) {
-                    if (S.last - S.chi < prm.stop_dchi2 || iter >= prm.max_iters) S.flags[1] = 0;
-                    S.last = S.chi;
+                    wave_sync();
+                    if (S.cont) solve_step();
                 }
                 lds_barrier();
             }
-            its += iter;
+            its += S.iter;
         }
         // outlier flags (frontend_lego.cpp:205-226); residual_ is "as last evaluated" except for the
         // features already flagged, which are recomputed at the final estimate
-        if (tid == 0) po_table(S, S.pose);
+        if (tid == 0) {
+            double q[4], t[3];
+            po_table_regs(S.pose, q, t);
+            for (int i = 0; i < 4; ++i) S.q[i] = q[i];
+            for (int i = 0; i < 3; ++i) S.t[i] = t[i];
+        }
         lds_barrier();
         const double delta = S.delta;
         for (int e = tid; e < O; e += FT) {
