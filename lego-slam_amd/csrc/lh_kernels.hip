@@ -1905,8 +1905,15 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
     }
     lds_barrier();
     // ---------------- forward substitution (unit L), the oracle's order ----------------
+    static_assert(GNMAX <= GT, "one row per thread in the solves' row updates");
     for (int K = 0; K < n; K += GNB) {
         const int kb = min(GNB, n - K);
+        // the block's columns of the rows below: loaded first (they do not depend on the solve), so
+        // their latency overlaps the diagonal block's chain
+        const int ib = K + kb + tid;
+        double Lb[GNB];
+#pragma unroll
+        for (int k = 0; k < GNB; ++k) Lb[k] = (ib < n && k < kb) ? gA[(size_t)ib * NG + K + k] : 0.0;
         if (wave == 0) {
             const int r = lane & (GNB - 1);
             double x = yv[K + r];
@@ -1915,7 +1922,7 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             for (int k = 0; k < GNB; ++k) Lr[k] = (r > k && K + r < n) ? pnl[(K + r) * GPS + k] : 0.0;
 #pragma unroll
             for (int k = 0; k < GNB; ++k) {
-                const double xk = __shfl(x, k);
+                const double xk = readlane_d(x, k);   // uniform: an SGPR pair, no LDS round trip
                 if (k < kb && r > k && r < kb) {
                     const bool same_panel = (r >> 3) == (k >> 3);
                     if (!same_panel || xk != 0.0) x -= Lr[k] * xk;
@@ -1924,15 +1931,12 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             if (lane < kb) yv[K + lane] = x;
         }
         lds_barrier();
-        for (int i = K + kb + tid; i < n; i += GT) {   // the block's columns, ascending; loads all in flight
-            double Lr[GNB];
-#pragma unroll
-            for (int k = 0; k < GNB; ++k) Lr[k] = k < kb ? gA[(size_t)i * NG + K + k] : 0.0;
-            double x = yv[i];
+        if (ib < n) {   // the block's columns, ascending
+            double x = yv[ib];
 #pragma unroll
             for (int k = 0; k < GNB; ++k)
-                if (k < kb) x -= Lr[k] * yv[K + k];
-            yv[i] = x;
+                if (k < kb) x -= Lb[k] * yv[K + k];
+            yv[ib] = x;
         }
         lds_barrier();
     }
@@ -1945,6 +1949,10 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
     // ---------------- back substitution (L^T), descending ----------------
     for (int K = ((n - 1) / GNB) * GNB; K >= 0; K -= GNB) {
         const int kb = min(GNB, n - K);
+        const int ia = tid;   // the rows above the block: their L^T entries, loaded ahead as above
+        double La[GNB];
+#pragma unroll
+        for (int k = 0; k < GNB; ++k) La[k] = (ia < K && k < kb) ? gA[(size_t)(K + k) * NG + ia] : 0.0;
         if (wave == 0) {
             const int r = lane & (GNB - 1);
             double x = yv[K + r];
@@ -1953,21 +1961,18 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             for (int k = 0; k < GNB; ++k) Lc[k] = (k > r && k < kb) ? pnl[(K + k) * GPS + r] : 0.0;
 #pragma unroll
             for (int k = GNB - 1; k >= 0; --k) {
-                const double xk = __shfl(x, k);
+                const double xk = readlane_d(x, k);
                 if (k < kb && r < k) x -= Lc[k] * xk;
             }
             if (lane < kb) yv[K + lane] = x;
         }
         lds_barrier();
-        for (int i = tid; i < K; i += GT) {   // the block's rows, descending; loads all in flight
-            double Lc[GNB];
-#pragma unroll
-            for (int k = 0; k < GNB; ++k) Lc[k] = k < kb ? gA[(size_t)(K + k) * NG + i] : 0.0;
-            double x = yv[i];
+        if (ia < K) {   // the block's rows, descending
+            double x = yv[ia];
 #pragma unroll
             for (int k = GNB - 1; k >= 0; --k)
-                if (k < kb) x -= Lc[k] * yv[K + k];
-            yv[i] = x;
+                if (k < kb) x -= La[k] * yv[K + k];
+            yv[ia] = x;
         }
         lds_barrier();
     }
