@@ -40,7 +40,9 @@ hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* cs
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
-                          lh_params prm, int mode, int* host_done, int seq, double* gA);
+                          lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS);
+hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
+                           double* gS, int P);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
                            double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
                            double* dxp, int ndxp, lh_ctrl* ctrl);
@@ -250,7 +252,7 @@ struct lh_handle {
     DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
     DevBuf<uint16_t> d_pair_pq;
     DevBuf<int32_t> d_obs_perm, d_lm_perm;
-    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_rs_stage,
+    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_gS, d_rs_stage,
         d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
@@ -465,6 +467,10 @@ int upload_impl(lh_handle* h, const lh_window* w) {
         const bool fresh = h->d_gA.n < ng * ng;
         HIPCHK(h->d_gA.ensure(ng * ng));
         if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
+        // k_dense's dense symmetric S, double-buffered with the committed state
+        const bool fresh_s = h->d_gS.n < 2 * ng * ng;
+        HIPCHK(h->d_gS.ensure(2 * ng * ng));
+        if (fresh_s) HIPCHK(hipMemsetAsync(h->d_gS.p, 0, h->d_gS.n * sizeof(double), h->stream));
     }
     HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
     HIPCHK(h->d_maxd.ensure(1));
@@ -572,9 +578,10 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     }
     {
         Prof pr(h, KC_CTRL);
+        if (h->P > LH_PMAX) HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p,
                               h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial,
-                              h->d_gA.p));
+                              h->d_gA.p, h->d_gS.p));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -872,7 +879,7 @@ void lh_destroy(lh_handle* h) {
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
-    h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
+    h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_gS.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
     h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();

@@ -1979,14 +1979,36 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
     CSTAMP(7);
 }
 
+// k_dense: the reduced system's S blocks (packed per pose pair, p <= q) into the dense symmetric n x n
+// matrix gS[1 - cur] (stride NG) that k_ctrl_g gathers from in pivot order.  One 64-thread block per
+// pair, launched after the exchange (when there is one) and before k_ctrl_g; gS is double-buffered
+// with the committed state (ctrl->cur), so a rejected trial keeps the committed copy.
+__global__ __launch_bounds__(64) void k_dense(const double* __restrict__ rs, const uint16_t* __restrict__ pair_pq,
+                                              const lh_ctrl* __restrict__ ctrl, double* __restrict__ gS, int P, int NG) {
+    const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
+    const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_reduce wrote no S blocks
+    const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
+    if (done || evo) return;
+    const lh_rs_layout LY = lh_rs_make(P);
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int p = pair_pq[2 * b], q = pair_pq[2 * b + 1];
+    if (lane >= 36) return;
+    const int a = lane / 6, c = lane - 6 * (lane / 6);
+    const double v = rs[LY.off_S + b * 36 + lane];
+    double* g = gS + (size_t)(1 - cur) * NG * NG;
+    g[(size_t)(6 * p + a) * NG + 6 * q + c] = v;
+    if (p != q) g[(size_t)(6 * q + c) * NG + 6 * p + a] = v;   // a diagonal block has both halves already
+}
+
 __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                                const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                                const uint32_t* __restrict__ rsmap, double* __restrict__ pose_mat,
                                                double* __restrict__ ptab, const double* __restrict__ ext,
                                                double* __restrict__ dxp, lh_params prm, int mode,
-                                               volatile int* __restrict__ host_done, int seq, double* __restrict__ gA) {
+                                               volatile int* __restrict__ host_done, int seq, double* __restrict__ gA,
+                                               const double* __restrict__ gS) {
     __shared__ double pnl[GNMAX * GPS];
-    __shared__ double dg[GNMAX], bsv[GNMAX], bpv[GNMAX], hdv[GNMAX], xs[GNMAX], yv[GNMAX];
+    __shared__ double dg[GNMAX], bsv[GNMAX], bpv[GNMAX], hdv[GNMAX], xs[GNMAX], yv[GNMAX], gkey[GNMAX];
     __shared__ int perm[GNMAX], iperm[GNMAX];
     __shared__ int s_flags[4];
     __shared__ double s_red[GT / 64], s_lam;
@@ -2047,10 +2069,12 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     CSTAMP(1);
 
     // ---------------- diagonal + lambda and right-hand sides (one round trip) ----------------
+    // S of the chosen system is k_dense's dense copy gS[cur] (cur after the decision: the candidate's
+    // on accept, the committed one on reject); the right-hand sides come from the packed system.
     const double* __restrict__ src = accept ? rs_stage : rs_commit;
+    const double* __restrict__ gSc = gS + (size_t)cur * NG * NG;
     for (int i = tid; i < n; i += GT) {
-        const int p = i / 6, a = i - 6 * (i / 6);
-        const double v = src[LY.off_S + (p * P - (p * (p - 1)) / 2) * 36 + 7 * a];   // S block (p, p), entry (a, a)
+        const double v = gSc[(size_t)i * NG + i];
         dg[i] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
         bsv[i] = src[LY.off_bs + i];
         bpv[i] = src[LY.off_bp + i];
@@ -2060,13 +2084,17 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     CSTAMP(2);
 
     // ---------------- pivot order: |diag| descending, ties by index, NaN last (as k_ctrl) ----------------
+    for (int i = tid; i < n; i += GT) {   // the sort keys once
+        const double d = fabs(dg[i]);
+        gkey[i] = (d == d) ? d : -1.0;
+    }
+    lds_barrier();
     for (int row = tid; row < n; row += GT) {
-        double di = fabs(dg[row]);
-        if (!(di == di)) di = -1.0;
+        const double di = gkey[row];
         int r = 0;
+#pragma unroll 8
         for (int j = 0; j < n; ++j) {
-            double d = fabs(dg[j]);
-            if (!(d == d)) d = -1.0;
+            const double d = gkey[j];
             r += (d > di) || (d == di && j < row);
         }
         perm[r] = row;
@@ -2081,34 +2109,38 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     lds_barrier();
     CSTAMP(3);
 
-    // ---------------- one pass over the system: commit, scatter into gA (permuted lower triangle) ----------------
-    for (int base = tid; base < LY.total; base += 16 * GT) {
-        double v[16];
-        uint32_t mp[16];
+    // ---------------- commit (the packed right-hand sides), gather gA (permuted lower triangle) ----------------
+    // S itself is double-buffered as gS (the decision picked the buffer): only the part after it commits
+    if (accept)
+        for (int i = LY.off_bs + tid; i < LY.total; i += GT) rs_commit[i] = src[i];
+    // gA(r, c) = S(perm r, perm c), r > c: a wave per row (lanes over columns), so its stores are
+    // contiguous and its loads fall in one row of gS; eight rows per wave at a time, 48 loads in flight
+    static_assert(GNMAX <= 6 * 64, "six 64-column chunks cover a row");
+    for (int r0 = wave; r0 < NG; r0 += 8 * (GT / 64)) {
+        double v[8][6];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int i = base + u * GT;
-            v[u] = i < LY.total ? src[i] : 0.0;
-            mp[u] = i < LY.off_bs ? rsmap[i] : 0u;
+        for (int u = 0; u < 8; ++u) {
+            const int r = r0 + u * (GT / 64);
+            const int pr = (r < n) ? perm[r] : 0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int c = 64 * j + lane;
+                v[u][j] = (c < r && r < n) ? gSc[(size_t)pr * NG + perm[c]] : 0.0;
+            }
         }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int i = base + u * GT;
-            if (accept && i < LY.total) rs_commit[i] = v[u];
-            if (i < LY.off_bs) {
-                const int ri = iperm[LH_RSMAP_ROW(mp[u])], rj = iperm[LH_RSMAP_COL(mp[u])];
-                if (!LH_RSMAP_DIAG(mp[u])) gA[(size_t)max(ri, rj) * NG + min(ri, rj)] = v[u];
-                else if (ri > rj) gA[(size_t)ri * NG + rj] = v[u];
+        for (int u = 0; u < 8; ++u) {
+            const int r = r0 + u * (GT / 64);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int c = 64 * j + lane;
+                if (c < r && r < NG) gA[(size_t)r * NG + c] = v[u][j];
             }
         }
     }
     for (int i = tid; i < NG; i += GT) {
         gA[(size_t)i * NG + i] = i < n ? dg[perm[i]] : 1.0;
         yv[i] = i < n ? bsv[perm[i]] : 0.0;
-    }
-    for (int x = tid; x < (NG - n) * NG; x += GT) {
-        const int r = n + x / NG, c = x - NG * (x / NG);
-        if (c < r) gA[(size_t)r * NG + c] = 0.0;
     }
     __syncthreads();   // global stores before the panel loads
     CSTAMP(4);
@@ -2663,12 +2695,20 @@ hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* cs
     return hipGetLastError();
 }
 
+hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
+                           double* gS, int P) {
+    if (P <= LH_PMAX) return hipSuccess;
+    const int NG = (6 * P + GNB - 1) & ~(GNB - 1);
+    hipLaunchKernelGGL(k_dense, dim3(P * (P + 1) / 2), dim3(64), 0, st, rs_stage, pair_pq, ctrl, gS, P, NG);
+    return hipGetLastError();
+}
+
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
-                          int* host_done, int seq, double* gA) {
+                          int* host_done, int seq, double* gA, const double* gS) {
     if (prm.P > LH_PMAX)
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
-                           dxp, prm, mode, (volatile int*)host_done, seq, gA);
+                           dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
                            prm, mode, (volatile int*)host_done, seq);
