@@ -84,7 +84,7 @@ typedef struct lh_options {
                                  non-positive-definite H_ll poisons the step, as the LU inverse's
                                  inf does (problem.cpp:396-400; the solve then rejects every trial);
                                  1: such landmarks are held fixed (no Schur term, no update)   */
-    int32_t trials_per_sync;  /* LM trials kept in flight ahead of the host poll (0: auto = 2)  */
+    int32_t trials_per_sync;  /* LM trials kept enqueued past the last one the device has decided (0: auto = 2; one while the next completed iteration reaches max_iters) */
     int32_t profile;          /* 1: time every kernel with HIP events (lh_kernel_stats)       */
     int32_t pcg_max_iters;    /* PCG: iteration cap; <= 0: 2 * rows (problem.cpp:422)          */
     double pcg_tol;           /* PCG: stop when ||r|| <= pcg_tol * ||b|| (1e-6, problem.cpp:597) */

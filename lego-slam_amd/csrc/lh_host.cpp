@@ -676,7 +676,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         // max_iters) until the device raises done.  hipStreamQuery at most every 50 ms turns a
         // device fault into an error return (each query delays the next launch by ~6 us).
         unsigned spin = 0;
-        const bool query_often = getenv("LH_QUERY_OFTEN") != nullptr;   // diagnostic A/B switch
+        static const bool query_often = getenv("LH_QUERY_OFTEN") != nullptr;   // diagnostic A/B switch (timing only)
         double t_query = now_ms();
         while (!hd[0] && enq < max_total) {
             const int pw = hd[1];   // 2 * (last live trial) + near, or -1 before the first
