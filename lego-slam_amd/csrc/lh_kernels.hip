@@ -483,9 +483,11 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     v4d acc[Cfg::NT];
 #pragma unroll
     for (int t = 0; t < Cfg::NT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
-    double task[Cfg::UMAX];
+    // per-pose sums: lane l owns the (slot, task) cells c = l + 64 i, c = 33 slot + task (all 64 lanes)
+    constexpr int NCELL = (Cfg::UMAX * LH_TASKS + 63) / 64;
+    double task[NCELL];
 #pragma unroll
-    for (int u = 0; u < Cfg::UMAX; ++u) task[u] = 0.0;
+    for (int u = 0; u < NCELL; ++u) task[u] = 0.0;
     double chi_acc = 0.0, scale_acc = 0.0, maxd = 0.0, ndeg = 0.0;
     STAMP_DECL
 
@@ -733,22 +735,24 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         }
         STAMP(3);
 
-        // ---- per-pose sums (H_pp, b_p, bsd): lane k < 33 adds task k of every landmark observing
-        //      the slot, in landmark (= lane) order ----
+        // ---- per-pose sums (H_pp, b_p, bsd): the owner of cell (slot, task) adds it over every
+        //      landmark observing the slot, in landmark (= lane) order ----
         wave_sync();
-        if (lane < LH_TASKS) {
+        {
             // every (landmark, slot) cell in landmark order: absent cells are +0.0, and adding
-            // them leaves every sum bit-identical to adding the present cells only
+            // them leaves every sum bit-identical to adding the present cells only.  Cell c of
+            // landmark l sits at scr[l * UMAX * 33 + c]: a wave's reads are contiguous.
 #pragma unroll
-            for (int uu = 0; uu < Cfg::UMAX; ++uu) {
-                if (uu < U) {
+            for (int i = 0; i < NCELL; ++i) {
+                const int c = lane + 64 * i;
+                if (c < U * LH_TASKS) {
                     double tv[LH_SB_LM];
 #pragma unroll
-                    for (int l = 0; l < LH_SB_LM; ++l) tv[l] = scr[(l * Cfg::UMAX + uu) * LH_TASKS + lane];
-                    double sacc = task[uu];
+                    for (int l = 0; l < LH_SB_LM; ++l) tv[l] = scr[l * Cfg::UMAX * LH_TASKS + c];
+                    double sacc = task[i];
 #pragma unroll
                     for (int l = 0; l < LH_SB_LM; ++l) sacc += tv[l];
-                    task[uu] = sacc;
+                    task[i] = sacc;
                 }
             }
         }
@@ -825,13 +829,12 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
                     const int idx = t * 256 + ((lane >> 4) + 4 * i) * 16 + (lane & 15);
                     sl[idx] = (first ? 0.0 : sl[idx]) + acc[t][i];
                 }
-            if (lane < LH_TASKS) {
 #pragma unroll
-                for (int uu = 0; uu < Cfg::UMAX; ++uu) {
-                    if (uu < U) {
-                        const int idx = Cfg::LS_TASK + uu * LH_TASKS + lane;
-                        sl[idx] = (first ? 0.0 : sl[idx]) + task[uu];
-                    }
+            for (int i = 0; i < NCELL; ++i) {
+                const int c = lane + 64 * i;
+                if (c < U * LH_TASKS) {
+                    const int idx = Cfg::LS_TASK + c;
+                    sl[idx] = (first ? 0.0 : sl[idx]) + task[i];
                 }
             }
             if (lane == 0) {
