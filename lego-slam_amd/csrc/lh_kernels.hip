@@ -2244,8 +2244,11 @@ __device__ __forceinline__ void po_swap6(double x[6], int k, int j) {
 }
 
 // The oracle's ldlt_solve (Eigen ldlt_inplace with diagonal pivoting + LDLT::_solve_impl) for n = 6
-// in registers: every lane holds the whole symmetric A and runs the same operations in the oracle's
-// order (contraction off), so x is bitwise the oracle's and no value crosses lanes.  Eigen's
+// in registers: every lane holds the whole symmetric A and runs the oracle's operations in the oracle's
+// order (contraction off), so no value crosses lanes.  One change: a division by a pivot is its
+// reciprocal (fast_rcp, one per pivot) times the element, as the k_ctrl LDL^T does.  The frontend's
+// sums of H and b already differ from the oracle's order, so its parity is to tolerance either way
+// (tests/test_frontend.py), and the 21 IEEE divisions were the longest part of the step.  Eigen's
 // in-place swaps on the lower triangle are a row and a column exchange of the full symmetric
 // storage: the unfactored block stays symmetric, so the upper entries the column exchange reads
 // equal the lower ones Eigen swaps in.  The pivot index is made wave-uniform (readfirstlane) so
@@ -2297,8 +2300,9 @@ __device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b
             continue;
         }
         if (k < 5 && valid) {
+            const double inv = fast_rcp(akk);
 #pragma unroll
-            for (int r = k + 1; r < 6; ++r) A[r][k] /= akk;
+            for (int r = k + 1; r < 6; ++r) A[r][k] *= inv;
         }
     }
     (void)all_zero;   // the solves run regardless (LDLT::_solve_impl)
@@ -2314,7 +2318,7 @@ __device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const double d = A[i][i];
-        x[i] = (fabs(d) > 2.2250738585072014e-308) ? x[i] / d : 0.0;
+        x[i] = (fabs(d) > 2.2250738585072014e-308) ? x[i] * fast_rcp(d) : 0.0;
     }
 #pragma unroll
     for (int k = 5; k >= 0; --k)
@@ -2419,6 +2423,21 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
     if (tid < 4) S.K[tid] = prm.K[tid];
     if (tid == 0) S.delta = prm.huber_delta;
     int its = 0;
+    STAMP_DECL   // diagnostic build: per-phase wave-cycles into lh_stamps[24..29]
+    // this thread's first edge, in registers for the whole launch (a frame of <= FT edges then reads
+    // no edge input from memory after this; further edges are read per pass)
+    double X0[3] = {0.0, 0.0, 0.0}, Z0[2] = {0.0, 0.0};
+    if (tid < O) {
+        X0[0] = X[3 * tid]; X0[1] = X[3 * tid + 1]; X0[2] = X[3 * tid + 2];
+        Z0[0] = Z[2 * tid]; Z0[1] = Z[2 * tid + 1];
+    }
+    auto edge_in = [&](int e, double (&Xe)[3], double& u, double& v) __attribute__((always_inline)) {
+        if (e == tid) {
+            Xe[0] = X0[0]; Xe[1] = X0[1]; Xe[2] = X0[2]; u = Z0[0]; v = Z0[1];
+        } else {
+            Xe[0] = X[3 * e]; Xe[1] = X[3 * e + 1]; Xe[2] = X[3 * e + 2]; u = Z[2 * e]; v = Z[2 * e + 1];
+        }
+    };
 
     // linearise at the table S.q / S.t: residuals -> R, per-wave sums -> S.part (then a barrier)
     auto linearise = [&]() __attribute__((always_inline)) {
@@ -2427,15 +2446,18 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
         for (int k = 0; k < FV; ++k) acc[k] = 0.0;
         const double delta = S.delta;
         for (int e = tid; e < O; e += FT) {
-            double r0, r1, J[12];
-            const double Xe[3] = {X[3 * e], X[3 * e + 1], X[3 * e + 2]};
-            po_edge(S.q, S.t, Xe, Z[2 * e], Z[2 * e + 1], S.K, r0, r1, J, true);
+            double r0, r1, J[12], Xe[3], u, v;
+            edge_in(e, Xe, u, v);
+            po_edge(S.q, S.t, Xe, u, v, S.K, r0, r1, J, true);
             R[2 * e] = r0;
             R[2 * e + 1] = r1;
             po_accumulate(r0, r1, J, delta, acc);
         }
+        STAMP(24);
         po_rows_to_parts(acc, S, tid);
+        STAMP(25);
         lds_barrier();
+        STAMP(26);
     };
     // wave 0: the four waves' parts -> S.sum (lane k < FV)
     auto finish_sums = [&]() __attribute__((always_inline)) {
@@ -2459,7 +2481,9 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
             bb[r] = S.b[r];
             A[r][r] += (prm.strategy == 0) ? lam : lam * A[r][r];
         }
+        STAMP(30);
         po_ldlt6_reg(A, bb, x);
+        STAMP(31);
         double cand[12], q[4], t[3];
         po_pose_add_wave(x, S.pose, S.qp, cand, q, t, lane);
         if (lane == 0) {
@@ -2518,30 +2542,36 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
                 if (wave == 0) {
                     finish_sums();
                     if (lane == 0) {
+                        // the controller's words into registers first (one batch of LDS loads), the
+                        // isGoodStepInLM arithmetic on them, the words back at the end
                         const double tchi = 0.5 * S.sum[27];
+                        double lam = S.lam, ni = S.ni, chi = S.chi, last = S.last;
+                        int iter = S.iter, fc = S.fc;
+                        double dx[6], bv[6], hd[6];
+                        for (int i = 0; i < 6; ++i) { dx[i] = S.dx[i]; bv[i] = S.b[i]; hd[i] = S.H[7 * i]; }
                         double scale = 0.0;
                         for (int i = 0; i < 6; ++i)
-                            scale += (prm.strategy == 0) ? S.dx[i] * (S.lam * S.dx[i] + S.b[i])
-                                                         : S.dx[i] * (S.lam * S.H[7 * i] * S.dx[i] + S.b[i]);
+                            scale += (prm.strategy == 0) ? dx[i] * (lam * dx[i] + bv[i])
+                                                         : dx[i] * (lam * hd[i] * dx[i] + bv[i]);
                         scale = 0.5 * scale;
                         scale += 1e-10;
-                        const double rho = (S.chi - tchi) / scale;
+                        const double rho = (chi - tchi) / scale;
                         const bool ok = rho > 0 && isfinite(tchi);
                         if (prm.strategy == 0) {
                             if (ok) {
                                 const double m = 2 * rho - 1;
                                 double alpha = 1.0 - m * m * m;
                                 alpha = fmin(alpha, 2.0 / 3.0);
-                                S.lam *= fmax(1.0 / 3.0, alpha);
-                                S.ni = 2;
-                                S.chi = tchi;
+                                lam *= fmax(1.0 / 3.0, alpha);
+                                ni = 2;
+                                chi = tchi;
                             } else {
-                                S.lam *= S.ni;
-                                S.ni *= 2;
+                                lam *= ni;
+                                ni *= 2;
                             }
                         } else {
-                            if (ok) { S.lam = fmax(S.lam / 9.0, 1e-7); S.chi = tchi; }
-                            else S.lam = fmin(S.lam * 11.0, 1e7);
+                            if (ok) { lam = fmax(lam / 9.0, 1e-7); chi = tchi; }
+                            else lam = fmin(lam * 11.0, 1e7);
                         }
                         bool inner_end;
                         if (ok) {
@@ -2550,22 +2580,26 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
                             load_system();
                             inner_end = true;
                         } else {
-                            S.fc += 1;                         // rollbackStates: S.pose untouched
-                            inner_end = S.fc >= prm.max_trials;
+                            fc += 1;                           // rollbackStates: S.pose untouched
+                            inner_end = fc >= prm.max_trials;
                         }
                         int cont = 1;
                         if (inner_end) {
-                            S.iter += 1;
-                            if (S.last - S.chi < prm.stop_dchi2 || S.iter >= prm.max_iters) cont = 0;
-                            S.last = S.chi;
-                            S.fc = 0;
+                            iter += 1;
+                            if (last - chi < prm.stop_dchi2 || iter >= prm.max_iters) cont = 0;
+                            last = chi;
+                            fc = 0;
                         }
+                        S.lam = lam; S.ni = ni; S.chi = chi; S.last = last; S.iter = iter; S.fc = fc;
                         S.cont = cont;
                     }
                     wave_sync();
+                    STAMP(27);
                     if (S.cont) solve_step();
+                    STAMP(28);
                 }
                 lds_barrier();
+                STAMP(29);
             }
             its += S.iter;
         }
@@ -2582,9 +2616,9 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
         for (int e = tid; e < O; e += FT) {
             double r0 = R[2 * e], r1 = R[2 * e + 1];
             if (flag[e]) {
-                double J[12];
-                const double Xe[3] = {X[3 * e], X[3 * e + 1], X[3 * e + 2]};
-                po_edge(S.q, S.t, Xe, Z[2 * e], Z[2 * e + 1], S.K, r0, r1, J, false);
+                double J[12], Xe[3], u, v;
+                edge_in(e, Xe, u, v);
+                po_edge(S.q, S.t, Xe, u, v, S.K, r0, r1, J, false);
                 R[2 * e] = r0;
                 R[2 * e + 1] = r1;
             }
@@ -2596,6 +2630,7 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
         if (round == 2 && tid == 0) S.delta = 0.0;     // setCostFunction(nullptr) (:223-225)
         lds_barrier();
     }
+    STAMP_FLUSH(24, 8);
     if (tid < 12) pose_out[12 * (size_t)f + tid] = S.pose[tid];
     // inliers: features.size() - cnt_outlier (:249)
     int cnt = 0;
