@@ -1252,7 +1252,11 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
             }
             const int gl = (NE >> 4) - 1, R = gl - tg + 1;
+#ifdef LH_CHAIN_ONLY
+            const int u = -1;
+#else
             const int u = wave_unit(wv);
+#endif
             if (u >= 0 && u < 2 * (R - 1)) {
                 const int g = gl - (u >> 1), nt = g - tg + 1, split = tg + ((nt + 1) >> 1);
                 const bool first = (u & 1) == 0;

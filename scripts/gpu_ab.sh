@@ -6,13 +6,13 @@ mkdir -p gpurun_out
 for r in 1 2; do
   for v in A B; do
     lib=$( [ $v = A ] && echo "$LIB_A" || echo "$LIB_B" )
-    LH_LIB=$lib timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu > gpurun_out/ab_$v$r.log 2>&1 || exit $?
+    LH_LIB=$lib timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu ${AB_ARGS:---no-extras} > gpurun_out/ab_$v$r.log 2>&1 || exit $?
     python3 - "$v" gpurun_out/ab_$v$r.log >> gpurun_out/ab.log <<'PY'
 import json, sys
 for l in open(sys.argv[2]):
     if l.startswith('{'):
         d = json.loads(l)
-        print(sys.argv[1], d['ms_per_step'], d['ms_per_step_with_kernel_events'], d['kernels_ms_per_solve'])
+        print(sys.argv[1], d['ms_per_step'], d['value'], d.get('roofline', {}).get('avg_launch_ms'))
 PY
   done
 done
