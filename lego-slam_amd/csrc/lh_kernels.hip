@@ -1178,32 +1178,48 @@ __device__ __forceinline__ int wave_unit(int w) {
 // holds its own row's result.  Every row r above the block then takes y_r -= sum_v L[KB+v][r]
 // x_b[v] (L^T row r in the upper triangle), x_b broadcast by readlane.  No LDS writes: the
 // compiler may hoist every block's operand loads.
+// The LDS operands of the back substitution never change while it runs, so no load waits for the
+// chain: the caller loads block b-1's ND_b row while block b computes, and each block issues its L^T
+// loads before its first DPP broadcast (all unconditional: a block past nb reads in-bounds padding it
+// never uses).  Loading them after the runtime nb guard put two dependent LDS round trips on the
+// chain per block: the compiler does not hoist loads across those branches.
 template <int KB>
-__device__ __forceinline__ void backsub_block(const double* __restrict__ A, const LdltBlockLds& F, int nb, int lane,
-                                              double& y0, double& y1) {
-    if (KB >= nb) return;
-    constexpr bool HI = KB >= 64;
-    constexpr int KL = KB & 63, R16 = KL & 15;
-    const double ys = HI ? y1 : y0;
-    double yb[8], nd[8];
-    yb[0] = bcast16<R16 + 0>(ys); yb[1] = bcast16<R16 + 1>(ys); yb[2] = bcast16<R16 + 2>(ys); yb[3] = bcast16<R16 + 3>(ys);
-    yb[4] = bcast16<R16 + 4>(ys); yb[5] = bcast16<R16 + 5>(ys); yb[6] = bcast16<R16 + 6>(ys); yb[7] = bcast16<R16 + 7>(ys);
+__device__ __forceinline__ void backsub_load_nd(const LdltBlockLds& F, int lane, double (&nd)[8]) {
 #pragma unroll
     for (int w = 0; w < 8; ++w) nd[w] = F.ND[KB >> 3][(lane & 7) * 8 + w];
+}
+
+// Back substitution x = L^-T z for block KB (compile-time, so every lane index below is an
+// immediate), one wave: y holds rows lane (y0) and lane + 64 (y1), already reduced by every block
+// above KB.  x_b = ND_b y_b: the block's 8 y values sit in lanes KB..KB+7 (mod 64), inside one
+// 16-lane row, and reach that row's lanes by DPP broadcast; lane KB+v computes x_b[v], so it
+// holds its own row's result.  Every row r above the block then takes y_r -= sum_v L[KB+v][r]
+// x_b[v] (L^T row r in the upper triangle), x_b broadcast by readlane.
+template <int KB>
+__device__ __forceinline__ void backsub_block(const double* __restrict__ A, const double (&nd)[8], int nb, int lane,
+                                              double& y0, double& y1) {
+    constexpr bool HI = KB >= 64;
+    constexpr int KL = KB & 63, R16 = KL & 15;
+    double l0[8], l1[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) l0[v] = A[lane * AS + KB + v];
+    if (HI) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) l1[v] = A[(lane + 64) * AS + KB + v];
+    }
+    if (KB >= nb) return;
+    const double ys = HI ? y1 : y0;
+    double yb[8];
+    yb[0] = bcast16<R16 + 0>(ys); yb[1] = bcast16<R16 + 1>(ys); yb[2] = bcast16<R16 + 2>(ys); yb[3] = bcast16<R16 + 3>(ys);
+    yb[4] = bcast16<R16 + 4>(ys); yb[5] = bcast16<R16 + 5>(ys); yb[6] = bcast16<R16 + 6>(ys); yb[7] = bcast16<R16 + 7>(ys);
     const double xv = ((nd[0] * yb[0] + nd[1] * yb[1]) + (nd[2] * yb[2] + nd[3] * yb[3])) +
                       ((nd[4] * yb[4] + nd[5] * yb[5]) + (nd[6] * yb[6] + nd[7] * yb[7]));
     double xb[8];
 #pragma unroll
     for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, KL + v);
-    double l0[8];
-#pragma unroll
-    for (int v = 0; v < 8; ++v) l0[v] = A[lane * AS + KB + v];
     const double s0 = ((l0[0] * xb[0] + l0[1] * xb[1]) + (l0[2] * xb[2] + l0[3] * xb[3])) +
                       ((l0[4] * xb[4] + l0[5] * xb[5]) + (l0[6] * xb[6] + l0[7] * xb[7]));
     if (HI) {
-        double l1[8];
-#pragma unroll
-        for (int v = 0; v < 8; ++v) l1[v] = A[(lane + 64) * AS + KB + v];
         const double s1 = ((l1[0] * xb[0] + l1[1] * xb[1]) + (l1[2] * xb[2] + l1[3] * xb[3])) +
                           ((l1[4] * xb[4] + l1[5] * xb[5]) + (l1[6] * xb[6] + l1[7] * xb[7]));
         y0 -= s0;
@@ -1273,22 +1289,39 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
     if (wv == 0) {
         double y0 = (lane < nb) ? F.z[lane] : 0.0, y1 = (lane + 64 < nb) ? F.z[lane + 64] : 0.0;
-        backsub_block<120>(A, F, nb, lane, y0, y1);
-        backsub_block<112>(A, F, nb, lane, y0, y1);
-        backsub_block<104>(A, F, nb, lane, y0, y1);
-        backsub_block<96>(A, F, nb, lane, y0, y1);
-        backsub_block<88>(A, F, nb, lane, y0, y1);
-        backsub_block<80>(A, F, nb, lane, y0, y1);
-        backsub_block<72>(A, F, nb, lane, y0, y1);
-        backsub_block<64>(A, F, nb, lane, y0, y1);
-        backsub_block<56>(A, F, nb, lane, y0, y1);
-        backsub_block<48>(A, F, nb, lane, y0, y1);
-        backsub_block<40>(A, F, nb, lane, y0, y1);
-        backsub_block<32>(A, F, nb, lane, y0, y1);
-        backsub_block<24>(A, F, nb, lane, y0, y1);
-        backsub_block<16>(A, F, nb, lane, y0, y1);
-        backsub_block<8>(A, F, nb, lane, y0, y1);
-        backsub_block<0>(A, F, nb, lane, y0, y1);
+        double nda[8], ndb[8];
+        backsub_load_nd<120>(F, lane, nda);
+        backsub_load_nd<112>(F, lane, ndb);
+        backsub_block<120>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<104>(F, lane, nda);
+        backsub_block<112>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<96>(F, lane, ndb);
+        backsub_block<104>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<88>(F, lane, nda);
+        backsub_block<96>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<80>(F, lane, ndb);
+        backsub_block<88>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<72>(F, lane, nda);
+        backsub_block<80>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<64>(F, lane, ndb);
+        backsub_block<72>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<56>(F, lane, nda);
+        backsub_block<64>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<48>(F, lane, ndb);
+        backsub_block<56>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<40>(F, lane, nda);
+        backsub_block<48>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<32>(F, lane, ndb);
+        backsub_block<40>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<24>(F, lane, nda);
+        backsub_block<32>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<16>(F, lane, ndb);
+        backsub_block<24>(A, nda, nb, lane, y0, y1);
+        backsub_load_nd<8>(F, lane, nda);
+        backsub_block<16>(A, ndb, nb, lane, y0, y1);
+        backsub_load_nd<0>(F, lane, ndb);
+        backsub_block<8>(A, nda, nb, lane, y0, y1);
+        backsub_block<0>(A, ndb, nb, lane, y0, y1);
         if (lane < NE) xsol[lane] = y0;
         if (lane + 64 < NE) xsol[lane + 64] = y1;
     }
