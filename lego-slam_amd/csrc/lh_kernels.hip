@@ -425,6 +425,8 @@ __device__ __forceinline__ void group_sum(double (&v)[N], int lg) {
     }
 }
 
+static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
+
 template <int T, bool TRIAL>
 __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
@@ -436,21 +438,28 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
 
-    if (__builtin_amdgcn_readfirstlane(ctrl->done)) return;
+    // The prologue's global loads go out in two dependent rounds: (1) the controller words and the
+    // chunk header (scalar), then every independent vector load, the first sub-batch's prefetch
+    // included; (2) the pose-table and pose-step values, whose addresses need the chunk's pose slots.
+    // Written as per-element loops, each loop iteration waited for its own loads (ten serialised
+    // round trips before the first sub-batch).
+    const int chunk = chunk_base + blockIdx.x;
+    const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
     // a trial of the final LM iteration (ctrl->evo, ctrl_lm_step): back substitution and the
     // candidate's evaluation only (landmark positions, rho0 per edge, chi2 and the gain scale)
     const bool evo = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->evo) != 0;
-    const int cand = 1 - cur;
     const double lambda = ctrl->lambda;
-    const int chunk = chunk_base + blockIdx.x;
+    const uint32_t* __restrict__ chw = reinterpret_cast<const uint32_t*>(chunks + chunk);
+    const uint32_t sb_begin = __builtin_amdgcn_readfirstlane(chw[0]), sb_end = __builtin_amdgcn_readfirstlane(chw[1]);
+    const int U = (int)(__builtin_amdgcn_readfirstlane(chw[2]) & 0xffu);   // lh_chunk: {sb_begin, sb_end, U, T, ...}
+    const uint32_t item_base = chunks[chunk].item_base;
+    if (done) return;
+    const int cand = 1 - cur;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loads, scalar loop
     const int ncam = prm.ncam;
     const int PT = prm.P * ncam * LH_PT;
-    const int U = chunks[chunk].U;
-    const uint32_t sb_begin = chunks[chunk].sb_begin, sb_end = chunks[chunk].sb_end;
-    const uint32_t item_base = chunks[chunk].item_base;
     const uint16_t* __restrict__ cpose = chunks[chunk].pose;
 
     double* scr = dsm + wave * Cfg::SCR;
@@ -460,22 +469,6 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     double* wt_n = wt_c + Cfg::UMAX * ncam * LH_PT_LDS;     // a chunk of T tiles has U <= UMAX poses
     double* wdx = wt_n + Cfg::UMAX * ncam * LH_PT_LDS;
     double* wext = wdx + Cfg::UMAX * 6;
-    {
-        const int per = ncam * LH_PT, ne = U * per;
-        for (int i = tid; i < ne; i += 256) {
-            const int sl = i / per, r = i - sl * per, ent = r / LH_PT;
-            const size_t g = (size_t)cpose[sl] * per + r;
-            const int l = (sl * ncam + ent) * LH_PT_LDS + (r - ent * LH_PT);
-            wt_c[l] = pose_tab[(size_t)cur * PT + g];
-            wt_n[l] = pose_tab[(size_t)cand * PT + g];
-        }
-        if (TRIAL)
-            for (int i = tid; i < 6 * U; i += 256) wdx[i] = dxp[6 * cpose[i / 6] + (i - 6 * (i / 6))];
-        for (int i = tid; i < ncam * LH_EXT; i += 256) wext[i] = ext[i];
-        // the chunk's pair rows (written by the epilogue)
-        uint32_t* wrow = reinterpret_cast<uint32_t*>(wext + ncam * LH_EXT);
-        for (int i = tid; i < U * (U + 1) / 2; i += 256) wrow[i] = crow[item_base + i];
-    }
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
     double* __restrict__ rn = rec + (size_t)cand * nrec * LH_REC;
@@ -514,6 +507,54 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         u_n = obs_uv[2 * (size_t)o];
         v_n = obs_uv[2 * (size_t)o + 1];
         r_n = rc2[(size_t)sbc * 64 + lane];
+    }
+    {
+        // round 1: the pose slot of each table element this thread copies, the extrinsics, the
+        // chunk's pair rows (written by the epilogue); round 2: the table values and the pose step.
+        // Every load is unconditional, its index clamped into range (a conditional load becomes a
+        // branch, and the wait at its join serialises the rounds again); only the LDS writes are guarded.
+        static_assert(6 * Cfg::UMAX <= 256 && Cfg::UMAX * (Cfg::UMAX + 1) / 2 <= 256 && 4 * LH_EXT <= 256,
+                      "one element per thread");
+        constexpr int NTAB = (Cfg::UMAX * 4 * LH_PT + 255) / 256;   // ncam <= 4
+        const int per = ncam * LH_PT, ne = U * per, nrow = U * (U + 1) / 2;
+        const int umax1 = max(U - 1, 0);
+        const uint32_t pmax1 = (uint32_t)(prm.P - 1);
+        int tsl[NTAB];
+        uint32_t tp[NTAB];
+#pragma unroll
+        for (int k = 0; k < NTAB; ++k) {
+            const int i = tid + 256 * k;
+            tsl[k] = min(i / per, umax1);
+            tp[k] = min((uint32_t)cpose[tsl[k]], pmax1);
+        }
+        const bool has_dx = TRIAL && tid < 6 * U;
+        const int di = min(tid / 6, umax1);
+        const uint32_t dp = min((uint32_t)cpose[di], pmax1);
+        const double ev = ext[min(tid, ncam * LH_EXT - 1)];
+        const uint32_t rw = crow[item_base + min(tid, max(nrow - 1, 0))];
+        double tc[NTAB], tn[NTAB];
+#pragma unroll
+        for (int k = 0; k < NTAB; ++k) {
+            const int i = tid + 256 * k;
+            const size_t g = (size_t)tp[k] * per + min(max(i - tsl[k] * per, 0), per - 1);
+            tc[k] = pose_tab[(size_t)cur * PT + g];
+            tn[k] = pose_tab[(size_t)cand * PT + g];
+        }
+        const double dv = TRIAL ? dxp[6 * dp + (tid - 6 * (tid / 6))] : 0.0;
+#pragma unroll
+        for (int k = 0; k < NTAB; ++k) {
+            const int i = tid + 256 * k;
+            if (i < ne) {
+                const int r = i - tsl[k] * per, ent = r / LH_PT;
+                const int l = (tsl[k] * ncam + ent) * LH_PT_LDS + (r - ent * LH_PT);
+                wt_c[l] = tc[k];
+                wt_n[l] = tn[k];
+            }
+        }
+        if (has_dx) wdx[tid] = dv;
+        if (tid < ncam * LH_EXT) wext[tid] = ev;
+        uint32_t* wrow = reinterpret_cast<uint32_t*>(wext + ncam * LH_EXT);
+        if (tid < nrow) wrow[tid] = rw;
     }
     lds_barrier();   // window tables
 

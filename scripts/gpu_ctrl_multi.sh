@@ -10,7 +10,7 @@ for v in ${VARIANTS:-1}; do
   tail -1 gpurun_out/cm/tests_v$v.log
 done
 for r in 1 2; do
-for v in 0 ${VARIANTS:-1}; do
+for v in ${ORDER:-0 ${VARIANTS:-1}}; do
   lib=$( [ $v = 0 ] && echo lego-slam_amd/lib/liblego_ba.so || echo lego-slam_amd/lib/liblego_ba_v$v.so )
   LH_LIB=$lib timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/cm/v$v.$r -o p --output-format csv -- \
     python3 bench.py --steps 300 --warmup 3 --no-cpu --no-extras > gpurun_out/cm/bench_v$v.$r.log 2>&1 || exit 1
@@ -19,7 +19,7 @@ for v in 0 ${VARIANTS:-1}; do
 import csv, sys
 for row in csv.DictReader(open(sys.argv[2])):
     n = row.get("Name", "")
-    if any(k in n for k in ("k_ctrl", "k_lin<3, true>", "k_reduce")):
+    if any(k in n for k in ("k_ctrl", "k_lin<3, true>", "k_lin<3, false>", "k_reduce")):
         print(sys.argv[1], n[:24], row.get("Calls"), row.get("AverageNs"))
 PY
   done
