@@ -1683,6 +1683,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
+    // both pose-matrix buffers (used after the solve) go to LDS; their load is issued first and
+    // unconditionally (clamped), so it shares the bulk's round trip instead of following it
+    const double pmv = pose_mat[min(tid, 24 * P - 1)];
     double vs[NLD], vc[NLD];
     uint32_t mp[NLD];
 #pragma unroll
@@ -1693,10 +1696,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         vc[u] = in ? rs_commit[i] : 0.0;
         mp[u] = i < LY.off_bs ? rsmap[i] : 0u;
     }
-    if (tid < 24 * P) {   // both pose-matrix buffers into LDS (used after the solve)
-        const int b = tid / (12 * P), i = tid - b * 12 * P;
-        s_pm[b][i] = pose_mat[(size_t)b * P * 12 + i];
-    }
+    if (tid < 24 * P) s_pm[tid / (12 * P)][tid - (tid / (12 * P)) * 12 * P] = pmv;
     if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
         double mx = 0.0;
 #pragma unroll
