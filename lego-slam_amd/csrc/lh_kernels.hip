@@ -938,12 +938,14 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     const lh_rs_layout LY = lh_rs_make(prm.P);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // the stop flag and this block's pair words are independent loads: one round trip for all
+    const int bq = b < LY.npairs ? b : 0;
+    const int ib = pair_ptr[bq], ie = pair_ptr[bq + 1];
+    const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_lin wrote the chunk scalars only
-    const int bq = b < LY.npairs ? b : 0;
-    const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
-    const int ib = pair_ptr[bq], ie = pair_ptr[bq + 1];
-    if (done || (evo && b < LY.npairs)) return;
+    // (p > q and ib > ie never hold: they make the exit test need the pair words, so the compiler issues
+    // them with the controller's instead of sinking them below the branch, a second round trip)
+    if ((done != 0) | ((evo != 0) & (b < LY.npairs)) | (p > q) | (ib > ie)) return;   // no short-circuit: one test
     if (b == LY.npairs) {
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
         for (int c = tid; c < n_chunks; c += RT) {
