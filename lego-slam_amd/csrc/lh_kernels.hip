@@ -2325,7 +2325,7 @@ __device__ __forceinline__ void po_swap6(double x[6], int k, int j) {
 
 // The oracle's ldlt_solve (Eigen ldlt_inplace with diagonal pivoting + LDLT::_solve_impl) for n = 6
 // in registers: every lane holds the whole symmetric A and runs the oracle's operations in the oracle's
-// order (contraction off), so no value crosses lanes.  One change: a division by a pivot is its
+// order, so no value crosses lanes.  Two changes: multiply-adds contract to FMAs, and a division by a pivot is its
 // reciprocal (fast_rcp, one per pivot) times the element, as the k_ctrl LDL^T does.  The frontend's
 // sums of H and b already differ from the oracle's order, so its parity is to tolerance either way
 // (tests/test_frontend.py), and the 21 IEEE divisions were the longest part of the step.  Eigen's
@@ -2333,6 +2333,7 @@ __device__ __forceinline__ void po_swap6(double x[6], int k, int j) {
 // storage: the unfactored block stays symmetric, so the upper entries the column exchange reads
 // equal the lower ones Eigen swaps in.  The pivot index is made wave-uniform (readfirstlane) so
 // the swaps are scalar branches over static registers.
+#pragma clang fp contract(fast)   // the 6x6 solve is parity-to-tolerance (see above): FMAs halve its chains
 __device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b)[6], double (&x)[6]) {
     double dd[6];
     int tr[6];
@@ -2408,6 +2409,7 @@ __device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b
     for (int k = 5; k >= 0; --k) po_swap6(x, k, tr[k]);
 }
 
+#pragma clang fp contract(off)
 // VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91),
 // on one wave: every lane computes the same result, except that lane 0 takes sin/cos(theta/2) and
 // lane 1 sin/cos(theta) in one sincos pass.  qT = the quaternion of SE3(T12) (d_q_from_R of its
