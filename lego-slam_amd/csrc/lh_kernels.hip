@@ -2409,6 +2409,96 @@ __device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b
     for (int k = 5; k >= 0; --k) po_swap6(x, k, tr[k]);
 }
 
+// The same solve on the damped system read from LDS (H full symmetric, b), with Eigen's pivot sequence found
+// first: Eigen's left-looking ldlt_inplace compares diagonal entries no earlier step has changed, so its
+// transpositions depend on the damped diagonal alone.  They are replayed on six (key, row) pairs, the
+// permuted system is loaded from LDS at the permuted addresses, the factorisation and the solves run
+// without swaps (the same operations on the same values as po_ldlt6_reg, so the same bits), and x goes back
+// to pose order through LDS.  This takes the 36-element row and column exchanges (a branch per candidate
+// row per step) off the chain.
+__device__ __forceinline__ void po_ldlt6_lds(const double* H, const double* bv, double lam, int strategy,
+                                             double* xs, double (&x)[6]) {
+    double key[6];
+    int pos[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const double h = H[7 * i];
+        key[i] = h + ((strategy == 0) ? lam : lam * h);
+        pos[i] = i;
+    }
+    bool all_zero = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int idx = k;
+        double big = fabs(key[k]);
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double di = fabs(key[i]);
+            if (di > big) { big = di; idx = i; }
+        }
+        idx = __builtin_amdgcn_readfirstlane(idx);
+        if (k == 0 && !(big > 0.0)) { all_zero = true; break; }   // Eigen: identity transpositions
+#pragma unroll
+        for (int m = k + 1; m < 6; ++m)
+            if (m == idx) {
+                const double t = key[k]; key[k] = key[m]; key[m] = t;
+                const int u = pos[k]; pos[k] = pos[m]; pos[m] = u;
+            }
+    }
+    double A[6][6], y[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) A[r][c] = H[6 * pos[r] + pos[c]];
+        A[r][r] += (strategy == 0) ? lam : lam * A[r][r];
+        y[r] = bv[pos[r]];
+    }
+    if (!all_zero) {
+        double dd[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            if (k > 0) {
+                double temp[6];
+#pragma unroll
+                for (int j = 0; j < k; ++j) temp[j] = dd[j] * A[k][j];
+#pragma unroll
+                for (int r = k; r < 6; ++r) {
+                    double si = 0.0;
+#pragma unroll
+                    for (int j = 0; j < k; ++j) si += A[r][j] * temp[j];
+                    A[r][k] -= si;
+                }
+            }
+            const double akk = A[k][k];
+            dd[k] = akk;
+            if (k < 5 && fabs(akk) > 0.0) {
+                const double inv = fast_rcp(akk);
+#pragma unroll
+                for (int r = k + 1; r < 6; ++r) A[r][k] *= inv;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (y[k] != 0.0)
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) y[i] -= A[i][k] * y[k];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const double d = A[i][i];
+        y[i] = (fabs(d) > 2.2250738585072014e-308) ? y[i] * fast_rcp(d) : 0.0;
+    }
+#pragma unroll
+    for (int k = 5; k >= 0; --k)
+#pragma unroll
+        for (int i = 0; i < k; ++i) y[i] -= A[k][i] * y[k];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) xs[pos[r]] = y[r];   // every lane writes the same value
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < 6; ++j) x[j] = xs[j];
+}
+
 #pragma clang fp contract(off)
 // VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91),
 // on one wave: every lane computes the same result, except that lane 0 takes sin/cos(theta/2) and
@@ -2450,7 +2540,7 @@ __device__ __forceinline__ void po_pose_add_wave(const double (&d_in)[6], const 
 
 struct PoShared {
     double pose[12], cand[12], q[4], t[3], qp[4], K[4];   // q/t: the table being linearised; qp: SE3(pose)'s q
-    double H[36], b[6], dx[6];
+    double H[36], b[6], dx[6], xs[6];   // xs: the 6x6 solution on its way back to pose order
     double part[FT / 64][FV];
     double sum[FV];
     double rows[FT][FV + 1];   // one thread's per-edge sums per row (odd stride: column reads spread over banks)
@@ -2554,17 +2644,24 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
     };
     // wave 0: (H + lambda D) dx = b, then the candidate pose and its table
     auto solve_step = [&]() __attribute__((always_inline)) {
-        double A[6][6], bb[6], x[6];
+        double x[6];
         const double lam = S.lam;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-#pragma unroll
-            for (int j = 0; j < 6; ++j) A[r][j] = S.H[6 * r + j];
-            bb[r] = S.b[r];
-            A[r][r] += (prm.strategy == 0) ? lam : lam * A[r][r];
-        }
         STAMP(30);
-        po_ldlt6_reg(A, bb, x);
+#ifdef LH_PO_SWAPS
+        {
+            double A[6][6], bb[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) A[r][j] = S.H[6 * r + j];
+                bb[r] = S.b[r];
+                A[r][r] += (prm.strategy == 0) ? lam : lam * A[r][r];
+            }
+            po_ldlt6_reg(A, bb, x);
+        }
+#else
+        po_ldlt6_lds(S.H, S.b, lam, prm.strategy, S.xs, x);
+#endif
         STAMP(31);
         double cand[12], q[4], t[3];
         po_pose_add_wave(x, S.pose, S.qp, cand, q, t, lane);
