@@ -2292,7 +2292,12 @@ __device__ __forceinline__ double po_rho0(double r0, double r1, double delta) {
     return e2;
 }
 
-// one edge's contributions: (J^T W) J upper triangle, -(rho1 J)^T r, rho0  (problem.cpp:300-330)
+// one edge's contributions: (J^T W) J upper triangle, -(rho1 J)^T r, rho0  (problem.cpp:300-330).
+// The products contract to FMAs: these sums are parity-to-tolerance (their order differs from the oracle's
+// anyway); edge_robust keeps the bitwise-mirrored gate (contraction is fixed where an expression is written).
+#ifndef LH_PO_ACC_NOFMA
+#pragma clang fp contract(fast)
+#endif
 __device__ __forceinline__ void po_accumulate(double r0, double r1, const double J[12], double delta, double acc[FV]) {
     EdgeEval E;
     E.r0 = r0; E.r1 = r1;
@@ -2314,6 +2319,7 @@ __device__ __forceinline__ void po_accumulate(double r0, double r1, const double
     for (int a = 0; a < 6; ++a) acc[21 + a] -= (E.rho1 * J[a]) * r0 + (E.rho1 * J[6 + a]) * r1;
     acc[27] += E.rho0;
 }
+#pragma clang fp contract(off)
 
 // swap x[k] and x[j] of a 6-register array, j wave-uniform (an SGPR): scalar branches over
 // static registers (an indexed select chain is lowered to a scratch array)
