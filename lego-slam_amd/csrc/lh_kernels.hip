@@ -2555,7 +2555,7 @@ struct PoShared {
 };
 
 // all FT threads: each thread's acc[FV] through LDS rows; per wave, lane 2k + h (k < FV) sums column k
-// over the wave's rows of parity h, in row order, and the two halves are added: S.part[wave].
+// over the wave's rows of parity h (four interleaved chains, fixed order), and the two halves are added: S.part[wave].
 // The caller's barrier follows.  Fixed order: a batch is bitwise reproducible.
 __device__ __forceinline__ void po_rows_to_parts(const double (&acc)[FV], PoShared& S, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
@@ -2564,9 +2564,18 @@ __device__ __forceinline__ void po_rows_to_parts(const double (&acc)[FV], PoShar
     wave_sync();
     if (lane < 2 * FV) {
         const int k = lane >> 1, h = lane & 1;
+#ifdef LH_PO_ONECHAIN
         double s = 0.0;
 #pragma unroll 8
         for (int i = 0; i < 32; ++i) s += S.rows[64 * wave + 2 * i + h][k];
+#else
+        // four interleaved chains (rows i mod 4), then ((c0 + c1) + (c2 + c3)): a fixed order, a quarter of the
+        // dependent adds
+        double c[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 32; ++i) c[i & 3] += S.rows[64 * wave + 2 * i + h][k];
+        double s = (c[0] + c[1]) + (c[2] + c[3]);
+#endif
         s += dpp_d<0xB1>(s);   // quad_perm [1,0,3,2]: the other parity's half
         if (h == 0) S.part[wave][k] = s;
     }
