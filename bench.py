@@ -10,7 +10,12 @@ Workloads (BASELINE.json configs); fp64 throughout (>= the refer
       and their observations per rank, poses replicated, one RCCL all-reduce of the reduced pose
       system per LM trial): the multi-GPU window (the N > 1 default), "scaling": "strong".  value
       counts iterations of the whole window (no factor N).  The N = 1 line carries the same window on
-      one GPU ("c4_1gpu") as the base of the scaling ratio.
+      one GPU ("c4_1gpu") as the base of the scaling ratio.  C4 runs in gate_mode 1 (the Huber gate's
+      analytically-zero rounding residue taken as 0): with the reference gate its trajectory depends
+      on the summation order, hence on the rank count (the oracle alone ends after 4 or 7 iterations
+      depending on its thread count, profiles/r03_c4_oracle_gate_envelope.json); in gate_mode 1 every
+      rank count runs the same trajectory (tests/test_multirank_gpu.py), so the N lines time the same
+      iterations and trials.
 
 Usage: python bench.py [--gpus N --steps K --warmup W] [--workload C3|C4]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -243,6 +248,7 @@ def main():
     torch.cuda.set_device(local)
 
     w = make_window(name, args.family, args.seed, rank, world)
+    gate = 1 if name == "C4" else 0
     comm_id = bytes(128)
     extra = {}
     if world > 1 and args.comm == "rccl":
@@ -254,7 +260,7 @@ def main():
             t = torch.from_numpy(buf)   # the library's pinned exchange buffer
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
         extra = dict(allreduce=allreduce)
-    solver = lego_ba.Solver(device=local, world_size=world, rank=rank, comm_id=comm_id,
+    solver = lego_ba.Solver(device=local, world_size=world, rank=rank, comm_id=comm_id, gate_mode=gate,
                             trials_per_sync=args.trials_per_sync, **extra)
     solver.upload(w)
 
@@ -308,9 +314,11 @@ def main():
                    "obs_this_rank": n_obs, "parallelism": f"landmark-shard x{world}",
                    "exchange": ("none" if world == 1 else ("RCCL all-reduce" if args.comm == "rccl"
                                                           else "host transport over gloo (rehearsal)"))},
+        "gate_mode": gate,
         "iterations_per_solve": iters / args.steps,
         "trials_per_solve": trials / args.steps,
         "trials_per_s": round(trials / dt, 3),
+        "ms_per_trial": round(dt / trials * 1e3, 5),
         "chi2_final": last["chi2_final"],
         "kernels_ms_per_solve_event_bracketed": {k: round(v[1] / nprof, 4) for k, v in ks.items()},
         "roofline": rl,
@@ -345,15 +353,46 @@ def main():
     # C4 on one GPU: the base of the N-GPU scaling ratio (SCALE lines run C4 sharded)
     if name == "C3":
         w4 = make_window("C4", args.family, args.seed, 0, 1)
-        s4 = lego_ba.Solver(device=local)
+        s4 = lego_ba.Solver(device=local, gate_mode=1)
         s4.upload(w4)
         s4.solve_resident()
         d4, i4, t4, l4 = time_solves(s4, 5, barrier)
         r4, _ = roofline(s4, len(w4["obs_pose"]), len(w4["lm_xyz"]), 8, f"C4-{args.family}-s{args.seed}", reps=10)
-        out["c4_1gpu"] = {"iterations_per_s": round(i4 / d4, 3), "ms_per_solve": round(d4 / 5 * 1e3, 3),
+        out["c4_1gpu"] = {"gate_mode": 1, "iterations_per_s": round(i4 / d4, 3), "ms_per_solve": round(d4 / 5 * 1e3, 3),
+                          "trials_per_s": round(t4 / d4, 3), "ms_per_trial": round(d4 / t4 * 1e3, 5),
                           "iterations_per_solve": i4 / 5, "trials_per_solve": t4 / 5, "chi2_final": l4["chi2_final"],
                           "k_lin_ms": r4["avg_launch_ms"], "k_lin_frac_fp64": r4["frac"]}
         s4.close()
+        # the per-rank work of C4 sharded N ways, measured on this one GPU: rank 0's shard (L / N
+        # landmarks, poses replicated) solved as a window of its own, per-trial kernel times (HIP
+        # events) and k_lin's FP64 fraction.  A sharded trial is k_lin + k_reduce on the shard, the
+        # all-reduce of the packed reduced system (the one term a single GPU cannot measure), and the
+        # same k_ctrl on every rank; the projection leaves the all-reduce out.
+        base_trial = d4 / t4 * 1e3
+        shards = {}
+        for n in (2, 4, 8):
+            ws = make_window("C4", args.family, args.seed, 0, n)
+            ss = lego_ba.Solver(device=local, gate_mode=1)
+            ss.upload(ws)
+            ss.solve_resident()
+            ss.set_profiling(True)
+            ss.kernel_stats_reset()
+            time_solves(ss, 3, barrier)
+            kst = ss.kernel_stats()
+            ss.set_profiling(False)
+            rs, _ = roofline(ss, len(ws["obs_pose"]), len(ws["lm_xyz"]), 8, "", reps=20)
+            per = {k: round(v[1] / max(1, v[0]), 5) for k, v in kst.items() if k in ("k_lin", "k_reduce", "k_ctrl")}
+            trial = sum(per.values())
+            shards[f"n{n}"] = {"landmarks": len(ws["lm_xyz"]), "obs": len(ws["obs_pose"]),
+                               "ms_per_trial_event_bracketed": per, "k_lin_replay_ms": rs["avg_launch_ms"],
+                               "k_lin_frac_fp64": rs["frac"], "trial_ms_excl_allreduce": round(trial, 5),
+                               "projected_speedup_excl_allreduce": round(base_trial / trial, 3)}
+            ss.close()
+            del ws
+        out["c4_shards_1gpu"] = dict(shards, note="per-rank kernel times of C4 sharded N ways, each shard solved "
+                                     "alone on this GPU (gate_mode 1); projected speedup = c4_1gpu ms_per_trial / "
+                                     "(k_lin + k_reduce + k_ctrl of the shard), the all-reduce excluded "
+                                     "(unmeasurable on one GPU); event brackets add ~5 us per kernel")
         del w4
     # survey-default family (the reference's live configuration: free gauge, 2 % outliers, left image
     # only).  Its C3 windows have landmarks running off to ~1e15 and are not reproducible under
@@ -368,6 +407,21 @@ def main():
                                 "ms_per_solve": round(dd / 5 * 1e3, 3), "iterations_per_solve": idd / 5,
                                 "trials_per_solve": tdd / 5, "chi2_final": ld["chi2_final"]}
     sd.close()
+    # the reference's live configuration with the reference Huber gate (gate_mode 0): survey-default
+    # C3 seed 0 (free gauge, left image only, 2 % outliers; backend_lego.cpp:67-79, 92-94), timed
+    # like value, with its own CPU baseline below and the oracle's reorder envelope as the parity check
+    wl = make_window("C3", "default", args.seed, 0, 1)
+    sl0 = lego_ba.Solver(device=local)
+    sl0.upload(wl)
+    sl0.solve_resident()
+    nl0 = max(5, min(200, args.steps // 5))
+    dl0, il0, tl0, ll0 = time_solves(sl0, nl0, barrier)
+    out["live_config_c3"] = {"family": "default (survey)", "seed": args.seed, "gate_mode": 0,
+                             "iterations_per_s": round(il0 / dl0, 3), "ms_per_solve": round(dl0 / nl0 * 1e3, 4),
+                             "trials_per_s": round(tl0 / dl0, 3), "ms_per_trial": round(dl0 / tl0 * 1e3, 5),
+                             "iterations_per_solve": il0 / nl0, "trials_per_solve": tl0 / nl0,
+                             "chi2_final": ll0["chi2_final"], "solves": nl0}
+    sl0.close()
     # the same window through the PCG reduced solve (BASELINE config 3 names "Schur + PCG"; the
     # reference's own solver, and value above, is the LDLT)
     sp = lego_ba.Solver(device=local, linear_solver=lego_ba.LH_SOLVER_PCG)
@@ -468,6 +522,31 @@ def main():
         out["native_build_matches_parity_build"] = bool(op["chi2_final"] == o["chi2_final"])
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
         od = oracle_bind.solve(wd, n_threads=threads, gate_mode=1, lib_path=lib_path)
+        # live configuration: CPU baseline on the same window, and the oracle's own outcomes under
+        # summation reorders (thread counts): the GPU's final chi2 must lie inside that envelope
+        lc = out["live_config_c3"]
+        env = [oracle_bind.solve(wl, n_threads=t, lib_path=lib_path) for t in sorted({1, 2, 8, threads})]
+        t0 = time.perf_counter()
+        its_l = ns_l = tr_l = 0
+        while True:
+            ol = oracle_bind.solve(wl, n_threads=threads, lib_path=lib_path)
+            its_l += ol["iterations"]
+            tr_l += ol["trials"]
+            ns_l += 1
+            ctl = time.perf_counter() - t0
+            if ctl >= args.cpu_seconds / 2:
+                break
+        lo = min(r["chi2_final"] for r in env)
+        hi = max(r["chi2_final"] for r in env)
+        lc["cpu_baseline"] = {"value": round(its_l / ctl, 4), "unit": "LM iterations/s", "cores": threads, "kind": "port",
+                              "trials_per_s": round(tr_l / ctl, 3),
+                              "sample": f"{ns_l} full solve(10)s of this window by the block-sparse oracle, {ctl:.1f} s"}
+        lc["speedup_vs_cpu"] = round(lc["iterations_per_s"] / lc["cpu_baseline"]["value"], 2)
+        lc["speedup_vs_cpu_trials"] = round(lc["trials_per_s"] / lc["cpu_baseline"]["trials_per_s"], 2)
+        lc["oracle_envelope"] = {"threads": sorted({1, 2, 8, threads}), "chi2_min": lo, "chi2_max": hi,
+                                 "iterations": sorted({r["iterations"] for r in env}),
+                                 "trials": sorted({r["trials"] for r in env})}
+        lc["gpu_chi2_in_oracle_envelope"] = bool(lo * (1 - 1e-6) <= ll0["chi2_final"] <= hi * (1 + 1e-6))
         out["survey_default_c3"]["chi2_rel_vs_oracle"] = abs(ld["chi2_final"] - od["chi2_final"]) / od["chi2_final"]
         out["survey_default_c3"]["oracle_iterations"] = od["iterations"]
         t0 = time.perf_counter()

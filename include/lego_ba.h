@@ -78,7 +78,12 @@ typedef struct lh_options {
     int32_t linear_solver;    /* lh_linear_solver                                             */
     int32_t verbose;          /* print the reference's per-iteration line problem.cpp:180-184 */
     int32_t device;           /* HIP device ordinal, -1 = current device                      */
-    int32_t world_size;       /* landmark shards (one process per GPU); 1 = single GPU        */
+    int32_t world_size;       /* landmark shards (one process per GPU); 1 = single GPU.  Every rank
+                                 must pass the same solver options (iteration caps, strategy, Huber
+                                 delta, tolerances, solver, gate, depth): lh_create compares them
+                                 across the ranks with one MAX all-reduce and returns LH_E_BADARG on
+                                 every rank when they differ (the collective count per solve is a
+                                 function of them)                                               */
     int32_t rank;             /* this process's shard                                         */
     int32_t degenerate_guard; /* 0: reference semantics: a landmark with one edge (rank-2 H_ll) or a
                                  non-positive-definite H_ll poisons the step, as the LU inverse's

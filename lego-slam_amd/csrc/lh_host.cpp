@@ -747,6 +747,45 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     return LH_OK;
 }
 
+// Every rank must run the same controller with the same options: the LM decisions are taken on
+// identical all-reduced sums, and the number of collectives a solve issues is a function of the stop
+// trial, the enqueue depth and max_iters x max_trials (solve_resident_impl).  Ranks whose options
+// differ would issue different collective counts and hang, so lh_create compares them once: each
+// rank contributes (v, -v) per option to a MAX all-reduce, and any rank whose v differs from the
+// maximum or minimum sees a mismatch (every rank returns LH_E_BADARG).
+int check_rank_options(lh_handle* h) {
+    const lh_options& o = h->opt;
+    const int depth = h->host_comm ? 1 : (o.trials_per_sync > 0 ? std::min(o.trials_per_sync, 32) : 2);
+    const double v[] = {(double)o.max_iters, (double)o.max_trials, (double)o.strategy, o.huber_delta, o.stop_dchi2,
+                        o.tau, o.lambda_cap, o.lambda_init, (double)o.linear_solver, (double)o.world_size,
+                        (double)o.degenerate_guard, (double)depth, (double)o.pcg_max_iters, o.pcg_tol,
+                        (double)o.gate_mode, (double)o.chunk_landmarks > 0 ? 1.0 : 0.0, (double)o.comm_mode};
+    constexpr int n = (int)(sizeof(v) / sizeof(v[0]));
+    double buf[2 * n];
+    for (int i = 0; i < n; ++i) { buf[i] = v[i]; buf[n + i] = -v[i]; }
+    if (h->host_comm) {
+        if (o.allreduce(o.allreduce_user, buf, 2 * n, 1) != 0) return LH_E_RCCL;
+    } else if (h->comm) {
+        DevBuf<double> d;
+        auto run = [&]() -> int {
+            HIPCHK(d.ensure(2 * n));
+            HIPCHK(hipMemcpyAsync(d.p, buf, sizeof(buf), hipMemcpyHostToDevice, h->stream));
+            NCCLCHK(ncclAllReduce(d.p, d.p, 2 * n, ncclFloat64, ncclMax, h->comm, h->stream));
+            HIPCHK(hipMemcpyAsync(buf, d.p, sizeof(buf), hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            return LH_OK;
+        };
+        const int st = run();
+        d.release();
+        if (st != LH_OK) return st;
+    } else {
+        return LH_OK;
+    }
+    for (int i = 0; i < n; ++i)
+        if (!(buf[i] == -buf[n + i])) return LH_E_BADARG;   // max != min somewhere (NaN options fail too)
+    return LH_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -842,7 +881,13 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
         lh_destroy(h);
         return LH_E_HIP;
     }
-    h->pool = new (std::nothrow) lh::Pool(opt->host_threads > 0 ? std::min(opt->host_threads, 64) : auto_host_threads());
+    // the pool starts std::threads, which throw std::system_error when the process may not create
+    // more (e.g. under a cgroup pids limit): no exception crosses the ABI
+    try {
+        h->pool = new lh::Pool(opt->host_threads > 0 ? std::min(opt->host_threads, 64) : auto_host_threads());
+    } catch (...) {
+        h->pool = nullptr;
+    }
     if (!h->pool) { lh_destroy(h); return LH_E_HIP; }
     h->host_comm = opt->world_size > 1 && opt->comm_mode == LH_COMM_HOST;
     // LH_FORCE_RCCL=1 builds a one-rank communicator on a single GPU, so the data-path
@@ -861,6 +906,10 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
             lh_destroy(h);
             return LH_E_RCCL;
         }
+    }
+    if (opt->world_size > 1) {
+        const int st = check_rank_options(h);
+        if (st != LH_OK) { lh_destroy(h); return st; }
     }
     *hp = h;
     return LH_OK;
@@ -938,7 +987,7 @@ void lh_kernel_stats_reset(lh_handle* h) {
 
 // Frontend::EstimateCurrentPose for a batch of frames (frontend_lego.cpp:157-250): upload, one
 // k_frames launch (one workgroup per frame), download.
-int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
+static int estimate_pose_impl(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
     if (!h || !in || !out) return LH_E_BADARG;
     const int F = in->n_frames;
     if (F < 0 || (F > 0 && (!in->obs_ptr || !in->pose_Tcw))) return LH_E_BADARG;
@@ -1024,7 +1073,7 @@ int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
 
 // LKOpticalFlow4Layer / LKOpticalFlow1Layer (algorithm.cpp:11-206): upload both images, build the
 // pyramids (k_lk_pyr per level and image), track every keypoint (k_lk_track), download.
-int lh_lk_track(lh_handle* h, const lh_lk_input* in, lh_lk_result* out) {
+static int lk_track_impl(lh_handle* h, const lh_lk_input* in, lh_lk_result* out) {
     if (!h || !in || !out) return LH_E_BADARG;
     if (in->levels != 1 && in->levels != LH_LK_MAX_LEVELS) return LH_E_BADARG;
     if (in->cols < 1 || in->rows < 1 || in->step < in->cols || in->n_points < 0) return LH_E_BADARG;
@@ -1051,9 +1100,15 @@ int lh_lk_track(lh_handle* h, const lh_lk_input* in, lh_lk_result* out) {
     HIPCHK(h->k_kp1.ensure(2 * (size_t)std::max(n, 1)));
     HIPCHK(h->k_kp2.ensure(2 * (size_t)std::max(n, 1)));
     HIPCHK(h->k_succ.ensure((size_t)std::max(n, 1)));
-    const size_t img_bytes = (size_t)in->rows * (size_t)in->step;
-    HIPCHK(hipMemcpyAsync(h->k_img[0].p, in->img1, img_bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->k_img[1].p, in->img2, img_bytes, hipMemcpyHostToDevice, s));
+    // the caller's last row guarantees only `cols` readable bytes (a cv::Mat ROI has step > cols):
+    // copy (rows - 1) * step + cols bytes and zero the rest of that row, which no tap reads as image
+    // data (GetPixelValue's out-of-buffer taps read 0, lh_lk.hip)
+    const size_t img_bytes = (size_t)(in->rows - 1) * (size_t)in->step + (size_t)in->cols;
+    const size_t tail = (size_t)in->rows * (size_t)in->step - img_bytes;
+    for (int im = 0; im < 2; ++im) {
+        HIPCHK(hipMemcpyAsync(h->k_img[im].p, im ? in->img2 : in->img1, img_bytes, hipMemcpyHostToDevice, s));
+        if (tail) HIPCHK(hipMemsetAsync(h->k_img[im].p + img_bytes, 0, tail, s));
+    }
     if (n > 0) {
         HIPCHK(hipMemcpyAsync(h->k_kp1.p, in->kp1, 2 * sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
         // without an initial guess kp2 is scaled but never read (dx = dy = 0 at the top level)
@@ -1089,6 +1144,23 @@ int lh_lk_track(lh_handle* h, const lh_lk_input* in, lh_lk_result* out) {
     out->time_ms = ms;
     h->event_next = 0;
     return LH_OK;
+}
+
+// the staging copies build std::vectors (par_copy): no exception crosses the ABI
+int lh_estimate_pose(lh_handle* h, const lh_frames* in, lh_frames_result* out) {
+    try {
+        return estimate_pose_impl(h, in, out);
+    } catch (...) {
+        return LH_E_HIP;
+    }
+}
+
+int lh_lk_track(lh_handle* h, const lh_lk_input* in, lh_lk_result* out) {
+    try {
+        return lk_track_impl(h, in, out);
+    } catch (...) {
+        return LH_E_HIP;
+    }
 }
 
 int lh_classify_outliers(const double* rchi2, int64_t n_obs, double chi2_th, uint8_t* is_outlier, double* th_out,

@@ -1311,11 +1311,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
             }
             const int gl = (NE >> 4) - 1, R = gl - tg + 1;
-#ifdef LH_CHAIN_ONLY
-            const int u = -1;
-#else
             const int u = wave_unit(wv);
-#endif
             if (u >= 0 && u < 2 * (R - 1)) {
                 const int g = gl - (u >> 1), nt = g - tg + 1, split = tg + ((nt + 1) >> 1);
                 const bool first = (u & 1) == 0;
@@ -2295,9 +2291,7 @@ __device__ __forceinline__ double po_rho0(double r0, double r1, double delta) {
 // one edge's contributions: (J^T W) J upper triangle, -(rho1 J)^T r, rho0  (problem.cpp:300-330).
 // The products contract to FMAs: these sums are parity-to-tolerance (their order differs from the oracle's
 // anyway); edge_robust keeps the bitwise-mirrored gate (contraction is fixed where an expression is written).
-#ifndef LH_PO_ACC_NOFMA
 #pragma clang fp contract(fast)
-#endif
 __device__ __forceinline__ void po_accumulate(double r0, double r1, const double J[12], double delta, double acc[FV]) {
     EdgeEval E;
     E.r0 = r0; E.r1 = r1;
@@ -2321,107 +2315,19 @@ __device__ __forceinline__ void po_accumulate(double r0, double r1, const double
 }
 #pragma clang fp contract(off)
 
-// swap x[k] and x[j] of a 6-register array, j wave-uniform (an SGPR): scalar branches over
-// static registers (an indexed select chain is lowered to a scratch array)
-__device__ __forceinline__ void po_swap6(double x[6], int k, int j) {
-#pragma unroll
-    for (int m = 0; m < 6; ++m)
-        if (m > k && m == j) { const double t = x[k]; x[k] = x[m]; x[m] = t; }
-}
-
-// The oracle's ldlt_solve (Eigen ldlt_inplace with diagonal pivoting + LDLT::_solve_impl) for n = 6
-// in registers: every lane holds the whole symmetric A and runs the oracle's operations in the oracle's
-// order, so no value crosses lanes.  Two changes: multiply-adds contract to FMAs, and a division by a pivot is its
-// reciprocal (fast_rcp, one per pivot) times the element, as the k_ctrl LDL^T does.  The frontend's
-// sums of H and b already differ from the oracle's order, so its parity is to tolerance either way
-// (tests/test_frontend.py), and the 21 IEEE divisions were the longest part of the step.  Eigen's
-// in-place swaps on the lower triangle are a row and a column exchange of the full symmetric
-// storage: the unfactored block stays symmetric, so the upper entries the column exchange reads
-// equal the lower ones Eigen swaps in.  The pivot index is made wave-uniform (readfirstlane) so
-// the swaps are scalar branches over static registers.
-#pragma clang fp contract(fast)   // the 6x6 solve is parity-to-tolerance (see above): FMAs halve its chains
-__device__ __forceinline__ void po_ldlt6_reg(double (&A)[6][6], const double (&b)[6], double (&x)[6]) {
-    double dd[6];
-    int tr[6];
-    bool all_zero = false;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        if (all_zero) continue;   // (no break: the loop must unroll, A stays in registers)
-        int idx = k;
-        double big = fabs(A[k][k]);
-#pragma unroll
-        for (int i = k + 1; i < 6; ++i) {
-            const double di = fabs(A[i][i]);
-            if (di > big) { big = di; idx = i; }
-        }
-        idx = __builtin_amdgcn_readfirstlane(idx);   // uniform: every lane scanned the same values
-        tr[k] = idx;
-#pragma unroll
-        for (int m = k + 1; m < 6; ++m) {
-            if (m == idx) {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) { const double t = A[k][j]; A[k][j] = A[m][j]; A[m][j] = t; }
-#pragma unroll
-                for (int i = 0; i < 6; ++i) { const double t = A[i][k]; A[i][k] = A[i][m]; A[i][m] = t; }
-            }
-        }
-        if (k > 0) {
-            double temp[6];
-#pragma unroll
-            for (int j = 0; j < k; ++j) temp[j] = dd[j] * A[k][j];
-#pragma unroll
-            for (int r = k; r < 6; ++r) {
-                double si = 0.0;
-#pragma unroll
-                for (int j = 0; j < k; ++j) si += A[r][j] * temp[j];
-                A[r][k] -= si;
-            }
-        }
-        const double akk = A[k][k];
-        dd[k] = akk;
-        const bool valid = fabs(akk) > 0.0;
-        if (k == 0 && !valid) {   // Eigen: identity transpositions, A left as it is
-#pragma unroll
-            for (int j = 0; j < 6; ++j) tr[j] = j;
-            all_zero = true;
-            continue;
-        }
-        if (k < 5 && valid) {
-            const double inv = fast_rcp(akk);
-#pragma unroll
-            for (int r = k + 1; r < 6; ++r) A[r][k] *= inv;
-        }
-    }
-    (void)all_zero;   // the solves run regardless (LDLT::_solve_impl)
-#pragma unroll
-    for (int i = 0; i < 6; ++i) x[i] = b[i];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) po_swap6(x, k, tr[k]);
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-        if (x[k] != 0.0)
-#pragma unroll
-            for (int i = k + 1; i < 6; ++i) x[i] -= A[i][k] * x[k];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const double d = A[i][i];
-        x[i] = (fabs(d) > 2.2250738585072014e-308) ? x[i] * fast_rcp(d) : 0.0;
-    }
-#pragma unroll
-    for (int k = 5; k >= 0; --k)
-#pragma unroll
-        for (int i = 0; i < k; ++i) x[i] -= A[k][i] * x[k];
-#pragma unroll
-    for (int k = 5; k >= 0; --k) po_swap6(x, k, tr[k]);
-}
-
-// The same solve on the damped system read from LDS (H full symmetric, b), with Eigen's pivot sequence found
-// first: Eigen's left-looking ldlt_inplace compares diagonal entries no earlier step has changed, so its
+// The oracle's ldlt_solve (Eigen ldlt_inplace with diagonal pivoting + LDLT::_solve_impl) for n = 6,
+// in registers: every lane holds the whole symmetric system and runs the oracle's operations in the
+// oracle's order, so no value crosses lanes.  Two changes: multiply-adds contract to FMAs, and a division
+// by a pivot is its reciprocal (fast_rcp, one per pivot) times the element, as the k_ctrl LDL^T does.  The
+// frontend's sums of H and b already differ from the oracle's order, so its parity is to tolerance
+// either way (tests/test_frontend.py), and the 21 IEEE divisions were the longest part of the step.
+// The damped system is read from LDS (H full symmetric, b), with Eigen's pivot sequence found first: Eigen's left-looking ldlt_inplace compares diagonal entries no earlier step has changed, so its
 // transpositions depend on the damped diagonal alone.  They are replayed on six (key, row) pairs, the
 // permuted system is loaded from LDS at the permuted addresses, the factorisation and the solves run
-// without swaps (the same operations on the same values as po_ldlt6_reg, so the same bits), and x goes back
-// to pose order through LDS.  This takes the 36-element row and column exchanges (a branch per candidate
-// row per step) off the chain.
+// without swaps (the same operations on the same values as Eigen's in-place swapping loop, so the same
+// bits as a swapping version), and x goes back to pose order through LDS.  This keeps the 36-element row
+// and column exchanges (a branch per candidate row per step) off the chain.
+#pragma clang fp contract(fast)   // the 6x6 solve is parity-to-tolerance (see above): FMAs halve its chains
 __device__ __forceinline__ void po_ldlt6_lds(const double* H, const double* bv, double lam, int strategy,
                                              double* xs, double (&x)[6]) {
     double key[6];
@@ -2564,18 +2470,12 @@ __device__ __forceinline__ void po_rows_to_parts(const double (&acc)[FV], PoShar
     wave_sync();
     if (lane < 2 * FV) {
         const int k = lane >> 1, h = lane & 1;
-#ifdef LH_PO_ONECHAIN
-        double s = 0.0;
-#pragma unroll 8
-        for (int i = 0; i < 32; ++i) s += S.rows[64 * wave + 2 * i + h][k];
-#else
         // four interleaved chains (rows i mod 4), then ((c0 + c1) + (c2 + c3)): a fixed order, a quarter of the
         // dependent adds
         double c[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int i = 0; i < 32; ++i) c[i & 3] += S.rows[64 * wave + 2 * i + h][k];
         double s = (c[0] + c[1]) + (c[2] + c[3]);
-#endif
         s += dpp_d<0xB1>(s);   // quad_perm [1,0,3,2]: the other parity's half
         if (h == 0) S.part[wave][k] = s;
     }
@@ -2662,21 +2562,7 @@ __global__ __launch_bounds__(FT) void k_frames(const int64_t* __restrict__ obs_p
         double x[6];
         const double lam = S.lam;
         STAMP(30);
-#ifdef LH_PO_SWAPS
-        {
-            double A[6][6], bb[6];
-#pragma unroll
-            for (int r = 0; r < 6; ++r) {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) A[r][j] = S.H[6 * r + j];
-                bb[r] = S.b[r];
-                A[r][r] += (prm.strategy == 0) ? lam : lam * A[r][r];
-            }
-            po_ldlt6_reg(A, bb, x);
-        }
-#else
         po_ldlt6_lds(S.H, S.b, lam, prm.strategy, S.xs, x);
-#endif
         STAMP(31);
         double cand[12], q[4], t[3];
         po_pose_add_wave(x, S.pose, S.qp, cand, q, t, lane);

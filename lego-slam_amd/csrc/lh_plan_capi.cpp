@@ -49,6 +49,7 @@ int lhp_plan_fill(const lh_window* w, int chunk_lm, int threads, lh_chunk* chunk
 // diagnostic: plan_structure's stage end times (ms from its start): index checks, CSR, per-landmark
 // sort + masks, span order, chunking, sub-batches, reduce-plan sizes; the last run of reps
 int lhp_plan_stages(const lh_window* w, int threads, int reps, double* out7) {
+    if (reps < 0 || !out7) return LH_E_BADARG;
     lh::Pool pool(threads > 0 ? threads : 1);
     lh::Plan pl;
     lh::PlanCfg cfg;
@@ -61,6 +62,7 @@ int lhp_plan_stages(const lh_window* w, int threads, int reps, double* out7) {
 }
 
 int lhp_plan_time(const lh_window* w, int chunk_lm, int threads, int reps, double* ms_structure, double* ms_fill) {
+    if (reps < 1 || !ms_structure || !ms_fill) return LH_E_BADARG;
     lh::Pool pool(threads > 0 ? threads : 1);
     lh::Plan pl;
     lh::PlanCfg cfg;

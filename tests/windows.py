@@ -19,7 +19,7 @@ import lego_ba
 STABLE = dict(right_frac=0.5, depth_max=30.0, pose_rot_sigma=0.0005, pose_trans_sigma=0.005, lm_sigma=0.02)
 
 
-def window(cfg, seed=0, family="default", fix_first=None, **kw):
+def _family_params(family, fix_first, kw):
     params = {}
     if family in ("stable", "stable_noout"):
         params.update(STABLE)
@@ -28,9 +28,27 @@ def window(cfg, seed=0, family="default", fix_first=None, **kw):
         if fix_first is None:
             fix_first = True
     params.update(kw)
-    w = lego_ba.config_window(cfg, seed=seed, **params)
+    return params, fix_first
+
+
+def _fix(w, fix_first):
     if fix_first:
         f = np.zeros(w["n_poses"], np.uint8)
         f[0] = 1
         w["pose_fixed"] = f
     return w
+
+
+def window(cfg, seed=0, family="default", fix_first=None, **kw):
+    params, fix_first = _family_params(family, fix_first, kw)
+    return _fix(lego_ba.config_window(cfg, seed=seed, **params), fix_first)
+
+
+def window_shard(cfg, l0, l1, seed=0, family="default", fix_first=None, **kw):
+    """Landmarks [l0, l1) of window(cfg, seed, family) and their observations, generated directly (the
+    generator draws each landmark from its own counter stream, so this equals slicing the whole
+    window, with shard-local landmark indices): one rank's unit in the landmark-sharded path."""
+    params, fix_first = _family_params(family, fix_first, kw)
+    c = dict(lego_ba.CONFIGS[cfg])
+    c.update(params)
+    return _fix(lego_ba.generate_window(seed=seed, lm_begin=l0, lm_end=l1, **c), fix_first)
