@@ -98,7 +98,8 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     if (w->n_poses > 0 && !w->pose_Tcw) return LH_E_BADARG;
     if (w->n_landmarks > 0 && !w->lm_xyz) return LH_E_BADARG;
     if (w->n_obs > 0 && (!w->obs_pose || !w->obs_lm || !w->obs_uv)) return LH_E_BADARG;
-    if (w->n_cams < 0 || w->n_cams > LH_MAX_CAMS || (w->n_cams > 0 && !w->cam_ext)) return LH_E_BADARG;
+    if (w->n_cams < 0 || (w->n_cams > 0 && !w->cam_ext)) return LH_E_BADARG;
+    if (w->n_cams > LH_MAX_CAMS) return LH_E_UNSUPPORTED;   // per-(pose, camera) tables sized for 4 cameras
     const int P = w->n_poses, L = w->n_landmarks;
     const int64_t O = w->n_obs;
     const int ncam = w->n_cams > 0 ? w->n_cams : 1;

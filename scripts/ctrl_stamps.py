@@ -45,7 +45,10 @@ if cfg.startswith("P"):   # k_ctrl_g's panel sub-phases, summed over the panels:
         d = (sub[i] - sub[i - 1]) / n if i > 1 else None
         if d is not None:
             print(f"    {nm:20s} {d:9.0f} cycles  {d / (tot_cyc / tot_ns) / 1000:6.2f} us")
-for b, nm in ((49, "steps 0-3"), (45, "steps 4+")):
-    k = max(st[b + 3], 1)
-    print(f"  LDLT {nm}: {k // max(n, 1)} per launch; per step: wave 0 chain {st[b] / k:.0f}, slowest other wave "
-          f"{st[b + 1] / k:.0f}, barrier to barrier {st[b + 2] / k:.0f} cycles")
+# per-step split of the LDL^T loop (lds_ldlt_solve stamps 46-51): wave 0's diagonal tile, its 8x8
+# factor, its wait at the step barrier; the other 15 waves' unit time and barrier wait (per wave)
+nl = max(st[51], 1)
+if st[51]:
+    print(f"  LDLT loop per launch: wave 0 diag tile {st[46] / nl:.0f}, factor {st[47] / nl:.0f}, barrier wait "
+          f"{st[48] / nl:.0f} cycles; other waves (mean per wave) unit {st[49] / nl / 15:.0f}, barrier wait "
+          f"{st[50] / nl / 15:.0f} cycles")

@@ -1,24 +1,32 @@
-# k_ctrl / k_ldlt_probe kernel durations under rocprofv3 for the default build (A) and lib/liblego_ba_x.so (B)
+#!/bin/bash
+# k_ctrl A/B: the k_ctrl parity tests on the current build, then rocprofv3 kernel traces of the C3
+# bench (300 solves) for the current build (A) and LIB_B, alternating twice; per-kernel averages.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/cab
+: > gpurun_out/cab/summary.txt
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_pcg.py -m gpu -x -q \
+    --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/cab/tests.log 2>&1 || { tail -30 gpurun_out/cab/tests.log; exit 1; }
+tail -1 gpurun_out/cab/tests.log
 for r in 1 2; do
 for v in A B; do
-  lib=$( [ $v = A ] && echo lego-slam_amd/lib/liblego_ba.so || echo lego-slam_amd/lib/liblego_ba_x.so )
-  LH_LIB=$lib timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/cab/$v$r -o p --output-format csv -- \
-    python3 bench.py --steps 300 --warmup 3 --no-cpu --no-extras > gpurun_out/cab/bench_$v$r.log 2>&1 || exit 1
-  LH_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/cab/p$v$r -o p --output-format csv -- \
-    python3 scripts/ldlt_probe_time.py > gpurun_out/cab/probe_$v$r.log 2>&1 || exit 1
-  for f in $(find gpurun_out/cab/$v$r gpurun_out/cab/p$v$r -name '*kernel_stats.csv'); do
-    python3 - "$v$r" "$f" >> gpurun_out/cab/summary.txt <<'PY'
+  lib=$( [ $v = A ] && echo lego-slam_amd/lib/liblego_ba.so || echo "$LIB_B" )
+  LH_LIB=$lib timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/cab/$v.$r -o p --output-format csv -- \
+    python3 bench.py --steps 300 --warmup 3 --no-cpu --no-extras > gpurun_out/cab/bench_$v.$r.log 2>&1 || exit 1
+  for f in $(find gpurun_out/cab/$v.$r -name '*kernel_stats.csv'); do
+    python3 - "$v.$r" "$f" >> gpurun_out/cab/summary.txt <<'PY'
 import csv, sys
 for row in csv.DictReader(open(sys.argv[2])):
     n = row.get("Name", "")
-    if any(k in n for k in ("k_ctrl", "k_ldlt_probe", "k_lin", "k_reduce")):
-        print(sys.argv[1], n[:40], row.get("Calls"), row.get("AverageNs"))
+    if any(k in n for k in ("k_ctrl", "k_lin<3, true>", "k_reduce")):
+        print(sys.argv[1], n[:24], row.get("Calls"), row.get("AverageNs"))
 PY
   done
+  python3 -c "
+import json,sys
+for l in open('gpurun_out/cab/bench_$v.$r.log'):
+    if l.startswith('{'): d=json.loads(l); print('$v.$r', 'ms_per_step', d['ms_per_step'], 'it/s', d['value'])" >> gpurun_out/cab/summary.txt
+  rm -rf gpurun_out/cab/$v.$r
 done
 done
 cat gpurun_out/cab/summary.txt
-grep -h '^{' gpurun_out/cab/bench_*.log | python3 -c "import sys,json; [print(json.loads(l)['value']) for l in sys.stdin]"

@@ -591,3 +591,45 @@ def test_final_iteration_trials_evaluate_only(cfg, family, kw, monkeypatch):
         assert full[k] == evo[k], k
     for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
         assert np.array_equal(full[k], evo[k]), k
+
+
+# ---------------------------------------------------------------------------------------------
+# Camera rigs of 3 and 4 cameras with non-identity extrinsic rotations (EdgeProjection takes any
+# Camera::pose_, lego_types.h:211-215, 229-253; the ABI allows 4 cameras).  Landmarks seen by up to
+# 16 poses through 4 cameras give k_lin<6> its largest LDS image (T = 6 with 4 cameras' pose tables).
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n_cams,kmin,kmax,mode", [(3, 8, 8, 0), (4, 8, 8, 0), (4, 2, 10, 1), (4, 11, 16, 1)])
+def test_multi_camera_rigs_with_rotated_extrinsics(n_cams, kmin, kmax, mode):
+    from windows import STABLE, multi_camera
+    w = lego_ba.generate_window(P=20, L=3000, k=kmin, k_max=kmax, seed=7, pose_mode=mode,
+                                **dict(STABLE, outlier_frac=0.0))
+    f = np.zeros(20, np.uint8)
+    f[0] = 1
+    w["pose_fixed"] = f
+    w = multi_camera(w, n_cams, seed=7)
+    assert set(np.unique(w["obs_cam"])) == set(range(n_cams))
+    # residual, robust weight and rho0 through the rotated extrinsics: bitwise the oracle's
+    g0 = lego_ba.Solver(max_iters=0).solve(w)
+    o0 = ob.solve(w, max_iters=0)
+    assert np.array_equal(g0["edge_robust_chi2"], o0["edge_robust_chi2"])
+    g = lego_ba.Solver(max_iters=1, max_trials=1).solve(w)
+    o = ob.solve(w, max_iters=1, max_trials=1)
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-7)
+    gf = lego_ba.Solver().solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 2, 8))
+    assert gf["iterations"] in its
+    assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+    assert gf["chi2_final"] < gf["chi2_initial"]
+
+
+def test_five_cameras_are_unsupported():
+    from windows import STABLE, multi_camera
+    w = multi_camera(lego_ba.generate_window(P=10, L=300, k=8, seed=1, **STABLE), 4, seed=1)
+    w["cam_ext"] = np.vstack([w["cam_ext"], w["cam_ext"][:1]])
+    w["obs_cam"] = w["obs_cam"].copy()
+    w["obs_cam"][:5] = 4
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.Solver().solve(w)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED

@@ -52,3 +52,45 @@ def window_shard(cfg, l0, l1, seed=0, family="default", fix_first=None, **kw):
     c = dict(lego_ba.CONFIGS[cfg])
     c.update(params)
     return _fix(lego_ba.generate_window(seed=seed, lm_begin=l0, lm_end=l1, **c), fix_first)
+
+
+def _rot(axis, angle):
+    a = np.asarray(axis, np.float64)
+    a = a / np.linalg.norm(a)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return np.eye(3) + np.sin(angle) * K + (1 - np.cos(angle)) * K @ K
+
+
+# extra camera rigs for the multi-camera windows: (rotation axis, angle, translation); camera 0 is the
+# generator's identity (KITTI left, dataset.cpp:36-42) and camera 1 its stereo baseline
+EXTRA_CAMS = [((0.0, 1.0, 0.0), 0.05, (0.20, -0.10, 0.05)),
+              ((1.0, 1.0, 0.3), 0.08, (-0.30, 0.05, 0.10))]
+
+
+def multi_camera(w, n_cams, seed=0, noise_px=1.0):
+    """Window `w` re-observed through a rig of n_cams (3 or 4) cameras: cameras 2, 3 have non-identity
+    extrinsic rotations (Camera::pose_, the ext of EdgeProjection's K * (ext * (T * X)),
+    lego_types.h:211-215).  Each observation is assigned a random camera and re-measured from the true
+    pose and landmark (float32 pixels + N(0, noise_px^2)), so the window stays consistent."""
+    rng = np.random.default_rng(1000 + seed)
+    ext = np.zeros((n_cams, 12))
+    ext[:2] = w["cam_ext"][:2]
+    for c in range(2, n_cams):
+        axis, ang, t = EXTRA_CAMS[c - 2]
+        ext[c, [0, 1, 2, 4, 5, 6, 8, 9, 10]] = _rot(axis, ang).reshape(9)
+        ext[c, [3, 7, 11]] = t
+    O = len(w["obs_pose"])
+    cam = rng.integers(0, n_cams, O).astype(np.uint8)
+    T = w["pose_true"][w["obs_pose"]].reshape(O, 3, 4)
+    X = w["lm_true"][w["obs_lm"]]
+    Pb = np.einsum("oij,oj->oi", T[:, :, :3], X) + T[:, :, 3]
+    E = ext[cam].reshape(O, 3, 4)
+    Pc = np.einsum("oij,oj->oi", E[:, :, :3], Pb) + E[:, :, 3]
+    fx, fy, cx, cy = w["K"]
+    u = (fx * Pc[:, 0] + cx * Pc[:, 2]) / Pc[:, 2] + rng.normal(0, noise_px, O)
+    v = (fy * Pc[:, 1] + cy * Pc[:, 2]) / Pc[:, 2] + rng.normal(0, noise_px, O)
+    out = dict(w)
+    out["cam_ext"] = ext
+    out["obs_cam"] = cam
+    out["obs_uv"] = np.stack([u, v], 1).astype(np.float32).astype(np.float64)
+    return out
