@@ -1047,7 +1047,8 @@ struct LdltBlockLds {
 };
 
 // 64-bit broadcast of lane L of each 16-lane row (DPP row_newbcast, two 32-bit moves): a few
-// cycles, where a readlane round trip through an SGPR costs ~45 on a dependent chain.
+// cycles, where a readlane round trip through an SGPR costs ~45 on a dependent chain.  (A single
+// v_fmac_f64_dpp from inline asm measured 10% faster but lost precision: not used.)
 template <int L>
 __device__ __forceinline__ double bcast16(double v) {
     const long long x = __double_as_longlong(v);
@@ -1056,15 +1057,31 @@ __device__ __forceinline__ double bcast16(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+template <int Q>
+__device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
+    const double d = bcast16<Q>(R[Q]);
+    dl[Q] = fabs(d) > 0.0 ? d : 1.0;          // Eigen ldlt_inplace: no scaling where !pivot_is_valid
+    const double inv = fast_rcp(dl[Q]);
+    const double coef = R[Q] * inv;
+    double u[8];
+    // W[j][Q] = lane j's R[Q], read before R[Q] becomes coef
+    if (Q < 1) u[1] = bcast16<1>(R[Q]);
+    if (Q < 2) u[2] = bcast16<2>(R[Q]);
+    if (Q < 3) u[3] = bcast16<3>(R[Q]);
+    if (Q < 4) u[4] = bcast16<4>(R[Q]);
+    if (Q < 5) u[5] = bcast16<5>(R[Q]);
+    if (Q < 6) u[6] = bcast16<6>(R[Q]);
+    if (Q < 7) u[7] = bcast16<7>(R[Q]);
+#pragma unroll
+    for (int j = Q + 1; j < 8; ++j) R[j] -= coef * u[j];
+    R[Q] = coef;
+}
+
 // LDL^T of the 8x8 diagonal block at (k0, k0) of A by one wave, Eigen ldlt_inplace order (L = W
-// where pivot_is_valid fails).  Every lane reads the block's lower triangle (broadcast LDS reads: one
-// address per instruction) and eliminates it redundantly in registers, so each column's pivot and
-// pre-scaled entries are in every lane with no cross-lane move on the chain.  In each 16-lane row
-// (four identical replicas), lane r < 8 then eliminates row r of the block and lane 8 + r row r of
-// the identity with those uniform multipliers: the same column operations turn the first into L and
-// the second into N = (Delta L^T)^-1, Delta = diag(D, 1 where invalid).  A lane's row operation is
-// the operation the redundant elimination applies to that row, in the same order, so the factor is
-// bitwise the one the DPP-broadcast version (pivots and column entries moved between lanes) made.
+// where pivot_is_valid fails).  In each 16-lane row (four identical replicas), lane r < 8 holds
+// row r of the block and lane 8 + r row r of the identity: the same column eliminations turn
+// the first into L and the second into N = (Delta L^T)^-1, Delta = diag(D, 1 where invalid), so
+// one instruction stream computes both.  Column q's pivot and entries move by DPP broadcast.
 // Writes D on A's diagonal and L^T above it (L[r][c] at A[c][r]), N, and ND = N Delta = L^-T.
 // For a row a below the block, l = a N is its forward substitution through the block and
 // l Delta its partially eliminated entries, so the trailing update of rows i, j is
@@ -1073,43 +1090,20 @@ __device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __
                                               int k0, int lane) {
     const int p = lane & 15, r = p & 7;
     const bool ident = p >= 8;
-    double w[36];   // w[i (i + 1) / 2 + j] = block entry (i, j), j <= i: uniform across the wave
+    double R[8], dl[8];
+    double v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int q = 0; q < 8; ++q) v[q] = A[(k0 + r) * AS + k0 + q];   // upper entries: garbage confined to this lane's upper part
 #pragma unroll
-        for (int j = 0; j <= i; ++j) w[i * (i + 1) / 2 + j] = A[(k0 + i) * AS + k0 + j];
-    double R[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const double v = A[(k0 + r) * AS + k0 + q];   // upper entries: garbage confined to this lane's upper part
-        R[q] = ident ? (q == r ? 1.0 : 0.0) : v;
-    }
-#pragma unroll
-    for (int Q = 0; Q < 8; ++Q) {
-        const double d = w[Q * (Q + 1) / 2 + Q];
-        const double dl = fabs(d) > 0.0 ? d : 1.0;   // Eigen ldlt_inplace: no scaling where !pivot_is_valid
-        const double inv = fast_rcp(dl);
-        // this lane's row: R[j] -= (R[Q] / d) W[j][Q], W[j][Q] the pre-scaled column entry
-        const double coef = R[Q] * inv;
-#pragma unroll
-        for (int j = Q + 1; j < 8; ++j) R[j] -= coef * w[j * (j + 1) / 2 + Q];
-        R[Q] = coef;
-        // the same operation on every row of the block's trailing triangle (the next columns' entries)
-#pragma unroll
-        for (int i = Q + 1; i < 8; ++i) {
-            const double li = w[i * (i + 1) / 2 + Q] * inv;
-#pragma unroll
-            for (int j = Q + 1; j <= i; ++j) w[i * (i + 1) / 2 + j] -= li * w[j * (j + 1) / 2 + Q];
-        }
-    }
-    // w's diagonal is final from its own step on (later steps update only columns past it), so the
-    // pivots are re-derived here rather than kept in a second array across the elimination
-    double dl[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const double d = w[q * (q + 1) / 2 + q];
-        dl[q] = fabs(d) > 0.0 ? d : 1.0;
-    }
+    for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
+    factor_column<0>(R, dl);
+    factor_column<1>(R, dl);
+    factor_column<2>(R, dl);
+    factor_column<3>(R, dl);
+    factor_column<4>(R, dl);
+    factor_column<5>(R, dl);
+    factor_column<6>(R, dl);
+    factor_column<7>(R, dl);
     if (lane < 8) {
 #pragma unroll
         for (int q = 0; q < 8; ++q)
@@ -1137,10 +1131,6 @@ __device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __
 __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const double* __restrict__ N,
                                               const double* __restrict__ ND, int k0, int rb, int jb0, int jb1,
                                               int skip_cb, bool store_l, int lane) {
-    // rb is loop-invariant per wave: without this the compiler hoists every per-lane LDS address of
-    // the tile row out of the step loop and keeps them live across it (spilling to scratch when the
-    // 8x8 factor needs its registers); recomputing them per step is a few VALU instructions
-    asm volatile("" : "+s"(rb));
     const int li = lane & 15, lk = lane >> 4, m0 = k0 + 8;
     const bool lo = li < 8;
     // every LDS read of this tile row is issued up front (tiles are disjoint and this step's
@@ -1811,11 +1801,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                 r += (d > di) || (d == di && part * 16 + u < row);
             }
         }
-        // ds_swizzle (xor mode, immediate pattern): no per-lane address register, which the compiler
-        // would otherwise keep live across the whole solve for the tail's shuffles
-        r += __builtin_amdgcn_ds_swizzle(r, 0x041F);
-        r += __builtin_amdgcn_ds_swizzle(r, 0x081F);
-        r += __builtin_amdgcn_ds_swizzle(r, 0x101F);
+        r += __shfl_xor(r, 1);
+        r += __shfl_xor(r, 2);
+        r += __shfl_xor(r, 4);
         if (part == 0 && row < NP) {
             const int rr = row < n ? r : row;
             perm[rr] = row;
