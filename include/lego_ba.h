@@ -101,7 +101,7 @@ typedef struct lh_options {
     int32_t chunk_landmarks;  /* landmarks per k_lin chunk; 0 = auto (~2 workgroups per CU)     */
     int32_t comm_mode;        /* lh_comm_mode (world_size > 1)                                  */
     int32_t host_threads;     /* window-preprocessing threads; 0 = auto (the CPUs this process may
-                                 use: affinity mask capped by the cgroup CPU quota, <= 16)       */
+                                 use: affinity mask capped by the cgroup CPU quota, <= 8)        */
     lh_allreduce_fn allreduce;  /* LH_COMM_HOST: the exchange                                    */
     void *allreduce_user;       /* its first argument                                            */
 } lh_options;
@@ -123,7 +123,9 @@ typedef struct lh_window {
     const uint32_t *obs_pose;  /* [n_obs] pose index                                                */
     const uint32_t *obs_lm;    /* [n_obs] landmark index                                            */
     const uint8_t *obs_cam;    /* [n_obs] camera index or NULL (all camera 0)                       */
-    const double *obs_uv;      /* [n_obs][2] pixel measurement (toVec2 of cv::KeyPoint, algorithm.h:37) */
+    const double *obs_uv;      /* [n_obs][2] pixel measurement: toVec2 of cv::KeyPoint::pt (algorithm.h:37),
+                                  i.e. float values widened; a value no float holds exactly (or a NaN) is
+                                  LH_E_BADARG (the device keeps the pixels as floats)                 */
     double K[4];               /* fx, fy, cx, cy (Camera::K, camera.h:36-41)                         */
     int32_t n_cams;            /* number of extrinsics in cam_ext (0 with cam_ext NULL = identity)   */
     const double *cam_ext;     /* [n_cams][12] row-major [R | t] camera extrinsic (Camera::pose_)    */

@@ -30,7 +30,7 @@ hipError_t lh_prepare_lin(int lds_limit);
 size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
-                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
+                         const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag,
                          long nslots, lh_params prm, int nrec, uint64_t fixed_mask);
@@ -214,7 +214,10 @@ int auto_host_threads() {
         }
         std::fclose(f);
     }
-    return std::max(1, std::min(16, n));
+    // the planner's passes are memory-bound and their pool meets at a barrier per pass: past 8 threads
+    // a shared box's scheduling noise costs more than the bandwidth they add (C3 planner: 0.74 ms at 8
+    // threads, 1.19 ms at 16, EPYC 9575F box with a 16-CPU quota)
+    return std::max(1, std::min(8, n));
 }
 
 }  // namespace
@@ -243,8 +246,11 @@ struct lh_handle {
     HostBuf<uint32_t> s_meta, s_items, s_pair_ptr, s_rsmap;
     HostBuf<uint16_t> s_pair_pq;
     HostBuf<int32_t> s_obs_perm, s_lm_perm;
-    HostBuf<double> s_uv, s_lm, s_qt, s_ptab, s_ext, s_rs;   // s_rs: the host-exchange buffer
+    HostBuf<float> s_uv;                                     // pixels, 2 floats per slot
+    HostBuf<double> s_lm, s_qt, s_ptab, s_ext, s_rs;         // s_rs: the host-exchange buffer
     HostBuf<double> s_out;                                   // pinned staging of the download
+    hipEvent_t ev_staging = nullptr;   // the upload's last copy out of the staging (reused by the next upload)
+    bool staging_pending = false;
 
     // device buffers
     DevBuf<lh_chunk> d_chunks;
@@ -252,7 +258,8 @@ struct lh_handle {
     DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
     DevBuf<uint16_t> d_pair_pq;
     DevBuf<int32_t> d_obs_perm, d_lm_perm;
-    DevBuf<double> d_uv, d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_gS, d_rs_stage,
+    DevBuf<float> d_uv;
+    DevBuf<double> d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_gS, d_rs_stage,
         d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
@@ -348,9 +355,35 @@ void collect_profile(lh_handle* h, int trials_run) {
     h->event_next = 0;
 }
 
-int upload_impl(lh_handle* h, const lh_window* w) {
+// the planner's slot batches go to the device as soon as they are final (plan_fill's on_slots), so
+// the copies of the largest arrays overlap the rest of the fill
+struct SlotCopy {
+    lh_handle* h;
+    hipError_t err;
+};
+void copy_slots(void* user, int64_t s0, int64_t s1) {
+    SlotCopy* c = static_cast<SlotCopy*>(user);
+    lh_handle* h = c->h;
+    if (c->err != hipSuccess || s1 <= s0) return;
+    const size_t n = (size_t)(s1 - s0);
+    hipStream_t st = h->stream;
+    hipError_t e = hipMemcpyAsync(h->d_meta.p + s0, h->s_meta.p + s0, n * sizeof(uint32_t), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h->d_uv.p + 2 * s0, h->s_uv.p + 2 * s0, 2 * n * sizeof(float), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h->d_obs_perm.p + s0, h->s_obs_perm.p + s0, n * sizeof(int32_t), hipMemcpyHostToDevice, st);
+    c->err = e;
+}
+
+// sync: return only once the copies are done (lh_upload); lh_solve leaves them queued ahead of its
+// kernels on the same stream.  Either way the next upload waits for them before it rewrites the staging.
+int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     const double t0 = now_ms();
     h->uploaded = false;
+    if (h->staging_pending) {
+        HIPCHK(hipEventSynchronize(h->ev_staging));
+        h->staging_pending = false;
+    }
     lh::PlanCfg cfg;
     cfg.chunk_lm = h->opt.chunk_landmarks;
     lh::Plan& pl = h->plan;
@@ -368,7 +401,49 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     h->n_slots = pl.n_slots;
     h->LY = lh_rs_make(P);
 
-    // ---- staging ----
+    // ---- device buffers (before the fill: its slot batches are copied as they complete) ----
+    const size_t PT = (size_t)P * ncam * LH_PT;
+    HIPCHK(h->d_chunks.ensure(pl.n_chunks));
+    HIPCHK(h->d_sbs.ensure(pl.n_sb));
+    HIPCHK(h->d_meta.ensure(pl.n_slots));
+    HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
+    HIPCHK(h->d_obs_perm.ensure(pl.n_slots));
+    HIPCHK(h->d_lm_perm.ensure(pl.n_rec));
+    HIPCHK(h->d_lm_in.ensure(3 * (size_t)pl.L));
+    HIPCHK(h->d_pair_ptr.ensure(pl.npairs + 1));
+    HIPCHK(h->d_items.ensure(pl.n_items));
+    HIPCHK(h->d_pair_pq.ensure(2 * (size_t)pl.npairs));
+    HIPCHK(h->d_rec.ensure(2 * (size_t)pl.n_rec * LH_REC));
+    HIPCHK(h->d_ptab.ensure(2 * PT));
+    HIPCHK(h->d_ptab_init.ensure(2 * PT));
+    HIPCHK(h->d_qt.ensure(24 * (size_t)P));
+    HIPCHK(h->d_qt_init.ensure(24 * (size_t)P));
+    HIPCHK(h->d_ext.ensure(LH_EXT * (size_t)ncam));
+    HIPCHK(h->d_rho.ensure(pl.n_slots));
+    HIPCHK(h->d_wflag.ensure(2 * (size_t)pl.n_slots));
+    HIPCHK(h->d_rows.ensure((size_t)pl.n_items * LH_ROW));
+    HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
+    HIPCHK(h->d_rs_stage.ensure(h->LY.total));
+    HIPCHK(h->d_rs_commit.ensure(h->LY.total));
+    if (P > LH_PMAX) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once (its unused upper triangle)
+        const size_t ng = (size_t)((6 * P + 31) & ~31);
+        const bool fresh = h->d_gA.n < ng * ng;
+        HIPCHK(h->d_gA.ensure(ng * ng));
+        if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
+        // k_dense's dense symmetric S, double-buffered with the committed state
+        const bool fresh_s = h->d_gS.n < 2 * ng * ng;
+        HIPCHK(h->d_gS.ensure(2 * ng * ng));
+        if (fresh_s) HIPCHK(hipMemsetAsync(h->d_gS.p, 0, h->d_gS.n * sizeof(double), h->stream));
+    }
+    HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
+    HIPCHK(h->d_maxd.ensure(1));
+    HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
+    HIPCHK(h->d_ctrl.ensure(1));
+    HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
+    HIPCHK(h->d_out_rho.ensure(pl.O));
+    if (h->host_comm) HIPCHK(h->s_rs.ensure(h->LY.total + 1));
+
+    // ---- staging and the fill ----
     HIPCHK(h->s_chunks.ensure(pl.n_chunks));
     HIPCHK(h->s_sbs.ensure(pl.n_sb));
     HIPCHK(h->s_meta.ensure(pl.n_slots));
@@ -382,7 +457,10 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(h->s_lm.ensure(3 * (size_t)pl.L));
     lh::PlanOut po{h->s_chunks.p, h->s_sbs.p, h->s_meta.p, h->s_uv.p, h->s_obs_perm.p, h->s_lm_perm.p,
                    h->s_items.p, h->s_pair_pq.p, h->s_rsmap.p, h->s_lm.p};
-    lh::plan_fill(w, pl, po, h->pool);
+    SlotCopy sc{h, hipSuccess};
+    const int batches = pl.n_slots >= (1 << 16) ? 4 : 1;
+    lh::plan_fill(w, pl, po, h->pool, copy_slots, &sc, batches);
+    HIPCHK(sc.err);
     std::memcpy(h->s_pair_ptr.p, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
 
     // ---- camera extrinsics (Sophus SE3 of Camera::pose_) and the initial pose tables ----
@@ -438,55 +516,12 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     const double t1 = now_ms();
 
-    // ---- device buffers and the copies ----
-    const size_t PT = (size_t)P * ncam * LH_PT;
-    HIPCHK(h->d_chunks.ensure(pl.n_chunks));
-    HIPCHK(h->d_sbs.ensure(pl.n_sb));
-    HIPCHK(h->d_meta.ensure(pl.n_slots));
-    HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
-    HIPCHK(h->d_obs_perm.ensure(pl.n_slots));
-    HIPCHK(h->d_lm_perm.ensure(pl.n_rec));
-    HIPCHK(h->d_lm_in.ensure(3 * (size_t)pl.L));
-    HIPCHK(h->d_pair_ptr.ensure(pl.npairs + 1));
-    HIPCHK(h->d_items.ensure(pl.n_items));
-    HIPCHK(h->d_pair_pq.ensure(2 * (size_t)pl.npairs));
-    HIPCHK(h->d_rec.ensure(2 * (size_t)pl.n_rec * LH_REC));
-    HIPCHK(h->d_ptab.ensure(2 * PT));
-    HIPCHK(h->d_ptab_init.ensure(2 * PT));
-    HIPCHK(h->d_qt.ensure(24 * (size_t)P));
-    HIPCHK(h->d_qt_init.ensure(24 * (size_t)P));
-    HIPCHK(h->d_ext.ensure(LH_EXT * (size_t)ncam));
-    HIPCHK(h->d_rho.ensure(pl.n_slots));
-    HIPCHK(h->d_wflag.ensure(2 * (size_t)pl.n_slots));
-    HIPCHK(h->d_rows.ensure((size_t)pl.n_items * LH_ROW));
-    HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
-    HIPCHK(h->d_rs_stage.ensure(h->LY.total));
-    HIPCHK(h->d_rs_commit.ensure(h->LY.total));
-    if (P > LH_PMAX) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once (its unused upper triangle)
-        const size_t ng = (size_t)((6 * P + 31) & ~31);
-        const bool fresh = h->d_gA.n < ng * ng;
-        HIPCHK(h->d_gA.ensure(ng * ng));
-        if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
-        // k_dense's dense symmetric S, double-buffered with the committed state
-        const bool fresh_s = h->d_gS.n < 2 * ng * ng;
-        HIPCHK(h->d_gS.ensure(2 * ng * ng));
-        if (fresh_s) HIPCHK(hipMemsetAsync(h->d_gS.p, 0, h->d_gS.n * sizeof(double), h->stream));
-    }
-    HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
-    HIPCHK(h->d_maxd.ensure(1));
-    HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
-    HIPCHK(h->d_ctrl.ensure(1));
-    HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
-    HIPCHK(h->d_out_rho.ensure(pl.O));
-    if (h->host_comm) HIPCHK(h->s_rs.ensure(h->LY.total + 1));
+    // ---- the remaining copies ----
     hipStream_t s = h->stream;
     auto up = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
         if (!bytes) return hipSuccess;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
     };
-    HIPCHK(up(h->d_meta.p, h->s_meta.p, pl.n_slots * sizeof(uint32_t)));
-    HIPCHK(up(h->d_uv.p, h->s_uv.p, 2 * pl.n_slots * sizeof(double)));
-    HIPCHK(up(h->d_obs_perm.p, h->s_obs_perm.p, pl.n_slots * sizeof(int32_t)));
     HIPCHK(up(h->d_lm_perm.p, h->s_lm_perm.p, (size_t)pl.n_rec * sizeof(int32_t)));
     HIPCHK(up(h->d_lm_in.p, h->s_lm.p, 3 * (size_t)pl.L * sizeof(double)));
     HIPCHK(up(h->d_chunks.p, h->s_chunks.p, (size_t)pl.n_chunks * sizeof(lh_chunk)));
@@ -498,7 +533,12 @@ int upload_impl(lh_handle* h, const lh_window* w) {
     HIPCHK(up(h->d_ptab_init.p, h->s_ptab.p, 2 * PT * sizeof(double)));
     HIPCHK(up(h->d_qt_init.p, h->s_qt.p, 24 * (size_t)P * sizeof(double)));
     HIPCHK(up(h->d_ext.p, h->s_ext.p, LH_EXT * (size_t)ncam * sizeof(double)));
-    HIPCHK(hipStreamSynchronize(s));   // the staging is reused by the next upload
+    HIPCHK(hipEventRecord(h->ev_staging, s));
+    h->staging_pending = true;
+    if (sync) {
+        HIPCHK(hipEventSynchronize(h->ev_staging));
+        h->staging_pending = false;
+    }
     h->last_prep_ms = t1 - t0;
     h->last_upload_ms = now_ms() - t0;
     h->uploaded = true;
@@ -631,13 +671,18 @@ int download(lh_handle* h, lh_result* out, int cur) {
         HIPCHK(lh_launch_gather(s, h->d_ctrl.p, h->d_rec.p, h->d_lm_perm.p, nl ? h->n_rec : 0, h->d_rho.p,
                                 h->d_obs_perm.p, ne ? (long)h->n_slots : 0L, h->d_out_xyz.p, h->d_out_rho.p));
         if (nl) HIPCHK(hipMemcpyAsync(st + np, h->d_out_xyz.p, nl * sizeof(double), hipMemcpyDeviceToHost, s));
-        if (ne) HIPCHK(hipMemcpyAsync(st + np + nl, h->d_out_rho.p, ne * sizeof(double), hipMemcpyDeviceToHost, s));
     }
+    // poses and landmarks are copied out of the staging while the per-edge chi2 is still in flight
+    hipEvent_t e_first = next_event(h);
+    if (!e_first) return LH_E_HIP;
+    HIPCHK(hipEventRecord(e_first, s));
+    if (ne) HIPCHK(hipMemcpyAsync(st + np + nl, h->d_out_rho.p, ne * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventSynchronize(e_first));
+    const ByteSeg seg[2] = {{out->pose_Tcw, st, np * sizeof(double)}, {out->lm_xyz, st + np, nl * sizeof(double)}};
+    par_copy(h, seg, 2);
     HIPCHK(hipStreamSynchronize(s));
-    const ByteSeg seg[3] = {{out->pose_Tcw, st, np * sizeof(double)},
-                            {out->lm_xyz, st + np, nl * sizeof(double)},
-                            {out->edge_robust_chi2, st + np + nl, ne * sizeof(double)}};
-    par_copy(h, seg, 3);
+    const ByteSeg seg_e = {out->edge_robust_chi2, st + np + nl, ne * sizeof(double)};
+    par_copy(h, &seg_e, 1);
     out->time_download_ms = now_ms() - t0;
     return LH_OK;
 }
@@ -889,6 +934,11 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
         h->pool = nullptr;
     }
     if (!h->pool) { lh_destroy(h); return LH_E_HIP; }
+    if (hipEventCreateWithFlags(&h->ev_staging, hipEventDisableTiming) != hipSuccess) {
+        h->ev_staging = nullptr;
+        lh_destroy(h);
+        return LH_E_HIP;
+    }
     h->host_comm = opt->world_size > 1 && opt->comm_mode == LH_COMM_HOST;
     // LH_FORCE_RCCL=1 builds a one-rank communicator on a single GPU, so the data-path
     // collectives (and their stream ordering) run in single-GPU tests too
@@ -934,6 +984,7 @@ void lh_destroy(lh_handle* h) {
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
     h->s_out.release();
+    if (h->ev_staging) (void)hipEventDestroy(h->ev_staging);
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -944,7 +995,7 @@ int lh_upload(lh_handle* h, const lh_window* in) {
     if (!h) return LH_E_BADARG;
     if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
     try {
-        return upload_impl(h, in);
+        return upload_impl(h, in, true);
     } catch (const std::bad_alloc&) {
         return LH_E_HIP;
     } catch (...) {
@@ -963,7 +1014,16 @@ int lh_solve_resident(lh_handle* h, lh_result* out) {
 }
 
 int lh_solve(lh_handle* h, const lh_window* in, lh_result* out) {
-    int st = lh_upload(h, in);
+    if (!h) return LH_E_BADARG;
+    if (hipSetDevice(h->device) != hipSuccess) return LH_E_HIP;
+    int st;
+    try {
+        st = upload_impl(h, in, false);   // the copies stay queued ahead of the solve's kernels
+    } catch (const std::bad_alloc&) {
+        return LH_E_HIP;
+    } catch (...) {
+        return LH_E_BADARG;
+    }
     if (st != LH_OK) return st;
     return lh_solve_resident(h, out);
 }

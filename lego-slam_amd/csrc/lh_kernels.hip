@@ -429,7 +429,7 @@ static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_
 
 template <int T, bool TRIAL>
 __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
-    const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const double* __restrict__ obs_uv,
+    const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const float* __restrict__ obs_uv,
     const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
     double* __restrict__ edge_rho, double* __restrict__ rows, double* __restrict__ csc,
@@ -504,8 +504,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         S_n = sbs[sbc];
         meta_n = obs_meta[o];
         if (TRIAL) wfl_n = wf_c[o];
-        u_n = obs_uv[2 * (size_t)o];
-        v_n = obs_uv[2 * (size_t)o + 1];
+        const float2 z = reinterpret_cast<const float2*>(obs_uv)[o];   // the float pixel, widened exactly
+        u_n = (double)z.x;
+        v_n = (double)z.y;
         r_n = rc2[(size_t)sbc * 64 + lane];
     }
     {
@@ -575,8 +576,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             S_n = sbs[sbn];
             meta_n = obs_meta[on];
             if (TRIAL) wfl_n = wf_c[on];
-            u_n = obs_uv[2 * (size_t)on];
-            v_n = obs_uv[2 * (size_t)on + 1];
+            const float2 z = reinterpret_cast<const float2*>(obs_uv)[on];
+            u_n = (double)z.x;
+            v_n = (double)z.y;
             r_n = rc2[(size_t)sbn * 64 + lane];
         }
         // landmark records through LDS: lane -> its landmark's record (records LH_REC_LDS apart)
@@ -2799,7 +2801,7 @@ hipError_t lh_prepare_lin(int lds_limit) {
 }
 
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
-                         const lh_subbatch* sbs, const double* obs_uv, const uint32_t* obs_meta, double* rec,
+                         const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag, long nslots,
                          lh_params prm, int nrec,

@@ -117,6 +117,10 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         for (int64_t o = b; o < e; ++o) {
             const uint32_t l = w->obs_lm[o];
             bd |= w->obs_pose[o] >= (uint32_t)P || l >= (uint32_t)L || (w->obs_cam && w->obs_cam[o] >= ncam);
+            // the measurement is a cv::KeyPoint's float pixel widened (toVec2, algorithm.h:37): the device
+            // keeps it as a float, so a value a float cannot hold exactly (or a NaN) is a bad argument
+            const double u = w->obs_uv[2 * o], v = w->obs_uv[2 * o + 1];
+            bd |= !((double)(float)u == u) || !((double)(float)v == v);
             us |= l < prev;
             prev = l;
         }
@@ -366,7 +370,8 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
 // ---------------------------------------------------------------------------------------------
 // plan_fill
 // ---------------------------------------------------------------------------------------------
-void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool) {
+void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool, SlotsReady on_slots, void* user,
+               int batches) {
     const int P = pl.P, NC = pl.n_chunks;
     // chunks and their sub-batches' observation slots, one task per chunk
     auto chunk_task = [&](int ci) {
@@ -400,8 +405,8 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
             auto pad = [&](int64_t s0, int64_t s1) {   // unused slots: a meta word without LH_META_VALID
                 for (int64_t s = s0; s < s1; ++s) {
                     out.meta[s] = 0u;
-                    out.uv[2 * s] = 0.0;
-                    out.uv[2 * s + 1] = 0.0;
+                    out.uv[2 * s] = 0.0f;
+                    out.uv[2 * s + 1] = 0.0f;
                     out.obs_perm[s] = -1;
                 }
             };
@@ -414,8 +419,8 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
                     const uint32_t p = w->obs_pose[o];
                     const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
                     out.meta[slot] = LH_META(p, cam, slot_of[p], q);
-                    out.uv[2 * slot] = w->obs_uv[2 * o];
-                    out.uv[2 * slot + 1] = w->obs_uv[2 * o + 1];
+                    out.uv[2 * slot] = (float)w->obs_uv[2 * o];   // exact: checked in plan_structure
+                    out.uv[2 * slot + 1] = (float)w->obs_uv[2 * o + 1];
                     out.obs_perm[slot] = (int32_t)o;
                 }
                 pad(slot, base + ((int64_t)(q + 1) << lg));
@@ -423,8 +428,16 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
             pad(base + ((int64_t)n << lg), base + LH_SB_OBS);
         }
     };
-    if (pool) pool->run(NC, chunk_task);
-    else for (int ci = 0; ci < NC; ++ci) chunk_task(ci);
+    // chunks in launch order own contiguous sub-batches, hence contiguous slots: batch b of the chunk
+    // pass finishes slots [64 chunk_sb0[c0], 64 chunk_sb0[c1])
+    const int nbat = std::max(1, std::min(batches, NC));
+    for (int b = 0; b < nbat; ++b) {
+        const int c0 = (int)((int64_t)NC * b / nbat), c1 = (int)((int64_t)NC * (b + 1) / nbat);
+        if (pool) pool->run(c1 - c0, [&](int i) { chunk_task(c0 + i); });
+        else for (int ci = c0; ci < c1; ++ci) chunk_task(ci);
+        if (on_slots && c1 > c0)
+            on_slots(user, (int64_t)pl.chunk_sb0[c0] * LH_SB_OBS, (int64_t)pl.chunk_sb0[c1] * LH_SB_OBS);
+    }
 
     // reduce plan: pose pair b owns the pair rows pair_ptr[b] .. pair_ptr[b+1], one per chunk whose
     // window holds both poses, in launch order (k_reduce sums them in this order: a fixed,

@@ -83,7 +83,8 @@ struct PlanOut {
     lh_chunk* chunks;        // [n_chunks]
     lh_subbatch* sbs;        // [n_sb]
     uint32_t* meta;          // [n_slots]
-    double* uv;              // [2 n_slots]
+    float* uv;               // [2 n_slots] pixels as float: toVec2 of cv::KeyPoint::pt (algorithm.h:37),
+                             // so every measurement is a float (plan_structure rejects one that is not)
     int32_t* obs_perm;       // [n_slots] slot -> window obs (-1: padding)
     int32_t* lm_perm;        // [n_rec] record -> window landmark (-1: padding)
     uint32_t* items;         // [n_items] per chunk (launch order), per slot pair (s <= t): its pair row
@@ -95,6 +96,11 @@ struct PlanOut {
 // lh_status.  LH_E_BADARG for out-of-range indices, LH_E_UNSUPPORTED outside the envelope
 // (DESIGN.md "Limits"), LH_E_EMPTY mirrors problem.cpp:157-161.
 int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Plan& pl, Pool* pool);
-void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool);
+// on_slots(slot_begin, slot_end), if given, is called on the calling thread each time the observation
+// slots [slot_begin, slot_end) (meta, uv, obs_perm) are final, in ascending order, so the caller can
+// start copying them while the rest is filled; `batches` splits the chunk pass for that.
+using SlotsReady = void (*)(void* user, int64_t slot_begin, int64_t slot_end);
+void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool, SlotsReady on_slots = nullptr,
+               void* user = nullptr, int batches = 1);
 
 }  // namespace lh

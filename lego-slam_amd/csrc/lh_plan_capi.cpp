@@ -30,7 +30,7 @@ int lhp_plan_sizes(const lh_window* w, int chunk_lm, int threads, int64_t* sizes
 }
 
 int lhp_plan_fill(const lh_window* w, int chunk_lm, int threads, lh_chunk* chunks, lh_subbatch* sbs, uint32_t* meta,
-                  double* uv, int32_t* obs_perm, int32_t* lm_perm, uint32_t* pair_ptr, uint32_t* items,
+                  float* uv, int32_t* obs_perm, int32_t* lm_perm, uint32_t* pair_ptr, uint32_t* items,
                   uint16_t* pair_pq, uint32_t* rsmap, double* lm_xyz) {
     lh::Pool pool(threads > 0 ? threads : 1);
     lh::Plan pl;
@@ -70,7 +70,8 @@ int lhp_plan_time(const lh_window* w, int chunk_lm, int threads, int reps, doubl
     std::vector<lh_chunk> chunks;
     std::vector<lh_subbatch> sbs;
     std::vector<uint32_t> meta, items, rsmap;
-    std::vector<double> uv, lm;
+    std::vector<float> uv;
+    std::vector<double> lm;
     std::vector<int32_t> operm, lperm;
     std::vector<uint16_t> pq;
     double ts = 0.0, tf = 0.0;

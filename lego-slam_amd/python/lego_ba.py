@@ -514,7 +514,7 @@ def plan_window(w, chunk_lm=0, threads=1):
     _check(_pl().lhp_plan_sizes(C.byref(ref.s), chunk_lm, threads, _ptr(sizes), _ptr(tg)), "lhp_plan_sizes")
     n_chunks, n_sb, n_items, npairs, n_rec, n_slots, fixed_mask = (int(x) for x in sizes)
     out = dict(chunks=np.zeros(n_chunks, CHUNK_DT), sbs=np.zeros(n_sb, SUBBATCH_DT),
-               meta=np.zeros(n_slots, np.uint32), uv=np.zeros((n_slots, 2)), obs_perm=np.zeros(n_slots, np.int32),
+               meta=np.zeros(n_slots, np.uint32), uv=np.zeros((n_slots, 2), np.float32), obs_perm=np.zeros(n_slots, np.int32),
                lm_perm=np.zeros(n_rec, np.int32), pair_ptr=np.zeros(npairs + 1, np.uint32),
                items=np.zeros(n_items, np.uint32), pair_pq=np.zeros((npairs, 2), np.uint16),
                rsmap=np.zeros(npairs * 36, np.uint32), lm_xyz=np.zeros((ref.s.n_landmarks, 3)))

@@ -167,3 +167,17 @@ def test_pool_back_to_back_jobs():
     for n in (2, 3, 17):
         runs = 20000
         assert lego_ba.pool_stress(8, runs, n) == runs * n * (n - 1) // 2
+
+
+@pytest.mark.parametrize("bad", [0.1, float("nan"), 1e300])
+def test_pixels_must_be_float_values(bad):
+    """obs_uv is toVec2 of a cv::KeyPoint's float pixel (algorithm.h:37); the device keeps pixels as floats,
+    so a measurement no float holds exactly is refused rather than silently rounded."""
+    w = window("C1", seed=0)
+    assert np.array_equal(w["obs_uv"].astype(np.float32).astype(np.float64), w["obs_uv"])
+    lego_ba.plan_window(w)
+    w["obs_uv"] = w["obs_uv"].copy()
+    w["obs_uv"][17, 1] = bad
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(w)
+    assert e.value.status == lego_ba.LH_E_BADARG
