@@ -11,7 +11,10 @@
 
 // ---- envelope ---------------------------------------------------------------
 #define LH_PMAX 21            // poses per window solved in LDS (reduced system n = 6P <= 126, k_ctrl)
-#define LH_PMAX_WIN 64        // pose masks (planner, k_lin's fixed-pose mask) are 64-bit
+#define LH_PMAX_WIN 64        // the dense packed reduced-system layout (every pose pair a block) and the
+                              // LDL^T in global memory (k_ctrl_g, 6P <= 384 rows)
+#define LH_PMAX_ANY 256       // poses per window at all (PCG on the block-sparse reduced system, k_ctrl_p);
+                              // a landmark's observing poses must lie within 64 consecutive ones
 #define LH_UMAX 16            // distinct poses in one chunk window (6U <= 96 rows); the reference window is
                               // 15 keyframes (map.h:82), so any landmark of it fits one chunk window
 #define LH_TMAX 6             // 16-row MFMA tiles per window side
@@ -91,9 +94,11 @@ struct lh_rs_layout {
     int npairs, off_S, off_bs, off_bp, off_hd, off_sc, total;
 };
 
-LH_HD static inline lh_rs_layout lh_rs_make(int P) {
+// npairs: the blocks of S (every pose pair up to LH_PMAX_WIN poses, P (P + 1) / 2; past it the pairs
+// a landmark couples plus every diagonal block)
+LH_HD static inline lh_rs_layout lh_rs_make(int P, int npairs) {
     lh_rs_layout L;
-    L.npairs = P * (P + 1) / 2;
+    L.npairs = npairs;
     L.off_S = 0;
     L.off_bs = L.npairs * 36;
     L.off_bp = L.off_bs + 6 * P;
@@ -115,6 +120,8 @@ struct lh_ctrl {
 
 struct lh_params {
     int32_t P, n, ncam, max_iters, max_trials, strategy, guard, lambda_given;
+    int32_t npairs;         // blocks of the reduced system (lh_rs_make)
+    int32_t pad0_;
     int32_t ext_identity;   // bit c: camera c's extrinsic is exactly the identity
     int32_t solver;         // 0 LDL^T (Eigen LDLT, problem.cpp:420), 1 PCG (problem.cpp:422, :584-614)
     int32_t gate_mode;      // 0 reference Huber gate (base_edge.cpp:55); 1 diagnostic (residue taken as 0)

@@ -33,14 +33,15 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag,
-                         long nslots, lh_params prm, int nrec, uint64_t fixed_mask);
+                         long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits);
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
-                          lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS);
+                          lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS,
+                          const int32_t* brow_ptr, const uint32_t* brow_ent);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
@@ -262,6 +263,9 @@ struct lh_handle {
     DevBuf<double> d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_gS, d_rs_stage,
         d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
+    DevBuf<uint64_t> d_fixed;    // fixed-pose bits (Plan::fixed_bits)
+    DevBuf<int32_t> d_brow_ptr;  // the reduced system's block rows (Plan::brow_ptr / brow_ent, k_ctrl_p)
+    DevBuf<uint32_t> d_brow_ent;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
     // frontend pose-only batch (lh_estimate_pose)
     // inputs and outputs each packed into one arena, so a call is one upload and one download
@@ -389,8 +393,9 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     lh::Plan& pl = h->plan;
     int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
     if (st != LH_OK) return st;
-    // past LH_PMAX poses the reduced system is solved in global memory (k_ctrl_g): LDL^T only
-    if (pl.P > LH_PMAX && h->opt.linear_solver != LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
+    // past LH_PMAX poses the reduced system is solved in global memory: LDL^T by k_ctrl_g (dense, up
+    // to LH_PMAX_WIN poses) or PCG by k_ctrl_p (block-sparse, up to LH_PMAX_ANY)
+    if (pl.P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
     // a chunk window must fit one CU's LDS
     for (int T = 1; T <= LH_TMAX; ++T)
         if (pl.tgroup_begin[T + 1] > pl.tgroup_begin[T] && lh_lin_smem(T, pl.ncam) > (size_t)h->lds_limit)
@@ -399,7 +404,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     h->P = P; h->L = pl.L; h->O = pl.O; h->ncam = ncam;
     h->n_rec = pl.n_rec;
     h->n_slots = pl.n_slots;
-    h->LY = lh_rs_make(P);
+    h->LY = lh_rs_make(P, pl.npairs);
 
     // ---- device buffers (before the fill: its slot batches are copied as they complete) ----
     const size_t PT = (size_t)P * ncam * LH_PT;
@@ -425,7 +430,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
-    if (P > LH_PMAX) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once (its unused upper triangle)
+    if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
         const size_t ng = (size_t)((6 * P + 31) & ~31);
         const bool fresh = h->d_gA.n < ng * ng;
         HIPCHK(h->d_gA.ensure(ng * ng));
@@ -437,6 +442,9 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     }
     HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
     HIPCHK(h->d_maxd.ensure(1));
+    HIPCHK(h->d_fixed.ensure(pl.fixed_bits.size()));
+    HIPCHK(h->d_brow_ptr.ensure(pl.brow_ptr.size()));
+    HIPCHK(h->d_brow_ent.ensure(pl.brow_ent.size()));
     HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
     HIPCHK(h->d_ctrl.ensure(1));
     HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
@@ -495,6 +503,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     // ---- params ----
     lh_params& prm = h->prm;
     prm.P = P;
+    prm.npairs = pl.npairs;
     prm.n = 6 * P;
     prm.ncam = ncam;
     prm.max_iters = h->opt.max_iters;
@@ -533,6 +542,10 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(up(h->d_ptab_init.p, h->s_ptab.p, 2 * PT * sizeof(double)));
     HIPCHK(up(h->d_qt_init.p, h->s_qt.p, 24 * (size_t)P * sizeof(double)));
     HIPCHK(up(h->d_ext.p, h->s_ext.p, LH_EXT * (size_t)ncam * sizeof(double)));
+    // (pageable: a few words; hipMemcpyAsync stages them before returning)
+    HIPCHK(up(h->d_fixed.p, pl.fixed_bits.data(), pl.fixed_bits.size() * sizeof(uint64_t)));
+    HIPCHK(up(h->d_brow_ptr.p, pl.brow_ptr.data(), pl.brow_ptr.size() * sizeof(int32_t)));
+    HIPCHK(up(h->d_brow_ent.p, pl.brow_ent.data(), pl.brow_ent.size() * sizeof(uint32_t)));
     HIPCHK(hipEventRecord(h->ev_staging, s));
     h->staging_pending = true;
     if (sync) {
@@ -564,7 +577,7 @@ int launch_lin(lh_handle* h, int trial) {
         HIPCHK(lh_launch_lin(T, trial, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p, h->d_meta.p, h->d_rec.p,
                              h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p, h->d_rho.p, h->d_rows.p,
                              h->d_csc.p, h->d_items.p, h->d_wflag.p, (long)h->n_slots, h->prm, h->n_rec,
-                             h->plan.fixed_mask));
+                             h->d_fixed.p));
         DBGSYNC("k_lin");
     }
     return LH_OK;
@@ -618,10 +631,11 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     }
     {
         Prof pr(h, KC_CTRL);
-        if (h->P > LH_PMAX) HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
+        if (h->P > LH_PMAX && h->prm.solver == LH_SOLVER_LDLT)
+            HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p,
                               h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial,
-                              h->d_gA.p, h->d_gS.p));
+                              h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p, h->d_brow_ent.p));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -979,7 +993,8 @@ void lh_destroy(lh_handle* h) {
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
     h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_gS.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
-    h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release();
+    h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release(); h->d_fixed.release();
+    h->d_brow_ptr.release(); h->d_brow_ent.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();

@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
     double* __restrict__ edge_rho, double* __restrict__ rows, double* __restrict__ csc,
     const uint32_t* __restrict__ crow, uint8_t* __restrict__ wflag, long nslots,
-    lh_params prm, int nrec, uint64_t fixed_mask, int chunk_base) {
+    lh_params prm, int nrec, const uint64_t* __restrict__ fixed_bits, int chunk_base) {
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
 
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 
         const bool has = (meta & LH_META_VALID) != 0u;
         const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta);
-        const bool pfixed = (fixed_mask >> p) & 1ull;
+        const bool pfixed = (fixed_bits[p >> 6] >> (p & 63)) & 1ull;
         const bool live = has && !pfixed;
         const double* e = wext + cam * LH_EXT;
         const bool ext_id = (prm.ext_identity >> cam) & 1;
@@ -937,7 +937,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                                                double* __restrict__ maxd_out, lh_params prm, int n_chunks) {
     STAMP_DECL
     __shared__ double part[3][RW][64];
-    const lh_rs_layout LY = lh_rs_make(prm.P);
+    const lh_rs_layout LY = lh_rs_make(prm.P, prm.npairs);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // the stop flag and this block's pair words are independent loads: one round trip for all
     const int bq = b < LY.npairs ? b : 0;
@@ -1625,23 +1625,28 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
             for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
         }
     };
-    if (wave < 2 && lane < P) {
-        double up[6];
-        pose_step(lane, up);
-        const double th = d_twist_theta(up);
-        double sn, cs;
-        sincos(wave == 0 ? 0.5 * th : th, &sn, &cs);
-        s_trig[lane][2 * wave] = sn;
-        s_trig[lane][2 * wave + 1] = cs;
-    } else if (wave == 2 && lane < P) {
-        const double* Tc = &s_pm[cur][lane * 12];
-        const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
-        d_q_from_R(Rc, s_qT[lane]);
+    // (one lane per pose; past 64 poses the lanes take every 64th)
+    if (wave < 2) {
+        for (int pi = lane; pi < P; pi += 64) {
+            double up[6];
+            pose_step(pi, up);
+            const double th = d_twist_theta(up);
+            double sn, cs;
+            sincos(wave == 0 ? 0.5 * th : th, &sn, &cs);
+            s_trig[pi][2 * wave] = sn;
+            s_trig[pi][2 * wave + 1] = cs;
+        }
+    } else if (wave == 2) {
+        for (int pi = lane; pi < P; pi += 64) {
+            const double* Tc = &s_pm[cur][pi * 12];
+            const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
+            d_q_from_R(Rc, s_qT[pi]);
+        }
     }
     lds_barrier();
     CSTAMP(9);
-    if (wave == 0 && lane < P) {
-        const int pidx = lane;
+    if (wave == 0)
+    for (int pidx = lane; pidx < P; pidx += 64) {
         double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
         pose_step(pidx, up);
         d_se3_exp_trig(up, s_trig[pidx][0], s_trig[pidx][1], s_trig[pidx][2], s_trig[pidx][3], qe, te);
@@ -1696,7 +1701,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
-    const lh_rs_layout LY = lh_rs_make(P);
+    const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2097,7 +2102,7 @@ __global__ __launch_bounds__(64) void k_dense(const double* __restrict__ rs, con
     const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_reduce wrote no S blocks
     const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
     if (done || evo) return;
-    const lh_rs_layout LY = lh_rs_make(P);
+    const lh_rs_layout LY = lh_rs_make(P, P * (P + 1) / 2);   // the dense packed layout (P <= LH_PMAX_WIN)
     const int b = blockIdx.x, lane = threadIdx.x;
     const int p = pair_pq[2 * b], q = pair_pq[2 * b + 1];
     if (lane >= 36) return;
@@ -2125,7 +2130,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NG = (n + GNB - 1) & ~(GNB - 1);
-    const lh_rs_layout LY = lh_rs_make(P);
+    const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2261,6 +2266,186 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
+}
+
+// ============================================================================
+// k_ctrl_p: the controller with the reduced pose system solved by PCG (lh_options.linear_solver =
+// PCG) past LH_PMAX poses, up to LH_PMAX_ANY (windows of many keyframes).  One
+// 1024-thread workgroup.  Same LM bookkeeping (ctrl_lm_step) and pose tail (ctrl_pose_tail) as the
+// other controllers.  S stays in the packed blocks k_reduce wrote (rs: one 6x6 block per pose pair
+// that some landmark couples, plus every diagonal block; lh_plan.cpp), never densified: the PCG's
+// S p walks each pose's block row (Plan::brow_ent, ascending column) straight from the packed
+// blocks, 6 rows per pose, one thread per row.  The algorithm is the reference's Problem::PCGSolver
+// (problem.cpp:584-614) with its first-step bug fixed, as the oracle's pcg_solve restates it: Jacobi
+// preconditioner on S + lambda D, stop when ||r|| <= pcg_tol ||b|| (1e-6, :597), at most 2 n steps
+// after the first (:422); a zero diagonal preconditions with 0.  The dot products are fixed-order
+// workgroup reductions (wave butterflies, then the 16 wave sums in order), so a solve is bitwise
+// repeatable; the sums' order differs from the oracle's sequential loops (parity to tolerance).
+// ============================================================================
+#define PNMAX (6 * LH_PMAX_ANY)
+#define PRT ((PNMAX + CT - 1) / CT)     // rows per thread
+
+// fixed-order workgroup sum of one value per thread (every thread gets the total); red: 16 doubles
+__device__ __forceinline__ double wg_sum(double v, double* red, int lane, int wave) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) red[wave] = v;
+    lds_barrier();
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < CT / 64; ++w) t += red[w];
+    return t;
+}
+
+__global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
+                                               const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
+                                               const int32_t* __restrict__ brow_ptr, const uint32_t* __restrict__ brow_ent,
+                                               double* __restrict__ pose_mat, double* __restrict__ ptab,
+                                               const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
+                                               int mode, volatile int* __restrict__ host_done, int seq) {
+    __shared__ double pv[PNMAX], bpv[PNMAX], hdv[PNMAX], xs[PNMAX];
+    __shared__ int s_flags[4];
+    __shared__ double s_red[3][CT / 64], s_lam;
+    __shared__ double s_pm[2][LH_PMAX_ANY * 12];
+    __shared__ double s_trig[LH_PMAX_ANY][4], s_qT[LH_PMAX_ANY][4];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = prm.P, n = 6 * P;
+    const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
+
+    // ---------------- controller words, pose matrices, max |diag| (mode 0), the LM decision ----------------
+    double tchi = 0.0, sl = 0.0, ndg = 0.0;
+    CtrlWords cw{};
+    if (tid == 0) {
+        cw = ctrl_load(ctrl);
+        tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
+        sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+        ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
+    }
+    for (int i = tid; i < 24 * P; i += CT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
+    {
+        double mx = 0.0;
+        if (mode == 0)
+            for (int i = tid; i < n; i += CT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
+        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+        if (lane == 0) s_red[0][wave] = mx;
+    }
+    lds_barrier();
+    if (tid == 0) {
+        double mdiag = 0.0;
+        if (mode == 0) {
+            for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[0][w]);
+            mdiag = fmax(*maxd_in, mdiag);
+        }
+        int done, accept, cur;
+        double lam_n;
+        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        s_flags[0] = done;
+        s_flags[1] = accept;
+        s_flags[2] = cur;
+        s_lam = lam_n;
+    }
+    lds_barrier();
+    const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
+    if (done) return;
+    const double lambda = s_lam;
+
+    // ---------------- the chosen system (the candidate's on accept, committed on it; else the committed one) ----------------
+    const double* __restrict__ src = accept ? rs_stage : rs_commit;
+    if (accept)
+        for (int i = tid; i < LY.total; i += CT) rs_commit[i] = rs_stage[i];
+    const double* __restrict__ Sb = src + LY.off_S;
+    // per thread rows r = tid + CT u: damped diagonal, Jacobi preconditioner, right-hand side
+    double dr[PRT], minv[PRT], x[PRT], rr[PRT], z[PRT], pp[PRT];
+    int e0[PRT], e1[PRT];
+#pragma unroll
+    for (int u = 0; u < PRT; ++u) {
+        const int r = tid + CT * u;
+        const bool in = r < n;
+        const int p = in ? r / 6 : 0, a = r - 6 * p;
+        e0[u] = in ? brow_ptr[p] : 0;
+        e1[u] = in ? brow_ptr[p + 1] : 0;
+        double sd = 0.0;
+        for (int e = e0[u]; e < e1[u]; ++e) {   // the diagonal block: the entry whose column is p itself
+            const uint32_t en = brow_ent[e];
+            if ((int)((en >> 1) & 0xFFF) == p && !(en & 1u)) sd = Sb[(size_t)(en >> 13) * 36 + 7 * a];
+        }
+        dr[u] = (prm.strategy == 0) ? sd + lambda : sd + lambda * sd;   // problem.cpp:408-418
+        minv[u] = (in && dr[u] != 0.0) ? 1.0 / dr[u] : 0.0;
+        rr[u] = in ? src[LY.off_bs + r] : 0.0;
+        x[u] = 0.0;
+        z[u] = minv[u] * rr[u];
+        pp[u] = z[u];
+        if (in) { bpv[r] = src[LY.off_bp + r]; hdv[r] = src[LY.off_hd + r]; }
+    }
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < PRT; ++u) { t0 += rr[u] * z[u]; t1 += rr[u] * rr[u]; }
+    double rz = wg_sum(t0, s_red[0], lane, wave);
+    const double bb = wg_sum(t1, s_red[1], lane, wave);
+    const double thr = prm.pcg_tol * sqrt(bb);
+    const int maxit = prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n;
+    int steps = 0;
+    if (bb > 0.0) {
+        for (;;) {
+#pragma unroll
+            for (int u = 0; u < PRT; ++u)
+                if (tid + CT * u < n) pv[tid + CT * u] = pp[u];
+            lds_barrier();
+            // w = (S + lambda D) p, row by row over the block row, columns ascending
+            double w[PRT], pw = 0.0;
+#pragma unroll
+            for (int u = 0; u < PRT; ++u) {
+                const int r = tid + CT * u;
+                const int p = r / 6, a = r - 6 * p;
+                double acc = 0.0;
+                for (int e = e0[u]; e < e1[u]; ++e) {
+                    const uint32_t en = brow_ent[e];
+                    const int q = (int)((en >> 1) & 0xFFF);
+                    const double* blk = Sb + (size_t)(en >> 13) * 36;
+                    const double* pq = pv + 6 * q;
+                    if (en & 1u) {   // block (q, p) read transposed: S(r, 6q + c) = blk(c, a)
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) acc += blk[6 * c + a] * pq[c];
+                    } else if (q == p) {   // the diagonal block, its diagonal damped
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) acc += (c == a ? dr[u] : blk[6 * a + c]) * pq[c];
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) acc += blk[6 * a + c] * pq[c];
+                    }
+                }
+                w[u] = acc;
+                pw += pp[u] * acc;
+            }
+            const double alpha = rz / wg_sum(pw, s_red[2], lane, wave);
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int u = 0; u < PRT; ++u) {
+                x[u] += alpha * pp[u];
+                rr[u] -= alpha * w[u];
+                z[u] = minv[u] * rr[u];
+                a0 += rr[u] * rr[u];
+                a1 += rr[u] * z[u];
+            }
+            const double rrn = wg_sum(a0, s_red[0], lane, wave);
+            const double rzn = wg_sum(a1, s_red[1], lane, wave);
+            ++steps;
+            if (!(sqrt(rrn) > thr) || steps >= maxit + 1) break;   // also stops on NaN
+            const double beta = rzn / rz;
+            rz = rzn;
+#pragma unroll
+            for (int u = 0; u < PRT; ++u) pp[u] = beta * pp[u] + z[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PRT; ++u) {
+        const int r = tid + CT * u;
+        if (r < n) { xs[r] = x[u]; dxp[r] = x[u]; }
+    }
+    if (tid == 0) ctrl->pcg_iters += steps;
+    lds_barrier();
+    ctrl_pose_tail<LH_PMAX_ANY, CT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red[0], s_pm, s_trig, s_qT, pose_mat,
+                                   ptab, ext);
 }
 
 // ============================================================================
@@ -2805,14 +2990,14 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag, long nslots,
                          lh_params prm, int nrec,
-                         uint64_t fixed_mask) {
+                         const uint64_t* fixed_bits) {
     if (nchunks <= 0) return hipSuccess;
     dim3 g(nchunks), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
         const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
         hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
-                           edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_mask, chunk_base);             \
+                           edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base);             \
     } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
@@ -2836,7 +3021,7 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks) {
-    const int npairs = prm.P * (prm.P + 1) / 2;
+    const int npairs = prm.npairs;
     hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, rows, csc, pair_ptr, pair_pq, ctrl,
                        rs_stage, maxd, prm, n_chunks);
     return hipGetLastError();
@@ -2852,8 +3037,12 @@ hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
-                          int* host_done, int seq, double* gA, const double* gS) {
-    if (prm.P > LH_PMAX)
+                          int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
+                          const uint32_t* brow_ent) {
+    if (prm.P > LH_PMAX && prm.solver == 1)
+        hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent, pose_mat,
+                           ptab, ext, dxp, prm, mode, (volatile int*)host_done, seq);
+    else if (prm.P > LH_PMAX)
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)

@@ -87,6 +87,20 @@ inline int popc(uint64_t m) { return __builtin_popcountll(m); }
 inline int chunk_tiles(uint64_t mask) { return (6 * popc(mask) + 15) / 16; }
 inline int pow2log(int k) { int g = 1, lg = 0; while (g < k) { g <<= 1; ++lg; } return lg; }
 
+// block index of pose pair (p, q), p <= q: the dense packed order up to LH_PMAX_WIN poses, else the
+// position in the sorted pair list (binary search)
+inline int pair_index(const Plan& pl, int p, int q) {
+    if (pl.P <= LH_PMAX_WIN) return p * pl.P - (p * (p - 1)) / 2 + (q - p);
+    const uint32_t key = (uint32_t)p << 16 | (uint32_t)q;
+    int lo = 0, hi = pl.npairs;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t k = (uint32_t)pl.pair_list[2 * mid] << 16 | pl.pair_list[2 * mid + 1];
+        if (k <= key) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -129,12 +143,13 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     });
     if (bad.load()) return LH_E_BADARG;
     if (!allow_empty && (O == 0 || (P + L) == 0)) return LH_E_EMPTY;   // problem.cpp:157-161
-    if (P > LH_PMAX_WIN) return LH_E_UNSUPPORTED;   // 64-bit pose masks (P > LH_PMAX: k_ctrl_g, global memory)
+    if (P > LH_PMAX_ANY) return LH_E_UNSUPPORTED;   // the reduced solve's LDS vectors (k_ctrl_p)
     if (O >= (int64_t)1 << 30) return LH_E_UNSUPPORTED;                 // int32 slot indices
-    pl.fixed_mask = 0;
+    pl.fixed_bits.assign((size_t)(P + 63) / 64 + 1, 0ull);
     if (w->pose_fixed)
         for (int p = 0; p < P; ++p)
-            if (w->pose_fixed[p]) pl.fixed_mask |= 1ull << p;
+            if (w->pose_fixed[p]) pl.fixed_bits[p >> 6] |= 1ull << (p & 63);
+    pl.fixed_mask = pl.fixed_bits[0];
 
     stage(0);
     // ---- landmark-major CSR ----
@@ -160,6 +175,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     stage(1);
     // ---- per landmark: ascending pose order, pose mask, envelope checks ----
     pl.lm_mask.assign((size_t)L, 0ull);
+    pl.lm_base.assign((size_t)L, 0);
     std::atomic<int> unsup{0};
     parallel_range(pool, L, 4096, [&](int64_t b, int64_t e) {
         bool us = false;
@@ -174,14 +190,20 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
                 while (j >= 0 && (w->obs_pose[s[j]] > pv || (w->obs_pose[s[j]] == pv && s[j] > v))) { s[j + 1] = s[j]; --j; }
                 s[j + 1] = v;
             }
+            // observing poses relative to the first one (ascending): bit i = pose base + i; a landmark
+            // must be seen within 64 consecutive keyframes (a sliding window's are, map.h:82)
             uint64_t m = 0;
+            const int base = k > 0 ? (int)w->obs_pose[s[0]] : 0;
             for (int64_t i = 0; i < k; ++i) {
-                const uint64_t bit = 1ull << w->obs_pose[s[i]];
+                const uint32_t rel = w->obs_pose[s[i]] - (uint32_t)base;
+                if (rel >= 64) { us = true; break; }
+                const uint64_t bit = 1ull << rel;
                 if (m & bit) us = true;   // two edges landmark -> same pose (DESIGN.md "Limits")
                 m |= bit;
             }
             if (popc(m) > LH_UMAX) us = true;
             pl.lm_mask[l] = m;
+            pl.lm_base[l] = base;
         }
         if (us) unsup.store(1);
     });
@@ -192,10 +214,11 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     //      counting sort (per-block histograms, prefix in bucket-major / block-minor order, so each
     //      bucket keeps landmark order), then a stable sort by mask inside the buckets that mix masks ----
     {
-        const int nb = std::max(P, 1) * std::max(P, 1);
+        // bucket (first pose, span): the order of (first pose, last pose), with P x 64 buckets
+        const int nb = std::max(P, 1) * 64;
         auto bucket = [&](int l) {
-            const uint64_t m = pl.lm_mask[l];
-            return __builtin_ctzll(m) * P + (63 - __builtin_clzll(m));
+            const uint64_t m = pl.lm_mask[l];   // bit 0 is the first pose
+            return pl.lm_base[l] * 64 + (63 - __builtin_clzll(m));
         };
         const int threads = pool ? pool->size() : 1;
         const int nblk = std::max(1, std::min(4 * threads, (L + 8191) / 8192));
@@ -261,16 +284,19 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     // landmarks while it holds < 8 and (n + 1) << lg <= 64 (landmark l owns the aligned lane group
     // [l*G, l*G + k_l) of its 64 slots, G = 2^lg the largest pow2ceil(k) in the sub-batch).
     std::vector<uint64_t> om((size_t)Lact);
+    std::vector<int32_t> ob((size_t)Lact);
     std::vector<uint8_t> olg((size_t)Lact);
     parallel_range(pool, Lact, 4096, [&](int64_t b, int64_t e) {
         for (int64_t i = b; i < e; ++i) {
             const int l = pl.order[i];
             om[i] = pl.lm_mask[l];
+            ob[i] = pl.lm_base[l];
             olg[i] = (uint8_t)pow2log((int)(pl.lm_ptr[l + 1] - pl.lm_ptr[l]));
         }
     });
     pl.chunk_lm0.clear();
     pl.chunk_mask.clear();
+    pl.chunk_base.clear();
     std::vector<int32_t> c_sb0;              // per chunk (creation order): its first sub-batch
     std::vector<int32_t> t_first;            // sub-batches in creation order: first position
     std::vector<uint8_t> t_lg;
@@ -282,17 +308,21 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         sb_n = 0;
     };
     for (int i = 0; i < Lact; ++i) {
-        const uint64_t m = om[i];
-        const bool fresh = pl.chunk_lm0.empty() || (i - pl.chunk_lm0.back()) >= chunk_lm ||
+        // the landmark's mask relative to the current chunk's base (landmarks come in ascending first
+        // pose, so the base is the chunk's first pose); past 64 poses from the base it starts a chunk
+        const int sh = pl.chunk_lm0.empty() ? 64 : ob[i] - pl.chunk_base.back();
+        const uint64_t m = (sh < 64 && (om[i] >> (63 - sh)) <= 1) ? om[i] << sh : 0ull;
+        const bool fresh = pl.chunk_lm0.empty() || m == 0 || (i - pl.chunk_lm0.back()) >= chunk_lm ||
                            popc(pl.chunk_mask.back() | m) > LH_UMAX ||
                            chunk_tiles(pl.chunk_mask.back() | m) > std::max(chunk_tiles(pl.chunk_mask.back()), chunk_tiles(m));
         if (fresh) {
             close_sb();
             pl.chunk_lm0.push_back(i);
             pl.chunk_mask.push_back(0ull);
+            pl.chunk_base.push_back(ob[i]);
             c_sb0.push_back((int32_t)t_first.size());
         }
-        pl.chunk_mask.back() |= m;
+        pl.chunk_mask.back() |= fresh ? om[i] : m;
         const int lgn = std::max(sb_lg, (int)olg[i]);
         if (sb_n > 0 && sb_n < LH_SB_LM && ((sb_n + 1) << lgn) <= LH_SB_OBS) {
             ++sb_n;
@@ -343,17 +373,54 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     pl.sb_lm0[pl.n_sb] = Lact;   // never read as a start: the last sub-batch ends at its chunk's end
 
     stage(5);
-    // ---- reduce plan sizes: per pose pair, the chunks touching it ----
-    pl.npairs = P * (P + 1) / 2;
+    // ---- reduce plan sizes: the reduced system's blocks (pose pairs p <= q) and, per block, the
+    //      chunks touching it.  Up to LH_PMAX_WIN poses every pair has a block (the dense packed layout
+    //      k_ctrl / k_ctrl_g scatter from); past it only the pairs some chunk touches, plus every
+    //      diagonal block (S is then block-sparse: a landmark couples poses within its 64-pose span) ----
+    pl.pair_list.clear();
+    if (P <= LH_PMAX_WIN) {
+        for (int p = 0; p < P; ++p)
+            for (int q = p; q < P; ++q) { pl.pair_list.push_back((uint16_t)p); pl.pair_list.push_back((uint16_t)q); }
+    } else {
+        std::vector<uint32_t> keys;
+        for (int p = 0; p < P; ++p) keys.push_back((uint32_t)p << 16 | (uint32_t)p);
+        for (int ci = 0; ci < NC; ++ci) {
+            const int c = pl.corder[ci], base = pl.chunk_base[c];
+            for (uint64_t a = pl.chunk_mask[c]; a; a &= a - 1)
+                for (uint64_t b = a; b; b &= b - 1)
+                    keys.push_back((uint32_t)(base + __builtin_ctzll(a)) << 16 | (uint32_t)(base + __builtin_ctzll(b)));
+        }
+        std::sort(keys.begin(), keys.end());
+        keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+        for (uint32_t k : keys) { pl.pair_list.push_back((uint16_t)(k >> 16)); pl.pair_list.push_back((uint16_t)(k & 0xFFFF)); }
+    }
+    pl.npairs = (int)(pl.pair_list.size() / 2);
+    // block rows: pairs (p', r), p' < r, read transposed (ascending p'), then pairs (r, q'), q' >= r
+    pl.brow_ptr.assign((size_t)P + 1, 0);
+    for (int b = 0; b < pl.npairs; ++b) {
+        const int p = pl.pair_list[2 * b], q = pl.pair_list[2 * b + 1];
+        pl.brow_ptr[p + 1]++;
+        if (q != p) pl.brow_ptr[q + 1]++;
+    }
+    for (int p = 0; p < P; ++p) pl.brow_ptr[p + 1] += pl.brow_ptr[p];
+    pl.brow_ent.assign((size_t)pl.brow_ptr[P], 0u);
+    {
+        std::vector<int32_t> fill(pl.brow_ptr.begin(), pl.brow_ptr.end() - 1);
+        for (int b = 0; b < pl.npairs; ++b) {   // transposed entries first: every pair (p', r) precedes (r, .)
+            const int p = pl.pair_list[2 * b], q = pl.pair_list[2 * b + 1];
+            if (q != p) pl.brow_ent[fill[q]++] = (uint32_t)b << 13 | (uint32_t)p << 1 | 1u;
+        }
+        for (int b = 0; b < pl.npairs; ++b) {
+            const int p = pl.pair_list[2 * b], q = pl.pair_list[2 * b + 1];
+            pl.brow_ent[fill[p]++] = (uint32_t)b << 13 | (uint32_t)q << 1;
+        }
+    }
     pl.pair_ptr.assign((size_t)pl.npairs + 1, 0u);
     for (int ci = 0; ci < NC; ++ci) {
-        const uint64_t m = pl.chunk_mask[pl.corder[ci]];
-        for (uint64_t a = m; a; a &= a - 1) {
-            const int p = __builtin_ctzll(a);
-            for (uint64_t b = a; b; b &= b - 1) {
-                const int q = __builtin_ctzll(b);
-                pl.pair_ptr[p * P - (p * (p - 1)) / 2 + (q - p) + 1]++;
-            }
+        const int c = pl.corder[ci], base = pl.chunk_base[c];
+        for (uint64_t a = pl.chunk_mask[c]; a; a &= a - 1) {
+            const int p = base + __builtin_ctzll(a);
+            for (uint64_t b = a; b; b &= b - 1) pl.pair_ptr[pair_index(pl, p, base + __builtin_ctzll(b)) + 1]++;
         }
     }
     for (int b = 0; b < pl.npairs; ++b) pl.pair_ptr[b + 1] += pl.pair_ptr[b];
@@ -381,10 +448,15 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
         std::memset(&ck, 0, sizeof(ck));
         ck.U = (uint8_t)popc(m);
         ck.T = (uint8_t)chunk_tiles(m);
-        int slot_of[64] = {0};
+        const int pbase = pl.chunk_base[c];
+        int slot_of[64] = {0};   // by pose - pbase
         {
             int s = 0;
-            for (uint64_t a = m; a; a &= a - 1) { const int p = __builtin_ctzll(a); ck.pose[s] = (uint16_t)p; slot_of[p] = s++; }
+            for (uint64_t a = m; a; a &= a - 1) {
+                const int r = __builtin_ctzll(a);
+                ck.pose[s] = (uint16_t)(pbase + r);
+                slot_of[r] = s++;
+            }
         }
         ck.sb_begin = (uint32_t)pl.chunk_sb0[ci];
         ck.sb_end = (uint32_t)pl.chunk_sb0[ci + 1];
@@ -418,7 +490,7 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
                     const int64_t o = pl.csr[r];
                     const uint32_t p = w->obs_pose[o];
                     const uint32_t cam = w->obs_cam ? w->obs_cam[o] : 0;
-                    out.meta[slot] = LH_META(p, cam, slot_of[p], q);
+                    out.meta[slot] = LH_META(p, cam, slot_of[p - (uint32_t)pbase], q);
                     out.uv[2 * slot] = (float)w->obs_uv[2 * o];   // exact: checked in plan_structure
                     out.uv[2 * slot + 1] = (float)w->obs_uv[2 * o + 1];
                     out.obs_perm[slot] = (int32_t)o;
@@ -446,28 +518,25 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
     {
         std::vector<uint32_t> cur(pl.pair_ptr.begin(), pl.pair_ptr.end() - 1);
         for (int ci = 0; ci < NC; ++ci) {
-            const uint64_t m = pl.chunk_mask[pl.corder[ci]];
+            const int c = pl.corder[ci], base = pl.chunk_base[c];
             int ps[64], U = 0;
-            for (uint64_t a = m; a; a &= a - 1) ps[U++] = __builtin_ctzll(a);
+            for (uint64_t a = pl.chunk_mask[c]; a; a &= a - 1) ps[U++] = base + __builtin_ctzll(a);
             uint32_t k = pl.chunk_ib[ci];
             for (int s = 0; s < U; ++s)
-                for (int t = s; t < U; ++t) {
-                    const int p = ps[s], q = ps[t];
-                    const int b = p * P - (p * (p - 1)) / 2 + (q - p);
-                    out.items[k++] = cur[b]++;
-                }
+                for (int t = s; t < U; ++t) out.items[k++] = cur[pair_index(pl, ps[s], ps[t])]++;
         }
     }
-    for (int p = 0, b = 0; p < P; ++p)
-        for (int q = p; q < P; ++q, ++b) { out.pair_pq[2 * b] = (uint16_t)p; out.pair_pq[2 * b + 1] = (uint16_t)q; }
+    std::memcpy(out.pair_pq, pl.pair_list.data(), pl.pair_list.size() * sizeof(uint16_t));
     // reduced-system element map for k_ctrl's register scatter: S element of pose pair (pi, pj),
     // pi <= pj, row a, col b -> global rows 6 pi + a, 6 pj + b (9 bits each), diagonal-block flag
-    for (int pi = 0, blk = 0; pi < P; ++pi)
-        for (int pj = pi; pj < P; ++pj, ++blk)
+    // (only the dense layouts, P <= LH_PMAX_WIN, are scattered; 9 bits hold rows < 512)
+    if (P <= LH_PMAX_WIN)
+        for (int blk = 0; blk < pl.npairs; ++blk) {
+            const int pi = pl.pair_list[2 * blk], pj = pl.pair_list[2 * blk + 1];
             for (int a = 0; a < 6; ++a)
                 for (int b = 0; b < 6; ++b)
-                    out.rsmap[(size_t)blk * 36 + 6 * a + b] =
-                        LH_RSMAP(6 * pi + a, 6 * pj + b, pi == pj);
+                    out.rsmap[(size_t)blk * 36 + 6 * a + b] = LH_RSMAP(6 * pi + a, 6 * pj + b, pi == pj);
+        }
     parallel_range(pool, 3 * (int64_t)pl.L, 1 << 16, [&](int64_t b, int64_t e) {
         if (e > b) std::memcpy(out.lm_xyz + b, w->lm_xyz + b, (size_t)(e - b) * sizeof(double));
     });

@@ -62,14 +62,22 @@ struct Plan {
     int n_rec = 0;                      // landmark records (8 per sub-batch)
     int64_t n_slots = 0;                // observation slots (64 per sub-batch)
     int tgroup_begin[LH_TMAX + 2] = {0};
-    uint64_t fixed_mask = 0;            // bit p: pose p is fixed
+    uint64_t fixed_mask = 0;            // bit p: pose p < 64 is fixed (fixed_bits[0])
+    std::vector<uint64_t> fixed_bits;   // [(P + 63) / 64] bit p % 64 of word p / 64: pose p is fixed
+    std::vector<uint16_t> pair_list;    // [2 npairs] (p, q), p <= q, of each reduced-system block
+    // the blocks by block row (the PCG's S p, k_ctrl_p): row p holds, in ascending column q, entry
+    // (b << 13) | (q << 1) | t for block b = pair (min(p, q), max(p, q)), t = 1 where it is read transposed
+    std::vector<int32_t> brow_ptr;      // [P + 1]
+    std::vector<uint32_t> brow_ent;     // [2 npairs - P]
     // ---- internal (reused across windows) ----
     std::vector<int64_t> lm_ptr;        // [L+1] CSR over landmarks
     std::vector<int64_t> csr;           // [O] window obs, landmark-major, ascending pose
-    std::vector<uint64_t> lm_mask;      // [L] observing-pose mask
+    std::vector<uint64_t> lm_mask;      // [L] observing-pose mask, bit i = pose lm_base + i
+    std::vector<int32_t> lm_base;       // [L] first observing pose
     std::vector<int32_t> order;         // [L_act] landmarks with edges, span order
     std::vector<int32_t> chunk_lm0;     // [n_chunks + 1] chunk c owns order[chunk_lm0[c] .. chunk_lm0[c+1])
-    std::vector<uint64_t> chunk_mask;   // [n_chunks] union pose mask
+    std::vector<uint64_t> chunk_mask;   // [n_chunks] union pose mask, bit i = pose chunk_base + i
+    std::vector<int32_t> chunk_base;    // [n_chunks]
     std::vector<int32_t> chunk_sb0;     // [n_chunks + 1] sub-batch prefix (chunks in T order)
     std::vector<int32_t> corder;        // [n_chunks] launch order (grouped by T) -> chunk
     std::vector<int32_t> sb_lm0;        // [n_sb + 1] sub-batch -> first position in order[]

@@ -386,12 +386,16 @@ def test_large_window_default_family_gate1():
 
 
 def test_window_envelope_edges():
-    """65 keyframes is past the 64-bit pose masks; PCG past 21 keyframes is not offered."""
+    """Past 64 keyframes the dense LDLT (k_ctrl_g) is not offered (PCG is, tests/test_pcg.py); past 256
+    keyframes nothing is."""
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.Solver().solve(lego_ba.generate_window(P=65, L=500, k=8, seed=4))
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
+    w = lego_ba.generate_window(P=256, L=500, k=8, seed=4)
+    w["pose_Tcw"] = np.vstack([w["pose_Tcw"], w["pose_Tcw"][-1:]])
+    w["n_poses"] = 257
     with pytest.raises(lego_ba.LhError) as e:
-        lego_ba.Solver(linear_solver=lego_ba.LH_SOLVER_PCG).solve(lego_ba.generate_window(P=22, L=500, k=8, seed=4))
+        lego_ba.Solver(linear_solver=lego_ba.LH_SOLVER_PCG).solve(w)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
 
 

@@ -59,7 +59,16 @@ def check_plan(w, pl):
     # reduce plan: one pair row per (chunk, slot pair of its window); pair b owns rows
     # ptr[b] .. ptr[b+1], in launch order; items[] maps each chunk's slot pairs to their rows
     items, ptr, pq = pl["items"].astype(np.int64), pl["pair_ptr"].astype(np.int64), pl["pair_pq"]
-    assert len(pq) == P * (P + 1) // 2 and ptr[-1] == len(items)
+    if P <= 64:   # the dense packed layout: every pose pair (p <= q) a block
+        assert len(pq) == P * (P + 1) // 2
+        bidx = lambda p, q: p * P - p * (p - 1) // 2 + (q - p)  # noqa: E731
+    else:         # block-sparse: the pairs some chunk couples plus every diagonal block, sorted
+        keys = [(int(a), int(b)) for a, b in pq]
+        assert keys == sorted(set(keys)) and all(a <= b for a, b in keys)
+        assert {(p, p) for p in range(P)} <= set(keys)
+        where = {k: i for i, k in enumerate(keys)}
+        bidx = lambda p, q: where[(p, q)]  # noqa: E731
+    assert ptr[-1] == len(items)
     U = ch["U"].astype(np.int64)
     expect = U * (U + 1) // 2
     assert len(items) == expect.sum()
@@ -72,7 +81,7 @@ def check_plan(w, pl):
         for s in range(U[ci]):
             for t in range(s, U[ci]):
                 p, q = int(ch["pose"][ci, s]), int(ch["pose"][ci, t])
-                b = p * P - p * (p - 1) // 2 + (q - p)
+                b = bidx(p, q)
                 r = items[k]
                 assert ptr[b] <= r < ptr[b + 1] and tuple(pq[b]) == (p, q)
                 chunk_of_row[r] = ci
@@ -142,12 +151,23 @@ def test_plan_envelope_and_errors():
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.plan_window(wide)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > 16 poses per landmark
-    check_plan(lego_ba.generate_window(P=64, L=300, k=8, seed=1), lego_ba.plan_window(
-        lego_ba.generate_window(P=64, L=300, k=8, seed=1), threads=2))   # 64 poses: 64-bit masks
-    p65 = lego_ba.generate_window(P=65, L=50, k=8, seed=1)
+    for P in (64, 65, 128, 256):   # dense pair layout up to 64 poses, block-sparse past it
+        wp = lego_ba.generate_window(P=P, L=40 * P, k=8, seed=1)
+        check_plan(wp, lego_ba.plan_window(wp, threads=2))
+    p257 = lego_ba.generate_window(P=256, L=50, k=8, seed=1)
+    p257["pose_Tcw"] = np.vstack([p257["pose_Tcw"], p257["pose_Tcw"][-1:]])   # an unobserved 257th pose
+    p257["n_poses"] = 257
     with pytest.raises(lego_ba.LhError) as e:
-        lego_ba.plan_window(p65)
-    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > LH_PMAX_WIN poses
+        lego_ba.plan_window(p257)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # > LH_PMAX_ANY poses
+    span = lego_ba.generate_window(P=100, L=20, k=8, seed=1)
+    span["obs_pose"] = span["obs_pose"].copy()
+    first = np.flatnonzero(span["obs_lm"] == 0)
+    span["obs_pose"][first[-1]] = 99                              # landmark 0 seen by poses 0.. and 99
+    assert span["obs_pose"][first[0]] < 99 - 63
+    with pytest.raises(lego_ba.LhError) as e:
+        lego_ba.plan_window(span)
+    assert e.value.status == lego_ba.LH_E_UNSUPPORTED           # a landmark spans > 64 keyframes
 
 
 def test_plan_unobserved_landmarks_and_fixed_mask():
