@@ -455,6 +455,28 @@ def main():
                          "iterations_per_solve": i64 / 5, "trials_per_solve": t64 / 5,
                          "k_ctrl_g_ms_per_trial": round(k64["k_ctrl"][1] / max(1, k64["k_ctrl"][0]), 4),
                          "kernels_ms_per_solve_event_bracketed": {k: round(v[1] / 2, 4) for k, v in k64.items()}}
+    # a 128-keyframe window of C3's size through the PCG reduced solve (k_ctrl_p,
+    # S p over the block-sparse pose-pair blocks), against the oracle's PCG below
+    w128 = lego_ba.generate_window(P=128, L=50000, k=8, seed=3, **dict(STABLE, outlier_frac=0.0))
+    f128 = np.zeros(128, np.uint8)
+    f128[0] = 1
+    w128["pose_fixed"] = f128
+    s128 = lego_ba.Solver(device=local, linear_solver=lego_ba.LH_SOLVER_PCG)
+    s128.upload(w128)
+    s128.solve_resident()
+    d128, i128, t128, l128 = time_solves(s128, 3, barrier)
+    s128.set_profiling(True)
+    s128.kernel_stats_reset()
+    r128 = s128.solve_resident()
+    k128 = s128.kernel_stats()
+    s128.set_profiling(False)
+    s128.close()
+    out["p128_window_pcg"] = {"keyframes": 128, "landmarks": 50000, "obs": len(w128["obs_pose"]),
+                              "iterations_per_s": round(i128 / d128, 3), "ms_per_solve": round(d128 / 3 * 1e3, 3),
+                              "iterations_per_solve": i128 / 3, "trials_per_solve": t128 / 3,
+                              "pcg_steps_per_trial": round(r128["pcg_iterations"] / max(1, r128["trials"]), 1),
+                              "k_ctrl_p_ms_per_trial": round(k128["k_ctrl"][1] / max(1, k128["k_ctrl"][0]), 4),
+                              "kernels_ms_per_solve_event_bracketed": {k: round(v[1], 4) for k, v in k128.items()}}
     # the frontend's pose-only LM (Frontend::EstimateCurrentPose): one frame the way
     # the reference calls it (frontend_lego.cpp:157, once per frame), and a batch of frames
     import frames
@@ -556,6 +578,14 @@ def main():
         out["p64_window"]["oracle_iterations"] = o64["iterations"]
         out["p64_window"]["cpu_oracle_iterations_per_s"] = round(o64["iterations"] / c64, 3)
         out["p64_window"]["cpu_oracle_threads"] = threads
+        t0 = time.perf_counter()
+        o128 = oracle_bind.solve(w128, n_threads=threads, linear_solver=1, lib_path=lib_path)
+        c128 = time.perf_counter() - t0
+        pc = out["p128_window_pcg"]
+        pc["chi2_rel_vs_oracle_pcg"] = abs(l128["chi2_final"] - o128["chi2_final"]) / o128["chi2_final"]
+        pc["oracle_iterations"] = o128["iterations"]
+        pc["cpu_oracle_iterations_per_s"] = round(o128["iterations"] / c128, 3)
+        pc["cpu_oracle_threads"] = threads
         t0 = time.perf_counter()
         ol = oracle_bind.lk_track(li1, li2, lk1, kp2_init=lki, lib_path=lib_path)
         out["lk_optical_flow"]["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
