@@ -121,7 +121,7 @@ struct lh_ctrl {
 struct lh_params {
     int32_t P, n, ncam, max_iters, max_trials, strategy, guard, lambda_given;
     int32_t npairs;         // blocks of the reduced system (lh_rs_make)
-    int32_t pad0_;
+    int32_t ext_rot_identity;   // bit c: camera c's extrinsic rotation is exactly the identity
     int32_t ext_identity;   // bit c: camera c's extrinsic is exactly the identity
     int32_t solver;         // 0 LDL^T (Eigen LDLT, problem.cpp:420), 1 PCG (problem.cpp:422, :584-614)
     int32_t gate_mode;      // 0 reference Huber gate (base_edge.cpp:55); 1 diagnostic (residue taken as 0)

@@ -238,22 +238,32 @@ struct EdgeEval {
     double Jl[6];    // 2 x 3
 };
 
-// residual_ = z - pi(K (ext (T X))), pi(q) = q / (q_z + 1e-18)   (lego_types.h:200-216)
-__device__ __forceinline__ void edge_residual(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
-                                              const double X[3], double u, double v, const lh_params& prm,
-                                              double& r0, double& r1) {
-    double Pb[3], Pc[3];
+// the camera point ext (T X) of computeResidual (lego_types.h:213).  An extrinsic rotation that is
+// exactly the identity is skipped: the quaternion rotation by (1, 0, 0, 0) returns its input exactly.
+__device__ __forceinline__ void edge_pc(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
+                                        bool ext_rot, const double X[3], double Pc[3]) {
+    double Pb[3];
     d_q_rotate(pt + LH_PT_QT, X, Pb);
 #pragma unroll
     for (int i = 0; i < 3; ++i) Pb[i] = Pb[i] + pt[LH_PT_TT + i];
     if (ext_id) {
 #pragma unroll
         for (int i = 0; i < 3; ++i) Pc[i] = Pb[i];       // identity quaternion and zero t: exact
+    } else if (ext_rot) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pc[i] = Pb[i] + e[4 + i];
     } else {
         d_q_rotate(e, Pb, Pc);
 #pragma unroll
         for (int i = 0; i < 3; ++i) Pc[i] = Pc[i] + e[4 + i];
     }
+}
+
+// residual_ = z - pi(K (ext (T X))), pi(q) = q / (q_z + 1e-18)   (lego_types.h:200-216); Pc = ext (T X)
+__device__ __forceinline__ void edge_residual(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
+                                              bool ext_rot, const double X[3], double u, double v, const lh_params& prm,
+                                              double& r0, double& r1, double Pc[3]) {
+    edge_pc(pt, e, ext_id, ext_rot, X, Pc);
     const double fx = prm.K[0], fy = prm.K[1], cx = prm.K[2], cy = prm.K[3];
     double p0 = fx * Pc[0] + cx * Pc[2];                  // + 0 * Pc[1]: exact
     double p1 = fy * Pc[1] + cy * Pc[2];
@@ -293,47 +303,6 @@ __device__ __forceinline__ void edge_robust(EdgeEval& E, const lh_params& prm) {
     }
 }
 
-// EdgeProjection::computeJacobians (lego_types.h:218-254) at Pc = (ext T) X
-__device__ __forceinline__ void edge_jacobians(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
-                                               const double X[3], const lh_params& prm, double Jp[12], double Jl[6]) {
-    double Pc[3];
-    d_q_rotate(pt + LH_PT_QET, X, Pc);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) Pc[i] = Pc[i] + pt[LH_PT_TET + i];
-    {
-#pragma clang fp contract(fast)   // the Jacobians are not on the bitwise-mirrored path (the residual is)
-    const double fx = prm.K[0], fy = prm.K[1];
-    const double x = Pc[0], y = Pc[1], z = Pc[2];
-    const double zi = 1.0 / (z + 1e-18);
-    const double zi2 = zi * zi;
-    Jp[0] = -fx * zi;              Jp[1] = 0.0;                  Jp[2] = fx * x * zi2;
-    Jp[3] = fx * x * y * zi2;      Jp[4] = -fx - fx * x * x * zi2; Jp[5] = fx * y * zi;
-    Jp[6] = 0.0;                   Jp[7] = -fy * zi;             Jp[8] = fy * y * zi2;
-    Jp[9] = fy + fy * y * y * zi2; Jp[10] = -fy * x * y * zi2;   Jp[11] = -fy * x * zi;
-    // j_j = (j_i(:, 0:3) * ext.rotationMatrix()) * T.rotationMatrix()
-    double A[6];
-    if (ext_id) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) A[3 * i + j] = Jp[6 * i + j];   // J * I: exact
-    } else {
-        const double* Re = e + 7;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-                A[3 * i + j] = Jp[6 * i] * Re[j] + Jp[6 * i + 1] * Re[3 + j] + Jp[6 * i + 2] * Re[6 + j];
-    }
-    const double* Rt = pt + LH_PT_RT;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            Jl[3 * i + j] = A[3 * i] * Rt[j] + A[3 * i + 1] * Rt[3 + j] + A[3 * i + 2] * Rt[6 + j];
-    }
-}
-
 #pragma clang fp contract(fast)
 
 // ============================================================================
@@ -355,6 +324,112 @@ __device__ __forceinline__ double fast_rsq(double a) {
     y = y * fma(-h * y, y, 1.5);
     y = y * fma(-h * y, y, 1.5);
     return y;
+}
+
+// EdgeProjection::computeJacobians (lego_types.h:218-254).  The reference evaluates them at
+// ((ext T) X) and the residual at (ext (T X)); here both use the residual's point, which differs
+// in rounding only (the Jacobians are not on the bitwise-mirrored path, and the back substitution
+// re-derives exactly the Jacobians its linearisation used).  j_i's structural zeros J(0,1) and
+// J(1,0) (lego_types.h:247-248) are left out of every product (lin_blocks); Jp[1], Jp[6] unset.
+__device__ __forceinline__ void edge_jac_pc(const double Pc[3], const double* __restrict__ Rt,
+                                            const double* __restrict__ e, bool ext_rot, const lh_params& prm,
+                                            double Jp[12], double Jl[6]) {
+    const double fx = prm.K[0], fy = prm.K[1];
+    const double x = Pc[0], y = Pc[1], z = Pc[2];
+    const double zi = fast_rcp(z + 1e-18);
+    const double zi2 = zi * zi;
+    Jp[0] = -fx * zi;              Jp[1] = 0.0;                  Jp[2] = fx * x * zi2;
+    Jp[3] = fx * x * y * zi2;      Jp[4] = -fx - fx * x * x * zi2; Jp[5] = fx * y * zi;
+    Jp[6] = 0.0;                   Jp[7] = -fy * zi;             Jp[8] = fy * y * zi2;
+    Jp[9] = fy + fy * y * y * zi2; Jp[10] = -fy * x * y * zi2;   Jp[11] = -fy * x * zi;
+    // j_j = (j_i(:, 0:3) * ext.rotationMatrix()) * T.rotationMatrix()
+    double A[6];
+    if (ext_rot) {   // J * I: exact
+        A[0] = Jp[0]; A[1] = 0.0; A[2] = Jp[2]; A[3] = 0.0; A[4] = Jp[7]; A[5] = Jp[8];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            Jl[j] = A[0] * Rt[j] + A[2] * Rt[6 + j];
+            Jl[3 + j] = A[4] * Rt[3 + j] + A[5] * Rt[6 + j];
+        }
+    } else {
+        const double* Re = e + 7;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            A[j] = Jp[0] * Re[j] + Jp[2] * Re[6 + j];
+            A[3 + j] = Jp[7] * Re[3 + j] + Jp[8] * Re[6 + j];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                Jl[3 * i + j] = A[3 * i] * Rt[j] + A[3 * i + 1] * Rt[3 + j] + A[3 * i + 2] * Rt[6 + j];
+    }
+}
+
+// J(r, a) of j_i (2 x 6) is structurally zero: J(0, 1), J(1, 0)
+__device__ __forceinline__ constexpr bool jz(int r, int a) { return (r == 0 && a == 1) || (r == 1 && a == 0); }
+
+// Jp(:, a) . (x0, x1) without the structural zero
+__device__ __forceinline__ double jdot(const double* Jp, int a, double x0, double x1) {
+    if (jz(0, a)) return Jp[6 + a] * x1;
+    if (jz(1, a)) return Jp[a] * x0;
+    return Jp[a] * x0 + Jp[6 + a] * x1;
+}
+
+// The per-edge blocks of the linearisation (problem.cpp:285-331): H_ll, b_l, H_pl into registers,
+// H_pp (21) and b_p (6) into the lane's row of the pose-sum image.  WI: every live edge of the wave
+// is an inlier, so W = I and dr = 1 exactly, and W J = J.
+template <bool WI>
+__device__ __forceinline__ void lin_blocks(const EdgeEval& E, bool pfixed, double dr, double (&hll)[6],
+                                           double (&bl)[3], double (&hpl)[18], double* __restrict__ trow) {
+    const double* Jp = E.Jp;
+    const double* Jl = E.Jl;
+    double WJl[6];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        WJl[c] = WI ? Jl[c] : E.W00 * Jl[c] + E.W01 * Jl[3 + c];
+        WJl[3 + c] = WI ? Jl[3 + c] : E.W10 * Jl[c] + E.W11 * Jl[3 + c];
+    }
+    hll[0] = Jl[0] * WJl[0] + Jl[3] * WJl[3];
+    hll[1] = Jl[0] * WJl[1] + Jl[3] * WJl[4];
+    hll[2] = Jl[0] * WJl[2] + Jl[3] * WJl[5];
+    hll[3] = Jl[1] * WJl[1] + Jl[4] * WJl[4];
+    hll[4] = Jl[1] * WJl[2] + Jl[4] * WJl[5];
+    hll[5] = Jl[2] * WJl[2] + Jl[5] * WJl[5];
+    const double dr0 = WI ? E.r0 : dr * E.r0, dr1 = WI ? E.r1 : dr * E.r1;   // rho' r
+#pragma unroll
+    for (int c = 0; c < 3; ++c) bl[c] = -(Jl[c] * dr0 + Jl[3 + c] * dr1);
+    if (pfixed) return;
+    if (WI) {
+        // H_pp(a, b) = sum over the rows r where neither J(r, a) nor J(r, b) is a structural zero
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 6; ++b) {
+                const bool u0 = !jz(0, a) && !jz(0, b), u1 = !jz(1, a) && !jz(1, b);
+                trow[k++] = u0 && u1 ? Jp[a] * Jp[b] + Jp[6 + a] * Jp[6 + b]
+                                     : (u0 ? Jp[a] * Jp[b] : (u1 ? Jp[6 + a] * Jp[6 + b] : 0.0));
+            }
+    } else {
+        double WJp[12];   // W J_p, column b: W (J(0, b), J(1, b)) with J's zero left out
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            WJp[b] = jz(1, b) ? E.W00 * Jp[b] : (jz(0, b) ? E.W01 * Jp[6 + b] : E.W00 * Jp[b] + E.W01 * Jp[6 + b]);
+            WJp[6 + b] = jz(1, b) ? E.W10 * Jp[b] : (jz(0, b) ? E.W11 * Jp[6 + b] : E.W10 * Jp[b] + E.W11 * Jp[6 + b]);
+        }
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 6; ++b) trow[k++] = jdot(Jp, a, WJp[b], WJp[6 + b]);
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) hpl[3 * a + c] = jdot(Jp, a, WJl[c], WJl[3 + c]);
+        trow[21 + a] = -jdot(Jp, a, dr0, dr1);
+    }
 }
 
 // LDS strides of k_lin's window pose tables and landmark-record stage, padded off the global
@@ -609,6 +684,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         const bool live = has && !pfixed;
         const double* e = wext + cam * LH_EXT;
         const bool ext_id = (prm.ext_identity >> cam) & 1;
+        const bool ext_rot = (prm.ext_rot_identity >> cam) & 1;
 
         // ---- back-substitution of the pending pose step (problem.cpp:426-429) ----
         if (TRIAL) {
@@ -616,17 +692,22 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (live) {
                 const double* pt = wt_c + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
+                double Pc[3];
                 if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
                     E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+                    edge_pc(pt, e, ext_id, ext_rot, X, Pc);
                 } else {
-                    edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
+                    edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
                     edge_robust(E, prm);
                 }
-                edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
+                edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
                 const double* d = wdx + 6 * slot;
                 double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
-                for (int a = 0; a < 6; ++a) { jd0 += E.Jp[a] * d[a]; jd1 += E.Jp[6 + a] * d[a]; }
+                for (int a = 0; a < 6; ++a) {
+                    if (!jz(0, a)) jd0 += E.Jp[a] * d[a];
+                    if (!jz(1, a)) jd1 += E.Jp[6 + a] * d[a];
+                }
                 const double y0 = E.W00 * jd0 + E.W01 * jd1, y1 = E.W10 * jd0 + E.W11 * jd1;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) v3[c] = E.Jl[c] * y0 + E.Jl[3 + c] * y1;
@@ -658,7 +739,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (has) {
                 const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
-                edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
+                double Pc[3];
+                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
                 edge_robust(E, prm);
                 edge_rho[o] = E.rho0;
                 chi_acc += E.rho0;
@@ -682,46 +764,17 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         if (has) {
             const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
             EdgeEval E;
-            edge_residual(pt, e, ext_id, X, u, v, prm, E.r0, E.r1);
+            double Pc[3];
+            edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
             edge_robust(E, prm);
-            edge_jacobians(pt, e, ext_id, X, prm, E.Jp, E.Jl);
+            edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
             edge_rho[o] = E.rho0;
             chi_acc += E.rho0;
-            wf_n[o] = (prm.huber_delta <= 0.0 || E.e2 <= prm.huber_delta * prm.huber_delta) ? 1 : 0;
+            const bool inl = prm.huber_delta <= 0.0 || E.e2 <= prm.huber_delta * prm.huber_delta;
+            wf_n[o] = inl ? 1 : 0;
             const double dr = (prm.huber_delta > 0.0) ? E.rho1 : 1.0;
-            double WJl[6];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                WJl[c] = E.W00 * E.Jl[c] + E.W01 * E.Jl[3 + c];
-                WJl[3 + c] = E.W10 * E.Jl[c] + E.W11 * E.Jl[3 + c];
-            }
-            hll[0] = E.Jl[0] * WJl[0] + E.Jl[3] * WJl[3];
-            hll[1] = E.Jl[0] * WJl[1] + E.Jl[3] * WJl[4];
-            hll[2] = E.Jl[0] * WJl[2] + E.Jl[3] * WJl[5];
-            hll[3] = E.Jl[1] * WJl[1] + E.Jl[4] * WJl[4];
-            hll[4] = E.Jl[1] * WJl[2] + E.Jl[4] * WJl[5];
-            hll[5] = E.Jl[2] * WJl[2] + E.Jl[5] * WJl[5];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) bl[c] = -((dr * E.Jl[c]) * E.r0 + (dr * E.Jl[3 + c]) * E.r1);
-            if (!pfixed) {
-                double WJp[12];
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    WJp[a] = E.W00 * E.Jp[a] + E.W01 * E.Jp[6 + a];
-                    WJp[6 + a] = E.W10 * E.Jp[a] + E.W11 * E.Jp[6 + a];
-                }
-                int k = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a)
-#pragma unroll
-                    for (int b = a; b < 6; ++b) trow[k++] = E.Jp[a] * WJp[b] + E.Jp[6 + a] * WJp[6 + b];
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) hpl[3 * a + c] = E.Jp[a] * WJl[c] + E.Jp[6 + a] * WJl[3 + c];
-                    trow[21 + a] = -((dr * E.Jp[a]) * E.r0 + (dr * E.Jp[6 + a]) * E.r1);
-                }
-            }
+            if (__ballot(!inl) == 0ull) lin_blocks<true>(E, pfixed, dr, hll, bl, hpl, trow);   // wave-uniform
+            else lin_blocks<false>(E, pfixed, dr, hll, bl, hpl, trow);
         }
         STAMP(1);
 
