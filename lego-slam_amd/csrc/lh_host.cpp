@@ -379,6 +379,30 @@ void copy_slots(void* user, int64_t s0, int64_t s1) {
     c->err = e;
 }
 
+// host copies between caller memory and pinned staging, in ~256 KB blocks over the planner's pool
+struct ByteSeg { void* dst; const void* src; size_t n; };
+void par_copy(lh_handle* h, const ByteSeg* seg, int nseg) {
+    const size_t blk = 262144;
+    size_t total = 0;
+    for (int k = 0; k < nseg; ++k) total += (seg[k].dst && seg[k].src) ? seg[k].n : 0;
+    if (total < 4 * blk) {   // waking the pool costs more than copying a small call's bytes
+        for (int k = 0; k < nseg; ++k)
+            if (seg[k].dst && seg[k].src && seg[k].n) std::memcpy(seg[k].dst, seg[k].src, seg[k].n);
+        return;
+    }
+    std::vector<std::pair<int, size_t>> jobs;
+    for (int k = 0; k < nseg; ++k)
+        if (seg[k].dst && seg[k].src)
+            for (size_t o = 0; o < seg[k].n; o += blk) jobs.emplace_back(k, o);
+    auto job = [&](int j) {
+        const ByteSeg& g = seg[jobs[j].first];
+        const size_t o = jobs[j].second, c = std::min(blk, g.n - o);
+        std::memcpy((uint8_t*)g.dst + o, (const uint8_t*)g.src + o, c);
+    };
+    if (h->pool && jobs.size() > 1) h->pool->run((int)jobs.size(), job);
+    else for (int j = 0; j < (int)jobs.size(); ++j) job(j);
+}
+
 // sync: return only once the copies are done (lh_upload); lh_solve leaves them queued ahead of its
 // kernels on the same stream.  Either way the next upload waits for them before it rewrites the staging.
 int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
@@ -388,11 +412,24 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         HIPCHK(hipEventSynchronize(h->ev_staging));
         h->staging_pending = false;
     }
+    // the landmark positions need no plan: they go out first and cross the link while the planner runs
+    if (w && w->n_landmarks > 0 && w->lm_xyz) {
+        const size_t nl = 3 * (size_t)w->n_landmarks;
+        HIPCHK(h->d_lm_in.ensure(nl));
+        HIPCHK(h->s_lm.ensure(nl));
+        const ByteSeg seg{h->s_lm.p, w->lm_xyz, nl * sizeof(double)};
+        par_copy(h, &seg, 1);
+        HIPCHK(hipMemcpyAsync(h->d_lm_in.p, h->s_lm.p, nl * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    }
     lh::PlanCfg cfg;
     cfg.chunk_lm = h->opt.chunk_landmarks;
     lh::Plan& pl = h->plan;
     int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
-    if (st != LH_OK) return st;
+    if (st != LH_OK) {
+        HIPCHK(hipEventRecord(h->ev_staging, h->stream));
+        h->staging_pending = true;
+        return st;
+    }
     // past LH_PMAX poses the reduced system is solved in global memory: LDL^T by k_ctrl_g (dense, up
     // to LH_PMAX_WIN poses) or PCG by k_ctrl_p (block-sparse, up to LH_PMAX_ANY)
     if (pl.P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
@@ -462,13 +499,17 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->s_pair_ptr.ensure(pl.npairs + 1));
     HIPCHK(h->s_pair_pq.ensure(2 * (size_t)pl.npairs));
     HIPCHK(h->s_rsmap.ensure((size_t)pl.npairs * 36));
-    HIPCHK(h->s_lm.ensure(3 * (size_t)pl.L));
     lh::PlanOut po{h->s_chunks.p, h->s_sbs.p, h->s_meta.p, h->s_uv.p, h->s_obs_perm.p, h->s_lm_perm.p,
-                   h->s_items.p, h->s_pair_pq.p, h->s_rsmap.p, h->s_lm.p};
+                   h->s_items.p, h->s_pair_pq.p, h->s_rsmap.p, nullptr};   // positions: copied out above
     SlotCopy sc{h, hipSuccess};
-    const int batches = pl.n_slots >= (1 << 16) ? 4 : 1;
-    lh::plan_fill(w, pl, po, h->pool, copy_slots, &sc, batches);
+    const int batches = pl.n_slots >= (1 << 16) ? 8 : 1;
+    const int fs = lh::plan_fill(w, pl, po, h->pool, copy_slots, &sc, batches);
     HIPCHK(sc.err);
+    if (fs != LH_OK) {   // a pixel that is not a float value; the slot copies already issued read the staging
+        HIPCHK(hipEventRecord(h->ev_staging, h->stream));
+        h->staging_pending = true;
+        return fs;
+    }
     std::memcpy(h->s_pair_ptr.p, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
 
     // ---- camera extrinsics (Sophus SE3 of Camera::pose_) and the initial pose tables ----
@@ -476,7 +517,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->s_qt.ensure(24 * (size_t)std::max(P, 1)));
     HIPCHK(h->s_ptab.ensure(2 * (size_t)std::max(P, 1) * ncam * LH_PT));
     double* ext = h->s_ext.p;
-    int ext_identity = 0;
+    int ext_identity = 0, ext_rot_identity = 0;
     for (int c = 0; c < ncam; ++c) {
         static const double I12[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
         const double* E = (w->n_cams > 0) ? w->cam_ext + 12 * c : I12;
@@ -488,8 +529,10 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         for (int i = 0; i < 4; ++i) e[i] = q[i];
         e[4] = E[3]; e[5] = E[7]; e[6] = E[11];
         for (int i = 0; i < 9; ++i) e[7 + i] = Rq[i];
-        if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0 && e[4] == 0.0 && e[5] == 0.0 && e[6] == 0.0)
-            ext_identity |= 1 << c;
+        if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0) {
+            ext_rot_identity |= 1 << c;
+            if (e[4] == 0.0 && e[5] == 0.0 && e[6] == 0.0) ext_identity |= 1 << c;
+        }
     }
     for (int p = 0; p < P; ++p) {
         const double* T = w->pose_Tcw + 12 * p;
@@ -513,6 +556,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     prm.gate_mode = h->opt.gate_mode;
     prm.lambda_given = h->opt.lambda_init >= 0.0;
     prm.ext_identity = ext_identity;
+    prm.ext_rot_identity = ext_rot_identity;
     prm.huber_delta = h->opt.huber_delta;
     prm.stop_dchi2 = h->opt.stop_dchi2;
     prm.tau = h->opt.tau;
@@ -532,7 +576,6 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
     };
     HIPCHK(up(h->d_lm_perm.p, h->s_lm_perm.p, (size_t)pl.n_rec * sizeof(int32_t)));
-    HIPCHK(up(h->d_lm_in.p, h->s_lm.p, 3 * (size_t)pl.L * sizeof(double)));
     HIPCHK(up(h->d_chunks.p, h->s_chunks.p, (size_t)pl.n_chunks * sizeof(lh_chunk)));
     HIPCHK(up(h->d_sbs.p, h->s_sbs.p, (size_t)pl.n_sb * sizeof(lh_subbatch)));
     HIPCHK(up(h->d_pair_ptr.p, h->s_pair_ptr.p, ((size_t)pl.npairs + 1) * sizeof(uint32_t)));
@@ -644,30 +687,6 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
 // Results into the caller's buffers: device -> pinned staging in one stream (poses, landmark
 // positions gathered into window order, per-edge rho0), then the staging is copied out on the
 // planner's threads (a pageable device-to-host copy runs at a fraction of the link).
-// host copies between caller memory and pinned staging, in ~256 KB blocks over the planner's pool
-struct ByteSeg { void* dst; const void* src; size_t n; };
-void par_copy(lh_handle* h, const ByteSeg* seg, int nseg) {
-    const size_t blk = 262144;
-    size_t total = 0;
-    for (int k = 0; k < nseg; ++k) total += (seg[k].dst && seg[k].src) ? seg[k].n : 0;
-    if (total < 4 * blk) {   // waking the pool costs more than copying a small call's bytes
-        for (int k = 0; k < nseg; ++k)
-            if (seg[k].dst && seg[k].src && seg[k].n) std::memcpy(seg[k].dst, seg[k].src, seg[k].n);
-        return;
-    }
-    std::vector<std::pair<int, size_t>> jobs;
-    for (int k = 0; k < nseg; ++k)
-        if (seg[k].dst && seg[k].src)
-            for (size_t o = 0; o < seg[k].n; o += blk) jobs.emplace_back(k, o);
-    auto job = [&](int j) {
-        const ByteSeg& g = seg[jobs[j].first];
-        const size_t o = jobs[j].second, c = std::min(blk, g.n - o);
-        std::memcpy((uint8_t*)g.dst + o, (const uint8_t*)g.src + o, c);
-    };
-    if (h->pool && jobs.size() > 1) h->pool->run((int)jobs.size(), job);
-    else for (int j = 0; j < (int)jobs.size(); ++j) job(j);
-}
-
 int download(lh_handle* h, lh_result* out, int cur) {
     hipStream_t s = h->stream;
     const int P = h->P;

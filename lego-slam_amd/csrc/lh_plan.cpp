@@ -18,30 +18,36 @@ Pool::Pool(int threads) {
 Pool::~Pool() {
     {
         std::lock_guard<std::mutex> g(mu_);
-        stop_ = true;
+        stop_.store(true);
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
 }
 
+// Hand-off protocol (every atomic seq_cst).  A worker counts itself in active_ *before* it loads
+// job_, and run() clears job_ *before* it waits for active_ to drain.  So a worker that loaded the
+// job pointer was counted before the clear, and run() does not return (the Job lives on its stack)
+// until that worker has left; a worker counted after the clear loads nullptr (or a later job, which
+// it may then help with: the same counting protects that one).
 void Pool::loop() {
     uint64_t seen = 0;
     for (;;) {
-        Job* job;
-        {
-            std::unique_lock<std::mutex> g(mu_);
-            cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-            if (stop_) return;
-            seen = gen_;
-            job = job_;
-            if (!job) continue;   // woke after run() retired this generation's job
-            ++active_;
+        uint64_t g = gen_.load();
+        for (unsigned spin = 0; g == seen && !stop_.load(); g = gen_.load()) {
+            __builtin_ia32_pause();
+            if (++spin >= kSpin) {
+                std::unique_lock<std::mutex> lk(mu_);
+                sleepers_.fetch_add(1);
+                cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
+                sleepers_.fetch_sub(1);
+            }
         }
-        for (int i = job->next.fetch_add(1); i < job->n; i = job->next.fetch_add(1)) (*job->fn)(i);
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            if (--active_ == 0) done_cv_.notify_all();
-        }
+        if (stop_.load()) return;
+        seen = g;
+        active_.fetch_add(1);
+        if (Job* job = job_.load())
+            for (int i = job->next.fetch_add(1); i < job->n; i = job->next.fetch_add(1)) (*job->fn)(i);
+        active_.fetch_sub(1);
     }
 }
 
@@ -54,19 +60,15 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
     Job job;
     job.fn = &fn;
     job.n = n;
-    {
+    job_.store(&job);
+    gen_.fetch_add(1);
+    if (sleepers_.load() > 0) {   // a sleeper checks gen_ under mu_ before it waits: no lost wake-up
         std::lock_guard<std::mutex> g(mu_);
-        job_ = &job;
-        ++gen_;
+        cv_.notify_all();
     }
-    cv_.notify_all();
     for (int i = job.next.fetch_add(1); i < n; i = job.next.fetch_add(1)) fn(i);
-    std::unique_lock<std::mutex> g(mu_);
-    // Retire the job under the lock first: a worker joins only while job_ is set (and counts itself
-    // in active_ under the same lock), so once active_ drops to 0 no thread can still touch `job`,
-    // which lives on this stack frame.  A worker that wakes late sees job_ == nullptr.
-    job_ = nullptr;
-    done_cv_.wait(g, [&] { return active_ == 0; });
+    job_.store(nullptr);
+    while (active_.load() != 0) __builtin_ia32_pause();
 }
 
 namespace {
@@ -123,21 +125,29 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         pl.t_stage[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_0).count();
     };
 
-    // ---- index checks and "already landmark-major" detection, one parallel pass ----
+    // ---- index checks and the landmark-major CSR, one parallel pass.  The CSR assumes the input is
+    //      already grouped by landmark (what Backend::Optimize's landmark loop produces) and is rebuilt
+    //      by a counting sort when it is not. ----
     std::atomic<int> bad{0}, unsorted{0};
+    pl.lm_ptr.assign((size_t)L + 1, 0);
+    pl.csr.resize((size_t)O);
     parallel_range(pool, O, 1 << 15, [&](int64_t b, int64_t e) {
         uint32_t prev = b > 0 ? w->obs_lm[b - 1] : 0;
         bool bd = false, us = false;
         for (int64_t o = b; o < e; ++o) {
             const uint32_t l = w->obs_lm[o];
-            bd |= w->obs_pose[o] >= (uint32_t)P || l >= (uint32_t)L || (w->obs_cam && w->obs_cam[o] >= ncam);
-            // the measurement is a cv::KeyPoint's float pixel widened (toVec2, algorithm.h:37): the device
-            // keeps it as a float, so a value a float cannot hold exactly (or a NaN) is a bad argument
-            const double u = w->obs_uv[2 * o], v = w->obs_uv[2 * o + 1];
-            bd |= !((double)(float)u == u) || !((double)(float)v == v);
+            const bool ok = w->obs_pose[o] < (uint32_t)P && l < (uint32_t)L && (!w->obs_cam || w->obs_cam[o] < ncam);
+            bd |= !ok;
             us |= l < prev;
+            pl.csr[o] = o;
+            if (ok && !us)   // the landmarks from the previous observation's (exclusive) to this one start here
+                for (int64_t q = o > 0 ? (int64_t)prev + 1 : 0; q <= (int64_t)l; ++q) pl.lm_ptr[q] = o;
             prev = l;
         }
+        // the measurement is a cv::KeyPoint's float pixel widened (toVec2, algorithm.h:37): the device
+        // keeps it as a float, so a value a float cannot hold exactly (or a NaN) is a bad argument
+        // (a loop of its own: it vectorises)
+        for (int64_t i = 2 * b; i < 2 * e; ++i) bd |= !((double)(float)w->obs_uv[i] == w->obs_uv[i]);
         if (bd) bad.store(1);
         if (us) unsorted.store(1);
     });
@@ -152,20 +162,10 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     pl.fixed_mask = pl.fixed_bits[0];
 
     stage(0);
-    // ---- landmark-major CSR ----
-    pl.lm_ptr.assign((size_t)L + 1, 0);
-    pl.csr.resize((size_t)O);
     if (!unsorted.load()) {
-        // input already grouped by landmark (what Backend::Optimize's landmark loop produces)
-        parallel_range(pool, O, 1 << 15, [&](int64_t b, int64_t e) {
-            for (int64_t o = b; o < e; ++o) {
-                pl.csr[o] = o;
-                const int64_t lo = o > 0 ? (int64_t)w->obs_lm[o - 1] + 1 : 0;
-                for (int64_t l = lo; l <= (int64_t)w->obs_lm[o]; ++l) pl.lm_ptr[l] = o;
-            }
-        });
         for (int64_t l = (O > 0 ? (int64_t)w->obs_lm[O - 1] + 1 : 0); l <= L; ++l) pl.lm_ptr[l] = O;
     } else {
+        std::fill(pl.lm_ptr.begin(), pl.lm_ptr.end(), 0);
         for (int64_t o = 0; o < O; ++o) pl.lm_ptr[w->obs_lm[o] + 1]++;
         for (int l = 0; l < L; ++l) pl.lm_ptr[l + 1] += pl.lm_ptr[l];
         std::vector<int64_t> pos(pl.lm_ptr.begin(), pl.lm_ptr.end() - 1);
@@ -210,6 +210,9 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     if (unsup.load()) return LH_E_UNSUPPORTED;
 
     stage(2);
+    std::vector<uint64_t>& om = pl.ord_mask;
+    std::vector<int32_t>& ob = pl.ord_base;
+    std::vector<uint8_t>& olg = pl.ord_lg;
     // ---- landmark order by observation span (first pose, last pose, mask), stable: a parallel
     //      counting sort (per-block histograms, prefix in bucket-major / block-minor order, so each
     //      bucket keeps landmark order), then a stable sort by mask inside the buckets that mix masks ----
@@ -242,11 +245,22 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
             }
         const int Lact0 = run;
         pl.order.resize((size_t)Lact0);
+        om.resize((size_t)Lact0);
+        ob.resize((size_t)Lact0);
+        olg.resize((size_t)Lact0);
+        // the chunking pass reads each landmark's mask, first pose and lane-group log in span order:
+        // written here with the order itself
+        auto put = [&](int32_t i, int l) {
+            pl.order[i] = l;
+            om[i] = pl.lm_mask[l];
+            ob[i] = pl.lm_base[l];
+            olg[i] = (uint8_t)pow2log((int)(pl.lm_ptr[l + 1] - pl.lm_ptr[l]));
+        };
         auto scatter_blk = [&](int k) {
             int32_t* h = hist.data() + (size_t)k * (nb + 1);
             const int l0 = k * bsz, l1 = std::min(L, l0 + bsz);
             for (int l = l0; l < l1; ++l)
-                if (pl.lm_mask[l]) pl.order[h[bucket(l)]++] = l;
+                if (pl.lm_mask[l]) put(h[bucket(l)]++, l);
         };
         if (pool) pool->run(nblk, scatter_blk);
         else for (int k = 0; k < nblk; ++k) scatter_blk(k);
@@ -260,6 +274,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
             const uint64_t m0 = pl.lm_mask[*s];
             if (std::all_of(s, e, [&](int32_t l) { return pl.lm_mask[l] == m0; })) return;
             std::stable_sort(s, e, [&](int32_t x, int32_t y) { return pl.lm_mask[x] < pl.lm_mask[y]; });
+            for (int32_t i = s0; i < e0; ++i) put(i, pl.order[i]);
         };
         if (pool) pool->run(nb, sort_bucket);
         else for (int bk = 0; bk < nb; ++bk) sort_bucket(bk);
@@ -277,23 +292,12 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     chunk_lm = ((chunk_lm + LH_SB_LM - 1) / LH_SB_LM) * LH_SB_LM;
     chunk_lm = std::max(32, std::min(256, chunk_lm));
     if (cfg.chunk_lm > 0) chunk_lm = std::max(LH_SB_LM, std::min(512, cfg.chunk_lm));
-    // One serial pass over the span order cuts the chunks and packs their sub-batches (the masks and
-    // lane-group logs gathered first, in parallel, so the pass reads them sequentially).
+    // One serial pass over the span order cuts the chunks and packs their sub-batches (the masks, first
+    // poses and lane-group logs in span order, om / ob / olg, so the pass reads them sequentially).
     // A chunk's MFMA tile count T is set by the union of its landmarks' poses: start a new chunk
     // rather than let the union grow past the larger of the two tile counts.  A sub-batch takes
     // landmarks while it holds < 8 and (n + 1) << lg <= 64 (landmark l owns the aligned lane group
     // [l*G, l*G + k_l) of its 64 slots, G = 2^lg the largest pow2ceil(k) in the sub-batch).
-    std::vector<uint64_t> om((size_t)Lact);
-    std::vector<int32_t> ob((size_t)Lact);
-    std::vector<uint8_t> olg((size_t)Lact);
-    parallel_range(pool, Lact, 4096, [&](int64_t b, int64_t e) {
-        for (int64_t i = b; i < e; ++i) {
-            const int l = pl.order[i];
-            om[i] = pl.lm_mask[l];
-            ob[i] = pl.lm_base[l];
-            olg[i] = (uint8_t)pow2log((int)(pl.lm_ptr[l + 1] - pl.lm_ptr[l]));
-        }
-    });
     pl.chunk_lm0.clear();
     pl.chunk_mask.clear();
     pl.chunk_base.clear();
@@ -437,8 +441,8 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
 // ---------------------------------------------------------------------------------------------
 // plan_fill
 // ---------------------------------------------------------------------------------------------
-void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool, SlotsReady on_slots, void* user,
-               int batches) {
+int plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool, SlotsReady on_slots, void* user,
+              int batches) {
     const int P = pl.P, NC = pl.n_chunks;
     // chunks and their sub-batches' observation slots, one task per chunk
     auto chunk_task = [&](int ci) {
@@ -537,9 +541,11 @@ void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* poo
                 for (int b = 0; b < 6; ++b)
                     out.rsmap[(size_t)blk * 36 + 6 * a + b] = LH_RSMAP(6 * pi + a, 6 * pj + b, pi == pj);
         }
-    parallel_range(pool, 3 * (int64_t)pl.L, 1 << 16, [&](int64_t b, int64_t e) {
-        if (e > b) std::memcpy(out.lm_xyz + b, w->lm_xyz + b, (size_t)(e - b) * sizeof(double));
-    });
+    if (out.lm_xyz)
+        parallel_range(pool, 3 * (int64_t)pl.L, 1 << 16, [&](int64_t b, int64_t e) {
+            if (e > b) std::memcpy(out.lm_xyz + b, w->lm_xyz + b, (size_t)(e - b) * sizeof(double));
+        });
+    return LH_OK;
 }
 
 }  // namespace lh

@@ -27,6 +27,10 @@
 namespace lh {
 
 // Persistent worker pool: run(n, fn) calls fn(i) for i in [0, n) on the workers and the caller.
+// The job hand-off is lock-free (Pool::loop); an idle worker polls the job generation briefly
+// (kSpin pauses) and then sleeps on the condition variable.  Polling longer (300 us after each job,
+// so that a planning pass's back-to-back jobs never wait for a wake-up) measured slower on the box's
+// 16-CPU cgroup share: lh_solve's preprocessing 1.80 ms against 1.49 ms.
 class Pool {
   public:
     explicit Pool(int threads);
@@ -40,14 +44,16 @@ class Pool {
         int n = 0;
         std::atomic<int> next{0};
     };
+    static constexpr unsigned kSpin = 256;
     void loop();
     std::vector<std::thread> workers_;
     std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    Job* job_ = nullptr;   // the live job of generation gen_, nullptr once run() retires it
-    int active_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::condition_variable cv_;
+    std::atomic<Job*> job_{nullptr};    // the live job, nullptr once run() retires it
+    std::atomic<uint64_t> gen_{0};      // bumped per job
+    std::atomic<int> active_{0};        // workers that may still touch job_'s job
+    std::atomic<int> sleepers_{0};
+    std::atomic<bool> stop_{false};
 };
 
 struct PlanCfg {
@@ -75,6 +81,9 @@ struct Plan {
     std::vector<uint64_t> lm_mask;      // [L] observing-pose mask, bit i = pose lm_base + i
     std::vector<int32_t> lm_base;       // [L] first observing pose
     std::vector<int32_t> order;         // [L_act] landmarks with edges, span order
+    std::vector<uint64_t> ord_mask;     // [L_act] lm_mask / lm_base / log2 lane group, in span order
+    std::vector<int32_t> ord_base;
+    std::vector<uint8_t> ord_lg;
     std::vector<int32_t> chunk_lm0;     // [n_chunks + 1] chunk c owns order[chunk_lm0[c] .. chunk_lm0[c+1])
     std::vector<uint64_t> chunk_mask;   // [n_chunks] union pose mask, bit i = pose chunk_base + i
     std::vector<int32_t> chunk_base;    // [n_chunks]
@@ -98,7 +107,7 @@ struct PlanOut {
     uint32_t* items;         // [n_items] per chunk (launch order), per slot pair (s <= t): its pair row
     uint16_t* pair_pq;       // [2 npairs]
     uint32_t* rsmap;         // [npairs * 36]
-    double* lm_xyz;          // [3 L] copy of the window's positions
+    double* lm_xyz;          // [3 L] copy of the window's positions (nullptr: not wanted)
 };
 
 // lh_status.  LH_E_BADARG for out-of-range indices, LH_E_UNSUPPORTED outside the envelope
@@ -108,7 +117,8 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
 // slots [slot_begin, slot_end) (meta, uv, obs_perm) are final, in ascending order, so the caller can
 // start copying them while the rest is filled; `batches` splits the chunk pass for that.
 using SlotsReady = void (*)(void* user, int64_t slot_begin, int64_t slot_end);
-void plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool, SlotsReady on_slots = nullptr,
-               void* user = nullptr, int batches = 1);
+// Returns LH_OK (the window was validated by plan_structure).
+int plan_fill(const lh_window* w, const Plan& pl, const PlanOut& out, Pool* pool, SlotsReady on_slots = nullptr,
+              void* user = nullptr, int batches = 1);
 
 }  // namespace lh

@@ -39,9 +39,9 @@ int lhp_plan_fill(const lh_window* w, int chunk_lm, int threads, lh_chunk* chunk
     const int st = lh::plan_structure(w, cfg, false, pl, &pool);
     if (st != LH_OK) return st;
     lh::PlanOut po{chunks, sbs, meta, uv, obs_perm, lm_perm, items, pair_pq, rsmap, lm_xyz};
-    lh::plan_fill(w, pl, po, &pool);
+    const int fs = lh::plan_fill(w, pl, po, &pool);
     std::memcpy(pair_ptr, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
-    return LH_OK;
+    return fs;
 }
 
 // mean over reps plans (after one warm-up) on a persistent pool: ms of plan_structure and of

@@ -330,11 +330,17 @@ class Solver:
         except Exception:
             pass
 
-    def _result(self, n_poses, n_lm, n_obs, trace_cap=64, want_states=True, want_edges=True):
+    def _result(self, n_poses, n_lm, n_obs, trace_cap=64, want_states=True, want_edges=True, reuse=None):
+        def buf(key, shape, want):
+            if not want:
+                return None
+            if reuse is not None and reuse.get(key) is not None and reuse[key].shape == shape:
+                return reuse[key]
+            return np.zeros(shape)
         out = dict(
-            pose_Tcw=np.zeros((n_poses, 12)) if want_states else None,
-            lm_xyz=np.zeros((n_lm, 3)) if want_states else None,
-            edge_robust_chi2=np.zeros(n_obs) if want_edges else None,
+            pose_Tcw=buf("pose_Tcw", (n_poses, 12), want_states),
+            lm_xyz=buf("lm_xyz", (n_lm, 3), want_states),
+            edge_robust_chi2=buf("edge_robust_chi2", (n_obs,), want_edges),
             trace_chi2=np.zeros(trace_cap), trace_lambda=np.zeros(trace_cap),
         )
         r = LhResult()
@@ -354,9 +360,11 @@ class Solver:
             out[f] = getattr(r, f)
         return out
 
-    def solve(self, w, trace_cap=64):
+    def solve(self, w, trace_cap=64, reuse=None):
+        """lh_solve on host buffers.  reuse: a previous call's result dict whose output arrays are
+        written again (a caller's persistent buffers) instead of freshly allocated ones."""
         ref = _WindowRef(w)
-        r, out = self._result(ref.s.n_poses, ref.s.n_landmarks, ref.s.n_obs, trace_cap)
+        r, out = self._result(ref.s.n_poses, ref.s.n_landmarks, ref.s.n_obs, trace_cap, reuse=reuse)
         _check(ba_lib().lh_solve(self.h, C.byref(ref.s), C.byref(r)), "lh_solve")
         return self._finish(r, out)
 

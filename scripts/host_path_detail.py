@@ -15,17 +15,18 @@ for th in (1, 4, 8, 16):
     st = lego_ba.plan_stages_ms(w, threads=th, reps=5)
     print(f"threads {th:2d} stage ends ms", " ".join(f"{x:.3f}" for x in st),
           "structure/fill ms", " ".join(f"{x:.3f}" for x in lego_ba.plan_time_ms(w, threads=th, reps=10)), flush=True)
-for lib in [None, os.environ.get("LIB_OLD")]:
+for lib in [None] + os.environ.get("LIB_OLD", "").split():
     if lib:
         lego_ba._balib = None
         lego_ba.BA_LIB = lib
     s = lego_ba.Solver()
-    s.solve(w)
-    rows = []
-    for _ in range(15):
-        t0 = time.perf_counter()
-        r = s.solve(w)
-        rows.append(((time.perf_counter() - t0) * 1e3, r["time_prep_ms"], r["time_upload_ms"], r["time_ms"], r["time_download_ms"]))
-    a = np.median(np.array(rows), axis=0)
-    print(lib or "current", "total %.3f prep %.3f upload %.3f solve %.3f download %.3f" % tuple(a), flush=True)
+    prev = s.solve(w)
+    for mode in ("fresh outputs", "reused outputs"):
+        rows = []
+        for _ in range(15):
+            t0 = time.perf_counter()
+            r = s.solve(w, reuse=prev if mode.startswith("reused") else None)
+            rows.append(((time.perf_counter() - t0) * 1e3, r["time_prep_ms"], r["time_upload_ms"], r["time_ms"], r["time_download_ms"]))
+        a = np.median(np.array(rows), axis=0)
+        print(lib or "current", mode, "total %.3f prep %.3f upload %.3f solve %.3f download %.3f" % tuple(a), flush=True)
     s.close()
