@@ -30,3 +30,17 @@ for lib in [None] + os.environ.get("LIB_OLD", "").split():
         a = np.median(np.array(rows), axis=0)
         print(lib or "current", mode, "total %.3f prep %.3f upload %.3f solve %.3f download %.3f" % tuple(a), flush=True)
     s.close()
+# lh_solve by planner thread count (the default is auto_host_threads: the usable CPUs, at most 8)
+lego_ba._balib = None
+lego_ba.BA_LIB = os.path.join(ROOT, "lego-slam_amd", "lib", "liblego_ba.so")
+for th in (4, 8, 12, 16):
+    s = lego_ba.Solver(host_threads=th)
+    prev = s.solve(w)
+    rows = []
+    for _ in range(15):
+        t0 = time.perf_counter()
+        r = s.solve(w, reuse=prev)
+        rows.append(((time.perf_counter() - t0) * 1e3, r["time_prep_ms"], r["time_upload_ms"], r["time_ms"], r["time_download_ms"]))
+    a = np.median(np.array(rows), axis=0)
+    print(f"host_threads {th:2d} total %.3f prep %.3f upload %.3f solve %.3f download %.3f" % tuple(a), flush=True)
+    s.close()
