@@ -215,9 +215,10 @@ int auto_host_threads() {
         }
         std::fclose(f);
     }
-    // the planner's passes are memory-bound and their pool meets at a barrier per pass: past 8 threads
-    // a shared box's scheduling noise costs more than the bandwidth they add (C3 planner: 0.74 ms at 8
-    // threads, 1.19 ms at 16, EPYC 9575F box with a 16-CPU quota)
+    // the planner's passes are memory-bound and their pool meets at a barrier per pass; its workers are
+    // pinned to the caller's last-level cache (lh_plan.cpp Pool), which has 8 cores on an EPYC 9575F.
+    // C3 lh_solve on such a box with a 16-CPU quota: 2.12 ms at 8 threads, 2.18 at 12, 2.16 at 16
+    // (unpinned: 3.55, 3.45, 2.69)
     return std::max(1, std::min(8, n));
 }
 

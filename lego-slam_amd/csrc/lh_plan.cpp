@@ -2,8 +2,13 @@
 // builds it into a host-only library (liblego_plan.so) and checks the plan's invariants.
 #include "lh_plan.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace lh {
@@ -11,8 +16,50 @@ namespace lh {
 // ---------------------------------------------------------------------------------------------
 // Pool
 // ---------------------------------------------------------------------------------------------
+namespace {
+// The CPUs that share the calling thread's last-level cache (sysfs cache/index3), within this
+// process's affinity mask: distinct physical cores first (sysfs lists them before their SMT siblings),
+// the calling thread's own CPU left out.  Empty when sysfs or the affinity mask cannot be read.
+std::vector<int> llc_cpus() {
+    std::vector<int> out;
+    const int self = sched_getcpu();
+    cpu_set_t mask;
+    if (self < 0 || sched_getaffinity(0, sizeof(mask), &mask) != 0) return out;
+    char path[96];
+    std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", self);
+    FILE* f = std::fopen(path, "r");
+    if (!f) return out;
+    char buf[512] = {0};
+    const bool ok = std::fgets(buf, sizeof(buf), f) != nullptr;
+    std::fclose(f);
+    if (!ok) return out;
+    for (char* tok = std::strtok(buf, ",\n"); tok; tok = std::strtok(nullptr, ",\n")) {
+        int a = 0, b = 0;
+        const int got = std::sscanf(tok, "%d-%d", &a, &b);
+        if (got < 1) continue;
+        if (got == 1) b = a;
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (c != self && CPU_ISSET(c, &mask)) out.push_back(c);
+    }
+    return out;
+}
+}  // namespace
+
+// Workers are pinned to the CPUs sharing the caller's last-level cache (LH_HOST_PIN=0 leaves them to
+// the scheduler): a GPU box exposes every host core to a process with a share of them, and a worker
+// the scheduler puts on the other socket runs a pass's block at a fraction of the others' speed.
 Pool::Pool(int threads) {
-    for (int i = 1; i < threads; ++i) workers_.emplace_back([this] { loop(); });
+    const char* pin_env = std::getenv("LH_HOST_PIN");
+    const std::vector<int> cpus = (pin_env && pin_env[0] == '0') ? std::vector<int>() : llc_cpus();
+    for (int i = 1; i < threads; ++i) {
+        workers_.emplace_back([this] { loop(); });
+        if (i - 1 < (int)cpus.size()) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus[i - 1], &one);
+            pthread_setaffinity_np(workers_.back().native_handle(), sizeof(one), &one);   // best effort
+        }
+    }
 }
 
 Pool::~Pool() {
