@@ -1457,79 +1457,115 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
 // the reference never adds the first step alpha*p to x (:595-596); here every step is applied.
 // A zero diagonal entry (STRATEGY1 with a fixed pose: 0 + lambda*0) preconditions with 0 instead of
 // Eigen's inf (which would turn the whole step into NaN).
-// Layout: one wave runs the whole iteration, with no workgroup barrier inside the loop.  The
-// system is first mirrored to full storage in LDS (the upper triangle is free in this variant).
-// Lane l owns rows l and l + 64: x, r, p and 1/d in registers; A p reads those rows from LDS and p
-// by broadcast; the three dots per step (p.q, r.z, r.r) are a fixed DPP/ds_bpermute butterfly over
-// the wave.  Round 1 ran eight threads per row over 16 waves with three barriers per step
-// (~3 us per step; this is ~0.6 us).
+// Layout: eight waves, the system cached in registers.  Wave w < 8 owns rows 16w .. 16w + 15; lane l
+// holds row 16w + (l & 15) at columns 32 (l >> 4) + j, j < 32 (32 doubles).  A matrix-vector product is
+// then 32 FMAs per lane on 16-byte broadcast reads of the vector, and a 2-level butterfly (lane ^ 16, 32) over
+// the four lanes sharing a row; each row's scalars (x, r, z, p, q, 1/d) are replicated over those
+// lanes.  Two workgroup barriers per step, the CG recurrence regrouped so that one product serves a
+// step: with z published, q = A p = A z + beta q_prev and p = z + beta p_prev (the same iteration,
+// rounded differently: parity to tolerance, as before).  The dot products are fixed-order sums
+// (16-row wave butterflies, then the 8 wave partials in order), so a solve is bitwise repeatable.
+// Waves 8-15 only keep the barrier count and the stop test (the r.r total, the same bits).  Per step
+// the SIMD issue is what costs: all 16 waves doing the row scalars' replicated work took 1.85 us per
+// step on C3; the round-2 layout (one wave, the system in LDS, an n-long FMA chain per row) ~2.5 us;
+// round 1 (eight threads per row, three barriers) ~3 us.
 // At most max_it steps (callers pass the reference cap + 1: its first step precedes its loop).
 // Returns the iteration count.  Must be called by all CT threads; xsol[r] = x in pivot order.
 __device__ __forceinline__ int lds_pcg_solve(double* __restrict__ A, double* __restrict__ xsol, double* __restrict__ pv,
-                             double* __restrict__ s_red2, int n, int tid, double tol_rel, int max_it) {
+                                             double* __restrict__ s_red2, int n, int tid, double tol_rel, int max_it) {
+    constexpr int PW = 8;   // PCG waves
+    static_assert(CT / 64 >= PW && NP == 16 * PW, "8 waves x 16 rows, 4 column blocks x 32");
     const int lane = tid & 63, wave = tid >> 6;
-    // full symmetric storage of the n x n system (rows and columns past n are never read)
-    for (int x = tid; x < n * n; x += CT) {
-        const int i = x / n, j = x - n * (x / n);
-        if (j > i) A[i * AS + j] = A[j * AS + i];
+    const bool act = wave < PW;
+    const int row = 16 * wave + (lane & 15), k = lane >> 4;
+    const bool vr = act && row < n;
+    double a[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const int c = 32 * k + j;
+        a[j] = (vr && c < n) ? A[max(row, c) * AS + min(row, c)] : 0.0;   // S(i, j) = A[max * AS + min]
     }
-    lds_barrier();
-    if (wave == 0) {
-        const int r0 = lane, r1 = lane + 64;
-        const bool v0 = r0 < n, v1 = r1 < n;
-        const double d0 = v0 ? A[r0 * AS + r0] : 0.0, d1 = v1 ? A[r1 * AS + r1] : 0.0;
-        const double i0 = (d0 != 0.0) ? 1.0 / d0 : 0.0, i1 = (d1 != 0.0) ? 1.0 / d1 : 0.0;
-        double rr0 = v0 ? A[NP * AS + r0] : 0.0, rr1 = v1 ? A[NP * AS + r1] : 0.0;
-        double x0 = 0.0, x1 = 0.0;
-        double z0 = rr0 * i0, z1 = rr1 * i1;
-        double p0 = z0, p1 = z1;
-        double t[2] = {rr0 * z0 + rr1 * z1, rr0 * rr0 + rr1 * rr1};
-        group_sum(t, 6);
-        double rz = t[0];
-        const double bnorm = sqrt(t[1]);
-        const double thr = tol_rel * bnorm;
-        int it = 0;
-        if (bnorm > 0.0) {
-#pragma clang loop unroll(disable)
-            while (it < max_it) {
-                pv[r0] = p0;
-                if (r1 < NP) pv[r1] = p1;
-                wave_sync();
-                // q = A p over the two rows, columns in order
-                double q0 = 0.0, q1 = 0.0;
-                const double* a0 = A + r0 * AS;
-                const double* a1 = A + (v1 ? r1 : r0) * AS;
-#pragma unroll 8
-                for (int c = 0; c < n; ++c) {
-                    const double pc = pv[c];
-                    q0 += a0[c] * pc;
-                    q1 += a1[c] * pc;
-                }
-                if (!v0) q0 = 0.0;
-                if (!v1) q1 = 0.0;
-                double pq[1] = {p0 * q0 + p1 * q1};
-                group_sum(pq, 6);
-                const double alpha = rz / pq[0];
-                x0 += alpha * p0; x1 += alpha * p1;
-                rr0 -= alpha * q0; rr1 -= alpha * q1;
-                z0 = rr0 * i0; z1 = rr1 * i1;
-                double u[2] = {rr0 * z0 + rr1 * z1, rr0 * rr0 + rr1 * rr1};
-                group_sum(u, 6);
-                ++it;
-                if (!(sqrt(u[1]) > thr)) break;       // also stops on NaN
-                const double beta = u[0] / rz;
-                rz = u[0];
-                p0 = z0 + beta * p0;
-                p1 = z1 + beta * p1;
-                wave_sync();                          // every lane's reads of pv before the next writes
-            }
+    const double d = vr ? A[row * AS + row] : 0.0;
+    const double id = (d != 0.0) ? 1.0 / d : 0.0;
+    double r = vr ? A[NP * AS + row] : 0.0;
+    double x = 0.0, z = r * id, p = 0.0, q = 0.0, beta = 0.0;
+    double* red_pq = s_red2;                                            // [PW] wave partials of p.q
+    double2* red_zr = reinterpret_cast<double2*>(s_red2 + 16);          // [PW] of (r.z, r.r)
+    auto rows16 = [&](double v) {       // the wave's 16 rows (every lane gets the sum)
+        double t[1] = {v};
+        group_sum(t, 4);
+        return t[0];
+    };
+    auto total = [&](const double* red) {   // in wave order
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < PW; ++w) t += red[w];
+        return t;
+    };
+    auto total2 = [&](double& tz, double& tr) {
+        tz = 0.0;
+        tr = 0.0;
+#pragma unroll
+        for (int w = 0; w < PW; ++w) {
+            const double2 t = red_zr[w];
+            tz += t.x;
+            tr += t.y;
         }
-        if (v0) xsol[r0] = x0;
-        if (v1) xsol[r1] = x1;
-        if (lane == 0) s_red2[0] = (double)it;
+    };
+    if (act) {
+        if (k == 0 && row < NP) pv[row] = z;
+        const double wrz = rows16(r * z), wrr = rows16(r * r);
+        if (lane == 0) red_zr[wave] = double2{wrz, wrr};
     }
     lds_barrier();
-    return (int)s_red2[0];
+    double rz, rr0;
+    total2(rz, rr0);
+    const double bnorm = sqrt(rr0);
+    const double thr = tol_rel * bnorm;
+    int it = 0;
+    if (bnorm > 0.0) {
+#pragma clang loop unroll(disable)
+        while (it < max_it) {
+            if (act) {
+                // s = A z (z published in pv), then q = s + beta q, p = z + beta p
+                double sp[4] = {0.0, 0.0, 0.0, 0.0};
+                const double2* pz = reinterpret_cast<const double2*>(pv + 32 * k);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const double2 v = pz[j];
+                    sp[(2 * j) & 3] += a[2 * j] * v.x;
+                    sp[(2 * j + 1) & 3] += a[2 * j + 1] * v.y;
+                }
+                double sv = (sp[0] + sp[1]) + (sp[2] + sp[3]);
+                sv += __shfl_xor(sv, 16);
+                sv += __shfl_xor(sv, 32);
+                q = sv + beta * q;
+                p = z + beta * p;
+                const double wpq = rows16(vr ? p * q : 0.0);
+                if (lane == 0) red_pq[wave] = wpq;
+            }
+            lds_barrier();
+            if (act) {
+                const double alpha = rz / total(red_pq);
+                x += alpha * p;
+                r -= alpha * q;
+                z = r * id;
+                const double wrz = rows16(vr ? r * z : 0.0), wrr = rows16(vr ? r * r : 0.0);
+                if (lane == 0) red_zr[wave] = double2{wrz, wrr};
+                if (k == 0 && row < NP) pv[row] = z;
+            }
+            lds_barrier();
+            ++it;
+            double rzn, rrn;
+            total2(rzn, rrn);
+            if (!(sqrt(rrn) > thr)) break;   // also stops on NaN; the same bits in every wave
+            beta = rzn / rz;
+            rz = rzn;
+        }
+    }
+    if (k == 0 && vr) xsol[row] = x;
+    lds_barrier();
+    return it;
 }
 
 struct CtrlWords {
@@ -1744,11 +1780,13 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done,
                                              int seq) {
     __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
-    __shared__ double dg[NP], bsv[NP], bpv[NP], hdv[NP], xs[NP];
+    __shared__ __attribute__((aligned(16))) double dg[NP];   // also the PCG's vector (16-byte reads)
+    __shared__ double bsv[NP], bpv[NP], hdv[NP], xs[NP];
     __shared__ __attribute__((aligned(16))) double yv[NP];
     __shared__ int perm[NP], iperm[NP];
     __shared__ int s_flags[4];
-    __shared__ double s_red[CT / 64], s_lam, s_pcg[48];
+    __shared__ double s_red[CT / 64], s_lam;
+    __shared__ __attribute__((aligned(16))) double s_pcg[48];
     __shared__ double s_pm[2][LH_PMAX * 12];
     __shared__ double s_trig[LH_PMAX][4], s_qT[LH_PMAX][4];
 
@@ -3186,7 +3224,7 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
                                                    double* __restrict__ x, int solver, double tol, int max_it,
                                                    int* __restrict__ iters) {
     __shared__ double A[(NP + 1) * AS];
-    __shared__ double dg[NP];
+    __shared__ __attribute__((aligned(16))) double dg[NP];
     __shared__ __attribute__((aligned(16))) double xsol[NP];
     __shared__ int perm[NP];
     const int tid = threadIdx.x, NE = (n + 15) & ~15;
@@ -3213,7 +3251,7 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     if (tid < NE) A[NP * AS + tid] = tid < n ? b[perm[tid]] : 0.0;
     lds_barrier();
     if (solver == 1) {
-        __shared__ double s_pcg[48];
+        __shared__ __attribute__((aligned(16))) double s_pcg[48];
         const int its = lds_pcg_solve(A, xsol, dg, s_pcg, n, tid, tol, (max_it > 0 ? max_it : 2 * n) + 1);
         if (tid == 0 && iters) *iters = its;
     } else {

@@ -88,7 +88,9 @@ def test_gpu_pcg_probe_matches_oracle(n):
     assert lib.lh_debug_pcg_probe(St.data_ptr(), bt.data_ptr(), n, 1e-6, 0, xt.data_ptr(), C.byref(it)) == 0
     x = xt.cpu().numpy()
     xo, so = ob.pcg_solve(S, b)
-    assert abs(it.value - so) <= 1
+    # these random systems take more steps than rows (n = 96: ~155), so rounding shapes the tail of the
+    # convergence and the step count moves with the order of the sums (the oracle's are sequential)
+    assert abs(it.value - so) <= max(2, 0.03 * so)
     assert np.linalg.norm(S @ x - b) <= 1.01e-6 * np.linalg.norm(b)
     assert np.linalg.norm(x - xo) <= 1e-5 * np.linalg.norm(xo)
 
