@@ -457,13 +457,30 @@ struct LinCfg {
 // butterfly sum over the aligned lane group of G = 1 << lg lanes (every lane gets the total):
 // v + v[lane^1], + [lane^2], + [lane^4], ... in that order.  Partners within a 16-lane row come
 // through DPP (plain VALU: quad_perm for ^1 and ^2, row rotations for ^4 and ^8); ^16 and ^32
-// through ds_bpermute.
+// through the permlane swaps.
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
     const long long x = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// v + v[lane ^ 16] and v + v[lane ^ 32] by the gfx950 half-row / half-wave swaps (plain VALU, no LDS
+// round trip as ds_bpermute takes).  With both operands v, permlane16_swap returns v[lane & ~16] and
+// v[lane | 16], permlane32_swap v[lane & 31] and v[32 + (lane & 31)]: their sum is v + the partner in
+// every lane (IEEE addition commutes, so the bits are those of v + partner).
+__device__ __forceinline__ double xor16_sum(double v) {
+    const long long x = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(x >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ double xor32_sum(double v) {
+    const long long x = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(x >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
 }
 
 // N values at once: one uniform branch per level and N independent DPP + add chains per level
@@ -492,11 +509,11 @@ __device__ __forceinline__ void group_sum(double (&v)[N], int lg) {
     }
     if (lg >= 5) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], 16);
+        for (int i = 0; i < N; ++i) v[i] = xor16_sum(v[i]);
     }
     if (lg >= 6) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], 32);
+        for (int i = 0; i < N; ++i) v[i] = xor32_sum(v[i]);
     }
 }
 
@@ -1537,8 +1554,8 @@ __device__ __forceinline__ int lds_pcg_solve(double* __restrict__ A, double* __r
                     sp[(2 * j + 1) & 3] += a[2 * j + 1] * v.y;
                 }
                 double sv = (sp[0] + sp[1]) + (sp[2] + sp[3]);
-                sv += __shfl_xor(sv, 16);
-                sv += __shfl_xor(sv, 32);
+                sv = xor16_sum(sv);
+                sv = xor32_sum(sv);
                 q = sv + beta * q;
                 p = z + beta * p;
                 const double wpq = rows16(vr ? p * q : 0.0);
@@ -2378,7 +2395,9 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 
 // fixed-order workgroup sum of one value per thread (every thread gets the total); red: 16 doubles
 __device__ __forceinline__ double wg_sum(double v, double* red, int lane, int wave) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    double g[1] = {v};
+    group_sum(g, 6);   // DPP and permlane butterflies, lane ^ 1 .. ^ 32
+    v = g[0];
     if (lane == 0) red[wave] = v;
     lds_barrier();
     double t = 0.0;
