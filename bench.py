@@ -136,6 +136,42 @@ def native_oracle():
         return None, "-O3 -ffp-contract=off -fopenmp (parity build; native build failed)"
 
 
+def cxx_caller_ms(w, reps):
+    """Median wall time of lh_solve on this window from the compiled C++ caller (tests/abi_caller.cpp,
+    window file format there), or None when the binary is missing or fails."""
+    exe = os.path.join(ROOT, "lego-slam_amd", "lib", "abi_caller")
+    if not os.path.exists(exe):
+        return None
+    O = len(w["obs_pose"])
+    ext = w.get("cam_ext")
+    fixed = w.get("pose_fixed")
+    with tempfile.TemporaryDirectory() as td:
+        win, res = os.path.join(td, "w.bin"), os.path.join(td, "r.bin")
+        with open(win, "wb") as f:
+            np.array([len(w["pose_Tcw"]), len(w["lm_xyz"])], np.int32).tofile(f)
+            np.array([O], np.int64).tofile(f)
+            np.array([0 if ext is None else len(ext), 0 if fixed is None else 1], np.int32).tofile(f)
+            np.asarray(w["K"], np.float64).tofile(f)
+            np.asarray(w["pose_Tcw"], np.float64).tofile(f)
+            if fixed is not None:
+                np.asarray(fixed, np.uint8).tofile(f)
+            np.asarray(w["lm_xyz"], np.float64).tofile(f)
+            np.asarray(w["obs_pose"], np.uint32).tofile(f)
+            np.asarray(w["obs_lm"], np.uint32).tofile(f)
+            np.asarray(w["obs_cam"] if w.get("obs_cam") is not None else np.zeros(O), np.uint8).tofile(f)
+            np.asarray(w["obs_uv"], np.float64).tofile(f)
+            if ext is not None:
+                np.asarray(ext, np.float64).tofile(f)
+        try:
+            r = subprocess.run([exe, win, res, str(reps)], capture_output=True, text=True, timeout=120)
+        except subprocess.TimeoutExpired:
+            return None
+        for line in r.stdout.splitlines():
+            if "lh_solve median" in line:
+                return round(float(line.split("lh_solve median")[1].split()[0]), 3)
+    return None
+
+
 def make_window(name, family, seed, rank, world):
     """Rank `rank`'s landmark shard of workload `name` (all of it with world = 1), generated directly."""
     from windows import STABLE
@@ -343,13 +379,17 @@ def main():
         runs.append(((time.perf_counter() - t0) * 1e3, r))
     runs.sort(key=lambda x: x[0])
     ms_h, rh = runs[2]
+    cxx = cxx_caller_ms(w, 15)
     out["host_buffer_path"] = {"ms_per_solve": round(ms_h, 3), "iterations_per_s": round(rh["iterations"] / ms_h * 1e3, 3),
+                               "cxx_caller_ms_per_solve": cxx,
+                               "cxx_caller_iterations_per_s": round(rh["iterations"] / cxx * 1e3, 3) if cxx else None,
                                "prep_ms": round(rh["time_prep_ms"], 3),
                                "copies_ms": round(rh["time_upload_ms"] - rh["time_prep_ms"], 3),
                                "solve_ms": round(rh["time_ms"], 3), "download_ms": round(rh["time_download_ms"], 3),
                                "note": "lh_solve(window in host memory): planner (prep) + pinned host-to-device copies + "
                                        "solve + outputs (poses, landmarks, per-edge rho) back into the caller's output arrays "
-                                       "(allocated once); median of 5"}
+                                       "(allocated once); median of 5, from Python; cxx_caller_*: the same call from the "
+                                       "compiled C++ caller (tests/abi_caller.cpp, the INTEGRATION.md flow), median of 15"}
     sh.close()
     # C4 on one GPU: the base of the N-GPU scaling ratio (SCALE lines run C4 sharded)
     if name == "C3":

@@ -20,5 +20,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r03p/st -o st -
     python3 bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/r03p/st.log 2>&1 || exit 1
 cp "$(find gpurun_out/r03p/st -name '*kernel_stats.csv' | head -1)" gpurun_out/r03p/r03_rocprof_kernel_stats_all.csv
 rm -rf gpurun_out/r03p/st gpurun_out/pmc/*/
+# the bench line reads the committed trace / PMC files: use this run's
+cp gpurun_out/r03p/r03_rocprof_k_lin.json gpurun_out/r03p/r03_pmc_k_lin.json profiles/
 timeout -k 10 400 python3 bench.py > gpurun_out/r03p/r03_bench.json 2> gpurun_out/r03p/r03_bench.err || exit 1
 tail -c 3000 gpurun_out/r03p/r03_bench.json

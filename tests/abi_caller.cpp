@@ -4,7 +4,11 @@
 // binary file, runs the reference's outlier pass (lh_classify_outliers, :163-194) and writes the
 // write-back values (:198-217) to an output file the test compares with the oracle.
 //
-//   abi_caller <window.bin> <result.bin>
+//   abi_caller <window.bin> <result.bin> [reps]
+//
+// With reps > 0 the same window is then solved reps more times into the same output buffers (the
+// caller's own, as Backend::Optimize keeps them), and the median wall time of one lh_solve is printed:
+// the drop-in call's cost as a C++ caller pays it (bench.py's host_buffer_path reports it).
 //
 // window.bin:  int32 P, int32 L, int64 O, int32 ncam, int32 has_fixed, double K[4],
 //              double pose[P][12], uint8 fixed[P] (if has_fixed), double lm[L][3],
@@ -13,6 +17,8 @@
 // result.bin:  int32 status, int32 iterations, int32 trials, int32 accepted, double chi2_initial,
 //              double chi2_final, double chi2_th, int64 n_inlier, int64 n_outlier,
 //              double pose[P][12], double lm[L][3], double edge_robust_chi2[O], uint8 is_outlier[O]
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -27,7 +33,8 @@ void wr(FILE* f, const T* p, size_t n) { if (n) fwrite(p, sizeof(T), n, f); }
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc != 3) { fprintf(stderr, "usage: %s window.bin result.bin\n", argv[0]); return 2; }
+    if (argc != 3 && argc != 4) { fprintf(stderr, "usage: %s window.bin result.bin [reps]\n", argv[0]); return 2; }
+    const int reps = argc == 4 ? atoi(argv[3]) : 0;
     FILE* f = fopen(argv[1], "rb");
     if (!f) { perror(argv[1]); return 2; }
     int32_t P = 0, L = 0, ncam = 0, has_fixed = 0;
@@ -74,6 +81,18 @@ int main(int argc, char** argv) {
     res.lm_xyz = lm_out.data();
     res.edge_robust_chi2 = rchi2.data();
     st = lh_solve(h, &win, &res);
+    if (st == LH_OK && reps > 0) {
+        std::vector<double> ms;
+        for (int i = 0; i < reps && st == LH_OK; ++i) {
+            const auto t0 = std::chrono::steady_clock::now();
+            st = lh_solve(h, &win, &res);
+            ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+        std::sort(ms.begin(), ms.end());
+        printf("abi_caller: lh_solve median %.4f ms over %d (min %.4f): prep %.4f upload %.4f solve %.4f download %.4f\n",
+               ms[ms.size() / 2], (int)ms.size(), ms[0], res.time_prep_ms, res.time_upload_ms, res.time_ms,
+               res.time_download_ms);
+    }
 
     // outlier pass (backend_lego.cpp:163-194)
     std::vector<uint8_t> is_outlier(O);
