@@ -474,6 +474,18 @@ def main():
                   "iterations_per_solve": ip / npcg, "pcg_steps_per_solve": rp["pcg_iterations"],
                   "chi2_rel_vs_ldlt": abs(rp["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
     sp.close()
+    # the same window with lh_options.precision = FP32_RESID (BASELINE config 2's "fp32 residuals + fp64
+    # accumulate"): k_lin's time and the solve's chi2 against the fp64 value line
+    sf = lego_ba.Solver(device=local, precision=lego_ba.LH_PREC_FP32_RESID)
+    sf.upload(w)
+    sf.solve_resident()
+    nf = max(3, min(20, args.steps // 4))
+    df, itf, tf, rf = time_solves(sf, nf, barrier)
+    out["fp32_resid"] = {"ms_per_solve": round(df / nf * 1e3, 4), "iterations_per_s": round(itf / df, 3),
+                         "iterations_per_solve": itf / nf, "trials_per_solve": tf / nf,
+                         "k_lin_ms": round(sf.time_lin_ms(reps=50), 5), "chi2_final": rf["chi2_final"],
+                         "chi2_rel_vs_fp64": abs(rf["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
+    sf.close()
     # a 64-keyframe window of C3's size (windows past 21 keyframes, the reduced
     # system of 384 rows solved in global memory by k_ctrl_g), against the oracle's final chi2
     from windows import STABLE

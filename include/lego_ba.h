@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define LH_ABI_VERSION 3
+#define LH_ABI_VERSION 4
 
 typedef enum lh_status {
     LH_OK = 0,
@@ -57,6 +57,13 @@ typedef enum lh_strategy { LH_STRATEGY_DEFAULT = 0, LH_STRATEGY_1 = 1 } lh_strat
    PCG is the reference's Jacobi-PCG (Problem::PCGSolver, :584-614), which it left commented out
    (:422), with its first-step bug fixed (:595-596 never add alpha*p to x). */
 typedef enum lh_linear_solver { LH_SOLVER_LDLT = 0, LH_SOLVER_PCG = 1 } lh_linear_solver;
+
+/* Arithmetic of the per-edge path.  FP64: double throughout, the residual a bitwise
+   mirror of the reference's (lego_types.h:200-216).  FP32_RESID: the camera point, residual, Huber
+   weight and Jacobians of each edge in float, every sum over edges (H blocks, b, chi2, the Schur
+   complement) in double: BASELINE config 2's "fp32 residuals + fp64 accumulate".  Parity to
+   tolerance, not to the bit. */
+typedef enum lh_precision { LH_PREC_FP64 = 0, LH_PREC_FP32_RESID = 1 } lh_precision;
 
 /* The per-trial exchange of a landmark-sharded solve (world_size > 1): RCCL on the handle's stream
    (one process per GPU), or a caller-supplied all-reduce over host buffers (any transport: MPI, gloo,
@@ -104,6 +111,8 @@ typedef struct lh_options {
                                  use: affinity mask capped by the cgroup CPU quota, <= 8)        */
     lh_allreduce_fn allreduce;  /* LH_COMM_HOST: the exchange                                    */
     void *allreduce_user;       /* its first argument                                            */
+    /* ---- ABI 4 ---- */
+    int32_t precision;        /* lh_precision (default LH_PREC_FP64)                             */
 } lh_options;
 
 /*

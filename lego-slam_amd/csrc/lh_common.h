@@ -129,6 +129,6 @@ struct lh_params {
     double huber_delta, stop_dchi2, tau, lambda_cap, lambda_init;
     double pcg_tol;         // PCG stop: ||r|| <= pcg_tol ||b|| (reference 1e-6, problem.cpp:597)
     int32_t pcg_max_it;     // PCG cap (<= 0: 2 * rows, problem.cpp:422)
-    int32_t pad_;
+    int32_t precision;      // lh_precision: 0 fp64 throughout, 1 fp32 per-edge residual/Jacobians (k_lin<T, TRIAL, true>)
     double K[4];
 };

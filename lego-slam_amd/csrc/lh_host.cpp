@@ -555,6 +555,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     prm.strategy = h->opt.strategy;
     prm.guard = h->opt.degenerate_guard;
     prm.gate_mode = h->opt.gate_mode;
+    prm.precision = h->opt.precision;
     prm.lambda_given = h->opt.lambda_init >= 0.0;
     prm.ext_identity = ext_identity;
     prm.ext_rot_identity = ext_rot_identity;
@@ -838,7 +839,8 @@ int check_rank_options(lh_handle* h) {
     const double v[] = {(double)o.max_iters, (double)o.max_trials, (double)o.strategy, o.huber_delta, o.stop_dchi2,
                         o.tau, o.lambda_cap, o.lambda_init, (double)o.linear_solver, (double)o.world_size,
                         (double)o.degenerate_guard, (double)depth, (double)o.pcg_max_iters, o.pcg_tol,
-                        (double)o.gate_mode, (double)o.chunk_landmarks > 0 ? 1.0 : 0.0, (double)o.comm_mode};
+                        (double)o.gate_mode, (double)o.chunk_landmarks > 0 ? 1.0 : 0.0, (double)o.comm_mode,
+                        (double)o.precision};
     constexpr int n = (int)(sizeof(v) / sizeof(v[0]));
     double buf[2 * n];
     for (int i = 0; i < n; ++i) { buf[i] = v[i]; buf[n + i] = -v[i]; }
@@ -915,6 +917,7 @@ void lh_default_options(lh_options* o) {
     o->host_threads = 0;
     o->allreduce = nullptr;
     o->allreduce_user = nullptr;
+    o->precision = LH_PREC_FP64;
 }
 
 int lh_comm_unique_id(uint8_t out[128]) {
@@ -936,6 +939,7 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     if (opt->linear_solver != LH_SOLVER_LDLT && opt->linear_solver != LH_SOLVER_PCG) return LH_E_BADARG;
     if (opt->linear_solver == LH_SOLVER_PCG && !(opt->pcg_tol >= 0.0)) return LH_E_BADARG;
     if (opt->gate_mode != 0 && opt->gate_mode != 1) return LH_E_BADARG;
+    if (opt->precision != LH_PREC_FP64 && opt->precision != LH_PREC_FP32_RESID) return LH_E_BADARG;
     if (opt->degenerate_guard != 0 && opt->degenerate_guard != 1) return LH_E_BADARG;
     if (opt->chunk_landmarks < 0 || opt->host_threads < 0) return LH_E_BADARG;
     if (opt->comm_mode != LH_COMM_RCCL && opt->comm_mode != LH_COMM_HOST) return LH_E_BADARG;
@@ -1128,6 +1132,7 @@ static int estimate_pose_impl(lh_handle* h, const lh_frames* in, lh_frames_resul
     prm.strategy = h->opt.strategy;
     prm.lambda_given = h->opt.lambda_init >= 0.0;
     prm.gate_mode = h->opt.gate_mode;
+    prm.precision = h->opt.precision;
     prm.huber_delta = h->opt.huber_delta;
     prm.stop_dchi2 = h->opt.stop_dchi2;
     prm.tau = h->opt.tau;

@@ -366,6 +366,91 @@ __device__ __forceinline__ void edge_jac_pc(const double Pc[3], const double* __
     }
 }
 
+// ---- lh_options.precision = LH_PREC_FP32_RESID (BASELINE config 2's "fp32 residuals + fp64
+//      accumulate"): the per-edge camera point, residual, Huber weight and Jacobians in float, widened to
+//      double before any product that is summed (H blocks, b, chi2, the Schur terms stay fp64).  Not a
+//      mirror of the reference's arithmetic: parity to tolerance (tests/test_precision.py). ----
+__device__ __forceinline__ void q_rotate_f(const double* q, const float v[3], float o[3]) {
+    const float w = (float)q[0], x = (float)q[1], y = (float)q[2], z = (float)q[3];
+    const float u0 = 2.0f * (y * v[2] - z * v[1]), u1 = 2.0f * (z * v[0] - x * v[2]), u2 = 2.0f * (x * v[1] - y * v[0]);
+    o[0] = v[0] + w * u0 + (y * u2 - z * u1);
+    o[1] = v[1] + w * u1 + (z * u0 - x * u2);
+    o[2] = v[2] + w * u2 + (x * u1 - y * u0);
+}
+
+// RES: residual and robust weight into E (else E's W is the caller's); JAC: Jacobians into E
+template <bool RES, bool JAC>
+__device__ __forceinline__ void edge_eval_f(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
+                                            bool ext_rot, const double X[3], double u, double v, const lh_params& prm,
+                                            EdgeEval& E) {
+    const float Xf[3] = {(float)X[0], (float)X[1], (float)X[2]};
+    float Pc[3];
+    q_rotate_f(pt + LH_PT_QT, Xf, Pc);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Pc[i] += (float)pt[LH_PT_TT + i];
+    if (!ext_id) {
+        if (!ext_rot) {
+            const float Pb[3] = {Pc[0], Pc[1], Pc[2]};
+            q_rotate_f(e, Pb, Pc);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pc[i] += (float)e[4 + i];
+    }
+    const float fx = (float)prm.K[0], fy = (float)prm.K[1];
+    const float zi = 1.0f / (Pc[2] + 1e-18f);
+    if (RES) {
+        const float cx = (float)prm.K[2], cy = (float)prm.K[3];
+        const float r0 = (float)u - (fx * Pc[0] + cx * Pc[2]) * zi, r1 = (float)v - (fy * Pc[1] + cy * Pc[2]) * zi;
+        const float e2 = r0 * r0 + r1 * r1;
+        float rho0 = e2, rho1 = 1.0f, rho2 = 0.0f, W00 = 1.0f, W01 = 0.0f, W11 = 1.0f;
+        const float delta = (float)prm.huber_delta;
+        if (prm.huber_delta > 0.0) {
+            const float d2 = delta * delta;
+            if (!(e2 <= d2)) {
+                const float sq = sqrtf(e2);
+                rho0 = 2.0f * sq * delta - d2;
+                rho1 = delta / sq;
+                rho2 = -0.5f * rho1 / e2;
+            }
+            W00 = rho1; W11 = rho1;
+            if (rho1 + 2.0f * rho2 * e2 > 0.0f && !(prm.gate_mode == 1 && e2 > d2)) {
+                const float s2 = 2.0f * rho2;
+                W00 += s2 * r0 * r0;
+                W01 = s2 * r0 * r1;
+                W11 += s2 * r1 * r1;
+            }
+        }
+        E.r0 = r0; E.r1 = r1; E.e2 = e2; E.rho0 = rho0; E.rho1 = rho1; E.rho2 = rho2;
+        E.W00 = W00; E.W01 = W01; E.W10 = W01; E.W11 = W11;
+    }
+    if (JAC) {
+        const float x = Pc[0], y = Pc[1], zi2 = zi * zi;
+        float J[12];
+        J[0] = -fx * zi;               J[1] = 0.0f;                   J[2] = fx * x * zi2;
+        J[3] = fx * x * y * zi2;       J[4] = -fx - fx * x * x * zi2; J[5] = fx * y * zi;
+        J[6] = 0.0f;                   J[7] = -fy * zi;               J[8] = fy * y * zi2;
+        J[9] = fy + fy * y * y * zi2;  J[10] = -fy * x * y * zi2;    J[11] = -fy * x * zi;
+        float A[6];
+        if (ext_rot) {
+            A[0] = J[0]; A[1] = 0.0f; A[2] = J[2]; A[3] = 0.0f; A[4] = J[7]; A[5] = J[8];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                A[j] = J[0] * (float)e[7 + j] + J[2] * (float)e[13 + j];
+                A[3 + j] = J[7] * (float)e[10 + j] + J[8] * (float)e[13 + j];
+            }
+        }
+        const double* Rt = pt + LH_PT_RT;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                E.Jl[3 * i + j] = (double)(A[3 * i] * (float)Rt[j] + A[3 * i + 1] * (float)Rt[3 + j] + A[3 * i + 2] * (float)Rt[6 + j]);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) E.Jp[k] = (double)J[k];
+    }
+}
+
 // J(r, a) of j_i (2 x 6) is structurally zero: J(0, 1), J(1, 0)
 __device__ __forceinline__ constexpr bool jz(int r, int a) { return (r == 0 && a == 1) || (r == 1 && a == 0); }
 
@@ -519,7 +604,7 @@ __device__ __forceinline__ void group_sum(double (&v)[N], int lg) {
 
 static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
 
-template <int T, bool TRIAL>
+template <int T, bool TRIAL, bool F32>
 __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const float* __restrict__ obs_uv,
     const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
@@ -709,15 +794,24 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (live) {
                 const double* pt = wt_c + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
-                double Pc[3];
-                if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
-                    E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
-                    edge_pc(pt, e, ext_id, ext_rot, X, Pc);
+                if constexpr (F32) {
+                    if (wfl) {
+                        E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+                        edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+                    } else {
+                        edge_eval_f<true, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+                    }
                 } else {
-                    edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                    edge_robust(E, prm);
+                    double Pc[3];
+                    if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
+                        E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+                        edge_pc(pt, e, ext_id, ext_rot, X, Pc);
+                    } else {
+                        edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                        edge_robust(E, prm);
+                    }
+                    edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
                 }
-                edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
                 const double* d = wdx + 6 * slot;
                 double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
@@ -756,9 +850,13 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (has) {
                 const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
-                double Pc[3];
-                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                edge_robust(E, prm);
+                if constexpr (F32) {
+                    edge_eval_f<true, false>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+                } else {
+                    double Pc[3];
+                    edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                    edge_robust(E, prm);
+                }
                 edge_rho[o] = E.rho0;
                 chi_acc += E.rho0;
             }
@@ -781,10 +879,14 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         if (has) {
             const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
             EdgeEval E;
-            double Pc[3];
-            edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-            edge_robust(E, prm);
-            edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
+            if constexpr (F32) {
+                edge_eval_f<true, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+            } else {
+                double Pc[3];
+                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                edge_robust(E, prm);
+                edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
+            }
             edge_rho[o] = E.rho0;
             chi_acc += E.rho0;
             const bool inl = prm.huber_delta <= 0.0 || E.e2 <= prm.huber_delta * prm.huber_delta;
@@ -3082,12 +3184,18 @@ size_t lh_lin_smem(int T, int ncam) {
 // device's per-workgroup LDS (hipDeviceAttributeMaxSharedMemoryPerBlock, read once by the host, which
 // also rejects windows whose chunks would exceed it), before any launch.
 hipError_t lh_prepare_lin(int lds_limit) {
-    const void* fns[] = {reinterpret_cast<const void*>(&k_lin<1, false>), reinterpret_cast<const void*>(&k_lin<1, true>),
-                         reinterpret_cast<const void*>(&k_lin<2, false>), reinterpret_cast<const void*>(&k_lin<2, true>),
-                         reinterpret_cast<const void*>(&k_lin<3, false>), reinterpret_cast<const void*>(&k_lin<3, true>),
-                         reinterpret_cast<const void*>(&k_lin<4, false>), reinterpret_cast<const void*>(&k_lin<4, true>),
-                         reinterpret_cast<const void*>(&k_lin<5, false>), reinterpret_cast<const void*>(&k_lin<5, true>),
-                         reinterpret_cast<const void*>(&k_lin<6, false>), reinterpret_cast<const void*>(&k_lin<6, true>)};
+    const void* fns[] = {reinterpret_cast<const void*>(&k_lin<1, false, false>), reinterpret_cast<const void*>(&k_lin<1, true, false>),
+                         reinterpret_cast<const void*>(&k_lin<2, false, false>), reinterpret_cast<const void*>(&k_lin<2, true, false>),
+                         reinterpret_cast<const void*>(&k_lin<3, false, false>), reinterpret_cast<const void*>(&k_lin<3, true, false>),
+                         reinterpret_cast<const void*>(&k_lin<4, false, false>), reinterpret_cast<const void*>(&k_lin<4, true, false>),
+                         reinterpret_cast<const void*>(&k_lin<5, false, false>), reinterpret_cast<const void*>(&k_lin<5, true, false>),
+                         reinterpret_cast<const void*>(&k_lin<6, false, false>), reinterpret_cast<const void*>(&k_lin<6, true, false>),
+                         reinterpret_cast<const void*>(&k_lin<1, false, true>), reinterpret_cast<const void*>(&k_lin<1, true, true>),
+                         reinterpret_cast<const void*>(&k_lin<2, false, true>), reinterpret_cast<const void*>(&k_lin<2, true, true>),
+                         reinterpret_cast<const void*>(&k_lin<3, false, true>), reinterpret_cast<const void*>(&k_lin<3, true, true>),
+                         reinterpret_cast<const void*>(&k_lin<4, false, true>), reinterpret_cast<const void*>(&k_lin<4, true, true>),
+                         reinterpret_cast<const void*>(&k_lin<5, false, true>), reinterpret_cast<const void*>(&k_lin<5, true, true>),
+                         reinterpret_cast<const void*>(&k_lin<6, false, true>), reinterpret_cast<const void*>(&k_lin<6, true, true>)};
     for (const void* f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_limit);
         if (e != hipSuccess) return e;
@@ -3106,8 +3214,12 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
         const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
-        hipLaunchKernelGGL((k_lin<TT, TR>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, dxp, \
-                           edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base);             \
+        if (prm.precision == 1)                                                                                    \
+            hipLaunchKernelGGL((k_lin<TT, TR, true>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
+                               dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base);    \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_lin<TT, TR, false>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
+                               dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base);    \
     } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;

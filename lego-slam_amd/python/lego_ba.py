@@ -121,8 +121,9 @@ def config_window(name, seed=0, **kw):
 # --------------------------------------------------------------------------
 
 LH_OK, LH_E_EMPTY, LH_E_BADARG, LH_E_HIP, LH_E_RCCL, LH_E_UNSUPPORTED, LH_E_STATE = range(7)
-LH_ABI_VERSION = 3
+LH_ABI_VERSION = 4
 LH_SOLVER_LDLT, LH_SOLVER_PCG = 0, 1
+LH_PREC_FP64, LH_PREC_FP32_RESID = 0, 1
 LH_COMM_RCCL, LH_COMM_HOST = 0, 1
 
 # lh_allreduce_fn: int (*)(void* user, double* buf, int64_t count, int32_t op)   (op 0 sum, 1 max)
@@ -140,6 +141,7 @@ class LhOptions(C.Structure):
         ("pcg_tol", C.c_double), ("comm_id", C.c_uint8 * 128),
         ("gate_mode", C.c_int32), ("chunk_landmarks", C.c_int32), ("comm_mode", C.c_int32),
         ("host_threads", C.c_int32), ("allreduce", C.c_void_p), ("allreduce_user", C.c_void_p),
+        ("precision", C.c_int32),
     ]
 
 

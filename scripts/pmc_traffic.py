@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 root, out_path, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-kern = "k_lin<3, true>"
+kern = "k_lin<3, true, false>"
 vals = defaultdict(list)
 for f in glob.glob(f"{root}/*/*_counter_collection.csv"):
     per = defaultdict(float)

@@ -58,7 +58,7 @@ int main(void) {
   P(lh_options, huber_delta) P(lh_options, linear_solver) P(lh_options, comm_id) P(lh_options, profile)
   P(lh_options, pcg_max_iters) P(lh_options, pcg_tol)
   P(lh_options, gate_mode) P(lh_options, chunk_landmarks) P(lh_options, comm_mode) P(lh_options, host_threads)
-  P(lh_options, allreduce) P(lh_options, allreduce_user)
+  P(lh_options, allreduce) P(lh_options, allreduce_user) P(lh_options, precision)
   P(lh_window, n_obs) P(lh_window, K) P(lh_window, cam_ext)
   P(lh_result, trace_cap) P(lh_result, chi2_initial) P(lh_result, time_ms) P(lh_result, pcg_iterations)
   P(lh_result, degenerate) P(lh_result, time_prep_ms) P(lh_result, time_upload_ms) P(lh_result, time_download_ms)
@@ -90,7 +90,8 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
 
 def test_default_options_mirror_reference_constants():
     o = lego_ba.default_options()
-    assert o.abi_version == lego_ba.LH_ABI_VERSION == 3
+    assert o.abi_version == lego_ba.LH_ABI_VERSION == 4
+    assert o.precision == lego_ba.LH_PREC_FP64          # double throughout: the residual mirrors the reference
     assert o.gate_mode == 0 and o.degenerate_guard == 0   # the reference's Huber gate and LU semantics
     assert o.comm_mode == lego_ba.LH_COMM_RCCL and o.chunk_landmarks == 0 and not o.allreduce
     assert o.linear_solver == lego_ba.LH_SOLVER_LDLT   # Eigen LDLT     problem.cpp:420

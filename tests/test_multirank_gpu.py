@@ -187,7 +187,7 @@ def _create_main(rank, world, port, opts_per_rank, q):
 
 
 @pytest.mark.parametrize("opts", [[{}, {}], [{"max_iters": 10}, {"max_iters": 9}], [{}, {"huber_delta": 1.0}],
-                                  [{"gate_mode": 1}, {}]])
+                                  [{"gate_mode": 1}, {}], [{"precision": 1}, {}]])
 def test_ranks_must_agree_on_solver_options(opts):
     """lh_create compares the solver options across ranks (one MAX all-reduce): ranks that would
     issue different collective counts per solve (or decide differently) are refused on every rank."""
