@@ -602,6 +602,22 @@ __device__ __forceinline__ void group_sum(double (&v)[N], int lg) {
     }
 }
 
+// max over the wave, every lane gets it: DPP within 16-lane rows, then the permlane swaps
+__device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, dpp_d<0xB1>(v));                                            // ^1
+    v = fmax(v, dpp_d<0x4E>(v));                                            // ^2
+    v = fmax(v, (__lane_id() & 4) ? dpp_d<0x124>(v) : dpp_d<0x12C>(v));     // ^4
+    v = fmax(v, dpp_d<0x128>(v));                                           // ^8
+    const long long x = __double_as_longlong(v);
+    auto lo = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(x >> 32), false, false);
+    v = fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]), __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
+    const long long y = __double_as_longlong(v);
+    lo = __builtin_amdgcn_permlane32_swap((unsigned)y, (unsigned)y, false, false);
+    hi = __builtin_amdgcn_permlane32_swap((unsigned)(y >> 32), (unsigned)(y >> 32), false, false);
+    return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]), __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
+}
+
 static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
 
 template <int T, bool TRIAL, bool F32>
@@ -1009,11 +1025,11 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     }
 
     // ---- combine the 4 waves, (w0 + w2) + (w1 + w3), and write the chunk slab ----
-    for (int off = 32; off > 0; off >>= 1) {
-        chi_acc += __shfl_xor(chi_acc, off);
-        scale_acc += __shfl_xor(scale_acc, off);
-        ndeg += __shfl_xor(ndeg, off);
-        maxd = fmax(maxd, __shfl_xor(maxd, off));
+    {   // the wave's totals: DPP and permlane butterflies (no LDS round trips); max |diag H_ll| likewise
+        double t3[3] = {chi_acc, scale_acc, ndeg};
+        group_sum(t3, 6);
+        chi_acc = t3[0]; scale_acc = t3[1]; ndeg = t3[2];
+        maxd = wave_max(maxd);
     }
     STAMP(9);
     lds_barrier();
