@@ -478,6 +478,8 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         HIPCHK(h->d_gS.ensure(2 * ng * ng));
         if (fresh_s) HIPCHK(hipMemsetAsync(h->d_gS.p, 0, h->d_gS.n * sizeof(double), h->stream));
     }
+    if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_PCG)   // k_ctrl_p's row-contiguous copy of S (36 per block-row entry)
+        HIPCHK(h->d_gA.ensure(pl.brow_ent.size() * 36));
     HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
     HIPCHK(h->d_maxd.ensure(1));
     HIPCHK(h->d_fixed.ensure(pl.fixed_bits.size()));

@@ -2529,10 +2529,12 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
                                                const int32_t* __restrict__ brow_ptr, const uint32_t* __restrict__ brow_ent,
                                                double* __restrict__ pose_mat, double* __restrict__ ptab,
                                                const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
-                                               int mode, volatile int* __restrict__ host_done, int seq) {
+                                               int mode, volatile int* __restrict__ host_done, int seq,
+                                               double* __restrict__ ell) {
     __shared__ double pv[PNMAX], bpv[PNMAX], hdv[PNMAX], xs[PNMAX];
     __shared__ int s_flags[4];
-    __shared__ double s_red[3][CT / 64], s_lam;
+    __shared__ __attribute__((aligned(16))) double s_red[3][CT / 64];
+    __shared__ double s_lam;
     __shared__ double s_pm[2][LH_PMAX_ANY * 12];
     __shared__ double s_trig[LH_PMAX_ANY][4], s_qT[LH_PMAX_ANY][4];
 
@@ -2605,64 +2607,117 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         pp[u] = z[u];
         if (in) { bpv[r] = src[LY.off_bp + r]; hdv[r] = src[LY.off_hd + r]; }
     }
-    double t0 = 0.0, t1 = 0.0;
+    // Each row's entries gathered once per solve into row-contiguous scratch: entry e of pose p's block
+    // row holds S(6p + a, 6q + c) at ell[(6 e + a) * 6 + c], the damped diagonal in place.  A step's
+    // S p then reads 48 contiguous bytes per entry, at addresses that need no index word first (the
+    // walk over the packed blocks put two dependent L2 round trips per entry on the chain).
 #pragma unroll
-    for (int u = 0; u < PRT; ++u) { t0 += rr[u] * z[u]; t1 += rr[u] * rr[u]; }
-    double rz = wg_sum(t0, s_red[0], lane, wave);
-    const double bb = wg_sum(t1, s_red[1], lane, wave);
+    for (int u = 0; u < PRT; ++u) {
+        const int r = tid + CT * u;
+        if (r >= n) continue;
+        const int p = r / 6, a = r - 6 * p;
+        for (int e = e0[u]; e < e1[u]; ++e) {
+            const uint32_t en = brow_ent[e];
+            const int q = (int)((en >> 1) & 0xFFF);
+            const double* blk = Sb + (size_t)(en >> 13) * 36;
+            double* dst = ell + ((size_t)6 * e + a) * 6;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                double val = (en & 1u) ? blk[6 * c + a] : blk[6 * a + c];   // (q, p) read transposed
+                if (!(en & 1u) && q == p && c == a) val = dr[u];              // the damped diagonal
+                dst[c] = val;
+            }
+        }
+    }
+    __syncthreads();   // the scratch is read back by the same threads: global stores visible to the loads below
+    // Two barriers per step: z is published in pv and one product serves the step, q = (S + lambda D) z +
+    // beta q_prev and p = z + beta p_prev (the same recurrence regrouped, as k_ctrl's PCG).  The dot
+    // products are fixed-order sums (wave butterflies, then the 16 wave partials in order).
+    double2* red2 = reinterpret_cast<double2*>(&s_red[1][0]);   // [16] (r.z, r.r) partials (s_red[1..2])
+    double* red_pq = s_red[0];
+    auto total2 = [&](double& tz, double& tr) {
+        tz = 0.0;
+        tr = 0.0;
+#pragma unroll
+        for (int w = 0; w < CT / 64; ++w) {
+            const double2 t = red2[w];
+            tz += t.x;
+            tr += t.y;
+        }
+    };
+    {
+        double t2[2] = {0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < PRT; ++u) {
+            t2[0] += rr[u] * z[u];
+            t2[1] += rr[u] * rr[u];
+            pp[u] = 0.0;
+            if (tid + CT * u < n) pv[tid + CT * u] = z[u];
+        }
+        group_sum(t2, 6);
+        if (lane == 0) red2[wave] = double2{t2[0], t2[1]};
+    }
+    lds_barrier();
+    double rz, bb;
+    total2(rz, bb);
     const double thr = prm.pcg_tol * sqrt(bb);
     const int maxit = prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n;
     int steps = 0;
+    double w[PRT], beta = 0.0;
+#pragma unroll
+    for (int u = 0; u < PRT; ++u) w[u] = 0.0;
     if (bb > 0.0) {
         for (;;) {
-#pragma unroll
-            for (int u = 0; u < PRT; ++u)
-                if (tid + CT * u < n) pv[tid + CT * u] = pp[u];
-            lds_barrier();
-            // w = (S + lambda D) p, row by row over the block row, columns ascending
-            double w[PRT], pw = 0.0;
+            // s = (S + lambda D) z, row by row over the block row, columns ascending
+            double pw[1] = {0.0};
 #pragma unroll
             for (int u = 0; u < PRT; ++u) {
                 const int r = tid + CT * u;
-                const int p = r / 6, a = r - 6 * p;
+                const int a = r - 6 * (r / 6);
                 double acc = 0.0;
+#pragma unroll 2
                 for (int e = e0[u]; e < e1[u]; ++e) {
-                    const uint32_t en = brow_ent[e];
-                    const int q = (int)((en >> 1) & 0xFFF);
-                    const double* blk = Sb + (size_t)(en >> 13) * 36;
+                    const int q = (int)((brow_ent[e] >> 1) & 0xFFF);
+                    const double2* row = reinterpret_cast<const double2*>(ell + ((size_t)6 * e + a) * 6);
+                    const double2 v0 = row[0], v1 = row[1], v2 = row[2];
                     const double* pq = pv + 6 * q;
-                    if (en & 1u) {   // block (q, p) read transposed: S(r, 6q + c) = blk(c, a)
-#pragma unroll
-                        for (int c = 0; c < 6; ++c) acc += blk[6 * c + a] * pq[c];
-                    } else if (q == p) {   // the diagonal block, its diagonal damped
-#pragma unroll
-                        for (int c = 0; c < 6; ++c) acc += (c == a ? dr[u] : blk[6 * a + c]) * pq[c];
-                    } else {
-#pragma unroll
-                        for (int c = 0; c < 6; ++c) acc += blk[6 * a + c] * pq[c];
-                    }
+                    acc += v0.x * pq[0];
+                    acc += v0.y * pq[1];
+                    acc += v1.x * pq[2];
+                    acc += v1.y * pq[3];
+                    acc += v2.x * pq[4];
+                    acc += v2.y * pq[5];
                 }
-                w[u] = acc;
-                pw += pp[u] * acc;
+                w[u] = acc + beta * w[u];
+                pp[u] = z[u] + beta * pp[u];
+                pw[0] += pp[u] * w[u];
             }
-            const double alpha = rz / wg_sum(pw, s_red[2], lane, wave);
-            double a0 = 0.0, a1 = 0.0;
+            group_sum(pw, 6);
+            if (lane == 0) red_pq[wave] = pw[0];
+            lds_barrier();
+            double tpw = 0.0;
+#pragma unroll
+            for (int wv = 0; wv < CT / 64; ++wv) tpw += red_pq[wv];
+            const double alpha = rz / tpw;
+            double a2[2] = {0.0, 0.0};
 #pragma unroll
             for (int u = 0; u < PRT; ++u) {
                 x[u] += alpha * pp[u];
                 rr[u] -= alpha * w[u];
                 z[u] = minv[u] * rr[u];
-                a0 += rr[u] * rr[u];
-                a1 += rr[u] * z[u];
+                a2[0] += rr[u] * z[u];
+                a2[1] += rr[u] * rr[u];
+                if (tid + CT * u < n) pv[tid + CT * u] = z[u];
             }
-            const double rrn = wg_sum(a0, s_red[0], lane, wave);
-            const double rzn = wg_sum(a1, s_red[1], lane, wave);
+            group_sum(a2, 6);
+            if (lane == 0) red2[wave] = double2{a2[0], a2[1]};
+            lds_barrier();
+            double rzn, rrn;
+            total2(rzn, rrn);
             ++steps;
             if (!(sqrt(rrn) > thr) || steps >= maxit + 1) break;   // also stops on NaN
-            const double beta = rzn / rz;
+            beta = rzn / rz;
             rz = rzn;
-#pragma unroll
-            for (int u = 0; u < PRT; ++u) pp[u] = beta * pp[u] + z[u];
         }
     }
 #pragma unroll
@@ -3279,7 +3334,7 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           const uint32_t* brow_ent) {
     if (prm.P > LH_PMAX && prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent, pose_mat,
-                           ptab, ext, dxp, prm, mode, (volatile int*)host_done, seq);
+                           ptab, ext, dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
     else if (prm.P > LH_PMAX)
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
