@@ -91,6 +91,14 @@ struct DevBuf {
 };
 
 // pinned host staging, grown on demand and reused across windows
+// A typed window into an arena (no ownership): the per-window tables share one device and one pinned
+// allocation so they cross the link as one copy (upload_impl)
+template <typename T>
+struct View {
+    T* p = nullptr;
+    size_t n = 0;
+    void release() { p = nullptr; n = 0; }
+};
 template <typename T>
 struct HostBuf {
     T* p = nullptr;
@@ -243,30 +251,40 @@ struct lh_handle {
     double last_prep_ms = 0.0, last_upload_ms = 0.0;
 
     // pinned staging of the upload
-    HostBuf<lh_chunk> s_chunks;
-    HostBuf<lh_subbatch> s_sbs;
-    HostBuf<uint32_t> s_meta, s_items, s_pair_ptr, s_rsmap;
-    HostBuf<uint16_t> s_pair_pq;
-    HostBuf<int32_t> s_obs_perm, s_lm_perm;
+    View<lh_chunk> s_chunks;                                  // the per-window tables: views into s_arena
+    View<lh_subbatch> s_sbs;
+    View<uint32_t> s_items, s_pair_ptr, s_rsmap, s_brow_ent;
+    View<uint16_t> s_pair_pq;
+    View<int32_t> s_lm_perm, s_brow_ptr;
+    View<uint64_t> s_fixed;
+    View<double> s_qt, s_ptab, s_ext;
+    HostBuf<uint8_t> s_arena;
+    size_t arena_bytes = 0;
+    HostBuf<uint32_t> s_meta;
+    HostBuf<int32_t> s_obs_perm;
     HostBuf<float> s_uv;                                     // pixels, 2 floats per slot
-    HostBuf<double> s_lm, s_qt, s_ptab, s_ext, s_rs;         // s_rs: the host-exchange buffer
+    HostBuf<double> s_lm, s_rs;                              // s_rs: the host-exchange buffer
     HostBuf<double> s_out;                                   // pinned staging of the download
     hipEvent_t ev_staging = nullptr;   // the upload's last copy out of the staging (reused by the next upload)
     bool staging_pending = false;
 
     // device buffers
-    DevBuf<lh_chunk> d_chunks;
-    DevBuf<lh_subbatch> d_sbs;
-    DevBuf<uint32_t> d_meta, d_pair_ptr, d_items, d_rsmap;
-    DevBuf<uint16_t> d_pair_pq;
-    DevBuf<int32_t> d_obs_perm, d_lm_perm;
+    View<lh_chunk> d_chunks;                                  // the per-window tables: views into d_arena
+    View<lh_subbatch> d_sbs;
+    View<uint32_t> d_pair_ptr, d_items, d_rsmap;
+    View<uint16_t> d_pair_pq;
+    View<int32_t> d_lm_perm;
+    View<double> d_ptab_init, d_qt_init, d_ext;
+    DevBuf<uint8_t> d_arena;
+    DevBuf<uint32_t> d_meta;
+    DevBuf<int32_t> d_obs_perm;
     DevBuf<float> d_uv;
-    DevBuf<double> d_lm_in, d_rec, d_ptab, d_ptab_init, d_qt, d_qt_init, d_ext, d_rho, d_rows, d_csc, d_gA, d_gS, d_rs_stage,
+    DevBuf<double> d_lm_in, d_rec, d_ptab, d_qt, d_rho, d_rows, d_csc, d_gA, d_gS, d_rs_stage,
         d_rs_commit, d_maxd, d_dxp, d_out_xyz, d_out_rho;
     DevBuf<lh_ctrl> d_ctrl;
-    DevBuf<uint64_t> d_fixed;    // fixed-pose bits (Plan::fixed_bits)
-    DevBuf<int32_t> d_brow_ptr;  // the reduced system's block rows (Plan::brow_ptr / brow_ent, k_ctrl_p)
-    DevBuf<uint32_t> d_brow_ent;
+    View<uint64_t> d_fixed;      // fixed-pose bits (Plan::fixed_bits)
+    View<int32_t> d_brow_ptr;    // the reduced system's block rows (Plan::brow_ptr / brow_ent, k_ctrl_p)
+    View<uint32_t> d_brow_ent;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
     // frontend pose-only batch (lh_estimate_pose)
     // inputs and outputs each packed into one arena, so a call is one upload and one download
@@ -404,13 +422,24 @@ void par_copy(lh_handle* h, const ByteSeg* seg, int nseg) {
     else for (int j = 0; j < (int)jobs.size(); ++j) job(j);
 }
 
+// Wait for an event by polling it: hipEventSynchronize measured ~2 ms for lh_upload's copies that the
+// solve path (which polls) sees finish within ~0.3 ms of the planner: the runtime's blocking wait
+// wakes the thread late.
+hipError_t spin_wait(hipEvent_t ev) {
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return q;
+        for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+    }
+}
+
 // sync: return only once the copies are done (lh_upload); lh_solve leaves them queued ahead of its
 // kernels on the same stream.  Either way the next upload waits for them before it rewrites the staging.
 int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     const double t0 = now_ms();
     h->uploaded = false;
     if (h->staging_pending) {
-        HIPCHK(hipEventSynchronize(h->ev_staging));
+        HIPCHK(spin_wait(h->ev_staging));
         h->staging_pending = false;
     }
     // the landmark positions need no plan: they go out first and cross the link while the planner runs
@@ -446,22 +475,51 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
 
     // ---- device buffers (before the fill: its slot batches are copied as they complete) ----
     const size_t PT = (size_t)P * ncam * LH_PT;
-    HIPCHK(h->d_chunks.ensure(pl.n_chunks));
-    HIPCHK(h->d_sbs.ensure(pl.n_sb));
+    // The per-window tables (all but the observation slots and the positions) live in one arena, on the
+    // device and in pinned staging, at the same offsets: they cross the link as one copy.  Each
+    // hipMemcpyAsync costs ~10 us of DMA-engine turnaround beside its transfer (rocprofv3 memory-copy
+    // trace of lh_upload), and the 13 small copies these were made most of the upload's tail.
+    {
+        size_t bytes = 0;
+        auto part = [&](size_t b) { const size_t o = bytes; bytes += (b + 255) & ~(size_t)255; return o; };
+        const size_t o_chunks = part(pl.n_chunks * sizeof(lh_chunk)), o_sbs = part((size_t)pl.n_sb * sizeof(lh_subbatch));
+        const size_t o_lmp = part((size_t)pl.n_rec * sizeof(int32_t)), o_pptr = part(((size_t)pl.npairs + 1) * sizeof(uint32_t));
+        const size_t o_items = part((size_t)pl.n_items * sizeof(uint32_t)), o_ppq = part(2 * (size_t)pl.npairs * sizeof(uint16_t));
+        const size_t o_rsmap = part((size_t)pl.npairs * 36 * sizeof(uint32_t)), o_ptab = part(2 * PT * sizeof(double));
+        const size_t o_qt = part(24 * (size_t)std::max(P, 1) * sizeof(double)), o_ext = part(LH_EXT * (size_t)ncam * sizeof(double));
+        const size_t o_fix = part(pl.fixed_bits.size() * sizeof(uint64_t)), o_bptr = part(pl.brow_ptr.size() * sizeof(int32_t));
+        const size_t o_bent = part(pl.brow_ent.size() * sizeof(uint32_t));
+        HIPCHK(h->d_arena.ensure(bytes));
+        HIPCHK(h->s_arena.ensure(bytes));
+        h->arena_bytes = bytes;
+        auto bind = [](auto& d, auto& st, uint8_t* dbase, uint8_t* sbase, size_t off, size_t count) {
+            using T = std::remove_pointer_t<decltype(d.p)>;
+            d.p = reinterpret_cast<T*>(dbase + off); d.n = count;
+            st.p = reinterpret_cast<T*>(sbase + off); st.n = count;
+        };
+        uint8_t* db = h->d_arena.p;
+        uint8_t* sb = h->s_arena.p;
+        bind(h->d_chunks, h->s_chunks, db, sb, o_chunks, pl.n_chunks);
+        bind(h->d_sbs, h->s_sbs, db, sb, o_sbs, pl.n_sb);
+        bind(h->d_lm_perm, h->s_lm_perm, db, sb, o_lmp, pl.n_rec);
+        bind(h->d_pair_ptr, h->s_pair_ptr, db, sb, o_pptr, pl.npairs + 1);
+        bind(h->d_items, h->s_items, db, sb, o_items, pl.n_items);
+        bind(h->d_pair_pq, h->s_pair_pq, db, sb, o_ppq, 2 * (size_t)pl.npairs);
+        bind(h->d_rsmap, h->s_rsmap, db, sb, o_rsmap, (size_t)pl.npairs * 36);
+        bind(h->d_ptab_init, h->s_ptab, db, sb, o_ptab, 2 * PT);
+        bind(h->d_qt_init, h->s_qt, db, sb, o_qt, 24 * (size_t)std::max(P, 1));
+        bind(h->d_ext, h->s_ext, db, sb, o_ext, LH_EXT * (size_t)ncam);
+        bind(h->d_fixed, h->s_fixed, db, sb, o_fix, pl.fixed_bits.size());
+        bind(h->d_brow_ptr, h->s_brow_ptr, db, sb, o_bptr, pl.brow_ptr.size());
+        bind(h->d_brow_ent, h->s_brow_ent, db, sb, o_bent, pl.brow_ent.size());
+    }
     HIPCHK(h->d_meta.ensure(pl.n_slots));
     HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
     HIPCHK(h->d_obs_perm.ensure(pl.n_slots));
-    HIPCHK(h->d_lm_perm.ensure(pl.n_rec));
     HIPCHK(h->d_lm_in.ensure(3 * (size_t)pl.L));
-    HIPCHK(h->d_pair_ptr.ensure(pl.npairs + 1));
-    HIPCHK(h->d_items.ensure(pl.n_items));
-    HIPCHK(h->d_pair_pq.ensure(2 * (size_t)pl.npairs));
     HIPCHK(h->d_rec.ensure(2 * (size_t)pl.n_rec * LH_REC));
     HIPCHK(h->d_ptab.ensure(2 * PT));
-    HIPCHK(h->d_ptab_init.ensure(2 * PT));
     HIPCHK(h->d_qt.ensure(24 * (size_t)P));
-    HIPCHK(h->d_qt_init.ensure(24 * (size_t)P));
-    HIPCHK(h->d_ext.ensure(LH_EXT * (size_t)ncam));
     HIPCHK(h->d_rho.ensure(pl.n_slots));
     HIPCHK(h->d_wflag.ensure(2 * (size_t)pl.n_slots));
     HIPCHK(h->d_rows.ensure((size_t)pl.n_items * LH_ROW));
@@ -480,11 +538,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     }
     if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_PCG)   // k_ctrl_p's row-contiguous copy of S (36 per block-row entry)
         HIPCHK(h->d_gA.ensure(pl.brow_ent.size() * 36));
-    HIPCHK(h->d_rsmap.ensure((size_t)pl.npairs * 36));
     HIPCHK(h->d_maxd.ensure(1));
-    HIPCHK(h->d_fixed.ensure(pl.fixed_bits.size()));
-    HIPCHK(h->d_brow_ptr.ensure(pl.brow_ptr.size()));
-    HIPCHK(h->d_brow_ent.ensure(pl.brow_ent.size()));
     HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
     HIPCHK(h->d_ctrl.ensure(1));
     HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
@@ -492,16 +546,9 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     if (h->host_comm) HIPCHK(h->s_rs.ensure(h->LY.total + 1));
 
     // ---- staging and the fill ----
-    HIPCHK(h->s_chunks.ensure(pl.n_chunks));
-    HIPCHK(h->s_sbs.ensure(pl.n_sb));
     HIPCHK(h->s_meta.ensure(pl.n_slots));
     HIPCHK(h->s_uv.ensure(2 * pl.n_slots));
     HIPCHK(h->s_obs_perm.ensure(pl.n_slots));
-    HIPCHK(h->s_lm_perm.ensure(pl.n_rec));
-    HIPCHK(h->s_items.ensure(pl.n_items));
-    HIPCHK(h->s_pair_ptr.ensure(pl.npairs + 1));
-    HIPCHK(h->s_pair_pq.ensure(2 * (size_t)pl.npairs));
-    HIPCHK(h->s_rsmap.ensure((size_t)pl.npairs * 36));
     lh::PlanOut po{h->s_chunks.p, h->s_sbs.p, h->s_meta.p, h->s_uv.p, h->s_obs_perm.p, h->s_lm_perm.p,
                    h->s_items.p, h->s_pair_pq.p, h->s_rsmap.p, nullptr};   // positions: copied out above
     SlotCopy sc{h, hipSuccess};
@@ -514,11 +561,11 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         return fs;
     }
     std::memcpy(h->s_pair_ptr.p, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
+    std::memcpy(h->s_fixed.p, pl.fixed_bits.data(), pl.fixed_bits.size() * sizeof(uint64_t));
+    std::memcpy(h->s_brow_ptr.p, pl.brow_ptr.data(), pl.brow_ptr.size() * sizeof(int32_t));
+    std::memcpy(h->s_brow_ent.p, pl.brow_ent.data(), pl.brow_ent.size() * sizeof(uint32_t));
 
     // ---- camera extrinsics (Sophus SE3 of Camera::pose_) and the initial pose tables ----
-    HIPCHK(h->s_ext.ensure(LH_EXT * (size_t)ncam));
-    HIPCHK(h->s_qt.ensure(24 * (size_t)std::max(P, 1)));
-    HIPCHK(h->s_ptab.ensure(2 * (size_t)std::max(P, 1) * ncam * LH_PT));
     double* ext = h->s_ext.p;
     int ext_identity = 0, ext_rot_identity = 0;
     for (int c = 0; c < ncam; ++c) {
@@ -579,24 +626,11 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         if (!bytes) return hipSuccess;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
     };
-    HIPCHK(up(h->d_lm_perm.p, h->s_lm_perm.p, (size_t)pl.n_rec * sizeof(int32_t)));
-    HIPCHK(up(h->d_chunks.p, h->s_chunks.p, (size_t)pl.n_chunks * sizeof(lh_chunk)));
-    HIPCHK(up(h->d_sbs.p, h->s_sbs.p, (size_t)pl.n_sb * sizeof(lh_subbatch)));
-    HIPCHK(up(h->d_pair_ptr.p, h->s_pair_ptr.p, ((size_t)pl.npairs + 1) * sizeof(uint32_t)));
-    HIPCHK(up(h->d_items.p, h->s_items.p, (size_t)pl.n_items * sizeof(uint32_t)));
-    HIPCHK(up(h->d_pair_pq.p, h->s_pair_pq.p, 2 * (size_t)pl.npairs * sizeof(uint16_t)));
-    HIPCHK(up(h->d_rsmap.p, h->s_rsmap.p, (size_t)pl.npairs * 36 * sizeof(uint32_t)));
-    HIPCHK(up(h->d_ptab_init.p, h->s_ptab.p, 2 * PT * sizeof(double)));
-    HIPCHK(up(h->d_qt_init.p, h->s_qt.p, 24 * (size_t)P * sizeof(double)));
-    HIPCHK(up(h->d_ext.p, h->s_ext.p, LH_EXT * (size_t)ncam * sizeof(double)));
-    // (pageable: a few words; hipMemcpyAsync stages them before returning)
-    HIPCHK(up(h->d_fixed.p, pl.fixed_bits.data(), pl.fixed_bits.size() * sizeof(uint64_t)));
-    HIPCHK(up(h->d_brow_ptr.p, pl.brow_ptr.data(), pl.brow_ptr.size() * sizeof(int32_t)));
-    HIPCHK(up(h->d_brow_ent.p, pl.brow_ent.data(), pl.brow_ent.size() * sizeof(uint32_t)));
+    HIPCHK(up(h->d_arena.p, h->s_arena.p, h->arena_bytes));   // every per-window table in one copy
     HIPCHK(hipEventRecord(h->ev_staging, s));
     h->staging_pending = true;
     if (sync) {
-        HIPCHK(hipEventSynchronize(h->ev_staging));
+        HIPCHK(spin_wait(h->ev_staging));
         h->staging_pending = false;
     }
     h->last_prep_ms = t1 - t0;
@@ -714,7 +748,7 @@ int download(lh_handle* h, lh_result* out, int cur) {
     if (!e_first) return LH_E_HIP;
     HIPCHK(hipEventRecord(e_first, s));
     if (ne) HIPCHK(hipMemcpyAsync(st + np + nl, h->d_out_rho.p, ne * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipEventSynchronize(e_first));
+    HIPCHK(spin_wait(e_first));
     const ByteSeg seg[2] = {{out->pose_Tcw, st, np * sizeof(double)}, {out->lm_xyz, st + np, nl * sizeof(double)}};
     par_copy(h, seg, 2);
     HIPCHK(hipStreamSynchronize(s));
@@ -1020,7 +1054,7 @@ void lh_destroy(lh_handle* h) {
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
     h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_gS.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
     h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release(); h->d_fixed.release();
-    h->d_brow_ptr.release(); h->d_brow_ent.release();
+    h->d_brow_ptr.release(); h->d_brow_ent.release(); h->d_arena.release(); h->s_arena.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
