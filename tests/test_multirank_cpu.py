@@ -9,7 +9,7 @@ full-window system; and the sharded window generator (bench.py's per-rank input)
 each rank exactly its slice of the global window.
 """
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -22,16 +22,16 @@ import oracle_bind as ob
 from windows import window
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _rendezvous_file():
+    # a file store: no TCP port to race for (a port probed free can be taken before the store binds it)
+    fd, path = tempfile.mkstemp(prefix="lh_rdzv_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
-def _rank_main(rank, world, port, cfg, seed, family, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _rank_main(rank, world, rdzv, cfg, seed, family, q):
+    dist.init_process_group("gloo", init_method="file://" + rdzv, rank=rank, world_size=world)
     try:
         w = window(cfg, seed=seed, family=family)
         L = len(w["lm_xyz"])
@@ -50,14 +50,18 @@ def test_landmark_shards_allreduce_to_full_reduced_system(cfg, seed, family):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, cfg, seed, family, q)) for r in range(world)]
+    rdzv = _rendezvous_file()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, rdzv, cfg, seed, family, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        got = q.get(timeout=120)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        if os.path.exists(rdzv):
+            os.unlink(rdzv)
     w = window(cfg, seed=seed, family=family)
     S, bs, chi2 = ob.reduced_system(w, n_threads=1)
     n = S.shape[0]

@@ -9,7 +9,7 @@ whole window, and both ranks must hold bit-identical poses.  (th
 collective count is covered by test_gpu_parity.py::test_collective_count_is_a_function_of_the_stop_trial.)
 """
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -17,22 +17,23 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _rendezvous_file():
+    # a file store: no TCP port to race for (a port probed free can be taken by an outgoing
+    # connection before the store binds it: EADDRINUSE was seen on a test box)
+    fd, path = tempfile.mkstemp(prefix="lh_rdzv_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
-def _rank_main(rank, world, port, cfg, seed, family, opts, q):
+def _rank_main(rank, world, rdzv, cfg, seed, family, opts, q):
     import torch
     import torch.distributed as dist
 
     import lego_ba
     from windows import window_shard
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + rdzv, rank=rank, world_size=world)
     try:
         def allreduce(buf, op):
             t = torch.from_numpy(buf)   # shares the library's host buffer
@@ -53,8 +54,8 @@ def run_sharded(cfg, seed, family, world=2, timeout=100, **opts):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, cfg, seed, family, opts, q)) for r in range(world)]
+    rdzv = _rendezvous_file()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, rdzv, cfg, seed, family, opts, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -67,6 +68,8 @@ def run_sharded(cfg, seed, family, world=2, timeout=100, **opts):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+        if os.path.exists(rdzv):
+            os.unlink(rdzv)
     for p in procs:
         assert p.exitcode == 0
     return out
@@ -163,15 +166,13 @@ def test_c4_sharded_solve_matches_oracle_and_one_rank(c4_gate1, world):
     assert rel(rho.sum(), one["edge_robust_chi2"].sum()) < 1e-9
 
 
-def _create_main(rank, world, port, opts_per_rank, q):
+def _create_main(rank, world, rdzv, opts_per_rank, q):
     import torch
     import torch.distributed as dist
 
     import lego_ba
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + rdzv, rank=rank, world_size=world)
     try:
         def allreduce(buf, op):
             t = torch.from_numpy(buf)
@@ -195,8 +196,8 @@ def test_ranks_must_agree_on_solver_options(opts):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_create_main, args=(r, 2, port, opts, q)) for r in range(2)]
+    rdzv = _rendezvous_file()
+    procs = [ctx.Process(target=_create_main, args=(r, 2, rdzv, opts, q)) for r in range(2)]
     for p in procs:
         p.start()
     got = {}
@@ -209,5 +210,7 @@ def test_ranks_must_agree_on_solver_options(opts):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+        if os.path.exists(rdzv):
+            os.unlink(rdzv)
     want = lego_ba.LH_OK if opts[0] == opts[1] else lego_ba.LH_E_BADARG
     assert got == {0: want, 1: want}
