@@ -39,8 +39,8 @@ hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* cs
                             lh_params prm, int n_chunks);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          const uint32_t* rsmap, double* pose_qt, double* ptab, const double* ext, double* dxp,
-                          lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS,
+                          const uint32_t* rsmap, const uint16_t* pair_pq, double* pose_qt, double* ptab, const double* ext,
+                          double* dxp, lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS,
                           const int32_t* brow_ptr, const uint32_t* brow_ent);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
@@ -714,7 +714,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
         Prof pr(h, KC_CTRL);
         if (h->P > LH_PMAX && h->prm.solver == LH_SOLVER_LDLT)
             HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
-        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_qt.p,
+        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_pair_pq.p, h->d_qt.p,
                               h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial,
                               h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p, h->d_brow_ent.p));
         DBGSYNC("k_ctrl");

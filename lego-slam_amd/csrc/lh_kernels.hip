@@ -1225,7 +1225,8 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
 #define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
 #define RS_MAX (LH_PMAX * (LH_PMAX + 1) / 2 * 36 + 18 * LH_PMAX + 8)
-#define NLD ((RS_MAX + CT - 1) / CT)
+#define ER 1008               // reduced-system elements per prefetch round: 28 whole 6x6 S blocks
+#define NLD ((RS_MAX + ER - 1) / ER)
 #define NBLK (LH_NPAD / 8)
 
 // Per-block products of the 8x8 diagonal-block factor (LDS, shared by all waves).
@@ -1463,8 +1464,10 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 }
 
 // Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
-// blocked LDL^T with the forward substitution, then the back substitution; xsol[r] = solution in
-// pivot order for r < n.  Shared with the k_ldlt_probe test hook.  Must be called by all CT threads.
+// blocked LDL^T with the forward substitution, then the back substitution; xsol[perm[r]] = the
+// solution's pivot-order entry r < n (perm == nullptr: xsol[r], pivot order).  While wave 0 runs the
+// back substitution, wave 1 runs idle() (the other waves wait at the final barrier).  Shared with the
+// k_ldlt_probe test hook.  Must be called by all CT threads.
 //
 // Step t eliminates block column k0 = 8t.  Interval t (one barrier each):
 //   wave 0:       the trailing update of the diagonal tile holding block t+1, then the factor
@@ -1473,7 +1476,9 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 //                 half tile rows (wave_unit), skipping wave 0's tile;
 //   wave 12 first: z_t = b_t N_t (Eigen's solve tolerance applied).
 // L lives in the upper triangle, so the raw block columns stay readable for the whole step.
-__device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid) {
+template <typename Idle>
+__device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid,
+                                               const int* __restrict__ perm, Idle&& idle) {
     const int lane = tid & 63, wave = tid >> 6;
     __shared__ __attribute__((aligned(16))) LdltBlockLds F;
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
@@ -1578,8 +1583,15 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         backsub_load_nd<0>(F, lane, ndb);
         backsub_block<8>(A, nda, nb, lane, y0, y1);
         backsub_block<0>(A, ndb, nb, lane, y0, y1);
-        if (lane < NE) xsol[lane] = y0;
-        if (lane + 64 < NE) xsol[lane + 64] = y1;
+        if (perm) {
+            if (lane < n) xsol[perm[lane]] = y0;
+            if (lane + 64 < n) xsol[perm[lane + 64]] = y1;
+        } else {
+            if (lane < NE) xsol[lane] = y0;
+            if (lane + 64 < NE) xsol[lane + 64] = y1;
+        }
+    } else if (wv == 1) {
+        idle();
     }
     lds_barrier();
     CSTAMP(7);
@@ -1906,10 +1918,86 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
     }
 }
 
+// k_ctrl's tail (P <= 32, s_qT already holding the committed quaternions): one barrier.  Every
+// wave sums its part of the gain denominator's pose part and stores the pose step; then wave 0
+// alone: spose (the wave partials in order, as ctrl_pose_tail), sin/cos(theta / 2) in lanes 0-31
+// and sin/cos(theta) in lanes 32-63 (one instruction stream, no LDS hand-off), the candidate pose
+// (VertexPose::add) in lane p, and the pose table of every (pose, camera).  The same operations as
+// ctrl_pose_tail, so the same bits.
+template <int NT>
+__device__ __forceinline__ void ctrl_pose_tail_w0(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
+                                                  int cur, const double* xs, const double* bpv, const double* hdv,
+                                                  double* s_red, double (*s_pm)[LH_PMAX * 12], const double (*s_qT)[4],
+                                                  double* __restrict__ pose_mat, double* __restrict__ ptab,
+                                                  const double* __restrict__ ext, double* __restrict__ dxp) {
+    static_assert(LH_PMAX <= 32, "one pose per lane of a wave half");
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = prm.P;
+    double sp = 0.0;
+    for (int i = tid; i < n; i += NT) {
+        const double d = xs[i], b = bpv[i];
+        sp += (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[i] * d + b);
+        dxp[i] = d;
+    }
+    for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
+    if (lane == 0) s_red[wave] = sp;
+    lds_barrier();
+    CSTAMP(9);
+    if (wave != 0) return;
+    if (lane == 0) {
+        double s2 = 0.0;
+        for (int w = 0; w < NT / 64; ++w) s2 += s_red[w];
+        ctrl->spose = s2;
+    }
+    const int cand = 1 - cur;
+    const int pidx = min(lane & 31, P - 1);
+    double up[6];
+    bool bad = false;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
+    if (bad) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
+    }
+    const double th = d_twist_theta(up);
+    double sn, cs;
+    sincos(lane < 32 ? 0.5 * th : th, &sn, &cs);
+    const double sf = __shfl_xor(sn, 32), cf = __shfl_xor(cs, 32);   // lanes 0-31: sin/cos(theta)
+    if (lane < P) {
+        double qe[4], te[3], qn[4], tr[3], Rn[9];
+        d_se3_exp_trig(up, sn, cs, sf, cf, qe, te);
+        const double* Tc = &s_pm[cur][lane * 12];
+        const double tc[3] = {Tc[3], Tc[7], Tc[11]};
+        d_q_mul(qe, s_qT[lane], qn);
+        d_q_rotate(qe, tc, tr);
+        d_R_from_q(qn, Rn);
+        double To[12];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
+            To[4 * i + 3] = te[i] + tr[i];
+        }
+        double* Tl = &s_pm[cand][lane * 12];   // the candidate buffer's LDS copy is free after the solve
+        double* Tg = pose_mat + (size_t)cand * P * 12 + lane * 12;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { Tl[i] = To[i]; Tg[i] = To[i]; }
+    }
+    wave_sync();
+    CSTAMP(10);
+    for (int pc = lane; pc < P * prm.ncam; pc += 64) {
+        const int pi = pc / prm.ncam, cam = pc - pi * prm.ncam;
+        double To[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pi * 12 + i];
+        d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pi * prm.ncam + cam) * LH_PT);
+    }
+    CSTAMP(11);
+}
+
 template <int SOLVER>
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
-                                             const uint32_t* __restrict__ rsmap,
+                                             const uint16_t* __restrict__ pair_pq,
                                              double* __restrict__ pose_mat, double* __restrict__ ptab,
                                              const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
                                              int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done,
@@ -1919,11 +2007,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     __shared__ double bsv[NP], bpv[NP], hdv[NP], xs[NP];
     __shared__ __attribute__((aligned(16))) double yv[NP];
     __shared__ int perm[NP], iperm[NP];
+    __shared__ __attribute__((aligned(16))) unsigned long long pkey[NP];   // pivot keys (pivot rank)
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
     __shared__ __attribute__((aligned(16))) double s_pcg[48];
     __shared__ double s_pm[2][LH_PMAX * 12];
-    __shared__ double s_trig[LH_PMAX][4], s_qT[LH_PMAX][4];
+    __shared__ double s_qT[LH_PMAX][4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
@@ -1943,23 +2032,29 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     // both pose-matrix buffers (used after the solve) go to LDS; their load is issued first and
     // unconditionally (clamped), so it shares the bulk's round trip instead of following it
+    // Only the staged system is loaded here: a trial is accepted far more often than not, and a
+    // rejected one loads the committed system after the decision (one more round trip).  Round u
+    // covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
+    // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
+    // element's rows need only the block's pose pair (p | q << 16, from the 840-byte pair table).
     const double pmv = pose_mat[min(tid, 24 * P - 1)];
-    double vs[NLD], vc[NLD];
+    const uint32_t* __restrict__ pqw = reinterpret_cast<const uint32_t*>(pair_pq);
+    const int e36 = tid % 36, ea = e36 / 6, eb = e36 - 6 * ea, blk0 = tid / 36;
+    const int ibase = (tid < ER) ? tid : (1 << 30);   // threads past ER hold no element
+    double vs[NLD];
     uint32_t mp[NLD];
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
-        const int i = u * CT + tid;
-        const bool in = i < LY.total;
-        vs[u] = in ? rs_stage[i] : 0.0;
-        vc[u] = in ? rs_commit[i] : 0.0;
-        mp[u] = i < LY.off_bs ? rsmap[i] : 0u;
+        const int i = u * ER + ibase;
+        vs[u] = (i < LY.total) ? rs_stage[i] : 0.0;
+        mp[u] = pqw[min(blk0 + (ER / 36) * u, max(LY.npairs - 1, 0))];
     }
     if (tid < 24 * P) s_pm[tid / (12 * P)][tid - (tid / (12 * P)) * 12 * P] = pmv;
     if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
         double mx = 0.0;
 #pragma unroll
         for (int u = 0; u < NLD; ++u) {
-            const int i = u * CT + tid;
+            const int i = u * ER + ibase;
             if (i >= LY.off_hd && i < LY.off_hd + n) mx = fmax(mx, fabs(vs[u]));
         }
         for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
@@ -1996,15 +2091,30 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     CSTAMP(1);
 
     // ---------------- 2. commit, diag + lambda, pivot order, scatter into LDS ----------------
+    if (!accept) {   // rollback: the committed system, with the new lambda
+#pragma unroll
+        for (int u = 0; u < NLD; ++u) {
+            const int i = u * ER + ibase;
+            vs[u] = (i < LY.total) ? rs_commit[i] : 0.0;
+        }
+    }
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
-        const int i = u * CT + tid;
-        const double v = accept ? vs[u] : vc[u];
-        vs[u] = v;
+        const int i = u * ER + ibase;
+        const double v = vs[u];
         if (accept && i < LY.total) rs_commit[i] = v;
+        // S element i: pose pair (p, q), p <= q, entry (ea, eb) -> rows 6 p + ea, 6 q + eb
+        const uint32_t pp = mp[u] & 0xffffu, qq = mp[u] >> 16;
+        mp[u] = LH_RSMAP(6 * pp + ea, 6 * qq + eb, pp == qq);
         if (i < LY.off_bs) {
             const int gi = LH_RSMAP_ROW(mp[u]), gj = LH_RSMAP_COL(mp[u]);
-            if (gi == gj) dg[gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
+            if (gi == gj) {
+                const double dv = (prm.strategy == 0) ? v + lambda : v + lambda * v;
+                dg[gi] = dv;
+                // pivot key: |d| ordered as its bits (+1), NaN below everything (0)
+                const double ad = fabs(dv);
+                pkey[gi] = (ad == ad) ? (unsigned long long)__double_as_longlong(ad) + 1ull : 0ull;
+            }
         } else if (i < LY.off_bp) {
             bsv[i - LY.off_bs] = v;
         } else if (i < LY.off_hd) {
@@ -2013,26 +2123,22 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             hdv[i - LY.off_hd] = v;
         }
     }
-    if (tid >= n && tid < NP) dg[tid] = __builtin_nan("");   // key -1 at an index above every real row: never counted
+    if (tid >= n && tid < NP) { dg[tid] = __builtin_nan(""); pkey[tid] = 0ull; }   // never counted: key 0, index above every real row
     lds_barrier();
     CSTAMP(2);
     {
         // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation.
-        // Eight threads per row, each counting over 16 of the 128 keys (dg[n..NP) are NaN).
+        // Eight threads per row, each counting over 16 of the 128 keys (integer compares of the
+        // keys written with dg; rows n..NP have key 0).
         const int row = tid >> 3, part = tid & 7;
         int r = 0;
         if (row < n) {
-            double di = fabs(dg[row]);
-            if (!(di == di)) di = -1.0;
-            double dj[16];
+            const unsigned long long ki = pkey[row];
+            unsigned long long kj[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) dj[u] = dg[part * 16 + u];
+            for (int u = 0; u < 16; ++u) kj[u] = pkey[part * 16 + u];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                double d = fabs(dj[u]);
-                if (!(d == d)) d = -1.0;
-                r += (d > di) || (d == di && part * 16 + u < row);
-            }
+            for (int u = 0; u < 16; ++u) r += (kj[u] > ki) | ((kj[u] == ki) & (part * 16 + u < row));
         }
         r += __shfl_xor(r, 1);
         r += __shfl_xor(r, 2);
@@ -2047,7 +2153,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     CSTAMP(3);
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
-        const int i = u * CT + tid;
+        const int i = u * ER + ibase;
         if (i < LY.off_bs) {
             const int ri = iperm[LH_RSMAP_ROW(mp[u])], rj = iperm[LH_RSMAP_COL(mp[u])];
             if (!LH_RSMAP_DIAG(mp[u])) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
@@ -2066,17 +2172,27 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     CSTAMP(4);
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
+    // The committed rotations' quaternions (SE3(estimate_) of VertexPose::add) need no step: an
+    // otherwise idle wave computes them while the step is solved.
+    auto qt_committed = [&] {
+        for (int pi = lane; pi < P; pi += 64) {
+            const double* Tc = &s_pm[cur][pi * 12];
+            const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
+            d_q_from_R(Rc, s_qT[pi]);
+        }
+    };
     if constexpr (SOLVER == 1) {
+        if (wave == 1) qt_committed();
         const int its = lds_pcg_solve(A, yv, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
         if (tid == 0) ctrl->pcg_iters += its;
+        if (tid < n) xs[perm[tid]] = yv[tid];
+        lds_barrier();
     } else {
-        lds_ldlt_solve(A, yv, n, NE, tid);
+        lds_ldlt_solve(A, xs, n, NE, tid, perm, qt_committed);
     }
-    if (tid < n) { xs[perm[tid]] = yv[tid]; dxp[perm[tid]] = yv[tid]; }
-    lds_barrier();
     CSTAMP(8);
 
-    ctrl_pose_tail<LH_PMAX, CT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
+    ctrl_pose_tail_w0<CT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_qT, pose_mat, ptab, ext, dxp);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -3329,9 +3445,9 @@ hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_
 }
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          const uint32_t* rsmap, double* pose_mat, double* ptab, const double* ext, double* dxp, lh_params prm, int mode,
-                          int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
-                          const uint32_t* brow_ent) {
+                          const uint32_t* rsmap, const uint16_t* pair_pq, double* pose_mat, double* ptab, const double* ext,
+                          double* dxp, lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS,
+                          const int32_t* brow_ptr, const uint32_t* brow_ent) {
     if (prm.P > LH_PMAX && prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent, pose_mat,
                            ptab, ext, dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
@@ -3339,10 +3455,10 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
-        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
+        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, pose_mat, ptab, ext, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     else
-        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext, dxp,
+        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, pose_mat, ptab, ext, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     return hipGetLastError();
 }
@@ -3457,7 +3573,7 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
         const int its = lds_pcg_solve(A, xsol, dg, s_pcg, n, tid, tol, (max_it > 0 ? max_it : 2 * n) + 1);
         if (tid == 0 && iters) *iters = its;
     } else {
-        lds_ldlt_solve(A, xsol, n, NE, tid);
+        lds_ldlt_solve(A, xsol, n, NE, tid, nullptr, [] {});
     }
     lds_barrier();
     if (tid < n) x[perm[tid]] = xsol[tid];
