@@ -52,3 +52,11 @@ if st[51]:
     print(f"  LDLT loop per launch: wave 0 diag tile {st[46] / nl:.0f}, factor {st[47] / nl:.0f}, barrier wait "
           f"{st[48] / nl:.0f} cycles; other waves (mean per wave) unit {st[49] / nl / 15:.0f}, barrier wait "
           f"{st[50] / nl / 15:.0f} cycles")
+# per step t of the LDL^T loop (stamps 64-127): wave 0's diagonal tile, factor and barrier wait (mean
+# per launch) and the slowest other wave's unit (the worst launch)
+if len(st) >= 128 and st[51]:
+    print("  step  w0 tile  w0 factor  w0 wait  worst unit")
+    for t in range(16):
+        a, b, c, m = st[64 + t] / nl, st[80 + t] / nl, st[96 + t] / nl, st[112 + t]
+        if a or b or c or m:
+            print(f"  {t:4d} {a:8.0f} {b:10.0f} {c:8.0f} {m:11d}")
