@@ -26,7 +26,7 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // summed over all waves into lh_stamps[] (cdna_hip_programming.md §7 "In-kernel
 // stamps").  The product build compiles these to nothing.
 #ifdef LH_STAMPS
-__device__ unsigned long long lh_stamps[64];
+__device__ unsigned long long lh_stamps[128];   // [64, 128): k_ctrl's LDL^T steps, per step (lds_ldlt_solve)
 #define STAMP_DECL unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_, sacc_[24] = {0};
 #define STAMP(i)                                                                   \
     do {                                                                           \
@@ -1490,8 +1490,15 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     // per-step split (diagnostic): wave 0's diagonal tile, its factor and its wait at the barrier;
     // the other waves' unit time and barrier wait (wave-cycles summed over waves)
     unsigned long long ss_[5] = {0, 0, 0, 0, 0}, sa_ = __builtin_amdgcn_s_memtime(), sb_;
+    // per step t: [64 + t] wave 0's diagonal tile, [80 + t] its factor, [96 + t] its barrier wait
+    // (sums over launches), [112 + t] the slowest other wave's unit in the worst launch (atomicMax)
 #define LDLT_SSTAMP(i) do { __builtin_amdgcn_sched_barrier(0); sb_ = __builtin_amdgcn_s_memtime(); \
-        ss_[i] += sb_ - sa_; sa_ = sb_; __builtin_amdgcn_sched_barrier(0); } while (0)
+        ss_[i] += sb_ - sa_; \
+        if (lane == 0 && (i) != 4) { \
+            const int ti_ = min(k0 >> 3, 15); \
+            if ((i) == 3) atomicMax(&lh_stamps[112 + ti_], sb_ - sa_); \
+            else atomicAdd(&lh_stamps[64 + 16 * ((i) == 0 ? 0 : (i) == 1 ? 1 : 2) + ti_], sb_ - sa_); } \
+        sa_ = sb_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define LDLT_SSTAMP(i)
 #endif
@@ -3650,10 +3657,10 @@ __global__ void k_mfma_probe(const double* A, const double* B, double* D) {
 
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset) {
 #ifdef LH_STAMPS
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lh_stamps), sizeof(unsigned long long) * (n < 64 ? n : 64));
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lh_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128));
     if (e != hipSuccess) return e;
     if (reset) {
-        unsigned long long z[64] = {0};
+        unsigned long long z[128] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(lh_stamps), z, sizeof(z));
     }
     return e;
