@@ -31,16 +31,17 @@ size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
-                         const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
+                         double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag,
-                         long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits);
+                         long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat,
+                         int writer);
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
                             lh_params prm, int n_chunks);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          const uint32_t* rsmap, const uint16_t* pair_pq, double* pose_qt, double* ptab, const double* ext,
-                          double* dxp, lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS,
+                          const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
+                          int* host_done, int seq, double* gA, const double* gS,
                           const int32_t* brow_ptr, const uint32_t* brow_ent);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
@@ -651,14 +652,20 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         }                                                                                               \
     } while (0)
 
+// One k_lin launch per tile count present.  In a trial, block 0 of the first launch (of a T = 1 launch
+// with no chunks when the window has none) stores the trial's candidate poses and pose tables.
 int launch_lin(lh_handle* h, int trial) {
     hipStream_t s = h->stream;
+    int writer = trial ? 1 : 0;
     for (int T = 1; T <= LH_TMAX; ++T) {
         const int c0 = h->plan.tgroup_begin[T], c1 = h->plan.tgroup_begin[T + 1];
+        const bool last = T == LH_TMAX;
+        if (c1 == c0 && !(writer && last)) continue;
         HIPCHK(lh_launch_lin(T, trial, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p, h->d_meta.p, h->d_rec.p,
                              h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p, h->d_rho.p, h->d_rows.p,
                              h->d_csc.p, h->d_items.p, h->d_wflag.p, (long)h->n_slots, h->prm, h->n_rec,
-                             h->d_fixed.p));
+                             h->d_fixed.p, h->d_qt.p, writer));
+        writer = 0;
         DBGSYNC("k_lin");
     }
     return LH_OK;
@@ -714,9 +721,9 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
         Prof pr(h, KC_CTRL);
         if (h->P > LH_PMAX && h->prm.solver == LH_SOLVER_LDLT)
             HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
-        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_pair_pq.p, h->d_qt.p,
-                              h->d_ptab.p, h->d_ext.p, h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial,
-                              h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p, h->d_brow_ent.p));
+        HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_pair_pq.p,
+                              h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial, h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p,
+                              h->d_brow_ent.p));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;

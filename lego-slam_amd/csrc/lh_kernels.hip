@@ -231,6 +231,37 @@ __device__ inline void d_pose_table(const double* T12, const double* __restrict_
     pt[23] = 0.0;
 }
 
+// VertexPose::add (lego_types.h, problem.cpp:433-455): estimate_ = (SE3::exp(dx) * SE3(estimate_)).matrix(),
+// the candidate [R|t] (row-major, 12) from the committed one Tc and the pose step dx (translation-first
+// twist; a non-finite step is skipped, as VertexPose::add's guard does).
+__device__ __forceinline__ void d_pose_candidate(const double (&Tc)[12], const double* dx, double (&To)[12]) {
+    double up[6];
+    bool bad = false;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) { up[a] = dx[a]; bad |= !isfinite(up[a]); }
+    if (bad) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) up[a] = 0.0;
+    }
+    const double th = d_twist_theta(up);
+    double sh, ch, st, ct;
+    sincos(0.5 * th, &sh, &ch);
+    sincos(th, &st, &ct);
+    double qe[4], te[3], qT[4], qn[4], tr[3], Rn[9];
+    d_se3_exp_trig(up, sh, ch, st, ct, qe, te);
+    const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
+    d_q_from_R(Rc, qT);
+    const double tc[3] = {Tc[3], Tc[7], Tc[11]};
+    d_q_mul(qe, qT, qn);
+    d_q_rotate(qe, tc, tr);
+    d_R_from_q(qn, Rn);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
+        To[4 * i + 3] = te[i] + tr[i];
+    }
+}
+
 struct EdgeEval {
     double r0, r1, e2, rho0, rho1, rho2;
     double W00, W01, W10, W11;
@@ -623,11 +654,12 @@ static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_
 template <int T, bool TRIAL, bool F32>
 __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const float* __restrict__ obs_uv,
-    const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, const double* __restrict__ pose_tab,
+    const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, double* __restrict__ pose_tab,
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
     double* __restrict__ edge_rho, double* __restrict__ rows, double* __restrict__ csc,
     const uint32_t* __restrict__ crow, uint8_t* __restrict__ wflag, long nslots,
-    lh_params prm, int nrec, const uint64_t* __restrict__ fixed_bits, int chunk_base) {
+    lh_params prm, int nrec, const uint64_t* __restrict__ fixed_bits, int chunk_base,
+    double* __restrict__ pose_mat, int writer) {
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
 
@@ -636,9 +668,28 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // included; (2) the pose-table and pose-step values, whose addresses need the chunk's pose slots.
     // Written as per-element loops, each loop iteration waited for its own loads (ten serialised
     // round trips before the first sub-batch).
-    const int chunk = chunk_base + blockIdx.x;
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
+    // The candidate poses of a trial (VertexPose::add of the step k_ctrl solved) are built here, not in
+    // the serial controller: every chunk builds its own window's candidate pose tables (wave 3, below),
+    // and block 0 of one launch per trial (writer) stores every candidate pose and its tables, which a
+    // later trial reads as committed and the caller as the result.
+    if (TRIAL && writer && blockIdx.x == 0) {
+        if (done) return;
+        const int P = prm.P, nc = prm.ncam, cnd = 1 - cur;
+        for (int p = threadIdx.x; p < P; p += 256) {
+            double Tc[12], To[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Tc[i] = pose_mat[(size_t)cur * P * 12 + p * 12 + i];
+            d_pose_candidate(Tc, dxp + 6 * p, To);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pose_mat[(size_t)cnd * P * 12 + p * 12 + i] = To[i];
+            for (int c = 0; c < nc; ++c)
+                d_pose_table(To, ext + LH_EXT * c, pose_tab + (size_t)cnd * P * nc * LH_PT + (p * nc + c) * LH_PT);
+        }
+        return;
+    }
+    const int chunk = chunk_base + blockIdx.x - ((TRIAL && writer) ? 1 : 0);
     // a trial of the final LM iteration (ctrl->evo, ctrl_lm_step): back substitution and the
     // candidate's evaluation only (landmark positions, rho0 per edge, chi2 and the gain scale)
     const bool evo = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->evo) != 0;
@@ -662,6 +713,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     double* wt_n = wt_c + Cfg::UMAX * ncam * LH_PT_LDS;     // a chunk of T tiles has U <= UMAX poses
     double* wdx = wt_n + Cfg::UMAX * ncam * LH_PT_LDS;
     double* wext = wdx + Cfg::UMAX * 6;
+    // after the pair-row map: the flag raised when wave 3 has built the candidate tables
+    int* cflag = reinterpret_cast<int*>(wext + ncam * LH_EXT + (Cfg::UMAX * (Cfg::UMAX + 1) / 2 + 1) / 2);
+    double pmc[12];
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
     double* __restrict__ rn = rec + (size_t)cand * nrec * LH_REC;
@@ -732,7 +786,12 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             const int i = tid + 256 * k;
             const size_t g = (size_t)tp[k] * per + min(max(i - tsl[k] * per, 0), per - 1);
             tc[k] = pose_tab[(size_t)cur * PT + g];
-            tn[k] = pose_tab[(size_t)cand * PT + g];
+            tn[k] = TRIAL ? 0.0 : pose_tab[(size_t)cand * PT + g];   // a trial builds its candidate tables
+        }
+        if (TRIAL && wave == LH_WAVES - 1) {   // the committed pose of slot lane (lane < U)
+            const uint32_t pp = min((uint32_t)cpose[min(lane, umax1)], pmax1);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pmc[i] = pose_mat[(size_t)cur * prm.P * 12 + pp * 12 + i];
         }
         const double dv = TRIAL ? dxp[6 * dp + (tid - 6 * (tid / 6))] : 0.0;
 #pragma unroll
@@ -742,15 +801,38 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
                 const int r = i - tsl[k] * per, ent = r / LH_PT;
                 const int l = (tsl[k] * ncam + ent) * LH_PT_LDS + (r - ent * LH_PT);
                 wt_c[l] = tc[k];
-                wt_n[l] = tn[k];
+                if (!TRIAL) wt_n[l] = tn[k];
             }
         }
         if (has_dx) wdx[tid] = dv;
         if (tid < ncam * LH_EXT) wext[tid] = ev;
         uint32_t* wrow = reinterpret_cast<uint32_t*>(wext + ncam * LH_EXT);
         if (tid < nrow) wrow[tid] = rw;
+        if (tid == 0) *cflag = 0;
     }
     lds_barrier();   // window tables
+    // A trial's candidate pose tables (wt_n): wave 3 composes the window's candidate poses (lane = slot)
+    // and their tables (lane = (slot, camera)) while the other waves start their first back
+    // substitution, which needs only the committed tables; they wait on cflag before their first
+    // evaluation at the candidate.  Wave 3 runs one sub-batch fewer than wave 0 in most chunks.
+    if (TRIAL && wave == LH_WAVES - 1) {
+        if (lane < U) {
+            double To[12];
+            d_pose_candidate(pmc, wdx + 6 * lane, To);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) scr[lane * 12 + i] = To[i];
+        }
+        wave_sync();
+        if (lane < U * ncam) {
+            const int sl = lane / ncam, c = lane - sl * ncam;
+            double To[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) To[i] = scr[sl * 12 + i];
+            d_pose_table(To, wext + c * LH_EXT, wt_n + (sl * ncam + c) * LH_PT_LDS);
+        }
+        __hip_atomic_store(cflag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    bool tabs_ready = !TRIAL;
 
     for (; sb < (int)sb_end; sb += LH_WAVES) {
         const lh_subbatch S = S_n;       // scalar words, prefetched one sub-batch ahead (sb is wave-uniform)
@@ -861,6 +943,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             }
         }
         STAMP(0);
+        if (!tabs_ready) {   // wave-uniform: once per wave
+            while (__hip_atomic_load(cflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+            tabs_ready = true;
+        }
 
         if (evo) {   // the same evaluation as below, without the linearisation
             if (has) {
@@ -1465,8 +1551,7 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 
 // Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
 // blocked LDL^T with the forward substitution, then the back substitution; xsol[perm[r]] = the
-// solution's pivot-order entry r < n (perm == nullptr: xsol[r], pivot order).  While wave 0 runs the
-// back substitution, wave 1 runs idle() (the other waves wait at the final barrier).  Shared with the
+// solution's pivot-order entry r < n (perm == nullptr: xsol[r], pivot order).  Shared with the
 // k_ldlt_probe test hook.  Must be called by all CT threads.
 //
 // Step t eliminates block column k0 = 8t.  Interval t (one barrier each):
@@ -1476,9 +1561,8 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 //                 half tile rows (wave_unit), skipping wave 0's tile;
 //   wave 12 first: z_t = b_t N_t (Eigen's solve tolerance applied).
 // L lives in the upper triangle, so the raw block columns stay readable for the whole step.
-template <typename Idle>
 __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid,
-                                               const int* __restrict__ perm, Idle&& idle) {
+                                               const int* __restrict__ perm) {
     const int lane = tid & 63, wave = tid >> 6;
     __shared__ __attribute__((aligned(16))) LdltBlockLds F;
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
@@ -1597,8 +1681,6 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
             if (lane < NE) xsol[lane] = y0;
             if (lane + 64 < NE) xsol[lane + 64] = y1;
         }
-    } else if (wv == 1) {
-        idle();
     }
     lds_barrier();
     CSTAMP(7);
@@ -1836,88 +1918,25 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
     lam_o = lam;
 }
 
-// The controller's tail, shared by both controllers (xs: the pose step in pose order, in LDS):
-// the pose part of the gain denominator (isGoodStepInLM's scale, problem.cpp:528-533, summed into
-// ctrl->spose), the candidate poses (VertexPose::add) and their pose tables.  All CT threads.
-template <int PM, int NT>
-__device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
-                                               int cur, const double* xs, const double* bpv, const double* hdv,
-                                               double* s_red, double (*s_pm)[PM * 12], double (*s_trig)[4],
-                                               double (*s_qT)[4], double* __restrict__ pose_mat,
-                                               double* __restrict__ ptab, const double* __restrict__ ext) {
+// The controllers' tail (xs: the pose step in pose order, in LDS): the pose part of the gain
+// denominator (isGoodStepInLM's scale, problem.cpp:528-533), the wave partials summed in wave order
+// into ctrl->spose, and (dxp non-null) the step stored for k_lin.  The candidate poses
+// (VertexPose::add) are built by the next k_lin (d_pose_candidate).  All NT threads.
+template <int NT>
+__device__ __forceinline__ void ctrl_step_tail(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
+                                               const double* xs, const double* bpv, const double* hdv, double* s_red,
+                                               double* __restrict__ dxp) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int P = prm.P;
-    // ---------------- pose part of the gain denominator; candidate poses ----------------
     double sp = 0.0;
     for (int i = tid; i < n; i += NT) {
         const double d = xs[i], b = bpv[i];
         sp += (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[i] * d + b);
+        if (dxp) dxp[i] = d;
     }
     for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
     if (lane == 0) s_red[wave] = sp;
-    const int cand = 1 - cur;
-    // VertexPose::add: estimate_ = (SE3::exp(update) * SE3(estimate_)).matrix(), one pose per
-    // lane in three steps: (1) wave 0 sin/cos(theta/2), wave 1 sin/cos(theta), wave 2 the current
-    // quaternion; (2) wave 0 composes; (3) one lane per (pose, camera) builds the pose table
-    auto pose_step = [&](int pidx, double up[6]) {
-        bool bad = false;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
-        if (bad) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
-        }
-    };
-    // (one lane per pose; past 64 poses the lanes take every 64th)
-    if (wave < 2) {
-        for (int pi = lane; pi < P; pi += 64) {
-            double up[6];
-            pose_step(pi, up);
-            const double th = d_twist_theta(up);
-            double sn, cs;
-            sincos(wave == 0 ? 0.5 * th : th, &sn, &cs);
-            s_trig[pi][2 * wave] = sn;
-            s_trig[pi][2 * wave + 1] = cs;
-        }
-    } else if (wave == 2) {
-        for (int pi = lane; pi < P; pi += 64) {
-            const double* Tc = &s_pm[cur][pi * 12];
-            const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
-            d_q_from_R(Rc, s_qT[pi]);
-        }
-    }
     lds_barrier();
     CSTAMP(9);
-    if (wave == 0)
-    for (int pidx = lane; pidx < P; pidx += 64) {
-        double up[6], qe[4], te[3], qn[4], tr[3], Rn[9];
-        pose_step(pidx, up);
-        d_se3_exp_trig(up, s_trig[pidx][0], s_trig[pidx][1], s_trig[pidx][2], s_trig[pidx][3], qe, te);
-        const double* Tc = &s_pm[cur][pidx * 12];
-        const double tc[3] = {Tc[3], Tc[7], Tc[11]};
-        d_q_mul(qe, s_qT[pidx], qn);
-        d_q_rotate(qe, tc, tr);
-        d_R_from_q(qn, Rn);
-        double* To = &s_pm[cand][pidx * 12];   // the candidate buffer's LDS copy is free after the solve
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
-            To[4 * i + 3] = te[i] + tr[i];
-        }
-    }
-    lds_barrier();
-    CSTAMP(10);
-    for (int i = tid; i < 12 * P; i += NT) pose_mat[(size_t)cand * P * 12 + i] = s_pm[cand][i];
-    for (int pc = tid - 64; pc < P * prm.ncam; pc += NT - 64) {   // threads 64.. (wave 0 stores pose_mat)
-        if (pc < 0) break;
-        const int pidx = pc / prm.ncam, cam = pc - pidx * prm.ncam;
-        double To[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pidx * 12 + i];
-        d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pidx * prm.ncam + cam) * LH_PT);
-    }
-    lds_barrier();
-    CSTAMP(11);
     if (tid == 0) {
         double s2 = 0.0;
         for (int w = 0; w < NT / 64; ++w) s2 += s_red[w];
@@ -1925,90 +1944,12 @@ __device__ __forceinline__ void ctrl_pose_tail(lh_ctrl* __restrict__ ctrl, const
     }
 }
 
-// k_ctrl's tail (P <= 32, s_qT already holding the committed quaternions): one barrier.  Every
-// wave sums its part of the gain denominator's pose part and stores the pose step; then wave 0
-// alone: spose (the wave partials in order, as ctrl_pose_tail), sin/cos(theta / 2) in lanes 0-31
-// and sin/cos(theta) in lanes 32-63 (one instruction stream, no LDS hand-off), the candidate pose
-// (VertexPose::add) in lane p, and the pose table of every (pose, camera).  The same operations as
-// ctrl_pose_tail, so the same bits.
-template <int NT>
-__device__ __forceinline__ void ctrl_pose_tail_w0(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
-                                                  int cur, const double* xs, const double* bpv, const double* hdv,
-                                                  double* s_red, double (*s_pm)[LH_PMAX * 12], const double (*s_qT)[4],
-                                                  double* __restrict__ pose_mat, double* __restrict__ ptab,
-                                                  const double* __restrict__ ext, double* __restrict__ dxp) {
-    static_assert(LH_PMAX <= 32, "one pose per lane of a wave half");
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int P = prm.P;
-    double sp = 0.0;
-    for (int i = tid; i < n; i += NT) {
-        const double d = xs[i], b = bpv[i];
-        sp += (prm.strategy == 0) ? d * (lambda * d + b) : d * (lambda * hdv[i] * d + b);
-        dxp[i] = d;
-    }
-    for (int off = 32; off > 0; off >>= 1) sp += __shfl_xor(sp, off);
-    if (lane == 0) s_red[wave] = sp;
-    lds_barrier();
-    CSTAMP(9);
-    if (wave != 0) return;
-    if (lane == 0) {
-        double s2 = 0.0;
-        for (int w = 0; w < NT / 64; ++w) s2 += s_red[w];
-        ctrl->spose = s2;
-    }
-    const int cand = 1 - cur;
-    const int pidx = min(lane & 31, P - 1);
-    double up[6];
-    bool bad = false;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) { up[a] = xs[6 * pidx + a]; bad |= !isfinite(up[a]); }
-    if (bad) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) up[a] = 0.0;   // VertexPose::add NaN/Inf guard
-    }
-    const double th = d_twist_theta(up);
-    double sn, cs;
-    sincos(lane < 32 ? 0.5 * th : th, &sn, &cs);
-    const double sf = __shfl_xor(sn, 32), cf = __shfl_xor(cs, 32);   // lanes 0-31: sin/cos(theta)
-    if (lane < P) {
-        double qe[4], te[3], qn[4], tr[3], Rn[9];
-        d_se3_exp_trig(up, sn, cs, sf, cf, qe, te);
-        const double* Tc = &s_pm[cur][lane * 12];
-        const double tc[3] = {Tc[3], Tc[7], Tc[11]};
-        d_q_mul(qe, s_qT[lane], qn);
-        d_q_rotate(qe, tc, tr);
-        d_R_from_q(qn, Rn);
-        double To[12];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            To[4 * i] = Rn[3 * i]; To[4 * i + 1] = Rn[3 * i + 1]; To[4 * i + 2] = Rn[3 * i + 2];
-            To[4 * i + 3] = te[i] + tr[i];
-        }
-        double* Tl = &s_pm[cand][lane * 12];   // the candidate buffer's LDS copy is free after the solve
-        double* Tg = pose_mat + (size_t)cand * P * 12 + lane * 12;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) { Tl[i] = To[i]; Tg[i] = To[i]; }
-    }
-    wave_sync();
-    CSTAMP(10);
-    for (int pc = lane; pc < P * prm.ncam; pc += 64) {
-        const int pi = pc / prm.ncam, cam = pc - pi * prm.ncam;
-        double To[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) To[i] = s_pm[cand][pi * 12 + i];
-        d_pose_table(To, ext + LH_EXT * cam, ptab + (size_t)cand * P * prm.ncam * LH_PT + (pi * prm.ncam + cam) * LH_PT);
-    }
-    CSTAMP(11);
-}
-
 template <int SOLVER>
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
-                                             const uint16_t* __restrict__ pair_pq,
-                                             double* __restrict__ pose_mat, double* __restrict__ ptab,
-                                             const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
-                                             int mode /* 0 init, 1 trial */, volatile int* __restrict__ host_done,
-                                             int seq) {
+                                             const uint16_t* __restrict__ pair_pq, double* __restrict__ dxp,
+                                             lh_params prm, int mode /* 0 init, 1 trial */,
+                                             volatile int* __restrict__ host_done, int seq) {
     __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
     __shared__ __attribute__((aligned(16))) double dg[NP];   // also the PCG's vector (16-byte reads)
     __shared__ double bsv[NP], bpv[NP], hdv[NP], xs[NP];
@@ -2018,8 +1959,6 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
     __shared__ __attribute__((aligned(16))) double s_pcg[48];
-    __shared__ double s_pm[2][LH_PMAX * 12];
-    __shared__ double s_qT[LH_PMAX][4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
@@ -2044,7 +1983,6 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
     // element's rows need only the block's pose pair (p | q << 16, from the 840-byte pair table).
-    const double pmv = pose_mat[min(tid, 24 * P - 1)];
     const uint32_t* __restrict__ pqw = reinterpret_cast<const uint32_t*>(pair_pq);
     const int e36 = tid % 36, ea = e36 / 6, eb = e36 - 6 * ea, blk0 = tid / 36;
     const int ibase = (tid < ER) ? tid : (1 << 30);   // threads past ER hold no element
@@ -2056,7 +1994,6 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         vs[u] = (i < LY.total) ? rs_stage[i] : 0.0;
         mp[u] = pqw[min(blk0 + (ER / 36) * u, max(LY.npairs - 1, 0))];
     }
-    if (tid < 24 * P) s_pm[tid / (12 * P)][tid - (tid / (12 * P)) * 12 * P] = pmv;
     if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
         double mx = 0.0;
 #pragma unroll
@@ -2085,7 +2022,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         s_lam = lam_n;
     }
     lds_barrier();
-    const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
+    const int done = s_flags[0], accept = s_flags[1];
     if (done) return;
     const double lambda = s_lam;
 #ifdef LH_STAMPS
@@ -2179,27 +2116,17 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     CSTAMP(4);
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
-    // The committed rotations' quaternions (SE3(estimate_) of VertexPose::add) need no step: an
-    // otherwise idle wave computes them while the step is solved.
-    auto qt_committed = [&] {
-        for (int pi = lane; pi < P; pi += 64) {
-            const double* Tc = &s_pm[cur][pi * 12];
-            const double Rc[9] = {Tc[0], Tc[1], Tc[2], Tc[4], Tc[5], Tc[6], Tc[8], Tc[9], Tc[10]};
-            d_q_from_R(Rc, s_qT[pi]);
-        }
-    };
     if constexpr (SOLVER == 1) {
-        if (wave == 1) qt_committed();
         const int its = lds_pcg_solve(A, yv, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
         if (tid == 0) ctrl->pcg_iters += its;
         if (tid < n) xs[perm[tid]] = yv[tid];
         lds_barrier();
     } else {
-        lds_ldlt_solve(A, xs, n, NE, tid, perm, qt_committed);
+        lds_ldlt_solve(A, xs, n, NE, tid, perm);
     }
     CSTAMP(8);
 
-    ctrl_pose_tail_w0<CT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_qT, pose_mat, ptab, ext, dxp);
+    ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, dxp);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -2464,8 +2391,7 @@ __global__ __launch_bounds__(64) void k_dense(const double* __restrict__ rs, con
 
 __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                                const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
-                                               const uint32_t* __restrict__ rsmap, double* __restrict__ pose_mat,
-                                               double* __restrict__ ptab, const double* __restrict__ ext,
+                                               const uint32_t* __restrict__ rsmap,
                                                double* __restrict__ dxp, lh_params prm, int mode,
                                                volatile int* __restrict__ host_done, int seq, double* __restrict__ gA,
                                                const double* __restrict__ gS) {
@@ -2474,8 +2400,6 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     __shared__ int perm[GNMAX], iperm[GNMAX];
     __shared__ int s_flags[4];
     __shared__ double s_red[GT / 64], s_lam;
-    __shared__ double s_pm[2][LH_PMAX_WIN * 12];
-    __shared__ double s_trig[LH_PMAX_WIN][4], s_qT[LH_PMAX_WIN][4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NG = (n + GNB - 1) & ~(GNB - 1);
@@ -2493,7 +2417,6 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
-    for (int i = tid; i < 24 * P; i += GT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
     {
         double mx = 0.0;
         if (mode == 0)
@@ -2610,7 +2533,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     for (int i = tid; i < n; i += GT) { xs[perm[i]] = yv[i]; dxp[perm[i]] = yv[i]; }
     lds_barrier();
     CSTAMP(8);
-    ctrl_pose_tail<LH_PMAX_WIN, GT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red, s_pm, s_trig, s_qT, pose_mat, ptab, ext);
+    ctrl_step_tail<GT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, nullptr);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -2620,7 +2543,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 // ============================================================================
 // k_ctrl_p: the controller with the reduced pose system solved by PCG (lh_options.linear_solver =
 // PCG) past LH_PMAX poses, up to LH_PMAX_ANY (windows of many keyframes).  One
-// 1024-thread workgroup.  Same LM bookkeeping (ctrl_lm_step) and pose tail (ctrl_pose_tail) as the
+// 1024-thread workgroup.  Same LM bookkeeping (ctrl_lm_step) and step tail (ctrl_step_tail) as the
 // other controllers.  S stays in the packed blocks k_reduce wrote (rs: one 6x6 block per pose pair
 // that some landmark couples, plus every diagonal block; lh_plan.cpp), never densified: the PCG's
 // S p walks each pose's block row (Plan::brow_ent, ascending column) straight from the packed
@@ -2650,16 +2573,13 @@ __device__ __forceinline__ double wg_sum(double v, double* red, int lane, int wa
 __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                                const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                                const int32_t* __restrict__ brow_ptr, const uint32_t* __restrict__ brow_ent,
-                                               double* __restrict__ pose_mat, double* __restrict__ ptab,
-                                               const double* __restrict__ ext, double* __restrict__ dxp, lh_params prm,
+                                               double* __restrict__ dxp, lh_params prm,
                                                int mode, volatile int* __restrict__ host_done, int seq,
                                                double* __restrict__ ell) {
     __shared__ double pv[PNMAX], bpv[PNMAX], hdv[PNMAX], xs[PNMAX];
     __shared__ int s_flags[4];
     __shared__ __attribute__((aligned(16))) double s_red[3][CT / 64];
     __shared__ double s_lam;
-    __shared__ double s_pm[2][LH_PMAX_ANY * 12];
-    __shared__ double s_trig[LH_PMAX_ANY][4], s_qT[LH_PMAX_ANY][4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P;
@@ -2674,7 +2594,6 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
-    for (int i = tid; i < 24 * P; i += CT) s_pm[i / (12 * P)][i - (i / (12 * P)) * 12 * P] = pose_mat[i];
     {
         double mx = 0.0;
         if (mode == 0)
@@ -2698,7 +2617,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         s_lam = lam_n;
     }
     lds_barrier();
-    const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
+    const int done = s_flags[0], accept = s_flags[1];
     if (done) return;
     const double lambda = s_lam;
 
@@ -2850,8 +2769,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
     }
     if (tid == 0) ctrl->pcg_iters += steps;
     lds_barrier();
-    ctrl_pose_tail<LH_PMAX_ANY, CT>(ctrl, prm, n, lambda, cur, xs, bpv, hdv, s_red[0], s_pm, s_trig, s_qT, pose_mat,
-                                   ptab, ext);
+    ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red[0], nullptr);
 }
 
 // ============================================================================
@@ -3352,7 +3270,7 @@ template <int T>
 static size_t lin_smem_bytes(int ncam) {
     using Cfg = LinCfg<T>;
     return sizeof(double) * ((size_t)LH_WAVES * Cfg::SCR + 2 * (size_t)Cfg::UMAX * ncam * LH_PT_LDS + Cfg::UMAX * 6 +
-                             (size_t)ncam * LH_EXT + (Cfg::UMAX * (Cfg::UMAX + 1) / 2 + 1) / 2);
+                             (size_t)ncam * LH_EXT + (Cfg::UMAX * (Cfg::UMAX + 1) / 2 + 1) / 2 + 1);
 }
 
 // ============================================================================
@@ -3399,21 +3317,23 @@ hipError_t lh_prepare_lin(int lds_limit) {
 
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
-                         const double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
+                         double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag, long nslots,
-                         lh_params prm, int nrec,
-                         const uint64_t* fixed_bits) {
-    if (nchunks <= 0) return hipSuccess;
-    dim3 g(nchunks), b(256);
+                         lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat, int writer) {
+    writer = (trial && writer) ? 1 : 0;   // block 0 stores the trial's candidate poses and tables
+    if (nchunks + writer <= 0) return hipSuccess;
+    dim3 g(nchunks + writer), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
         const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
         if (prm.precision == 1)                                                                                    \
             hipLaunchKernelGGL((k_lin<TT, TR, true>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
-                               dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base);    \
+                               dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base,     \
+                               pose_mat, writer);                                                                  \
         else                                                                                                       \
             hipLaunchKernelGGL((k_lin<TT, TR, false>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
-                               dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base);    \
+                               dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base,     \
+                               pose_mat, writer);                                                                  \
     } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
@@ -3452,20 +3372,20 @@ hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_
 }
 
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
-                          const uint32_t* rsmap, const uint16_t* pair_pq, double* pose_mat, double* ptab, const double* ext,
-                          double* dxp, lh_params prm, int mode, int* host_done, int seq, double* gA, const double* gS,
-                          const int32_t* brow_ptr, const uint32_t* brow_ent) {
+                          const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
+                          int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
+                          const uint32_t* brow_ent) {
     if (prm.P > LH_PMAX && prm.solver == 1)
-        hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent, pose_mat,
-                           ptab, ext, dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
+        hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
+                           dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
     else if (prm.P > LH_PMAX)
-        hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap, pose_mat, ptab, ext,
+        hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
-        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, pose_mat, ptab, ext, dxp,
+        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     else
-        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, pose_mat, ptab, ext, dxp,
+        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     return hipGetLastError();
 }
@@ -3580,7 +3500,7 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
         const int its = lds_pcg_solve(A, xsol, dg, s_pcg, n, tid, tol, (max_it > 0 ? max_it : 2 * n) + 1);
         if (tid == 0 && iters) *iters = its;
     } else {
-        lds_ldlt_solve(A, xsol, n, NE, tid, nullptr, [] {});
+        lds_ldlt_solve(A, xsol, n, NE, tid, nullptr);
     }
     lds_barrier();
     if (tid < n) x[perm[tid]] = xsol[tid];
