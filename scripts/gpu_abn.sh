@@ -7,7 +7,7 @@ mkdir -p gpurun_out/abn
 : > gpurun_out/abn/summary.txt
 lib_of() { [ "$1" = A ] && echo lego-slam_amd/lib/liblego_ba.so || echo lego-slam_amd/lib/liblego_ba_$1.so; }
 for v in $VARIANTS; do
-  LH_LIB=$(lib_of $v) timeout -k 10 300 python -u -m pytest tests/test_golden.py -m gpu -x -q --timeout 120 \
+  LH_LIB=$(lib_of $v) timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_golden.py} -m gpu -x -q --timeout 120 \
       --timeout-method thread -p no:cacheprovider > gpurun_out/abn/tests_$v.log 2>&1 || { tail -30 gpurun_out/abn/tests_$v.log; exit 1; }
   echo "$v $(tail -1 gpurun_out/abn/tests_$v.log)" >> gpurun_out/abn/summary.txt
 done
