@@ -1260,10 +1260,13 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     // follow from the pair's row range alone, so every load of the pair is in flight together.
     double vs = 0.0, vh = 0.0;
     const int w_u = __builtin_amdgcn_readfirstlane(wave);
-    for (int base = ib + w_u; base < ie; base += 8 * RW) {
-        double x[8], y[8];
+    // 24 rows per wave per round: a C3 diagonal pair's ~300 rows arrive in one round trip (8 took three:
+    // 6.67 -> 6.44 us per launch; 16 took two and measured 7.2, its doubled loads per round slower)
+    constexpr int LH_RED_ROWS = 24;
+    for (int base = ib + w_u; base < ie; base += LH_RED_ROWS * RW) {
+        double x[LH_RED_ROWS], y[LH_RED_ROWS];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < LH_RED_ROWS; ++u) {
             const int it = base + u * RW;
             const bool in = it < ie;
             const double* row = rows + (size_t)(in ? it : ib) * LH_ROW;
@@ -1271,7 +1274,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
             y[u] = (in && act_h) ? row[off_h] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { vs += x[u]; vh += y[u]; }
+        for (int u = 0; u < LH_RED_ROWS; ++u) { vs += x[u]; vh += y[u]; }
     }
     part[0][wave][lane] = vs;
     part[1][wave][lane] = vh;
