@@ -436,7 +436,20 @@ hipError_t spin_wait(hipEvent_t ev) {
 
 // sync: return only once the copies are done (lh_upload); lh_solve leaves them queued ahead of its
 // kernels on the same stream.  Either way the next upload waits for them before it rewrites the staging.
+int upload_body(lh_handle* h, const lh_window* w, bool sync);
+
+// Every exit after the first copy out of the pinned staging is queued must leave ev_staging recorded
+// behind it, or the next upload could rewrite (or reallocate) the staging while that DMA still reads
+// it: the error returns (LH_E_UNSUPPORTED envelope checks, a failed HIP call) record it here.
 int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
+    const int st = upload_body(h, w, sync);
+    if (st != LH_OK && !h->staging_pending && h->ev_staging) {
+        if (hipEventRecord(h->ev_staging, h->stream) == hipSuccess) h->staging_pending = true;
+    }
+    return st;
+}
+
+int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     const double t0 = now_ms();
     h->uploaded = false;
     if (h->staging_pending) {
@@ -455,6 +468,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     lh::PlanCfg cfg;
     cfg.chunk_lm = h->opt.chunk_landmarks;
     lh::Plan& pl = h->plan;
+    cfg.rank_invariant_pairs = h->opt.world_size > 1;
     int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
     if (st != LH_OK) {
         HIPCHK(hipEventRecord(h->ev_staging, h->stream));

@@ -6,6 +6,8 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <cfloat>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -48,15 +50,26 @@ std::vector<int> llc_cpus() {
 // Workers are pinned to the CPUs sharing the caller's last-level cache (LH_HOST_PIN=0 leaves them to
 // the scheduler): a GPU box exposes every host core to a process with a share of them, and a worker
 // the scheduler puts on the other socket runs a pass's block at a fraction of the others' speed.
+// Only one live pool per process pins (a second handle's pool would stack its workers on the same
+// cores), and rank processes of one box (LOCAL_RANK) start at disjoint offsets into the LLC's list.
+namespace {
+std::atomic<int> g_pinned_pools{0};
+}
+
 Pool::Pool(int threads) {
     const char* pin_env = std::getenv("LH_HOST_PIN");
-    const std::vector<int> cpus = (pin_env && pin_env[0] == '0') ? std::vector<int>() : llc_cpus();
+    const bool want_pin = !(pin_env && pin_env[0] == '0');
+    int expected = 0;
+    pinned_ = want_pin && g_pinned_pools.compare_exchange_strong(expected, 1);
+    const std::vector<int> cpus = pinned_ ? llc_cpus() : std::vector<int>();
+    int offset = 0;
+    if (const char* lr = std::getenv("LOCAL_RANK")) offset = std::max(0, std::atoi(lr)) * std::max(threads - 1, 1);
     for (int i = 1; i < threads; ++i) {
         workers_.emplace_back([this] { loop(); });
-        if (i - 1 < (int)cpus.size()) {
+        if (!cpus.empty() && (offset + i - 1) < 4 * (int)cpus.size()) {
             cpu_set_t one;
             CPU_ZERO(&one);
-            CPU_SET(cpus[i - 1], &one);
+            CPU_SET(cpus[(offset + i - 1) % cpus.size()], &one);
             pthread_setaffinity_np(workers_.back().native_handle(), sizeof(one), &one);   // best effort
         }
     }
@@ -69,6 +82,7 @@ Pool::~Pool() {
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
+    if (pinned_) g_pinned_pools.store(0);
 }
 
 // Hand-off protocol (every atomic seq_cst).  A worker counts itself in active_ *before* it loads
@@ -115,7 +129,12 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
     }
     for (int i = job.next.fetch_add(1); i < n; i = job.next.fetch_add(1)) fn(i);
     job_.store(nullptr);
-    while (active_.load() != 0) __builtin_ia32_pause();
+    // bounded spin: a worker preempted while counted in active_ (oversubscribed or on the caller's
+    // own core) must get the CPU back, so after a short pause loop the caller yields
+    for (unsigned spin = 0; active_.load() != 0; ++spin) {
+        if (spin < kSpin) __builtin_ia32_pause();
+        else std::this_thread::yield();
+    }
 }
 
 namespace {
@@ -193,8 +212,13 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         }
         // the measurement is a cv::KeyPoint's float pixel widened (toVec2, algorithm.h:37): the device
         // keeps it as a float, so a value a float cannot hold exactly (or a NaN) is a bad argument
-        // (a loop of its own: it vectorises)
-        for (int64_t i = 2 * b; i < 2 * e; ++i) bd |= !((double)(float)w->obs_uv[i] == w->obs_uv[i]);
+        // (a loop of its own: it vectorises).  Only in-range finite values are converted: the
+        // double -> float conversion of a value past FLT_MAX is undefined, and +-inf would compare equal.
+        for (int64_t i = 2 * b; i < 2 * e; ++i) {
+            const double x = w->obs_uv[i];
+            const bool fin = std::fabs(x) <= (double)FLT_MAX;
+            bd |= !(fin && (double)(float)(fin ? x : 0.0) == x);
+        }
         if (bd) bad.store(1);
         if (us) unsorted.store(1);
     });
@@ -432,6 +456,15 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     if (P <= LH_PMAX_WIN) {
         for (int p = 0; p < P; ++p)
             for (int q = p; q < P; ++q) { pl.pair_list.push_back((uint16_t)p); pl.pair_list.push_back((uint16_t)q); }
+    } else if (cfg.rank_invariant_pairs) {
+        // landmark-sharded solve: every rank must lay out (and all-reduce) the same blocks, and a
+        // rank sees only its own chunks, so the list is every pair a landmark could couple (a
+        // landmark's poses lie within 64 consecutive keyframes), whatever this rank's shard holds
+        for (int p = 0; p < P; ++p)
+            for (int q = p; q < P && q - p < 64; ++q) {
+                pl.pair_list.push_back((uint16_t)p);
+                pl.pair_list.push_back((uint16_t)q);
+            }
     } else {
         std::vector<uint32_t> keys;
         for (int p = 0; p < P; ++p) keys.push_back((uint32_t)p << 16 | (uint32_t)p);

@@ -54,10 +54,12 @@ class Pool {
     std::atomic<int> active_{0};        // workers that may still touch job_'s job
     std::atomic<int> sleepers_{0};
     std::atomic<bool> stop_{false};
+    bool pinned_ = false;               // this pool holds the process's one pinned worker set
 };
 
 struct PlanCfg {
     int chunk_lm = 0;      // landmarks per chunk; 0 = auto (~512 chunks, 2 workgroups per CU)
+    bool rank_invariant_pairs = false;   // P > LH_PMAX_WIN: list every pair within the 64-pose span (sharded solves)
 };
 
 struct Plan {

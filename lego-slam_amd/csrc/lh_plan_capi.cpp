@@ -16,11 +16,13 @@ double now_ms() {
 extern "C" {
 
 // sizes[0..6] = n_chunks, n_sb, n_items, npairs, n_rec, n_slots, fixed_mask; tgroup[0..LH_TMAX+1]
-int lhp_plan_sizes(const lh_window* w, int chunk_lm, int threads, int64_t* sizes, int32_t* tgroup) {
+// rank_invariant: the block list a landmark-sharded (world_size > 1) handle uses past LH_PMAX_WIN poses
+int lhp_plan_sizes(const lh_window* w, int chunk_lm, int threads, int64_t* sizes, int32_t* tgroup, int rank_invariant) {
     lh::Pool pool(threads > 0 ? threads : 1);
     lh::Plan pl;
     lh::PlanCfg cfg;
     cfg.chunk_lm = chunk_lm;
+    cfg.rank_invariant_pairs = rank_invariant != 0;
     const int st = lh::plan_structure(w, cfg, false, pl, &pool);
     if (st != LH_OK) return st;
     const int64_t v[7] = {pl.n_chunks, pl.n_sb, pl.n_items, pl.npairs, pl.n_rec, pl.n_slots, (int64_t)pl.fixed_mask};
@@ -31,11 +33,12 @@ int lhp_plan_sizes(const lh_window* w, int chunk_lm, int threads, int64_t* sizes
 
 int lhp_plan_fill(const lh_window* w, int chunk_lm, int threads, lh_chunk* chunks, lh_subbatch* sbs, uint32_t* meta,
                   float* uv, int32_t* obs_perm, int32_t* lm_perm, uint32_t* pair_ptr, uint32_t* items,
-                  uint16_t* pair_pq, uint32_t* rsmap, double* lm_xyz) {
+                  uint16_t* pair_pq, uint32_t* rsmap, double* lm_xyz, int rank_invariant) {
     lh::Pool pool(threads > 0 ? threads : 1);
     lh::Plan pl;
     lh::PlanCfg cfg;
     cfg.chunk_lm = chunk_lm;
+    cfg.rank_invariant_pairs = rank_invariant != 0;
     const int st = lh::plan_structure(w, cfg, false, pl, &pool);
     if (st != LH_OK) return st;
     lh::PlanOut po{chunks, sbs, meta, uv, obs_perm, lm_perm, items, pair_pq, rsmap, lm_xyz};

@@ -15,16 +15,19 @@
 //   * Stop (:32-36) also writes the keyframe trajectory (KITTI pose format, T_wc per keyframe) to the file
 //     named by LEGO_BA_TRAJECTORY, if set: the reference writes none, and the KITTI-00 comparison needs it.
 //
-// This file needs the reference's headers (Sophus, Eigen, OpenCV, glog through common_include.h), none of
-// which exist in the build image, so it is not compiled here.  Everything it does beyond member access is
-// in lh_backend.h, which tests/backend_loop_test.cpp compiles and runs against the library on the GPU with
-// stand-in SLAM types of its own (tests/test_backend_loop.py).  The KITTI-00 end-to-end run (BASELINE
-// config 5) is therefore untested.
+// The reference's headers need Sophus, Eigen, OpenCV and glog (through common_include.h), none of which
+// exist in the build image.  The CPU suite compiles this file unchanged against minimal mock headers of
+// the legoslam types it touches (tests/mock_legoslam/legoslam/*.h), and the GPU suite links it into a
+// driver that runs the Backend thread on a window through those types (tests/backend_hip_driver.cpp,
+// tests/test_backend_loop.py).  The KITTI-00 end-to-end run (BASELINE config 5) stays untested: no
+// dataset and no reference libraries here.
 #include "legoslam/backend.h"
 
 #include <cstdlib>
+#include <functional>
 #include <memory>
 
+#include "legoslam/algorithm.h"   // toVec2 (backend_lego.cpp includes it too)
 #include "legoslam/feature.h"
 #include "legoslam/map.h"
 #include "legoslam/mappoint.h"

@@ -504,8 +504,8 @@ def _pl():
             raise RuntimeError(f"{PLAN_LIB} not built (run __graft_entry__.build())")
         lib = C.CDLL(PLAN_LIB)
         vp = C.c_void_p
-        lib.lhp_plan_sizes.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, vp, vp]
-        lib.lhp_plan_fill.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int] + [vp] * 11
+        lib.lhp_plan_sizes.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, vp, vp, C.c_int]
+        lib.lhp_plan_fill.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int] + [vp] * 11 + [C.c_int]
         lib.lhp_plan_time.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]
         if hasattr(lib, "lhp_plan_stages"):   # diagnostic entry point
@@ -516,12 +516,14 @@ def _pl():
     return _planlib
 
 
-def plan_window(w, chunk_lm=0, threads=1):
-    """The device layout lh_upload builds for window `w` (lh_plan.cpp), as numpy arrays."""
+def plan_window(w, chunk_lm=0, threads=1, rank_invariant=False):
+    """The device layout lh_upload builds for window `w` (lh_plan.cpp), as numpy arrays.  rank_invariant:
+    the block list of a landmark-sharded handle (world_size > 1) past 64 poses."""
     ref = _WindowRef(w)
     sizes = np.zeros(7, np.int64)
     tg = np.zeros(LH_TMAX + 2, np.int32)
-    _check(_pl().lhp_plan_sizes(C.byref(ref.s), chunk_lm, threads, _ptr(sizes), _ptr(tg)), "lhp_plan_sizes")
+    _check(_pl().lhp_plan_sizes(C.byref(ref.s), chunk_lm, threads, _ptr(sizes), _ptr(tg), int(rank_invariant)),
+           "lhp_plan_sizes")
     n_chunks, n_sb, n_items, npairs, n_rec, n_slots, fixed_mask = (int(x) for x in sizes)
     out = dict(chunks=np.zeros(n_chunks, CHUNK_DT), sbs=np.zeros(n_sb, SUBBATCH_DT),
                meta=np.zeros(n_slots, np.uint32), uv=np.zeros((n_slots, 2), np.float32), obs_perm=np.zeros(n_slots, np.int32),
@@ -529,7 +531,8 @@ def plan_window(w, chunk_lm=0, threads=1):
                items=np.zeros(n_items, np.uint32), pair_pq=np.zeros((npairs, 2), np.uint16),
                rsmap=np.zeros(npairs * 36, np.uint32), lm_xyz=np.zeros((ref.s.n_landmarks, 3)))
     k = ("chunks", "sbs", "meta", "uv", "obs_perm", "lm_perm", "pair_ptr", "items", "pair_pq", "rsmap", "lm_xyz")
-    _check(_pl().lhp_plan_fill(C.byref(ref.s), chunk_lm, threads, *[_ptr(out[n]) for n in k]), "lhp_plan_fill")
+    _check(_pl().lhp_plan_fill(C.byref(ref.s), chunk_lm, threads, *[_ptr(out[n]) for n in k], int(rank_invariant)),
+           "lhp_plan_fill")
     out.update(tgroup_begin=tg, fixed_mask=fixed_mask)
     return out
 

@@ -14,7 +14,7 @@ from windows import window
 META_VALID = 1 << 23
 
 
-def check_plan(w, pl):
+def check_plan(w, pl, rank_invariant=False):
     O = len(w["obs_pose"])
     L = len(w["lm_xyz"])
     P = w["n_poses"]
@@ -66,6 +66,8 @@ def check_plan(w, pl):
         keys = [(int(a), int(b)) for a, b in pq]
         assert keys == sorted(set(keys)) and all(a <= b for a, b in keys)
         assert {(p, p) for p in range(P)} <= set(keys)
+        if rank_invariant:   # every pair within the 64-pose span, whatever the shard holds
+            assert keys == [(p, q) for p in range(P) for q in range(p, min(P, p + 64))]
         where = {k: i for i, k in enumerate(keys)}
         bidx = lambda p, q: where[(p, q)]  # noqa: E731
     assert ptr[-1] == len(items)
@@ -189,7 +191,7 @@ def test_pool_back_to_back_jobs():
         assert lego_ba.pool_stress(8, runs, n) == runs * n * (n - 1) // 2
 
 
-@pytest.mark.parametrize("bad", [0.1, float("nan"), 1e300])
+@pytest.mark.parametrize("bad", [0.1, float("nan"), 1e300, float("inf"), -float("inf"), 3.5e38])
 def test_pixels_must_be_float_values(bad):
     """obs_uv is toVec2 of a cv::KeyPoint's float pixel (algorithm.h:37); the device keeps pixels as floats,
     so a measurement no float holds exactly is refused rather than silently rounded."""
@@ -201,3 +203,34 @@ def test_pixels_must_be_float_values(bad):
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.plan_window(w)
     assert e.value.status == lego_ba.LH_E_BADARG
+
+
+def test_sharded_block_list_is_rank_invariant():
+    """Past 64 poses the reduced system keeps only the blocks some chunk couples.  A
+    landmark-sharded solve all-reduces that packed buffer every trial, so each rank must lay out the
+    same blocks although it plans only its own landmarks: world_size > 1 handles list every pair
+    within the 64-pose span (shards with different lists would sum unrelated blocks)."""
+    P, L = 80, 3200
+    w = lego_ba.generate_window(P=P, L=L, k=8, seed=3)
+    first = np.full(L, P)
+    np.minimum.at(first, w["obs_lm"], w["obs_pose"])
+    shards = []
+    for keep in (first < P // 2, first >= P // 2):   # shards that couple different pose pairs
+        idx = np.flatnonzero(keep)
+        remap = np.full(L, -1)
+        remap[idx] = np.arange(len(idx))
+        o = keep[w["obs_lm"]]
+        s = dict(w, lm_xyz=w["lm_xyz"][idx], obs_lm=remap[w["obs_lm"][o]].astype(w["obs_lm"].dtype))
+        for k in ("obs_pose", "obs_cam", "obs_uv"):
+            s[k] = w[k][o]
+        shards.append(s)
+    own = [lego_ba.plan_window(s, threads=2) for s in shards]
+    inv = [lego_ba.plan_window(s, threads=2, rank_invariant=True) for s in shards]
+    for s, pl in zip(shards, inv):
+        check_plan(s, pl, rank_invariant=True)
+    assert np.array_equal(inv[0]["pair_pq"], inv[1]["pair_pq"])
+    # the per-shard lists differ (what made the unguarded all-reduce wrong) and each is a subset
+    assert not np.array_equal(own[0]["pair_pq"], own[1]["pair_pq"])
+    full = {tuple(map(int, k)) for k in inv[0]["pair_pq"]}
+    for pl in own:
+        assert {tuple(map(int, k)) for k in pl["pair_pq"]} <= full
