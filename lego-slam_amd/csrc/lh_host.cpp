@@ -36,13 +36,13 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat,
                          int writer);
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
-                            const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
-                            lh_params prm, int n_chunks);
+                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* maxd,
+                            lh_params prm, int n_chunks, int mode, int* host_done, int seq);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS,
-                          const int32_t* brow_ptr, const uint32_t* brow_ent);
+                          const int32_t* brow_ptr, const uint32_t* brow_ent, const uint16_t* units);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
@@ -256,6 +256,7 @@ struct lh_handle {
     View<lh_subbatch> s_sbs;
     View<uint32_t> s_items, s_pair_ptr, s_rsmap, s_brow_ent;
     View<uint16_t> s_pair_pq;
+    View<uint16_t> s_units;                                   // k_ctrl's work units (lh_ctrl_units)
     View<int32_t> s_lm_perm, s_brow_ptr;
     View<uint64_t> s_fixed;
     View<double> s_qt, s_ptab, s_ext;
@@ -273,7 +274,7 @@ struct lh_handle {
     View<lh_chunk> d_chunks;                                  // the per-window tables: views into d_arena
     View<lh_subbatch> d_sbs;
     View<uint32_t> d_pair_ptr, d_items, d_rsmap;
-    View<uint16_t> d_pair_pq;
+    View<uint16_t> d_pair_pq, d_units;
     View<int32_t> d_lm_perm;
     View<double> d_ptab_init, d_qt_init, d_ext;
     DevBuf<uint8_t> d_arena;
@@ -504,6 +505,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         const size_t o_qt = part(24 * (size_t)std::max(P, 1) * sizeof(double)), o_ext = part(LH_EXT * (size_t)ncam * sizeof(double));
         const size_t o_fix = part(pl.fixed_bits.size() * sizeof(uint64_t)), o_bptr = part(pl.brow_ptr.size() * sizeof(int32_t));
         const size_t o_bent = part(pl.brow_ent.size() * sizeof(uint32_t));
+        const size_t o_units = part(16 * LH_NSTEP * sizeof(uint16_t));
         HIPCHK(h->d_arena.ensure(bytes));
         HIPCHK(h->s_arena.ensure(bytes));
         h->arena_bytes = bytes;
@@ -527,6 +529,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         bind(h->d_fixed, h->s_fixed, db, sb, o_fix, pl.fixed_bits.size());
         bind(h->d_brow_ptr, h->s_brow_ptr, db, sb, o_bptr, pl.brow_ptr.size());
         bind(h->d_brow_ent, h->s_brow_ent, db, sb, o_bent, pl.brow_ent.size());
+        bind(h->d_units, h->s_units, db, sb, o_units, 16 * LH_NSTEP);
     }
     HIPCHK(h->d_meta.ensure(pl.n_slots));
     HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
@@ -608,6 +611,35 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         }
     }
 
+    // ---- k_ctrl's work units: the envelope of S in natural pose order.  Pose p's first coupled pose is
+    //      the lowest pose of any chunk window holding p (a chunk writes a block for every pair of its
+    //      window).  A sharded solve factors the sum of every rank's blocks, whose union this rank
+    //      cannot see: it takes the dense envelope. ----
+    if (P <= LH_PMAX) {
+        int32_t fcb[8];
+        for (int I = 0; I < 8; ++I) fcb[I] = 0;
+        if (h->opt.world_size == 1) {
+            std::vector<int> pf(P);
+            for (int p = 0; p < P; ++p) pf[p] = p;
+            for (size_t c = 0; c < pl.chunk_mask.size(); ++c) {
+                const uint64_t m = pl.chunk_mask[c];
+                if (!m) continue;
+                const int lo = pl.chunk_base[c] + __builtin_ctzll(m);
+                for (uint64_t b = m; b; b &= b - 1) {
+                    const int p = pl.chunk_base[c] + __builtin_ctzll(b);
+                    pf[p] = std::min(pf[p], lo);
+                }
+            }
+            const int n = 6 * P, NE = (n + 15) & ~15;
+            for (int I = 0; I < NE / 16; ++I) {
+                int f = 1 << 20;
+                for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
+                fcb[I] = f >> 3;
+            }
+        }
+        lh_ctrl_units(6 * P, fcb, h->s_units.p);
+    }
+
     // ---- params ----
     lh_params& prm = h->prm;
     prm.P = P;
@@ -632,6 +664,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.pcg_tol = h->opt.pcg_tol;
     prm.pcg_max_it = h->opt.pcg_max_iters;
     prm.no_evo = getenv("LH_NO_EVO") != nullptr;
+    prm.dec_in_reduce = (P <= LH_PMAX && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     const double t1 = now_ms();
 
@@ -714,7 +747,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     {
         Prof pr(h, KC_REDUCE);
         HIPCHK(lh_launch_reduce(s, h->d_rows.p, h->d_csc.p, h->d_pair_ptr.p, h->d_pair_pq.p, h->d_ctrl.p,
-                                h->d_rs_stage.p, h->d_maxd.p, h->prm, h->plan.n_chunks));
+                                h->d_rs_stage.p, h->d_maxd.p, h->prm, h->plan.n_chunks, mode, h->d_done, h->cur_trial));
         DBGSYNC("k_reduce");
     }
     if (h->comm) {
@@ -737,7 +770,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
             HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_pair_pq.p,
                               h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial, h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p,
-                              h->d_brow_ent.p));
+                              h->d_brow_ent.p, h->d_units.p));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;

@@ -397,10 +397,13 @@ __device__ __forceinline__ void edge_jac_pc(const double Pc[3], const double* __
     }
 }
 
-// ---- lh_options.precision = LH_PREC_FP32_RESID (BASELINE config 2's "fp32 residuals + fp64
-//      accumulate"): the per-edge camera point, residual, Huber weight and Jacobians in float, widened to
-//      double before any product that is summed (H blocks, b, chi2, the Schur terms stay fp64).  Not a
-//      mirror of the reference's arithmetic: parity to tolerance (tests/test_precision.py). ----
+// ---- lh_options.precision = LH_PREC_FP32_RESID (BASELINE config 3's "fp32 residuals + fp64
+//      accumulate"): the Jacobians (camera point, projection derivative, chain through the extrinsic and
+//      the pose rotation) in float, widened to double before any product that is summed.  The residual,
+//      the Huber weight, rho0, chi2, b and the gain ratio stay the fp64 mirror of the reference's
+//      arithmetic: a float residual carries ~3e-5 px of rounding, which decides LM
+//      steps on weakly conditioned windows.  The step is Gauss-Newton on a Jacobian
+//      rounded to float: parity to tolerance (tests/test_precision.py). ----
 __device__ __forceinline__ void q_rotate_f(const double* q, const float v[3], float o[3]) {
     const float w = (float)q[0], x = (float)q[1], y = (float)q[2], z = (float)q[3];
     const float u0 = 2.0f * (y * v[2] - z * v[1]), u1 = 2.0f * (z * v[0] - x * v[2]), u2 = 2.0f * (x * v[1] - y * v[0]);
@@ -895,13 +898,15 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (live) {
                 const double* pt = wt_c + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
-                if constexpr (F32) {
+                if constexpr (F32) {   // fp64 residual and weight (as below), fp32 Jacobians
                     if (wfl) {
                         E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
-                        edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
                     } else {
-                        edge_eval_f<true, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+                        double Pc[3];
+                        edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                        edge_robust(E, prm);
                     }
+                    edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
                 } else {
                     double Pc[3];
                     if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
@@ -955,13 +960,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             if (has) {
                 const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
-                if constexpr (F32) {
-                    edge_eval_f<true, false>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
-                } else {
-                    double Pc[3];
-                    edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                    edge_robust(E, prm);
-                }
+                double Pc[3];
+                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                edge_robust(E, prm);
                 edge_rho[o] = E.rho0;
                 chi_acc += E.rho0;
             }
@@ -984,14 +985,11 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         if (has) {
             const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
             EdgeEval E;
-            if constexpr (F32) {
-                edge_eval_f<true, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
-            } else {
-                double Pc[3];
-                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                edge_robust(E, prm);
-                edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
-            }
+            double Pc[3];
+            edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+            edge_robust(E, prm);
+            if constexpr (F32) edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+            else edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
             edge_rho[o] = E.rho0;
             chi_acc += E.rho0;
             const bool inl = prm.huber_delta <= 0.0 || E.e2 <= prm.huber_delta * prm.huber_delta;
@@ -1198,6 +1196,123 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 }
 
 // ============================================================================
+// LM bookkeeping shared by the controllers (isGoodStepInLM, computeLambdaInitLM)
+// ============================================================================
+struct CtrlWords {
+    double chi, lam, ni, last, spose, chi0;
+    int iter, fc, trials, nacc, done, cur, tl;
+};
+__device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl) {
+    CtrlWords w;
+    w.chi = ctrl->chi; w.lam = ctrl->lambda; w.ni = ctrl->ni; w.last = ctrl->last_chi; w.spose = ctrl->spose;
+    w.chi0 = ctrl->chi2_initial;
+    w.iter = ctrl->iter; w.fc = ctrl->false_cnt; w.trials = ctrl->trials; w.nacc = ctrl->accepted;
+    w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
+    return w;
+}
+__device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
+                                             int mode, double mdiag, double tchi, double sl, double ndg,
+                                             volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
+                                             int& cur_o, double& lam_o) {
+    double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
+    int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
+    int done = w.done, cur = w.cur;
+    int accept = 0, trace = 0;
+    if (!done) {
+        if (mode == 0) {
+            // computeLambdaInitLM (problem.cpp:470-504)
+            ni = 2.0;
+            chi = tchi;
+            chi0 = tchi;
+            if (prm.strategy == 0) {
+                if (!prm.lambda_given) {
+                    double m = fmin(prm.lambda_cap, mdiag);
+                    lam = prm.tau * m;
+                } else {
+                    lam = prm.lambda_init;
+                }
+            } else {
+                lam = 1e-5;
+            }
+            last = 1e20;
+            iter = 0; fc = 0; trials = 0; nacc = 0; tl = 0;
+            ctrl->nonpd = (int)ndg;
+            cur = 1 - cur;           // the initial linearisation becomes the committed one
+            accept = 1;
+            if (prm.max_iters <= 0) done = 1;
+            else trace = 1;
+        } else {
+            // isGoodStepInLM (problem.cpp:520-581)
+            double scale = 0.5 * (spose + sl);
+            scale += 1e-10;
+            const double rho = (chi - tchi) / scale;
+            const bool ok = rho > 0 && isfinite(tchi);
+            if (prm.strategy == 0) {
+                if (ok) {
+                    const double m = 2 * rho - 1;
+                    double alpha = 1.0 - m * m * m;   // std::pow(2 rho - 1, 3), problem.cpp:541 (within an ulp)
+                    alpha = fmin(alpha, 2.0 / 3.0);
+                    lam *= fmax(1.0 / 3.0, alpha);
+                    ni = 2;
+                    chi = tchi;
+                } else {
+                    lam *= ni;
+                    ni *= 2;
+                }
+            } else {
+                if (ok) { lam = fmax(lam / 9.0, 1e-7); chi = tchi; }
+                else lam = fmin(lam * 11.0, 1e7);
+            }
+            trials += 1;
+            bool inner_end;
+            if (ok) {
+                nacc += 1;
+                cur = 1 - cur;       // commit candidate landmarks, caches and poses
+                accept = 1;
+                fc = 0;
+                inner_end = true;
+            } else {
+                fc += 1;             // rollbackStates: the committed buffers are untouched
+                inner_end = fc >= prm.max_trials;
+            }
+            if (inner_end) {
+                iter += 1;
+                if (last - chi < prm.stop_dchi2) done = 1;
+                last = chi;
+                if (!done && iter >= prm.max_iters) done = 1;
+                if (!done) { fc = 0; trace = 1; }
+            }
+        }
+        if (trace) {
+            if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
+            tl += 1;
+        }
+        ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
+        ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
+        ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+        // The next trial is in the final iteration when one more completed iteration reaches max_iters.
+        // Its decision then either stops the loop (accept, or the last rejection) or leads to another
+        // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).
+        const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
+        ctrl->evo = (done || prm.no_evo) ? 0 : near;
+        // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
+        // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
+        // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
+        // trial ahead when near, so a stop by max_iters leaves nothing enqueued past it); it never
+        // advances past the stop trial, which bounds how many trials (and all-reduces) any rank
+        // can have enqueued.  One 32-bit store: the host never sees a torn pair.
+        if (host_done) {
+            if (done) host_done[0] = 1;
+            else host_done[1] = 2 * seq + near;
+        }
+    }
+    done_o = done;
+    accept_o = accept;
+    cur_o = cur;
+    lam_o = lam;
+}
+
+// ============================================================================
 // k_reduce: fixed-order sum of chunk slabs into the reduced pose system.
 // Block b < npairs handles pose pair (pp[b], pq[b]); block npairs the scalars.
 // ============================================================================
@@ -1208,10 +1323,14 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
 #define RT 1024
 #define RW (RT / 64)
 
+// With prm.dec_in_reduce (one rank, P <= LH_PMAX) the scalar block also takes the trial's LM decision
+// (isGoodStepInLM on its chi2 and gain-scale sums, the controller update, the host words): k_ctrl
+// then reads accept / lambda with its prefetch instead of deciding on one thread behind it.
 __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, const double* __restrict__ csc,
                                                const uint32_t* __restrict__ pair_ptr, const uint16_t* __restrict__ pair_pq,
-                                               const lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
-                                               double* __restrict__ maxd_out, lh_params prm, int n_chunks) {
+                                               lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
+                                               double* __restrict__ maxd_out, lh_params prm, int n_chunks, int mode,
+                                               volatile int* __restrict__ host_done, int seq) {
     STAMP_DECL
     __shared__ double part[3][RW][64];
     const lh_rs_layout LY = lh_rs_make(prm.P, prm.npairs);
@@ -1245,6 +1364,13 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
             rs[LY.off_sc + LH_SC_NDEG] = a2;
             rs[LY.off_sc + LH_SC_MAXD] = m;
             *maxd_out = m;
+            if (prm.dec_in_reduce && mode != 0) {
+                const CtrlWords cw = ctrl_load(ctrl);
+                int d_o, a_o, c_o;
+                double l_o;
+                ctrl_lm_step(ctrl, cw, prm, 1, 0.0, 0.5 * a0, a1, a2, host_done, seq, d_o, a_o, c_o, l_o);
+                ctrl->acc_last = a_o;
+            }
         }
         return;
     }
@@ -1301,17 +1427,19 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
 // k_ctrl: LM controller + reduced-system solve, one workgroup of 1024 threads (16 waves: the
 // LDLT's trailing updates are latency-bound MFMA chains, four waves per SIMD overlap them).
 //
-//  1. one global round trip: every thread prefetches its slice of BOTH reduced
-//     systems (staged candidate linearisation and committed one) plus the
-//     controller and pose matrices, while thread 0 runs isGoodStepInLM;
-//  2. the chosen system is scattered straight from registers into LDS in Eigen's
-//     LDLT pivot order (problem.cpp:420; left-looking Eigen LDLT pivots on the
-//     ORIGINAL |diag|, so the order is a static sort), committing it on accept;
-//  3. right-looking blocked LDL^T (8-column blocks, one barrier per block), see
-//     lds_ldlt_solve; the right-hand side rides along as row NP (forward substitution);
-//  4. blocked back substitution in one wave; candidate poses (VertexPose::add).
-// The matrix is padded to NE = ceil16(n) with identity rows: no bounds tests in
-// the inner loops.
+//  1. one global round trip: every thread prefetches its slice of the staged reduced system and
+//     the LM decision k_reduce took (one rank: prm.dec_in_reduce); otherwise thread 0 runs
+//     isGoodStepInLM behind the prefetch (the initial linearisation, sharded solves);
+//  2. the chosen system (the committed one on a rejection) is scattered straight from registers
+//     into LDS in natural pose order, lambda on the diagonal (problem.cpp:408-418), committing it on
+//     accept.  The solve is LDL^T without pivoting: S + lambda D is symmetric positive
+//     (semi)definite, where Eigen's LDLT (problem.cpp:420) pivots on the largest diagonal; the two
+//     agree to rounding (a zero pivot -- a fixed pose under STRATEGY1 -- is skipped as Eigen's
+//     pivot_is_valid does, and its component solved as 0);
+//  3. right-looking blocked LDL^T (8-column blocks, one barrier per block) over the envelope of S
+//     only (lh_ctrl_units), see lds_ldlt_solve; the right-hand side rides along as row NP;
+//  4. blocked back substitution in one wave; the step and the gain's pose part.
+// The matrix is padded to NE = ceil16(n) with identity rows: no bounds tests in the inner loops.
 // ============================================================================
 #define CT 1024
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
@@ -1485,18 +1613,6 @@ __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const doub
     }
 }
 
-// Work units of one elimination step over the active tile rows tg..7: unit 2i and 2i+1 are the
-// two halves of the tile columns of row 7 - i (i < R - 1; the first half also stores L^T and
-// updates the rhs), the last unit is row tg's L^T and rhs (its one tile is wave 0's).  Units
-// go to waves in this order: waves w, w+4, w+8, w+12 share a SIMD, and wave 0 runs the
-// critical chain, so its SIMD-mates 4, 8, 12 come last (lightest units).
-__device__ __forceinline__ int wave_unit(int w) {
-    // order: 1 2 3 5 6 7 9 10 11 13 14 15 4 8 12
-    if (w == 0) return -1;
-    if (w & 3) return (w >> 2) * 3 + (w & 3) - 1;
-    return 11 + (w >> 2);
-}
-
 // Back substitution x = L^-T z for block KB (compile-time, so every lane index below is an
 // immediate), one wave: y holds rows lane (y0) and lane + 64 (y1), already reduced by every block
 // above KB.  x_b = ND_b y_b: the block's 8 y values sit in lanes KB..KB+7 (mod 64), inside one
@@ -1555,20 +1671,21 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
     }
 }
 
-// Phases 3-4 of k_ctrl on a permuted, padded system already in LDS (A lower + rhs row NP):
-// blocked LDL^T with the forward substitution, then the back substitution; xsol[perm[r]] = the
-// solution's pivot-order entry r < n (perm == nullptr: xsol[r], pivot order).  Shared with the
+// Phases 3-4 of k_ctrl on a padded system already in LDS (A lower + rhs row NP, zeros in the upper
+// triangle): blocked LDL^T with the forward substitution, then the back substitution; xsol[perm[r]] =
+// the solution's entry r < n (perm == nullptr: xsol[r]).  units: the per-step work units in LDS
+// (lh_ctrl_units: the envelope of S decides which tile rows a step touches).  Shared with the
 // k_ldlt_probe test hook.  Must be called by all CT threads.
 //
 // Step t eliminates block column k0 = 8t.  Interval t (one barrier each):
-//   wave 0:       the trailing update of the diagonal tile holding block t+1, then the factor
-//                 of block t+1 (N by step parity, ND per block);
-//   the other waves: L_I (stored transposed), T_I, the rhs update and A_IJ -= T_I a_J^T, by
-//                 half tile rows (wave_unit), skipping wave 0's tile;
+//   wave 0:       the trailing update of the diagonal tile holding block t+1 (when its envelope
+//                 reaches block t), then the factor of block t+1 (N by step parity, ND per block);
+//   waves 1-15:   their unit of step t: L_I (stored transposed), T_I, the rhs update and
+//                 A_IJ -= T_I a_J^T over the unit's tile columns;
 //   wave 12 first: z_t = b_t N_t (Eigen's solve tolerance applied).
 // L lives in the upper triangle, so the raw block columns stay readable for the whole step.
 __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid,
-                                               const int* __restrict__ perm) {
+                                               const int* __restrict__ perm, const uint16_t* __restrict__ units) {
     const int lane = tid & 63, wave = tid >> 6;
     __shared__ __attribute__((aligned(16))) LdltBlockLds F;
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
@@ -1605,23 +1722,18 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         }
         if (m0 < nb) {
             const int g0 = m0 >> 4;               // tile row/col of the next diagonal block
-            const int tg = g0;                    // first tile row with rows >= m0 (and first tile column)
+            const uint32_t uw = __builtin_amdgcn_readfirstlane(units[wv * LH_NSTEP + t]);
             if (wv == 0) {
-                ldlt_tile_row(A, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
-                wave_sync();
+                if (uw & LH_UNIT_VALID) {
+                    ldlt_tile_row(A, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
+                    wave_sync();
+                }
                 LDLT_SSTAMP(0);
                 factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
                 LDLT_SSTAMP(1);
-            }
-            const int gl = (NE >> 4) - 1, R = gl - tg + 1;
-            const int u = wave_unit(wv);
-            if (u >= 0 && u < 2 * (R - 1)) {
-                const int g = gl - (u >> 1), nt = g - tg + 1, split = tg + ((nt + 1) >> 1);
-                const bool first = (u & 1) == 0;
-                ldlt_tile_row(A, N, ND, k0, 16 * g, first ? 16 * tg : 16 * split, first ? 16 * split : 16 * g + 16, -1,
-                              first, lane);
-            } else if (u == 2 * (R - 1)) {
-                ldlt_tile_row(A, N, ND, k0, 16 * g0, 0, 0, -1, true, lane);   // row tg: L^T and rhs only
+            } else if (uw & LH_UNIT_VALID) {
+                const int I = uw & 7, jb0 = (uw >> 3) & 7, jb1 = (uw >> 6) & 15;
+                ldlt_tile_row(A, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
             if (wv != 0) LDLT_SSTAMP(3);
         }
@@ -1810,120 +1922,6 @@ __device__ __forceinline__ int lds_pcg_solve(double* __restrict__ A, double* __r
     return it;
 }
 
-struct CtrlWords {
-    double chi, lam, ni, last, spose, chi0;
-    int iter, fc, trials, nacc, done, cur, tl;
-};
-__device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl) {
-    CtrlWords w;
-    w.chi = ctrl->chi; w.lam = ctrl->lambda; w.ni = ctrl->ni; w.last = ctrl->last_chi; w.spose = ctrl->spose;
-    w.chi0 = ctrl->chi2_initial;
-    w.iter = ctrl->iter; w.fc = ctrl->false_cnt; w.trials = ctrl->trials; w.nacc = ctrl->accepted;
-    w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
-    return w;
-}
-__device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
-                                             int mode, double mdiag, double tchi, double sl, double ndg,
-                                             volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
-                                             int& cur_o, double& lam_o) {
-    double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
-    int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
-    int done = w.done, cur = w.cur;
-    int accept = 0, trace = 0;
-    if (!done) {
-        if (mode == 0) {
-            // computeLambdaInitLM (problem.cpp:470-504)
-            ni = 2.0;
-            chi = tchi;
-            chi0 = tchi;
-            if (prm.strategy == 0) {
-                if (!prm.lambda_given) {
-                    double m = fmin(prm.lambda_cap, mdiag);
-                    lam = prm.tau * m;
-                } else {
-                    lam = prm.lambda_init;
-                }
-            } else {
-                lam = 1e-5;
-            }
-            last = 1e20;
-            iter = 0; fc = 0; trials = 0; nacc = 0; tl = 0;
-            ctrl->nonpd = (int)ndg;
-            cur = 1 - cur;           // the initial linearisation becomes the committed one
-            accept = 1;
-            if (prm.max_iters <= 0) done = 1;
-            else trace = 1;
-        } else {
-            // isGoodStepInLM (problem.cpp:520-581)
-            double scale = 0.5 * (spose + sl);
-            scale += 1e-10;
-            const double rho = (chi - tchi) / scale;
-            const bool ok = rho > 0 && isfinite(tchi);
-            if (prm.strategy == 0) {
-                if (ok) {
-                    const double m = 2 * rho - 1;
-                    double alpha = 1.0 - m * m * m;   // std::pow(2 rho - 1, 3), problem.cpp:541 (within an ulp)
-                    alpha = fmin(alpha, 2.0 / 3.0);
-                    lam *= fmax(1.0 / 3.0, alpha);
-                    ni = 2;
-                    chi = tchi;
-                } else {
-                    lam *= ni;
-                    ni *= 2;
-                }
-            } else {
-                if (ok) { lam = fmax(lam / 9.0, 1e-7); chi = tchi; }
-                else lam = fmin(lam * 11.0, 1e7);
-            }
-            trials += 1;
-            bool inner_end;
-            if (ok) {
-                nacc += 1;
-                cur = 1 - cur;       // commit candidate landmarks, caches and poses
-                accept = 1;
-                fc = 0;
-                inner_end = true;
-            } else {
-                fc += 1;             // rollbackStates: the committed buffers are untouched
-                inner_end = fc >= prm.max_trials;
-            }
-            if (inner_end) {
-                iter += 1;
-                if (last - chi < prm.stop_dchi2) done = 1;
-                last = chi;
-                if (!done && iter >= prm.max_iters) done = 1;
-                if (!done) { fc = 0; trace = 1; }
-            }
-        }
-        if (trace) {
-            if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
-            tl += 1;
-        }
-        ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
-        ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
-        ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
-        // The next trial is in the final iteration when one more completed iteration reaches max_iters.
-        // Its decision then either stops the loop (accept, or the last rejection) or leads to another
-        // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).
-        const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
-        ctrl->evo = (done || prm.no_evo) ? 0 : near;
-        // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
-        // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
-        // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
-        // trial ahead when near, so a stop by max_iters leaves nothing enqueued past it); it never
-        // advances past the stop trial, which bounds how many trials (and all-reduces) any rank
-        // can have enqueued.  One 32-bit store: the host never sees a torn pair.
-        if (host_done) {
-            if (done) host_done[0] = 1;
-            else host_done[1] = 2 * seq + near;
-        }
-    }
-    done_o = done;
-    accept_o = accept;
-    cur_o = cur;
-    lam_o = lam;
-}
-
 // The controllers' tail (xs: the pose step in pose order, in LDS): the pose part of the gain
 // denominator (isGoodStepInLM's scale, problem.cpp:528-533), the wave partials summed in wave order
 // into ctrl->spose, and (dxp non-null) the step stored for k_lin.  The candidate poses
@@ -1953,15 +1951,13 @@ __device__ __forceinline__ void ctrl_step_tail(lh_ctrl* __restrict__ ctrl, const
 template <int SOLVER>
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
-                                             const uint16_t* __restrict__ pair_pq, double* __restrict__ dxp,
-                                             lh_params prm, int mode /* 0 init, 1 trial */,
+                                             const uint16_t* __restrict__ pair_pq, const uint16_t* __restrict__ units,
+                                             double* __restrict__ dxp, lh_params prm, int mode /* 0 init, 1 trial */,
                                              volatile int* __restrict__ host_done, int seq) {
-    __shared__ double A[(NP + 1) * AS];   // permuted S + lambda D (lower); L and D in place; row NP = rhs -> z / D
-    __shared__ __attribute__((aligned(16))) double dg[NP];   // also the PCG's vector (16-byte reads)
-    __shared__ double bsv[NP], bpv[NP], hdv[NP], xs[NP];
-    __shared__ __attribute__((aligned(16))) double yv[NP];
-    __shared__ int perm[NP], iperm[NP];
-    __shared__ __attribute__((aligned(16))) unsigned long long pkey[NP];   // pivot keys (pivot rank)
+    __shared__ double A[(NP + 1) * AS];   // S + lambda D (lower); L^T above, D in place; row NP = rhs -> z / D
+    __shared__ __attribute__((aligned(16))) double dg[NP];   // the PCG's vector (16-byte reads)
+    __shared__ double bpv[NP], hdv[NP], xs[NP];
+    __shared__ uint16_t s_units[16 * LH_NSTEP];
     __shared__ int s_flags[4];
     __shared__ double s_red[CT / 64], s_lam;
     __shared__ __attribute__((aligned(16))) double s_pcg[48];
@@ -1969,26 +1965,33 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
     const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
+    const bool decided = mode != 0 && prm.dec_in_reduce;   // k_reduce took this trial's LM decision
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    // ---------------- 1. prefetch (one round trip); the controller's words first ----------------
+    // ---------------- 1. prefetch (one round trip) ----------------
     double tchi = 0.0, sl = 0.0, ndg = 0.0;
     CtrlWords cw{};
-    if (tid == 0) {
+    if (!decided && tid == 0) {
         cw = ctrl_load(ctrl);
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
-    // both pose-matrix buffers (used after the solve) go to LDS; their load is issued first and
-    // unconditionally (clamped), so it shares the bulk's round trip instead of following it
-    // Only the staged system is loaded here: a trial is accepted far more often than not, and a
-    // rejected one loads the committed system after the decision (one more round trip).  Round u
-    // covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
+    // the decision's words: uniform loads in the same round trip as the system
+    int done = 0, accept = 0;
+    double lambda = 0.0;
+    if (decided) {
+        done = __builtin_amdgcn_readfirstlane(ctrl->done);
+        accept = __builtin_amdgcn_readfirstlane(ctrl->acc_last);
+        lambda = ctrl->lambda;
+    }
+    // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
     // element's rows need only the block's pose pair (p | q << 16, from the 840-byte pair table).
+    // Only the staged system is loaded here: a trial is accepted far more often than not, and a
+    // rejected one loads the committed system after the decision (one more round trip).
     const uint32_t* __restrict__ pqw = reinterpret_cast<const uint32_t*>(pair_pq);
     const int e36 = tid % 36, ea = e36 / 6, eb = e36 - 6 * ea, blk0 = tid / 36;
     const int ibase = (tid < ER) ? tid : (1 << 30);   // threads past ER hold no element
@@ -2000,37 +2003,41 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         vs[u] = (i < LY.total) ? rs_stage[i] : 0.0;
         mp[u] = pqw[min(blk0 + (ER / 36) * u, max(LY.npairs - 1, 0))];
     }
-    if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
-        double mx = 0.0;
-#pragma unroll
-        for (int u = 0; u < NLD; ++u) {
-            const int i = u * ER + ibase;
-            if (i >= LY.off_hd && i < LY.off_hd + n) mx = fmax(mx, fabs(vs[u]));
-        }
-        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
-        if (lane == 0) s_red[wave] = mx;
-        lds_barrier();
-    }
+    uint32_t unit2 = 0;   // two unit words per thread (SOLVER 0)
+    if (SOLVER == 0 && tid < 8 * LH_NSTEP) unit2 = reinterpret_cast<const uint32_t*>(units)[tid];
 
-    // ---------------- LM bookkeeping (thread 0) ----------------
-    if (tid == 0) {
-        double mdiag = 0.0;
-        if (mode == 0) {
-            for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
-            mdiag = fmax(*maxd_in, mdiag);
+    if (!decided) {
+        if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
+            double mx = 0.0;
+#pragma unroll
+            for (int u = 0; u < NLD; ++u) {
+                const int i = u * ER + ibase;
+                if (i >= LY.off_hd && i < LY.off_hd + n) mx = fmax(mx, fabs(vs[u]));
+            }
+            for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+            if (lane == 0) s_red[wave] = mx;
+            lds_barrier();
         }
-        int done, accept, cur;
-        double lam_n;
-        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
-        s_flags[0] = done;
-        s_flags[1] = accept;
-        s_flags[2] = cur;
-        s_lam = lam_n;
+        // ---------------- LM bookkeeping (thread 0) ----------------
+        if (tid == 0) {
+            double mdiag = 0.0;
+            if (mode == 0) {
+                for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
+                mdiag = fmax(*maxd_in, mdiag);
+            }
+            int d_o, a_o, c_o;
+            double lam_n;
+            ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            s_flags[0] = d_o;
+            s_flags[1] = a_o;
+            s_lam = lam_n;
+        }
+        lds_barrier();
+        done = s_flags[0];
+        accept = s_flags[1];
+        lambda = s_lam;
     }
-    lds_barrier();
-    const int done = s_flags[0], accept = s_flags[1];
     if (done) return;
-    const double lambda = s_lam;
 #ifdef LH_STAMPS
     if (tid == 0) {
         atomicAdd(&lh_stamps[32], ct_start);
@@ -2040,7 +2047,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #endif
     CSTAMP(1);
 
-    // ---------------- 2. commit, diag + lambda, pivot order, scatter into LDS ----------------
+    // ---------------- 2. commit, diag + lambda, scatter into LDS (natural order) ----------------
     if (!accept) {   // rollback: the committed system, with the new lambda
 #pragma unroll
         for (int u = 0; u < NLD; ++u) {
@@ -2053,82 +2060,48 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         const int i = u * ER + ibase;
         const double v = vs[u];
         if (accept && i < LY.total) rs_commit[i] = v;
-        // S element i: pose pair (p, q), p <= q, entry (ea, eb) -> rows 6 p + ea, 6 q + eb
-        const uint32_t pp = mp[u] & 0xffffu, qq = mp[u] >> 16;
-        mp[u] = LH_RSMAP(6 * pp + ea, 6 * qq + eb, pp == qq);
         if (i < LY.off_bs) {
-            const int gi = LH_RSMAP_ROW(mp[u]), gj = LH_RSMAP_COL(mp[u]);
+            // S element i: pose pair (p, q), p <= q, entry (ea, eb) -> rows 6 p + ea, 6 q + eb.  The
+            // upper slot of every off-diagonal entry is zeroed: the factor stores L^T there where the
+            // envelope reaches, and the back substitution reads zeros elsewhere.
+            const int pp = (int)(mp[u] & 0xffffu), qq = (int)(mp[u] >> 16);
+            const int gi = 6 * pp + ea, gj = 6 * qq + eb;
+            const int hi = max(gi, gj), lo = min(gi, gj);
             if (gi == gj) {
-                const double dv = (prm.strategy == 0) ? v + lambda : v + lambda * v;
-                dg[gi] = dv;
-                // pivot key: |d| ordered as its bits (+1), NaN below everything (0)
-                const double ad = fabs(dv);
-                pkey[gi] = (ad == ad) ? (unsigned long long)__double_as_longlong(ad) + 1ull : 0ull;
+                A[gi * AS + gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
+            } else if (pp != qq || gi > gj) {
+                A[hi * AS + lo] = v;
+                A[lo * AS + hi] = 0.0;
             }
         } else if (i < LY.off_bp) {
-            bsv[i - LY.off_bs] = v;
+            A[NP * AS + (i - LY.off_bs)] = v;
         } else if (i < LY.off_hd) {
             bpv[i - LY.off_bp] = v;
         } else if (i < LY.off_hd + n) {
             hdv[i - LY.off_hd] = v;
         }
     }
-    if (tid >= n && tid < NP) { dg[tid] = __builtin_nan(""); pkey[tid] = 0ull; }   // never counted: key 0, index above every real row
-    lds_barrier();
-    CSTAMP(2);
-    {
-        // |diag| descending; total order (NaN last, ties by index) keeps perm a permutation.
-        // Eight threads per row, each counting over 16 of the 128 keys (integer compares of the
-        // keys written with dg; rows n..NP have key 0).
-        const int row = tid >> 3, part = tid & 7;
-        int r = 0;
-        if (row < n) {
-            const unsigned long long ki = pkey[row];
-            unsigned long long kj[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) kj[u] = pkey[part * 16 + u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) r += (kj[u] > ki) | ((kj[u] == ki) & (part * 16 + u < row));
-        }
-        r += __shfl_xor(r, 1);
-        r += __shfl_xor(r, 2);
-        r += __shfl_xor(r, 4);
-        if (part == 0 && row < NP) {
-            const int rr = row < n ? r : row;
-            perm[rr] = row;
-            iperm[row] = rr;
-        }
+    if (tid >= n && tid < NE) {   // identity padding rows
+        A[tid * AS + tid] = 1.0;
+        A[NP * AS + tid] = 0.0;
     }
-    lds_barrier();
-    CSTAMP(3);
-#pragma unroll
-    for (int u = 0; u < NLD; ++u) {
-        const int i = u * ER + ibase;
-        if (i < LY.off_bs) {
-            const int ri = iperm[LH_RSMAP_ROW(mp[u])], rj = iperm[LH_RSMAP_COL(mp[u])];
-            if (!LH_RSMAP_DIAG(mp[u])) A[max(ri, rj) * AS + min(ri, rj)] = vs[u];
-            else if (ri > rj) A[ri * AS + rj] = vs[u];
-        }
-    }
-    if (tid < NE) {
-        A[tid * AS + tid] = tid < n ? dg[perm[tid]] : 1.0;
-        A[NP * AS + tid] = tid < n ? bsv[perm[tid]] : 0.0;
-    }
-    for (int x = tid; x < (NE - n) * NE; x += CT) {   // identity padding rows
+    for (int x = tid; x < (NE - n) * NE; x += CT) {
         const int r = n + x / NE, c = x - NE * (x / NE);
-        if (c < r) A[r * AS + c] = 0.0;
+        if (c < r) {
+            A[r * AS + c] = 0.0;
+            A[c * AS + r] = 0.0;
+        }
     }
+    if (SOLVER == 0 && tid < 8 * LH_NSTEP) reinterpret_cast<uint32_t*>(s_units)[tid] = unit2;
     lds_barrier();
     CSTAMP(4);
 
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
     if constexpr (SOLVER == 1) {
-        const int its = lds_pcg_solve(A, yv, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
+        const int its = lds_pcg_solve(A, xs, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
         if (tid == 0) ctrl->pcg_iters += its;
-        if (tid < n) xs[perm[tid]] = yv[tid];
-        lds_barrier();
     } else {
-        lds_ldlt_solve(A, xs, n, NE, tid, perm);
+        lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units);
     }
     CSTAMP(8);
 
@@ -3361,11 +3334,11 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 }
 
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
-                            const uint16_t* pair_pq, const lh_ctrl* ctrl, double* rs_stage, double* maxd,
-                            lh_params prm, int n_chunks) {
+                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* maxd,
+                            lh_params prm, int n_chunks, int mode, int* host_done, int seq) {
     const int npairs = prm.npairs;
     hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, rows, csc, pair_ptr, pair_pq, ctrl,
-                       rs_stage, maxd, prm, n_chunks);
+                       rs_stage, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq);
     return hipGetLastError();
 }
 
@@ -3380,7 +3353,7 @@ hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
-                          const uint32_t* brow_ent) {
+                          const uint32_t* brow_ent, const uint16_t* units) {
     if (prm.P > LH_PMAX && prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
@@ -3388,10 +3361,10 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
-        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, dxp,
+        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     else
-        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, dxp,
+        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units, dxp,
                            prm, mode, (volatile int*)host_done, seq);
     return hipGetLastError();
 }
@@ -3469,47 +3442,36 @@ hipError_t lh_launch_gather(hipStream_t st, const lh_ctrl* ctrl, const double* r
     return hipGetLastError();
 }
 
-// ---- LDL^T probe (tests): x = (S)^-1 b through k_ctrl's pivot order, LDS layout and
-//      lds_ldlt_solve, for a dense symmetric S (row-major n x n, n <= LH_NPAD) ----
+// ---- LDL^T probe (tests): x = (S)^-1 b through k_ctrl's LDS layout and lds_ldlt_solve (natural
+//      order, a dense envelope) or lds_pcg_solve, for a dense symmetric S (row-major n x n, n <= LH_NPAD) ----
 __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S, const double* __restrict__ b, int n,
                                                    double* __restrict__ x, int solver, double tol, int max_it,
                                                    int* __restrict__ iters) {
     __shared__ double A[(NP + 1) * AS];
     __shared__ __attribute__((aligned(16))) double dg[NP];
     __shared__ __attribute__((aligned(16))) double xsol[NP];
-    __shared__ int perm[NP];
+    __shared__ uint16_t s_units[16 * LH_NSTEP];
     const int tid = threadIdx.x, NE = (n + 15) & ~15;
-    if (tid < NP) dg[tid] = tid < n ? S[(size_t)tid * n + tid] : __builtin_nan("");
-    lds_barrier();
-    if (tid < n) {
-        double di = fabs(dg[tid]);
-        if (!(di == di)) di = -1.0;
-        int r = 0;
-        for (int j = 0; j < NP; ++j) {
-            double d = fabs(dg[j]);
-            if (!(d == d)) d = -1.0;
-            r += (d > di) || (d == di && j < tid);
-        }
-        perm[r] = tid;
-    } else if (tid < NP) {
-        perm[tid] = tid;
+    if (tid == 0) {
+        int32_t fcb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        lh_ctrl_units(n, fcb, s_units);
     }
-    lds_barrier();
     for (int e = tid; e < NE * NE; e += CT) {
         const int r = e / NE, c = e - NE * (e / NE);
-        if (c <= r) A[r * AS + c] = (r < n) ? ((c < n) ? S[(size_t)perm[r] * n + perm[c]] : 0.0) : (r == c ? 1.0 : 0.0);
+        if (c <= r) A[r * AS + c] = (r < n) ? ((c < n) ? S[(size_t)r * n + c] : 0.0) : (r == c ? 1.0 : 0.0);
+        else A[r * AS + c] = 0.0;
     }
-    if (tid < NE) A[NP * AS + tid] = tid < n ? b[perm[tid]] : 0.0;
+    if (tid < NE) A[NP * AS + tid] = tid < n ? b[tid] : 0.0;
     lds_barrier();
     if (solver == 1) {
         __shared__ __attribute__((aligned(16))) double s_pcg[48];
         const int its = lds_pcg_solve(A, xsol, dg, s_pcg, n, tid, tol, (max_it > 0 ? max_it : 2 * n) + 1);
         if (tid == 0 && iters) *iters = its;
     } else {
-        lds_ldlt_solve(A, xsol, n, NE, tid, nullptr);
+        lds_ldlt_solve(A, xsol, n, NE, tid, nullptr, s_units);
     }
     lds_barrier();
-    if (tid < n) x[perm[tid]] = xsol[tid];
+    if (tid < n) x[tid] = xsol[tid];
 }
 
 // ---- the same probe through k_ctrl_g's global-memory solve (LH_NPAD < n <= 6 LH_PMAX_WIN):

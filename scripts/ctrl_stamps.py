@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import lego_ba  # noqa: E402
 from windows import window  # noqa: E402
 
-NAMES = ["start", "prefetch + LM logic", "commit + diag", "pivot rank", "scatter into LDS", "block 0 factor",
+NAMES = ["start", "prefetch + LM decision", "commit + diag", "pivot rank", "scatter into LDS", "block 0 factor",
          "LDLT steps", "back substitution", "dx scatter", "trig / q_T", "pose compose", "pose / table stores", "tail"]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 if cfg.startswith("P"):   # P<n>: an n-keyframe window of C3's size (n > 21: k_ctrl_g; its phase 5 is unused)
@@ -34,8 +34,12 @@ tot_cyc = (cyc[-1] - cyc[0]) / n
 tot_ns = (st[63] - st[62]) / n * 10.0
 print(f"{cfg}: {n} live k_ctrl launches, {tot_cyc:.0f} cycles = {tot_ns / 1000:.2f} us start-to-end "
       f"(clock {tot_cyc / tot_ns:.2f} GHz)")
+prev = 0
 for i in range(1, len(NAMES)):
-    d = (cyc[i] - cyc[i - 1]) / n
+    if cyc[i] == 0:   # a phase this build does not stamp (round 4: no pivot rank, no separate commit)
+        continue
+    d = (cyc[i] - cyc[prev]) / n
+    prev = i
     print(f"  {NAMES[i]:22s} {d:9.0f} cycles {d / tot_cyc * 100:5.1f}%  {d / (tot_cyc / tot_ns) / 1000:6.2f} us")
 if cfg.startswith("P"):   # k_ctrl_g's panel sub-phases, summed over the panels: (a) load, (b) diagonal
     # block, (c) rows below, (d)+(e) write-back and trailing tiles (stamps 13-16 follow stamp 5)
