@@ -272,9 +272,10 @@ int lh_lk_track(lh_handle *h, const lh_lk_input *in, lh_lk_result *out);
 /* ---- test hooks (not part of the reference interface) ---- */
 /* f64 MFMA accumulator-layout probe: D(16x16) = A(16x4) * B(4x16), device pointers, row-major */
 int lh_debug_mfma_probe(const double *A, const double *B, double *D);
-/* k_ctrl's reduced-system solve (Eigen-LDLT pivot order, blocked LDL^T, back substitution) on a
-   dense symmetric n x n S (row-major), n <= 384: x = S^-1 b.  Device pointers.  n > 128 runs k_ctrl_g's
-   global-memory solve (the windows of 22..64 keyframes). */
+/* k_ctrl's reduced-system solve (natural order, blocked LDL^T over a dense envelope, back
+   substitution) on a dense symmetric n x n S (row-major), n <= 384: x = S^-1 b.  Device pointers.
+   n > 128 runs k_ctrl_g's global-memory solve (Eigen-LDLT pivot order: dense windows of 22..64
+   keyframes). */
 int lh_debug_ldlt_probe(const double* S, const double* b, int n, double* x);
 /* k_ctrl's PCG solve (same LDS layout and pivot order) on a dense symmetric n x n S, n <= 128:
    x ~= S^-1 b to ||r|| <= tol ||b|| within max_iters (<= 0: 2n).  Device pointers; *iters host. */
@@ -290,6 +291,9 @@ int lh_debug_stamps(unsigned long long *out, int n, int reset);
 int lh_debug_time_lin(lh_handle *h, int reps, double *ms);
 /* reduced-system all-reduces (data-path collectives) the last solve issued on this rank */
 int lh_debug_comm_count(lh_handle *h, int64_t *n);
+/* the controller the uploaded window's trials run: 0 k_ctrl (LDS, <= 21 poses), 1 k_ctrl_g (dense
+   LDL^T in global memory), 2 k_ctrl_p (PCG on the block-sparse system), 3 k_ctrl_b (banded LDL^T) */
+int lh_debug_controller(lh_handle *h, int *which);
 
 #ifdef __cplusplus
 }

@@ -115,7 +115,8 @@ struct lh_ctrl {
     int32_t nonpd;             // rank-deficient H_ll landmarks at the initial linearisation
     int32_t pcg_iters;         // PCG iterations summed over the solve's trials
     int32_t evo;               // the next trial is in the final LM iteration: k_lin evaluates only
-    int32_t acc_last;          // the last decided trial was accepted (k_reduce's decision, read by k_ctrl)
+    int32_t acc_hist[2];       // trial seq's LM decision (accepted) at [seq & 1]: read by its controller, and by
+                               // the next trial's k_reduce when it commits the staged system (commit_in_reduce)
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
 };
 
@@ -131,66 +132,90 @@ struct lh_params {
     double pcg_tol;         // PCG stop: ||r|| <= pcg_tol ||b|| (reference 1e-6, problem.cpp:597)
     int32_t pcg_max_it;     // PCG cap (<= 0: 2 * rows, problem.cpp:422)
     int32_t precision;      // lh_precision: 0 fp64 throughout, 1 fp32 per-edge residual/Jacobians (k_lin<T, TRIAL, true>)
-    int32_t dec_in_reduce;  // 1: k_reduce's scalar block takes the LM decision (one rank, P <= LH_PMAX)
+    int32_t dec_in_reduce;  // 1: k_reduce's scalar block takes the LM decision (one rank; k_ctrl, k_ctrl_b)
+    int32_t commit_in_reduce;   // 1: k_reduce copies an accepted trial's staged blocks to the committed system
+                                //    before it overwrites them (k_ctrl_b: no one-CU copy of a large system)
     double K[4];
 };
 
-// ---- k_ctrl's work units -------------------------------------
+// ---- the controllers' work units ------------------------
 // The reduced system is factored in natural pose order, so its nonzeros stay within the envelope of
 // S (row r's first nonzero column: the first pose any chunk couples with r's pose).  Step t of the
 // blocked LDL^T eliminates block column 8t; a 16-row tile row I takes part iff its envelope reaches
 // that column: tile_fcb[I] (its first nonzero 8-column block) <= t.  Per step, the trailing tiles of
-// the active tile rows are dealt to waves 1..15 (wave 0 runs the diagonal tile and the next block's
-// factor): one tile per unit when they fit, else half tile rows.  Unit word (u16), units[w * 16 + t]:
-// bit 15 valid, bit 14 store L^T and the rhs row, bits 0-2 tile row, 3-5 first tile column, 6-9 end
-// tile column (exclusive).  Wave 0's word: bit 15 = its diagonal tile is active.
+// the active tile rows are dealt to the unit waves (wave 0 runs the diagonal tile and the next block's
+// factor): one tile per unit when they fit, else half tile rows.  Unit word (u16) of wave w at step t,
+// units[w * nstep_max + t]: bit 15 valid, bit 14 store L^T and the rhs row, bits 0-2 tile row, 3-5
+// first tile column, 6-9 end tile column (exclusive), all relative to g0 = (8t + 8) / 16, the tile
+// holding the next diagonal block.  Wave 0's word: bit 15 = its diagonal tile is active.
+// Returns the most units any step needed (more than the waves given: the table is incomplete).
 #define LH_UNIT_VALID 0x8000u
 #define LH_UNIT_STORE 0x4000u
 #define LH_NSTEP (LH_NPAD / 8)
 LH_HD static inline uint16_t lh_unit(int I, int jb0, int jb1, bool store) {
     return (uint16_t)(LH_UNIT_VALID | (store ? LH_UNIT_STORE : 0u) | (uint32_t)I | ((uint32_t)jb0 << 3) | ((uint32_t)jb1 << 6));
 }
-LH_HD static inline void lh_ctrl_units(int n, const int32_t* tile_fcb, uint16_t* units) {
+LH_HD static inline int lh_ctrl_units(int n, const int32_t* tile_fcb, const int* order, int nwaves, int nstep_max,
+                                      uint16_t* units) {
     const int NE = (n + 15) & ~15, nb = (n + 7) & ~7, gl = NE / 16 - 1;
-    // waves off wave 0's SIMD first (waves w, w+4, w+8, w+12 share one), heaviest unit first
-    const int order[15] = {1, 2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12};
-    for (int i = 0; i < 16 * LH_NSTEP; ++i) units[i] = 0;
-    for (int t = 0; t < LH_NSTEP; ++t) {
+    int worst = 0;
+    for (int i = 0; i < 16 * nstep_max; ++i) units[i] = 0;
+    for (int t = 0; t < nstep_max; ++t) {
         const int m0 = 8 * t + 8;
         if (m0 >= nb) break;
         const int g0 = m0 >> 4;
         const bool act0 = tile_fcb[g0] <= t;
         if (act0) units[t] = (uint16_t)LH_UNIT_VALID;
         uint16_t item[16];
-        int cost[16], ni = 0, tiles = 0;
-        int jmin[8] = {0};
-        for (int I = g0 + 1; I <= gl; ++I) {
+        int cost[16], ni = 0, tiles = 0, rows = 0;
+        int jmin[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int gend = (gl < g0 + 7) ? gl : g0 + 7;   // relative indices fit 3 bits
+        for (int I = g0 + 1; I <= gend; ++I) {
             if (tile_fcb[I] > t) continue;
             int j = g0;
             while (j < I && tile_fcb[j] > t) ++j;
-            jmin[I] = j;
+            jmin[I - g0] = j;
             tiles += I - j + 1;
+            ++rows;
         }
-        const bool per_tile = tiles + (act0 ? 1 : 0) <= 15;
-        if (act0) { item[ni] = lh_unit(g0, 0, 0, true); cost[ni++] = 6; }
-        for (int I = g0 + 1; I <= gl; ++I) {
+        for (int I = gend + 1; I <= gl; ++I)   // a band wider than 8 tile rows: not representable
+            if (tile_fcb[I] <= t) worst = 99;
+        const bool per_tile = tiles + (act0 ? 1 : 0) <= nwaves;
+        const int need = per_tile ? tiles + (act0 ? 1 : 0) : 2 * rows + (act0 ? 1 : 0);
+        worst = need > worst ? need : worst;
+        if (act0) { item[ni] = lh_unit(0, 0, 0, true); cost[ni++] = 6; }
+        for (int I = g0 + 1; I <= gend; ++I) {
             if (tile_fcb[I] > t) continue;
-            const int j0 = jmin[I], nt = I - j0 + 1;
+            const int j0 = jmin[I - g0], nt = I - j0 + 1, ir = I - g0, jr = j0 - g0;
             if (per_tile) {
-                for (int J = j0; J <= I; ++J) { item[ni] = lh_unit(I, J, J + 1, J == j0); cost[ni++] = (J == j0) ? 8 : 6; }
+                for (int J = 0; J < nt; ++J) { item[ni] = lh_unit(ir, jr + J, jr + J + 1, J == 0); cost[ni++] = J == 0 ? 8 : 6; }
             } else if (nt == 1) {
-                item[ni] = lh_unit(I, j0, I + 1, true); cost[ni++] = 8;
+                item[ni] = lh_unit(ir, jr, jr + 1, true); cost[ni++] = 8;
             } else {
-                const int split = j0 + ((nt + 1) >> 1);
-                item[ni] = lh_unit(I, j0, split, true); cost[ni++] = 6 + 2 * (split - j0);
-                item[ni] = lh_unit(I, split, I + 1, false); cost[ni++] = 4 + 2 * (I + 1 - split);
+                const int split = (nt + 1) >> 1;
+                item[ni] = lh_unit(ir, jr, jr + split, true); cost[ni++] = 6 + 2 * split;
+                item[ni] = lh_unit(ir, jr + split, jr + nt, false); cost[ni++] = 4 + 2 * (nt - split);
             }
+            if (ni > 14) break;
         }
         for (int a = 1; a < ni; ++a)   // stable insertion sort, cost descending
             for (int b = a; b > 0 && cost[b] > cost[b - 1]; --b) {
                 const int c = cost[b]; cost[b] = cost[b - 1]; cost[b - 1] = c;
                 const uint16_t u = item[b]; item[b] = item[b - 1]; item[b - 1] = u;
             }
-        for (int i = 0; i < ni && i < 15; ++i) units[order[i] * LH_NSTEP + t] = item[i];
+        for (int i = 0; i < ni && i < nwaves; ++i) units[order[i] * nstep_max + t] = item[i];
     }
+    return worst;
 }
+// k_ctrl: all 15 waves take units, wave 0's SIMD-mates (4, 8, 12) last
+#define LH_ORDER_CTRL {1, 2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12}
+// k_ctrl_b: waves 12-15 stream tile rows into the window instead
+#define LH_ORDER_BAND {1, 2, 3, 5, 6, 7, 9, 10, 11, 4, 8}
+
+// k_ctrl_b's per-window tables (bblk null: no banded controller for this window)
+struct lh_band_args {
+    const int32_t* bblk;     // [P * 64] block of pose pair (p, p + d), -1 if absent
+    const uint16_t* units;   // [16 waves][6 LH_PMAX_ANY / 8 steps] unit words
+    double* Lg;              // [ceil16(6P)][128] L rows
+    double* NDg;             // [steps][64] ND per block
+};

@@ -36,13 +36,13 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat,
                          int writer);
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
-                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* maxd,
+                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
                             lh_params prm, int n_chunks, int mode, int* host_done, int seq);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS,
-                          const int32_t* brow_ptr, const uint32_t* brow_ent, const uint16_t* units);
+                          const int32_t* brow_ptr, const uint32_t* brow_ent, const uint16_t* units, lh_band_args band);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
@@ -257,6 +257,8 @@ struct lh_handle {
     View<uint32_t> s_items, s_pair_ptr, s_rsmap, s_brow_ent;
     View<uint16_t> s_pair_pq;
     View<uint16_t> s_units;                                   // k_ctrl's work units (lh_ctrl_units)
+    View<uint16_t> s_bunits;                                  // k_ctrl_b's work units
+    View<int32_t> s_bblk;                                     // k_ctrl_b's pair -> block table
     View<int32_t> s_lm_perm, s_brow_ptr;
     View<uint64_t> s_fixed;
     View<double> s_qt, s_ptab, s_ext;
@@ -274,7 +276,10 @@ struct lh_handle {
     View<lh_chunk> d_chunks;                                  // the per-window tables: views into d_arena
     View<lh_subbatch> d_sbs;
     View<uint32_t> d_pair_ptr, d_items, d_rsmap;
-    View<uint16_t> d_pair_pq, d_units;
+    View<uint16_t> d_pair_pq, d_units, d_bunits;
+    View<int32_t> d_bblk;
+    DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64)
+    bool band = false;            // this window's LDL^T runs in k_ctrl_b
     View<int32_t> d_lm_perm;
     View<double> d_ptab_init, d_qt_init, d_ext;
     DevBuf<uint8_t> d_arena;
@@ -476,9 +481,39 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         h->staging_pending = true;
         return st;
     }
-    // past LH_PMAX poses the reduced system is solved in global memory: LDL^T by k_ctrl_g (dense, up
-    // to LH_PMAX_WIN poses) or PCG by k_ctrl_p (block-sparse, up to LH_PMAX_ANY)
-    if (pl.P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT) return LH_E_UNSUPPORTED;
+    // past LH_PMAX poses: LDL^T by k_ctrl_b when the reduced system is banded in natural pose order
+    // (any P up to LH_PMAX_ANY, one rank), else by k_ctrl_g (dense, up to LH_PMAX_WIN poses); PCG by
+    // k_ctrl_p (block-sparse, up to LH_PMAX_ANY)
+    static const int kBandSteps = 6 * LH_PMAX_ANY / 8;
+    std::vector<uint16_t> bunits;
+    h->band = false;
+    if (pl.P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && h->opt.world_size == 1 && !h->comm &&
+        !getenv("LH_NO_BAND")) {
+        const int n = 6 * pl.P, NE = (n + 15) & ~15, NT = NE / 16;
+        std::vector<int> pf(pl.P);
+        for (int p = 0; p < pl.P; ++p) pf[p] = p;
+        for (size_t c = 0; c < pl.chunk_mask.size(); ++c) {
+            const uint64_t m = pl.chunk_mask[c];
+            if (!m) continue;
+            const int lo = pl.chunk_base[c] + __builtin_ctzll(m);
+            for (uint64_t b = m; b; b &= b - 1) pf[pl.chunk_base[c] + __builtin_ctzll(b)] = std::min(pf[pl.chunk_base[c] + __builtin_ctzll(b)], lo);
+        }
+        std::vector<int32_t> fcb(NT);
+        bool ok = true;
+        for (int I = 0; I < NT; ++I) {
+            int f = 1 << 20;
+            for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
+            fcb[I] = f >> 3;
+            if (I >= 8 && fcb[I] < 2 * I - 13) ok = false;   // a tile row must enter the window before it is used
+        }
+        if (ok) {
+            bunits.resize(16 * (size_t)kBandSteps);
+            const int order[11] = LH_ORDER_BAND;
+            ok = lh_ctrl_units(n, fcb.data(), order, 11, kBandSteps, bunits.data()) <= 11;
+        }
+        h->band = ok;
+    }
+    if (pl.P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
     // a chunk window must fit one CU's LDS
     for (int T = 1; T <= LH_TMAX; ++T)
         if (pl.tgroup_begin[T + 1] > pl.tgroup_begin[T] && lh_lin_smem(T, pl.ncam) > (size_t)h->lds_limit)
@@ -506,6 +541,8 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         const size_t o_fix = part(pl.fixed_bits.size() * sizeof(uint64_t)), o_bptr = part(pl.brow_ptr.size() * sizeof(int32_t));
         const size_t o_bent = part(pl.brow_ent.size() * sizeof(uint32_t));
         const size_t o_units = part(16 * LH_NSTEP * sizeof(uint16_t));
+        const size_t o_bunits = part(h->band ? bunits.size() * sizeof(uint16_t) : 0);
+        const size_t o_bblk = part(h->band ? (size_t)P * 64 * sizeof(int32_t) : 0);
         HIPCHK(h->d_arena.ensure(bytes));
         HIPCHK(h->s_arena.ensure(bytes));
         h->arena_bytes = bytes;
@@ -530,6 +567,8 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         bind(h->d_brow_ptr, h->s_brow_ptr, db, sb, o_bptr, pl.brow_ptr.size());
         bind(h->d_brow_ent, h->s_brow_ent, db, sb, o_bent, pl.brow_ent.size());
         bind(h->d_units, h->s_units, db, sb, o_units, 16 * LH_NSTEP);
+        bind(h->d_bunits, h->s_bunits, db, sb, o_bunits, h->band ? bunits.size() : 0);
+        bind(h->d_bblk, h->s_bblk, db, sb, o_bblk, h->band ? (size_t)P * 64 : 0);
     }
     HIPCHK(h->d_meta.ensure(pl.n_slots));
     HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
@@ -544,7 +583,11 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
-    if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
+    if (h->band) {   // k_ctrl_b's L rows and ND blocks; L entries outside the envelope are never written: zero
+        const size_t NE = (size_t)((6 * P + 15) & ~15);
+        HIPCHK(h->d_band.ensure(NE * 128 + (size_t)(6 * LH_PMAX_ANY / 8) * 64));
+        HIPCHK(hipMemsetAsync(h->d_band.p, 0, NE * 128 * sizeof(double), h->stream));
+    } else if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
         const size_t ng = (size_t)((6 * P + 31) & ~31);
         const bool fresh = h->d_gA.n < ng * ng;
         HIPCHK(h->d_gA.ensure(ng * ng));
@@ -637,7 +680,18 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
                 fcb[I] = f >> 3;
             }
         }
-        lh_ctrl_units(6 * P, fcb, h->s_units.p);
+        const int order[15] = LH_ORDER_CTRL;
+        lh_ctrl_units(6 * P, fcb, order, 15, LH_NSTEP, h->s_units.p);
+    }
+
+    if (h->band) {
+        std::memcpy(h->s_bunits.p, bunits.data(), bunits.size() * sizeof(uint16_t));
+        int32_t* bb = h->s_bblk.p;
+        for (size_t i = 0; i < (size_t)P * 64; ++i) bb[i] = -1;
+        for (int b = 0; b < pl.npairs; ++b) {
+            const int p = pl.pair_list[2 * b], q = pl.pair_list[2 * b + 1];
+            if (q - p < 64) bb[p * 64 + (q - p)] = b;
+        }
     }
 
     // ---- params ----
@@ -664,7 +718,8 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.pcg_tol = h->opt.pcg_tol;
     prm.pcg_max_it = h->opt.pcg_max_iters;
     prm.no_evo = getenv("LH_NO_EVO") != nullptr;
-    prm.dec_in_reduce = (P <= LH_PMAX && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
+    prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
+    prm.commit_in_reduce = h->band ? 1 : 0;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     const double t1 = now_ms();
 
@@ -734,6 +789,12 @@ int host_exchange(lh_handle* h, int mode) {
     return LH_OK;
 }
 
+lh_band_args band_args(lh_handle* h) {
+    if (!h->band) return lh_band_args{nullptr, nullptr, nullptr, nullptr};
+    const size_t NE = (size_t)((6 * h->P + 15) & ~15);
+    return lh_band_args{h->d_bblk.p, h->d_bunits.p, h->d_band.p, h->d_band.p + NE * 128};
+}
+
 // One LM trial (mode 1) or the initial linearisation (mode 0).  *stopped is set (host transport
 // only) when the device had already stopped: no exchange and no k_ctrl were issued.
 int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
@@ -747,7 +808,8 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     {
         Prof pr(h, KC_REDUCE);
         HIPCHK(lh_launch_reduce(s, h->d_rows.p, h->d_csc.p, h->d_pair_ptr.p, h->d_pair_pq.p, h->d_ctrl.p,
-                                h->d_rs_stage.p, h->d_maxd.p, h->prm, h->plan.n_chunks, mode, h->d_done, h->cur_trial));
+                                h->d_rs_stage.p, h->d_rs_commit.p, h->d_maxd.p, h->prm, h->plan.n_chunks, mode, h->d_done,
+                                h->cur_trial));
         DBGSYNC("k_reduce");
     }
     if (h->comm) {
@@ -766,11 +828,11 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     }
     {
         Prof pr(h, KC_CTRL);
-        if (h->P > LH_PMAX && h->prm.solver == LH_SOLVER_LDLT)
+        if (h->P > LH_PMAX && h->prm.solver == LH_SOLVER_LDLT && !h->band)
             HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_pair_pq.p,
                               h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial, h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p,
-                              h->d_brow_ent.p, h->d_units.p));
+                              h->d_brow_ent.p, h->d_units.p, band_args(h)));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -1106,7 +1168,7 @@ void lh_destroy(lh_handle* h) {
     h->d_pair_ptr.release(); h->d_items.release(); h->d_pair_pq.release(); h->d_lm_in.release();
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
-    h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_gS.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release();
+    h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_gS.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release(); h->d_band.release();
     h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release(); h->d_fixed.release();
     h->d_brow_ptr.release(); h->d_brow_ent.release(); h->d_arena.release(); h->s_arena.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
@@ -1484,6 +1546,13 @@ int lh_debug_time_lin(lh_handle* h, int reps, double* ms) {
 int lh_debug_comm_count(lh_handle* h, int64_t* n) {
     if (!h || !n) return LH_E_BADARG;
     *n = h->n_coll;
+    return LH_OK;
+}
+
+int lh_debug_controller(lh_handle* h, int* which) {
+    if (!h || !which) return LH_E_BADARG;
+    if (!h->uploaded) return LH_E_STATE;
+    *which = h->P <= LH_PMAX ? 0 : h->band ? 3 : h->prm.solver == LH_SOLVER_PCG ? 2 : 1;
     return LH_OK;
 }
 

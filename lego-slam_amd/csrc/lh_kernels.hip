@@ -1290,6 +1290,7 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
         ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
         ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+        ctrl->acc_hist[seq & 1] = accept;
         // The next trial is in the final iteration when one more completed iteration reaches max_iters.
         // Its decision then either stops the loop (accept, or the last rejection) or leads to another
         // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).
@@ -1326,11 +1327,15 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
 // With prm.dec_in_reduce (one rank, P <= LH_PMAX) the scalar block also takes the trial's LM decision
 // (isGoodStepInLM on its chi2 and gain-scale sums, the controller update, the host words): k_ctrl
 // then reads accept / lambda with its prefetch instead of deciding on one thread behind it.
+// With prm.commit_in_reduce each pair block first copies its staged entries to the committed system
+// when the previous trial was accepted (before this trial overwrites them; an evaluate-only trial
+// copies and writes nothing): a controller that factors a large system then never copies it.
 __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, const double* __restrict__ csc,
                                                const uint32_t* __restrict__ pair_ptr, const uint16_t* __restrict__ pair_pq,
                                                lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
-                                               double* __restrict__ maxd_out, lh_params prm, int n_chunks, int mode,
-                                               volatile int* __restrict__ host_done, int seq) {
+                                               double* __restrict__ rs_commit, double* __restrict__ maxd_out,
+                                               lh_params prm, int n_chunks, int mode, volatile int* __restrict__ host_done,
+                                               int seq) {
     STAMP_DECL
     __shared__ double part[3][RW][64];
     const lh_rs_layout LY = lh_rs_make(prm.P, prm.npairs);
@@ -1341,6 +1346,16 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_lin wrote the chunk scalars only
+    if (prm.commit_in_reduce && mode != 0 && b < LY.npairs && done == 0 && wave == 0) {
+        if (__builtin_amdgcn_readfirstlane(ctrl->acc_hist[(seq - 1) & 1])) {
+            if (lane < 36) rs_commit[LY.off_S + b * 36 + lane] = rs[LY.off_S + b * 36 + lane];
+            if (p == q && lane >= 36 && lane < 54) {
+                const int k = lane - 36, part_off = (k < 6) ? LY.off_bs : (k < 12) ? LY.off_bp : LY.off_hd;
+                const int i = part_off + 6 * p + (k % 6);
+                rs_commit[i] = rs[i];
+            }
+        }
+    }
     // (p > q and ib > ie never hold: they make the exit test need the pair words, so the compiler issues
     // them with the controller's instead of sinking them below the branch, a second round trip)
     if ((done != 0) | ((evo != 0) & (b < LY.npairs)) | (p > q) | (ib > ie)) return;   // no short-circuit: one test
@@ -1369,7 +1384,6 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                 int d_o, a_o, c_o;
                 double l_o;
                 ctrl_lm_step(ctrl, cw, prm, 1, 0.0, 0.5 * a0, a1, a2, host_done, seq, d_o, a_o, c_o, l_o);
-                ctrl->acc_last = a_o;
             }
         }
         return;
@@ -1488,6 +1502,34 @@ __device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
     R[Q] = coef;
 }
 
+// Where the blocked LDL^T keeps its operands (the same code serves both controllers):
+//  LdsSys  (k_ctrl, n <= LH_NPAD): the whole system in LDS, row stride AS, the rhs as row NP, L^T in
+//          the upper triangle (L[r][c] at A[c][r]) for the back substitution;
+//  BandSys (k_ctrl_b, banded windows past LH_PMAX poses): a 128-row circular window of the lower band
+//          in LDS (row r at r mod 128, column c at c mod 128: no two live entries of a band narrower
+//          than the window share a slot), the rhs in its own LDS array, L rows to global memory
+//          (L[r][c] at Lg[r * LH_LBW + c - r + LH_LBW], c in [r - LH_LBW, r)).
+struct LdsSys {
+    double* A;
+    __device__ __forceinline__ double& at(int r, int c) const { return A[r * AS + c]; }
+    __device__ __forceinline__ double& rhs(int r) const { return A[NP * AS + r]; }
+    __device__ __forceinline__ void store_l(int r, int c, double v) const { A[c * AS + r] = v; }
+    __device__ __forceinline__ void store_nd(int, int, double2) const {}   // ND stays in LDS (LdltBlockLds)
+};
+#define LH_LBW 128   // k_ctrl_b: L entries kept per row (columns r - 128 .. r - 1)
+struct BandSys {
+    double* A;   // LDS, 128 rows of stride AS
+    double* y;   // LDS rhs
+    double* Lg;  // global, LH_LBW per row
+    __device__ __forceinline__ double& at(int r, int c) const { return A[(r & 127) * AS + (c & 127)]; }
+    __device__ __forceinline__ double& rhs(int r) const { return y[r]; }
+    double* NDg; // global, 64 per 8-column block: the back substitution's block solves
+    __device__ __forceinline__ void store_l(int r, int c, double v) const { Lg[(size_t)r * LH_LBW + (c - r + LH_LBW)] = v; }
+    __device__ __forceinline__ void store_nd(int k0, int i2, double2 v) const {
+        reinterpret_cast<double2*>(NDg + 8 * k0)[i2] = v;
+    }
+};
+
 // LDL^T of the 8x8 diagonal block at (k0, k0) of A by one wave, Eigen ldlt_inplace order (L = W
 // where pivot_is_valid fails).  In each 16-lane row (four identical replicas), lane r < 8 holds
 // row r of the block and lane 8 + r row r of the identity: the same column eliminations turn
@@ -1497,14 +1539,15 @@ __device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
 // For a row a below the block, l = a N is its forward substitution through the block and
 // l Delta its partially eliminated entries, so the trailing update of rows i, j is
 // L_i Delta L_j^T = T_i a_j^T with T_i = L_i ND^T.
-__device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __restrict__ No, double* __restrict__ NDo,
-                                              int k0, int lane) {
+template <class S>
+__device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ No, double* __restrict__ NDo, int k0,
+                                              int lane) {
     const int p = lane & 15, r = p & 7;
     const bool ident = p >= 8;
     double R[8], dl[8];
     double v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = A[(k0 + r) * AS + k0 + q];   // upper entries: garbage confined to this lane's upper part
+    for (int q = 0; q < 8; ++q) v[q] = A.at(k0 + r, k0 + q);   // upper entries: garbage confined to this lane's upper part
 #pragma unroll
     for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
     factor_column<0>(R, dl);
@@ -1518,7 +1561,7 @@ __device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __
     if (lane < 8) {
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-            if (q <= r) A[(k0 + q) * AS + k0 + r] = (q == r) ? dl[q] : R[q];
+            if (q <= r) A.at(k0 + q, k0 + r) = (q == r) ? dl[q] : R[q];
     } else if (lane < 16) {
         double2* n2 = reinterpret_cast<double2*>(No + 8 * r);
         double2* d2 = reinterpret_cast<double2*>(NDo + 8 * r);
@@ -1526,6 +1569,7 @@ __device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __
         for (int q = 0; q < 4; ++q) {
             n2[q] = double2{R[2 * q], R[2 * q + 1]};
             d2[q] = double2{R[2 * q] * dl[2 * q], R[2 * q + 1] * dl[2 * q + 1]};
+            A.store_nd(k0, 4 * r + q, d2[q]);
         }
     }
 }
@@ -1539,23 +1583,23 @@ __device__ __forceinline__ void factor_block8(double* __restrict__ A, double* __
 //   A_IJ -= T_I a_J^T  for the tile columns J in [jb0, jb1) except skip_cb (lower part, cols >= m0).
 // Every operand is the block column as it was before this step: no panel pass and no barrier
 // between the elimination of the column and the trailing update.
-__device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const double* __restrict__ N,
-                                              const double* __restrict__ ND, int k0, int rb, int jb0, int jb1,
-                                              int skip_cb, bool store_l, int lane) {
+template <class S>
+__device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restrict__ N, const double* __restrict__ ND,
+                                              int k0, int rb, int jb0, int jb1, int skip_cb, bool store_l, int lane) {
     const int li = lane & 15, lk = lane >> 4, m0 = k0 + 8;
     const bool lo = li < 8;
     // every LDS read of this tile row is issued up front (tiles are disjoint and this step's
     // writes never touch block column k0, so no read here can see a write of this step)
     const double na0 = lo ? N[lk * 8 + li] : 0.0, na1 = lo ? N[(lk + 4) * 8 + li] : 0.0;
     const double da0 = lo ? ND[li * 8 + lk] : 0.0, da1 = lo ? ND[li * 8 + 4 + lk] : 0.0;
-    const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
+    const double a0 = A.at(rb + li, k0 + lk), a1 = A.at(rb + li, k0 + 4 + lk);
     int cb = (jb0 == skip_cb) ? jb0 + 16 : jb0;
     double b0 = 0.0, b1 = 0.0, old[4] = {0.0, 0.0, 0.0, 0.0};
     if (cb < jb1) {
-        b0 = A[(cb + li) * AS + k0 + lk];
-        b1 = A[(cb + li) * AS + k0 + 4 + lk];
+        b0 = A.at(cb + li, k0 + lk);
+        b1 = A.at(cb + li, k0 + 4 + lk);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) old[q] = A[(rb + lk + 4 * q) * AS + cb + li];
+        for (int q = 0; q < 4; ++q) old[q] = A.at(rb + lk + 4 * q, cb + li);
     }
     v4d l = {0.0, 0.0, 0.0, 0.0};
     l = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, a0, l, 0, 0, 0);
@@ -1566,13 +1610,13 @@ __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const doub
     t = __builtin_amdgcn_mfma_f64_16x16x4f64(da1, l[1], t, 0, 0, 0);
     // t[q] = T[rb+li][lk+4q] (q = 0, 1)
     if (store_l) {
-        const double rb0 = (li == 0) ? A[NP * AS + k0 + lk] : 0.0, rb1 = (li == 0) ? A[NP * AS + k0 + 4 + lk] : 0.0;
+        const double rb0 = (li == 0) ? A.rhs(k0 + lk) : 0.0, rb1 = (li == 0) ? A.rhs(k0 + 4 + lk) : 0.0;
         double rold[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) rold[q] = A[NP * AS + rb + lk + 4 * q];
+        for (int q = 0; q < 4; ++q) rold[q] = A.rhs(rb + lk + 4 * q);
         if (rb + li >= m0) {
-            A[(k0 + lk) * AS + rb + li] = l[0];
-            A[(k0 + 4 + lk) * AS + rb + li] = l[1];
+            A.store_l(rb + li, k0 + lk, l[0]);
+            A.store_l(rb + li, k0 + 4 + lk, l[1]);
         }
         v4d u = {0.0, 0.0, 0.0, 0.0};
         u = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], rb0, u, 0, 0, 0);
@@ -1582,7 +1626,7 @@ __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const doub
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = rb + lk + 4 * q;
-                if (row >= m0) A[NP * AS + row] = rold[q] - u[q];
+                if (row >= m0) A.rhs(row) = rold[q] - u[q];
             }
         }
     }
@@ -1592,10 +1636,10 @@ __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const doub
         if (nc == skip_cb) nc += 16;
         double nb0 = 0.0, nb1 = 0.0, nold[4] = {0.0, 0.0, 0.0, 0.0};
         if (nc < jb1) {
-            nb0 = A[(nc + li) * AS + k0 + lk];
-            nb1 = A[(nc + li) * AS + k0 + 4 + lk];
+            nb0 = A.at(nc + li, k0 + lk);
+            nb1 = A.at(nc + li, k0 + 4 + lk);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) nold[q] = A[(rb + lk + 4 * q) * AS + nc + li];
+            for (int q = 0; q < 4; ++q) nold[q] = A.at(rb + lk + 4 * q, nc + li);
         }
         v4d acc = {0.0, 0.0, 0.0, 0.0};
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], b0, acc, 0, 0, 0);
@@ -1604,7 +1648,7 @@ __device__ __forceinline__ void ldlt_tile_row(double* __restrict__ A, const doub
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = rb + lk + 4 * q;
-            if (row >= m0 && col >= m0 && col <= row) A[row * AS + col] = old[q] - acc[q];
+            if (row >= m0 && col >= m0 && col <= row) A.at(row, col) = old[q] - acc[q];
         }
         cb = nc;
         b0 = nb0; b1 = nb1;
@@ -1690,7 +1734,8 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     __shared__ __attribute__((aligned(16))) LdltBlockLds F;
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    if (wv == 0) factor_block8(A, F.N[0], F.ND[0], 0, lane);
+    const LdsSys SY{A};
+    if (wv == 0) factor_block8(SY, F.N[0], F.ND[0], 0, lane);
     lds_barrier();
     CSTAMP(5);
 #ifdef LH_STAMPS
@@ -1725,15 +1770,15 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
             const uint32_t uw = __builtin_amdgcn_readfirstlane(units[wv * LH_NSTEP + t]);
             if (wv == 0) {
                 if (uw & LH_UNIT_VALID) {
-                    ldlt_tile_row(A, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
+                    ldlt_tile_row(SY, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
                     wave_sync();
                 }
                 LDLT_SSTAMP(0);
-                factor_block8(A, F.N[par ^ 1], F.ND[t + 1], m0, lane);
+                factor_block8(SY, F.N[par ^ 1], F.ND[t + 1], m0, lane);
                 LDLT_SSTAMP(1);
             } else if (uw & LH_UNIT_VALID) {
-                const int I = uw & 7, jb0 = (uw >> 3) & 7, jb1 = (uw >> 6) & 15;
-                ldlt_tile_row(A, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
+                const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
+                ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
             if (wv != 0) LDLT_SSTAMP(3);
         }
@@ -1984,7 +2029,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     double lambda = 0.0;
     if (decided) {
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
-        accept = __builtin_amdgcn_readfirstlane(ctrl->acc_last);
+        accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
     }
     // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
@@ -2513,6 +2558,260 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     lds_barrier();
     CSTAMP(8);
     ctrl_step_tail<GT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, nullptr);
+    CSTAMP(12);
+#ifdef LH_STAMPS
+    if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+}
+
+// ============================================================================
+// k_ctrl_b: the controller for windows past LH_PMAX poses whose reduced system is banded (the
+// reference's live solver, LDL^T, problem.cpp:420, at any window size).  In
+// natural pose order a sliding window's S is block-banded: a landmark couples the poses of its run
+// of keyframes, so row r's nonzeros start at its envelope fc(r) >= r - 104 (the host checks this per
+// window, lh_host.cpp; other windows go to k_ctrl_g or PCG).  The blocked LDL^T of k_ctrl then needs
+// only 8 tile rows (128 rows) of S at a time: the window holds them in one CU's LDS as a circular
+// buffer (BandSys), and waves 12-15 stream the next tile row in (its block-index loads two steps
+// ahead, its values one step ahead, written into the slots of the tile row that just retired).  L goes
+// to global memory row by row, ND per block; the back substitution (one wave) reads them back.  The
+// per-step work units come from the same envelope (lh_ctrl_units over 11 unit waves).  One 1024-thread
+// workgroup; the LM bookkeeping is k_reduce's (dec_in_reduce: one rank) or thread 0's (the initial
+// linearisation); k_reduce also commits accepted systems (commit_in_reduce), so nothing here copies S.
+// ============================================================================
+#define BNMAX (6 * LH_PMAX_ANY)         // largest reduced system (1536 rows)
+#define BSTEP_MAX (BNMAX / 8)           // LDL^T steps
+#define BLOAD 12                        // first loader wave
+
+// S(r, c), c <= r < n, of the packed system: block (pose(c), pose(r)) through the per-window table
+// bblk[p * 64 + d] (the block of pose pair (p, p + d), -1 where no chunk couples them)
+__device__ __forceinline__ int band_block(const int32_t* __restrict__ bblk, int r, int c, int n) {
+    const int pc = c / 6, pr = r / 6, d = pr - pc;
+    return (c <= r && r < n && d < 64) ? bblk[pc * 64 + d] : -1;
+}
+__device__ __forceinline__ double band_value(const double* __restrict__ src, int blk, int r, int c, double lambda,
+                                             int strategy, int n) {
+    double v = (blk >= 0) ? src[(size_t)blk * 36 + (c % 6) * 6 + (r % 6)] : 0.0;
+    if (r == c) {
+        if (r >= n) v = 1.0;   // identity padding
+        else v = (strategy == 0) ? v + lambda : v + lambda * v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const double* __restrict__ rs_commit,
+                                               const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
+                                               const int32_t* __restrict__ bblk, const uint16_t* __restrict__ bunits,
+                                               double* __restrict__ Lg, double* __restrict__ NDg, double* __restrict__ dxp,
+                                               lh_params prm, int mode, volatile int* __restrict__ host_done, int seq) {
+    __shared__ double A[128 * AS];                          // the circular window of the lower band
+    __shared__ __attribute__((aligned(16))) double y[BNMAX];   // rhs (forward substitution), then x
+    __shared__ double z[BNMAX];                             // D^-1 L^-1 b
+    __shared__ __attribute__((aligned(16))) double Nl[2][64], NDl[2][64];
+    __shared__ int s_flags[4];
+    __shared__ double s_red[CT / 64], s_lam;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15, nb = (n + 7) & ~7, NT = NE / 16, nstep = nb / 8;
+    const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
+    const bool decided = mode != 0 && prm.dec_in_reduce;
+#ifdef LH_STAMPS
+    const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    // ---------------- the decision ----------------
+    int done = 0, accept = 0;
+    double lambda = 0.0;
+    if (decided) {
+        done = __builtin_amdgcn_readfirstlane(ctrl->done);
+        accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
+        lambda = ctrl->lambda;
+    } else {
+        double tchi = 0.0, sl = 0.0, ndg = 0.0;
+        CtrlWords cw{};
+        if (tid == 0) {
+            cw = ctrl_load(ctrl);
+            tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
+            sl = rs_stage[LY.off_sc + LH_SC_SCALE];
+            ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
+        }
+        double mx = 0.0;
+        if (mode == 0)
+            for (int i = tid; i < n; i += CT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
+        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+        if (lane == 0) s_red[wave] = mx;
+        lds_barrier();
+        if (tid == 0) {
+            double mdiag = 0.0;
+            if (mode == 0) {
+                for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
+                mdiag = fmax(*maxd_in, mdiag);
+            }
+            int d_o, a_o, c_o;
+            double lam_n;
+            ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            s_flags[0] = d_o;
+            s_flags[1] = a_o;
+            s_lam = lam_n;
+        }
+        lds_barrier();
+        done = s_flags[0];
+        accept = s_flags[1];
+        lambda = s_lam;
+    }
+    if (done) return;
+#ifdef LH_STAMPS
+    if (tid == 0) {
+        atomicAdd(&lh_stamps[32], ct_start);
+        atomicAdd(&lh_stamps[61], 1ull);
+        atomicAdd(&lh_stamps[62], rt_start);
+    }
+#endif
+    CSTAMP(1);
+    const double* __restrict__ src = accept ? rs_stage : rs_commit;
+
+    // ---------------- the rhs, the first 8 tile rows, this wave's unit words ----------------
+    for (int i = tid; i < NE; i += CT) y[i] = (i < n) ? src[LY.off_bs + i] : 0.0;
+    {
+        constexpr int PER = 128 * 128 / CT;   // 16 elements of the first window per thread
+        const int r0 = tid >> 3, cseg = (tid & 7) * 16;
+        int bk[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) bk[k] = band_block(bblk, r0, cseg + k, n);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = cseg + k;
+            A[r0 * AS + c] = (r0 < NE && c <= r0) ? band_value(src, bk[k], r0, c, lambda, prm.strategy, n) : 0.0;
+        }
+    }
+    uint32_t uwa = 0, uwb = 0;   // this wave's unit words: steps 2j, 2j + 1 in u32 j (lane j, lane j + 64)
+    {
+        const uint32_t* uw32 = reinterpret_cast<const uint32_t*>(bunits + (size_t)wv * BSTEP_MAX);
+        uwa = uw32[lane];
+        if (lane + 64 < BSTEP_MAX / 2) uwb = uw32[lane + 64];
+    }
+    auto unit_word = [&](int t) -> uint32_t {
+        const int j = t >> 1;
+        const uint32_t w = (j < 64) ? __builtin_amdgcn_readlane(uwa, j & 63) : __builtin_amdgcn_readlane(uwb, j & 63);
+        return (t & 1) ? (w >> 16) : (w & 0xffffu);
+    };
+    // loader state (waves 12-15): lane q of 256 owns row 16 I + (q >> 4), columns 16 (I - 7) + 8 (q & 15) + k
+    const int lq = tid - 64 * BLOAD, lrow = lq >> 4, lcol = (lq & 15) * 8;
+    int lbk[8];
+    double lval[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { lbk[k] = -1; lval[k] = 0.0; }
+    lds_barrier();
+    CSTAMP(4);
+
+    const BandSys SY{A, y, Lg, NDg};
+    if (wv == 0) factor_block8(SY, Nl[0], NDl[0], 0, lane);
+    lds_barrier();
+    CSTAMP(5);
+    for (int t = 0; t < nstep; ++t) {
+        const int k0 = 8 * t, par = t & 1, m0 = k0 + 8;
+        const double* N = Nl[par];
+        const double* ND = NDl[par];
+        if (wv == BLOAD && lane < 8) {   // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
+            double zz = 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) zz += y[k0 + q] * N[q * 8 + lane];
+            const double d = SY.at(k0 + lane, k0 + lane);
+            z[k0 + lane] = fabs(d) > 2.2250738585072014e-308 ? zz : 0.0;
+        }
+        if (m0 < nb) {
+            const int g0 = m0 >> 4;
+            const uint32_t uw = unit_word(t);
+            if (wv == 0) {
+                if (uw & LH_UNIT_VALID) {
+                    ldlt_tile_row(SY, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
+                    wave_sync();
+                }
+                factor_block8(SY, Nl[par ^ 1], NDl[par ^ 1], m0, lane);
+            } else if (wv < BLOAD && (uw & LH_UNIT_VALID)) {
+                const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
+                ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
+            }
+        }
+        if (wv >= BLOAD) {
+            // tile row I enters the window at step 2 I - 14, into the slots of tile row I - 8 (retired
+            // after step 2 I - 15); its block indices are loaded at step 2 I - 16, its values at 2 I - 15
+            if ((t & 1) == 0) {
+                const int Iw = t / 2 + 7;
+                if (Iw >= 8 && Iw < NT) {
+                    const int r = 16 * Iw + lrow;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int c = 16 * (Iw - 7) + lcol + k;
+                        SY.at(r, c) = (c <= r) ? lval[k] : 0.0;
+                    }
+                }
+                const int Ia = t / 2 + 8;
+                if (Ia < NT) {
+                    const int r = 16 * Ia + lrow;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) lbk[k] = band_block(bblk, r, 16 * (Ia - 7) + lcol + k, n);
+                }
+            } else {
+                const int Ib = (t - 1) / 2 + 8;
+                if (Ib < NT) {
+                    const int r = 16 * Ib + lrow;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int c = 16 * (Ib - 7) + lcol + k;
+                        lval[k] = (c <= r && r < NE) ? band_value(src, lbk[k], r, c, lambda, prm.strategy, n) : 0.0;
+                    }
+                }
+            }
+        }
+        lds_barrier();
+    }
+    __syncthreads();   // L and ND rows in global memory, z in LDS
+    CSTAMP(6);
+
+    // ---------------- back substitution x = L^-T z, blocks descending, one wave ----------------
+    // For block KB: x_b = ND_b y_b (lanes 0..7), then every row r in [KB - 128, KB) takes
+    // y_r -= sum_v L[KB+v][r] x_b[v] (lane l: rows KB - 128 + l and KB - 64 + l); the next block's
+    // L rows and ND are loaded while this one computes.
+    if (wv == 0) {
+        for (int i = lane; i < NE; i += 64) y[i] = z[i];
+        double la[8], lb[8], nd[8];
+        auto load_blk = [&](int KB, double (&l1)[8], double (&l2)[8], double (&ndv)[8]) {
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const double* Lr = Lg + (size_t)(KB + v) * LH_LBW;
+                l1[v] = (lane >= v) ? Lr[lane - v] : 0.0;          // row KB - 128 + lane
+                l2[v] = Lr[64 + lane - v];                          // row KB - 64 + lane
+                ndv[v] = NDg[8 * KB + (lane & 7) * 8 + v];
+            }
+        };
+        load_blk(nb - 8, la, lb, nd);
+        for (int KB = nb - 8; KB >= 0; KB -= 8) {
+            double ca[8], cb[8], cn[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) { ca[v] = la[v]; cb[v] = lb[v]; cn[v] = nd[v]; }
+            if (KB >= 8) load_blk(KB - 8, la, lb, nd);
+            double yb[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) yb[w] = y[KB + w];
+            const double xv = ((cn[0] * yb[0] + cn[1] * yb[1]) + (cn[2] * yb[2] + cn[3] * yb[3])) +
+                              ((cn[4] * yb[4] + cn[5] * yb[5]) + (cn[6] * yb[6] + cn[7] * yb[7]));
+            double xb[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, v);
+            const int ra = KB - 128 + lane, rb = KB - 64 + lane;
+            const double sa = ((ca[0] * xb[0] + ca[1] * xb[1]) + (ca[2] * xb[2] + ca[3] * xb[3])) +
+                              ((ca[4] * xb[4] + ca[5] * xb[5]) + (ca[6] * xb[6] + ca[7] * xb[7]));
+            const double sb = ((cb[0] * xb[0] + cb[1] * xb[1]) + (cb[2] * xb[2] + cb[3] * xb[3])) +
+                              ((cb[4] * xb[4] + cb[5] * xb[5]) + (cb[6] * xb[6] + cb[7] * xb[7]));
+            if (ra >= 0) y[ra] -= sa;
+            if (rb >= 0) y[rb] -= sb;
+            if (lane < 8) y[KB + lane] = xv;
+            wave_sync();
+        }
+    }
+    __syncthreads();
+    CSTAMP(8);
+    ctrl_step_tail<CT>(ctrl, prm, n, lambda, y, src + LY.off_bp, src + LY.off_hd, s_red, dxp);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -3334,11 +3633,11 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 }
 
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
-                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* maxd,
+                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
                             lh_params prm, int n_chunks, int mode, int* host_done, int seq) {
     const int npairs = prm.npairs;
     hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, rows, csc, pair_ptr, pair_pq, ctrl,
-                       rs_stage, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq);
+                       rs_stage, rs_commit, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq);
     return hipGetLastError();
 }
 
@@ -3353,8 +3652,11 @@ hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
-                          const uint32_t* brow_ent, const uint16_t* units) {
-    if (prm.P > LH_PMAX && prm.solver == 1)
+                          const uint32_t* brow_ent, const uint16_t* units, lh_band_args band) {
+    if (prm.P > LH_PMAX && prm.solver == 0 && band.bblk)
+        hipLaunchKernelGGL(k_ctrl_b, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk, band.units,
+                           band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq);
+    else if (prm.P > LH_PMAX && prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
     else if (prm.P > LH_PMAX)
@@ -3454,7 +3756,8 @@ __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S,
     const int tid = threadIdx.x, NE = (n + 15) & ~15;
     if (tid == 0) {
         int32_t fcb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        lh_ctrl_units(n, fcb, s_units);
+        const int order[15] = LH_ORDER_CTRL;
+        lh_ctrl_units(n, fcb, order, 15, LH_NSTEP, s_units);
     }
     for (int e = tid; e < NE * NE; e += CT) {
         const int r = e / NE, c = e - NE * (e / NE);

@@ -204,7 +204,7 @@ ABI_SYMBOLS = [
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
     "lh_estimate_pose", "lh_lk_track",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
-    "lh_debug_time_lin", "lh_debug_comm_count",
+    "lh_debug_time_lin", "lh_debug_comm_count", "lh_debug_controller",
 ]
 
 _balib = None
@@ -238,6 +238,7 @@ def ba_lib():
         lib.lh_debug_event_floor.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         lib.lh_debug_time_lin.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
         lib.lh_debug_comm_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+        lib.lh_debug_controller.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         _balib = lib
     return _balib
 
@@ -451,6 +452,13 @@ class Solver:
         ms = C.c_double(0.0)
         _check(ba_lib().lh_debug_time_lin(self.h, reps, C.byref(ms)), "lh_debug_time_lin")
         return ms.value
+
+    def controller(self):
+        """The controller the uploaded window runs (lh_debug_controller): 'k_ctrl', 'k_ctrl_g', 'k_ctrl_p'
+        or 'k_ctrl_b'."""
+        v = C.c_int(0)
+        _check(ba_lib().lh_debug_controller(self.h, C.byref(v)), "lh_debug_controller")
+        return ("k_ctrl", "k_ctrl_g", "k_ctrl_p", "k_ctrl_b")[v.value]
 
     def comm_count(self):
         """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""

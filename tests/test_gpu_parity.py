@@ -341,14 +341,17 @@ def _stable_window(P, L, seed, **kw):
 
 @pytest.mark.parametrize("P,L,seed,mode", [(22, 3000, 4, 0), (32, 4000, 1, 0), (40, 3000, 3, 1), (64, 6000, 2, 0)])
 def test_large_windows_global_memory_solve(P, L, seed, mode):
-    """Windows past 21 keyframes (the reference solver takes any number, problem.cpp:277-279):
-    the reduced system (6P up to 384 rows) is solved in global memory by k_ctrl_g.  One trial at
-    the single-trial bar, then the full solve at the north-star bar (chi2 1e-6, poses and
-    landmarks 1e-6) against the oracle on reproducible windows.  mode 1: landmarks seen by random
-    keyframe subsets (chunk windows of several tile counts, a dense reduced system)."""
+    """Windows past 21 keyframes (the reference solver takes any number, problem.cpp:277-279).
+    Sliding-window structure (mode 0: landmarks seen by runs of 8 consecutive keyframes) gives a
+    banded reduced system, factored by k_ctrl_b; mode 1 (landmarks seen by random keyframe subsets:
+    chunk windows of several tile counts, a dense reduced system) by k_ctrl_g in global memory.  One
+    trial at the single-trial bar, then the full solve at the north-star bar (chi2 1e-6, poses and
+    landmarks 1e-6) against the oracle on reproducible windows."""
     kw = dict(pose_mode=1, k_min=2, k_max=8) if mode else {}
     w = _stable_window(P, L, seed, **kw)
-    g = lego_ba.Solver(max_iters=1, max_trials=1).solve(w)
+    s1 = lego_ba.Solver(max_iters=1, max_trials=1)
+    g = s1.solve(w)
+    assert s1.controller() == ("k_ctrl_g" if mode else "k_ctrl_b")
     o = ob.solve(w, max_iters=1, max_trials=1)
     assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-12
     assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
@@ -358,6 +361,30 @@ def test_large_windows_global_memory_solve(P, L, seed, mode):
     of, spread, its = oracle_envelope(w, threads=(1, 2, 8))
     assert gf["iterations"] in its
     assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+    assert np.allclose(gf["pose_Tcw"], of["pose_Tcw"], atol=1e-6)
+    assert np.allclose(gf["lm_xyz"], of["lm_xyz"], atol=1e-6)
+
+
+@pytest.mark.parametrize("P,L,seed", [(96, 6000, 1), (128, 8000, 1), (128, 8000, 3), (256, 12000, 1)])
+def test_banded_ldlt_past_64_keyframes(P, L, seed):
+    """The reference's live solver (LDL^T, problem.cpp:420) on windows of 96 to 256 keyframes: the banded
+    controller (k_ctrl_b) streams the band of S through one CU's LDS.  One trial at the single-trial
+    bar, the full solve at the north-star bar against the oracle's LDLT (windows the oracle reproduces
+    across thread counts)."""
+    w = _stable_window(P, L, seed)
+    s1 = lego_ba.Solver(max_iters=1, max_trials=1)
+    g = s1.solve(w)
+    assert s1.controller() == "k_ctrl_b"
+    o = ob.solve(w, max_iters=1, max_trials=1)
+    assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-12
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-7)
+    gf = lego_ba.Solver().solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 8))
+    assert spread < 1e-12
+    assert gf["iterations"] == of["iterations"] and gf["trials"] == of["trials"]
+    assert rel(gf["chi2_final"], of["chi2_final"]) < 1e-6
     assert np.allclose(gf["pose_Tcw"], of["pose_Tcw"], atol=1e-6)
     assert np.allclose(gf["lm_xyz"], of["lm_xyz"], atol=1e-6)
 
@@ -386,10 +413,21 @@ def test_large_window_default_family_gate1():
 
 
 def test_window_envelope_edges():
-    """Past 64 keyframes the dense LDLT (k_ctrl_g) is not offered (PCG is, tests/test_pcg.py); past 256
-    keyframes nothing is."""
+    """Past 64 keyframes LDLT runs when the reduced system is banded (k_ctrl_b); a window whose S is not
+    (landmarks coupling keyframes 40 apart) is refused there (the dense k_ctrl_g stops at 64; PCG takes
+    it, tests/test_pcg.py); past 256 keyframes nothing is."""
+    w = lego_ba.generate_window(P=65, L=500, k=8, seed=4)
+    s = lego_ba.Solver(max_iters=1)
+    s.solve(w)
+    assert s.controller() == "k_ctrl_b"
+    L = len(w["lm_xyz"])
+    wide = dict(w, lm_xyz=np.vstack([w["lm_xyz"], w["lm_xyz"][:20]]))
+    wide["obs_pose"] = np.concatenate([w["obs_pose"], np.tile([0, 40], 20)]).astype(w["obs_pose"].dtype)
+    wide["obs_lm"] = np.concatenate([w["obs_lm"], np.repeat(np.arange(L, L + 20), 2)]).astype(w["obs_lm"].dtype)
+    wide["obs_cam"] = np.concatenate([w["obs_cam"], np.zeros(40, w["obs_cam"].dtype)])
+    wide["obs_uv"] = np.vstack([w["obs_uv"], w["obs_uv"][:40]])
     with pytest.raises(lego_ba.LhError) as e:
-        lego_ba.Solver().solve(lego_ba.generate_window(P=65, L=500, k=8, seed=4))
+        lego_ba.Solver().solve(wide)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
     w = lego_ba.generate_window(P=256, L=500, k=8, seed=4)
     w["pose_Tcw"] = np.vstack([w["pose_Tcw"], w["pose_Tcw"][-1:]])

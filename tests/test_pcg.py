@@ -146,7 +146,7 @@ def _many_pose_window(P, L, seed, **kw):
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("P,L,seed,kw", [(22, 2000, 1, {}), (40, 3000, 2, {}), (64, 4000, 2, {}), (96, 5000, 3, {}),
-                                         (128, 6000, 3, {}), (128, 6000, 1, {})])
+                                         (128, 6000, 3, {}), (128, 6000, 1, {}), (256, 12000, 1, {})])
 def test_gpu_pcg_many_keyframes(P, L, seed, kw):
     """Windows past 21 keyframes through PCG, past 64 with the block-sparse
     reduced system (k_ctrl_p: S p over the packed pose-pair blocks, never densified): one trial at the
@@ -178,10 +178,12 @@ def test_gpu_pcg_many_keyframes(P, L, seed, kw):
 
 @pytest.mark.gpu
 def test_many_keyframes_envelope():
-    """Past 64 keyframes the LDLT (dense, k_ctrl_g) is not offered; PCG takes up to 256."""
+    """Past 64 keyframes a banded window runs LDLT (k_ctrl_b) as well as PCG (k_ctrl_p, up to 256)."""
     w = _many_pose_window(80, 2000, 5)
-    with pytest.raises(lego_ba.LhError) as e:
-        lego_ba.Solver().solve(w)
-    assert e.value.status == lego_ba.LH_E_UNSUPPORTED
-    g = lego_ba.Solver(linear_solver=lego_ba.LH_SOLVER_PCG, max_iters=2).solve(w)
-    assert g["chi2_final"] < g["chi2_initial"]
+    s = lego_ba.Solver(max_iters=2)
+    a = s.solve(w)
+    assert s.controller() == "k_ctrl_b" and a["chi2_final"] < a["chi2_initial"]
+    sp = lego_ba.Solver(linear_solver=lego_ba.LH_SOLVER_PCG, max_iters=2)
+    g = sp.solve(w)
+    assert sp.controller() == "k_ctrl_p" and g["chi2_final"] < g["chi2_initial"]
+    assert abs(g["chi2_final"] - a["chi2_final"]) / a["chi2_final"] < 1e-6
