@@ -2670,7 +2670,10 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     const double* __restrict__ src = accept ? rs_stage : rs_commit;
 
     // ---------------- the rhs, the first 8 tile rows, this wave's unit words ----------------
-    for (int i = tid; i < NE; i += CT) y[i] = (i < n) ? src[LY.off_bs + i] : 0.0;
+    for (int i = tid; i < NE; i += CT) {
+        y[i] = (i < n) ? src[LY.off_bs + i] : 0.0;
+        z[i] = 0.0;
+    }
     {
         constexpr int PER = 128 * 128 / CT;   // 16 elements of the first window per thread
         const int r0 = tid >> 3, cseg = (tid & 7) * 16;

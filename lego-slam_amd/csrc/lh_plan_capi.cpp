@@ -103,6 +103,18 @@ int lhp_plan_time(const lh_window* w, int chunk_lm, int threads, int reps, doubl
 extern "C" {
 // Pool stress for the CPU suite: `runs` back-to-back small jobs on one persistent pool (late-waking
 // workers must never touch a retired job).  Returns the sum of all indices visited.
+// the controllers' per-step work units (lh_common.h lh_ctrl_units) for an n-row system whose tile row I
+// first reaches 8-column block fcb[I]: band 0 -> k_ctrl's table (15 unit waves, LH_NSTEP steps), band 1
+// -> k_ctrl_b's (11 unit waves, 6 LH_PMAX_ANY / 8 steps).  Returns the most units a step needed.
+int lhp_ctrl_units(int n, const int32_t* fcb, int band, uint16_t* units) {
+    if (band) {
+        const int order[11] = LH_ORDER_BAND;
+        return lh_ctrl_units(n, fcb, order, 11, 6 * LH_PMAX_ANY / 8, units);
+    }
+    const int order[15] = LH_ORDER_CTRL;
+    return lh_ctrl_units(n, fcb, order, 15, LH_NSTEP, units);
+}
+
 int64_t lhp_pool_stress(int threads, int runs, int n) {
     lh::Pool pool(threads > 0 ? threads : 1);
     std::atomic<int64_t> s{0};

@@ -519,6 +519,7 @@ def _pl():
         if hasattr(lib, "lhp_plan_stages"):   # diagnostic entry point
             lib.lhp_plan_stages.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, vp]
         lib.lhp_pool_stress.argtypes = [C.c_int, C.c_int, C.c_int]
+        lib.lhp_ctrl_units.argtypes = [C.c_int, vp, C.c_int, vp]
         lib.lhp_pool_stress.restype = C.c_int64
         _planlib = lib
     return _planlib
@@ -543,6 +544,16 @@ def plan_window(w, chunk_lm=0, threads=1, rank_invariant=False):
            "lhp_plan_fill")
     out.update(tgroup_begin=tg, fixed_mask=fixed_mask)
     return out
+
+
+def ctrl_units(n, fcb, band=False):
+    """The controllers' per-step work-unit table (lh_ctrl_units) for an n-row reduced system whose tile row
+    I first reaches 8-column block fcb[I]: (units[16 waves][steps] as uint16, most units a step needed)."""
+    steps = 6 * 256 // 8 if band else 16
+    f = np.ascontiguousarray(fcb, np.int32)
+    u = np.zeros(16 * steps, np.uint16)
+    worst = _pl().lhp_ctrl_units(int(n), _ptr(f), int(bool(band)), _ptr(u))
+    return u.reshape(16, steps), worst
 
 
 def pool_stress(threads, runs, n):
