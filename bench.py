@@ -487,7 +487,7 @@ def main():
                          "chi2_rel_vs_fp64": abs(rf["chi2_final"] - last["chi2_final"]) / last["chi2_final"]}
     sf.close()
     # a 64-keyframe window of C3's size (windows past 21 keyframes, the reduced
-    # system of 384 rows solved in global memory by k_ctrl_g), against the oracle's final chi2
+    # system of 384 rows: banded, k_ctrl_b), against the oracle's final chi2
     from windows import STABLE
     w64 = lego_ba.generate_window(P=64, L=50000, k=8, seed=args.seed, **dict(STABLE, outlier_frac=0.0))
     f64 = np.zeros(64, np.uint8)
@@ -495,6 +495,7 @@ def main():
     w64["pose_fixed"] = f64
     s64 = lego_ba.Solver(device=local)
     s64.upload(w64)
+    ctl64 = s64.controller()
     s64.solve_resident()
     d64, i64, t64, l64 = time_solves(s64, 5, barrier)
     s64.set_profiling(True)
@@ -503,11 +504,43 @@ def main():
     k64 = s64.kernel_stats()
     s64.set_profiling(False)
     s64.close()
-    out["p64_window"] = {"keyframes": 64, "landmarks": 50000, "obs": len(w64["obs_pose"]),
+    out["p64_window"] = {"keyframes": 64, "landmarks": 50000, "obs": len(w64["obs_pose"]), "controller": ctl64,
                          "iterations_per_s": round(i64 / d64, 3), "ms_per_solve": round(d64 / 5 * 1e3, 3),
                          "iterations_per_solve": i64 / 5, "trials_per_solve": t64 / 5,
-                         "k_ctrl_g_ms_per_trial": round(k64["k_ctrl"][1] / max(1, k64["k_ctrl"][0]), 4),
+                         "controller_ms_per_trial": round(k64["k_ctrl"][1] / max(1, k64["k_ctrl"][0]), 4),
                          "kernels_ms_per_solve_event_bracketed": {k: round(v[1] / 2, 4) for k, v in k64.items()}}
+    # the same 64 keyframes through the dense global-memory LDL^T (k_ctrl_g, LH_NO_BAND), the round-3 path
+    os.environ["LH_NO_BAND"] = "1"
+    sg = lego_ba.Solver(device=local)
+    sg.upload(w64)
+    os.environ.pop("LH_NO_BAND")
+    sg.solve_resident()
+    sg.set_profiling(True)
+    sg.kernel_stats_reset()
+    time_solves(sg, 2, barrier)
+    kg = sg.kernel_stats()
+    out["p64_window"]["dense_k_ctrl_g_ms_per_trial"] = round(kg["k_ctrl"][1] / max(1, kg["k_ctrl"][0]), 4)
+    sg.close()
+    # windows of 128 and 256 keyframes through the reference's LDL^T (banded, k_ctrl_b)
+    for P_ in (128, 256):
+        wb = lego_ba.generate_window(P=P_, L=50000, k=8, seed=3, **dict(STABLE, outlier_frac=0.0))
+        fb_ = np.zeros(P_, np.uint8)
+        fb_[0] = 1
+        wb["pose_fixed"] = fb_
+        sb = lego_ba.Solver(device=local)
+        sb.upload(wb)
+        sb.solve_resident()
+        db, ib, tb, _ = time_solves(sb, 3, barrier)
+        sb.set_profiling(True)
+        sb.kernel_stats_reset()
+        time_solves(sb, 1, barrier)
+        kb = sb.kernel_stats()
+        out[f"p{P_}_window_ldlt"] = {"keyframes": P_, "landmarks": 50000, "obs": len(wb["obs_pose"]),
+                                     "controller": sb.controller(), "iterations_per_s": round(ib / db, 3),
+                                     "ms_per_solve": round(db / 3 * 1e3, 3), "trials_per_solve": tb / 3,
+                                     "controller_ms_per_trial": round(kb["k_ctrl"][1] / max(1, kb["k_ctrl"][0]), 4)}
+        sb.set_profiling(False)
+        sb.close()
     # a 128-keyframe window of C3's size through the PCG reduced solve (k_ctrl_p,
     # S p over the block-sparse pose-pair blocks), against the oracle's PCG below
     w128 = lego_ba.generate_window(P=128, L=50000, k=8, seed=3, **dict(STABLE, outlier_frac=0.0))

@@ -443,6 +443,7 @@ hipError_t spin_wait(hipEvent_t ev) {
 // sync: return only once the copies are done (lh_upload); lh_solve leaves them queued ahead of its
 // kernels on the same stream.  Either way the next upload waits for them before it rewrites the staging.
 int upload_body(lh_handle* h, const lh_window* w, bool sync);
+int rank_max(lh_handle* h, double* buf, int n);
 
 // Every exit after the first copy out of the pinned staging is queued must leave ev_staging recorded
 // behind it, or the next upload could rewrite (or reallocate) the staging while that DMA still reads
@@ -656,12 +657,11 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
 
     // ---- k_ctrl's work units: the envelope of S in natural pose order.  Pose p's first coupled pose is
     //      the lowest pose of any chunk window holding p (a chunk writes a block for every pair of its
-    //      window).  A sharded solve factors the sum of every rank's blocks, whose union this rank
-    //      cannot see: it takes the dense envelope. ----
+    //      window); a sharded solve takes the minimum over the ranks (one MAX all-reduce at upload). ----
     if (P <= LH_PMAX) {
         int32_t fcb[8];
         for (int I = 0; I < 8; ++I) fcb[I] = 0;
-        if (h->opt.world_size == 1) {
+        {
             std::vector<int> pf(P);
             for (int p = 0; p < P; ++p) pf[p] = p;
             for (size_t c = 0; c < pl.chunk_mask.size(); ++c) {
@@ -672,6 +672,13 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
                     const int p = pl.chunk_base[c] + __builtin_ctzll(b);
                     pf[p] = std::min(pf[p], lo);
                 }
+            }
+            if (h->host_comm || h->comm) {   // a sharded solve factors the sum of every rank's blocks: the union
+                std::vector<double> neg(P);
+                for (int p = 0; p < P; ++p) neg[p] = -(double)pf[p];
+                const int st_r = rank_max(h, neg.data(), P);
+                if (st_r != LH_OK) return st_r;
+                for (int p = 0; p < P; ++p) pf[p] = (int)(-neg[p]);
             }
             const int n = 6 * P, NE = (n + 15) & ~15;
             for (int I = 0; I < NE / 16; ++I) {
@@ -985,6 +992,27 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
 // differ would issue different collective counts and hang, so lh_create compares them once: each
 // rank contributes (v, -v) per option to a MAX all-reduce, and any rank whose v differs from the
 // maximum or minimum sees a mismatch (every rank returns LH_E_BADARG).
+// MAX over the ranks of buf[0..n), in place (host transport or RCCL); a no-op on one rank
+int rank_max(lh_handle* h, double* buf, int n) {
+    if (h->host_comm) {
+        if (h->opt.allreduce(h->opt.allreduce_user, buf, n, 1) != 0) return LH_E_RCCL;
+    } else if (h->comm) {
+        DevBuf<double> d;
+        auto run = [&]() -> int {
+            HIPCHK(d.ensure(n));
+            HIPCHK(hipMemcpyAsync(d.p, buf, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            NCCLCHK(ncclAllReduce(d.p, d.p, n, ncclFloat64, ncclMax, h->comm, h->stream));
+            HIPCHK(hipMemcpyAsync(buf, d.p, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            return LH_OK;
+        };
+        const int st = run();
+        d.release();
+        return st;
+    }
+    return LH_OK;
+}
+
 int check_rank_options(lh_handle* h) {
     const lh_options& o = h->opt;
     const int depth = h->host_comm ? 1 : (o.trials_per_sync > 0 ? std::min(o.trials_per_sync, 32) : 2);
@@ -996,24 +1024,9 @@ int check_rank_options(lh_handle* h) {
     constexpr int n = (int)(sizeof(v) / sizeof(v[0]));
     double buf[2 * n];
     for (int i = 0; i < n; ++i) { buf[i] = v[i]; buf[n + i] = -v[i]; }
-    if (h->host_comm) {
-        if (o.allreduce(o.allreduce_user, buf, 2 * n, 1) != 0) return LH_E_RCCL;
-    } else if (h->comm) {
-        DevBuf<double> d;
-        auto run = [&]() -> int {
-            HIPCHK(d.ensure(2 * n));
-            HIPCHK(hipMemcpyAsync(d.p, buf, sizeof(buf), hipMemcpyHostToDevice, h->stream));
-            NCCLCHK(ncclAllReduce(d.p, d.p, 2 * n, ncclFloat64, ncclMax, h->comm, h->stream));
-            HIPCHK(hipMemcpyAsync(buf, d.p, sizeof(buf), hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            return LH_OK;
-        };
-        const int st = run();
-        d.release();
-        if (st != LH_OK) return st;
-    } else {
-        return LH_OK;
-    }
+    if (!h->host_comm && !h->comm) return LH_OK;
+    const int st = rank_max(h, buf, 2 * n);
+    if (st != LH_OK) return st;
     for (int i = 0; i < n; ++i)
         if (!(buf[i] == -buf[n + i])) return LH_E_BADARG;   // max != min somewhere (NaN options fail too)
     return LH_OK;
