@@ -1798,7 +1798,6 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         }
     }
 #endif
-#undef LDLT_SSTAMP
     CSTAMP(6);
 
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
@@ -2244,6 +2243,10 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
             if (wave == 0 && lane < GNB)
                 for (int j = lane + 1; j < GNB; ++j) pnl[lane * GPS + j] = pnl[lane * GPS + lane] * pnl[j * GPS + lane];
             lds_barrier();
+            // the W rows' LDS addresses off an opaque zero: one base register and immediate offsets (with
+            // constant addresses the compiler kept ~160 of them in VGPRs across the loop, and spilled)
+            int z0 = 0;
+            asm volatile("" : "+v"(z0));
             for (int r = GNB + tid; r < m; r += GT) {
                 double a[GNB];
 #pragma unroll
@@ -2253,7 +2256,7 @@ __device__ __forceinline__ void g_ldlt_solve(double* __restrict__ gA, int NG, in
                     const double l = a[k] * ginv[k];
                     a[k] = l;
 #pragma unroll
-                    for (int j = k + 1; j < GNB; ++j) a[j] -= l * pnl[k * GPS + j];
+                    for (int j = k + 1; j < GNB; ++j) a[j] -= l * pnl[z0 + k * GPS + j];
                     __builtin_amdgcn_sched_barrier(0);   // one step's loads at a time (register budget)
                 }
 #pragma unroll
@@ -2710,6 +2713,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     if (wv == 0) factor_block8(SY, Nl[0], NDl[0], 0, lane);
     lds_barrier();
     CSTAMP(5);
+#ifdef LH_STAMPS
+    unsigned long long ss_[5] = {0, 0, 0, 0, 0}, sa_ = __builtin_amdgcn_s_memtime(), sb_;
+#endif
     for (int t = 0; t < nstep; ++t) {
         const int k0 = 8 * t, par = t & 1, m0 = k0 + 8;
         const double* N = Nl[par];
@@ -2729,11 +2735,14 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                     ldlt_tile_row(SY, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
                     wave_sync();
                 }
+                LDLT_SSTAMP(0);
                 factor_block8(SY, Nl[par ^ 1], NDl[par ^ 1], m0, lane);
+                LDLT_SSTAMP(1);
             } else if (wv < BLOAD && (uw & LH_UNIT_VALID)) {
                 const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
                 ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
+            if (wv != 0) LDLT_SSTAMP(3);
         }
         if (wv >= BLOAD) {
             // tile row I enters the window at step 2 I - 14, into the slots of tile row I - 8 (retired
@@ -2767,49 +2776,88 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             }
         }
         lds_barrier();
+        if (wv == 0) LDLT_SSTAMP(2); else LDLT_SSTAMP(4);
     }
+#ifdef LH_STAMPS
+    if (lane == 0) {
+        if (wv == 0) {
+            atomicAdd(&lh_stamps[46], ss_[0]);
+            atomicAdd(&lh_stamps[47], ss_[1]);
+            atomicAdd(&lh_stamps[48], ss_[2]);
+            atomicAdd(&lh_stamps[51], 1ull);
+        } else {
+            atomicAdd(&lh_stamps[49], ss_[3]);
+            atomicAdd(&lh_stamps[50], ss_[4]);
+        }
+    }
+#endif
     __syncthreads();   // L and ND rows in global memory, z in LDS
     CSTAMP(6);
 
     // ---------------- back substitution x = L^-T z, blocks descending, one wave ----------------
-    // For block KB: x_b = ND_b y_b (lanes 0..7), then every row r in [KB - 128, KB) takes
-    // y_r -= sum_v L[KB+v][r] x_b[v] (lane l: rows KB - 128 + l and KB - 64 + l); the next block's
-    // L rows and ND are loaded while this one computes.
+    // The rows a block updates (L[KB+v][r] != 0 needs r >= KB + v - 104) live in registers: lane l,
+    // slot s holds the row r = l + 64 s (mod 128) of the window [KB - 120, KB + 8), so the block's own 8
+    // rows sit in 8 consecutive lanes of one 16-lane row (DPP broadcasts, as k_ctrl's backsub_block),
+    // and once solved their lanes take the rows 128 below, which enter the window for the next block.
+    // Per block: x_b = ND_b y_b, then every other held row takes y_r -= sum_v L[KB+v][r] x_b[v]; the
+    // next block's L rows and ND are loaded while this one computes.
+    // every block's ND into the (now free) window's LDS first
+    double* NDs = A;
+    for (int i = tid; i < 8 * nb; i += CT) NDs[i] = NDg[i];
+    lds_barrier();
     if (wv == 0) {
-        for (int i = lane; i < NE; i += 64) y[i] = z[i];
-        double la[8], lb[8], nd[8];
-        auto load_blk = [&](int KB, double (&l1)[8], double (&l2)[8], double (&ndv)[8]) {
+        auto row_of = [&](int KB, int sl) { const int lo = KB - 120; return lo + ((lane + 64 * sl - lo) & 127); };
+        auto load_blk = [&](int KB, double (&l0)[8], double (&l1)[8]) {
+            const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
-                const double* Lr = Lg + (size_t)(KB + v) * LH_LBW;
-                l1[v] = (lane >= v) ? Lr[lane - v] : 0.0;          // row KB - 128 + lane
-                l2[v] = Lr[64 + lane - v];                          // row KB - 64 + lane
-                ndv[v] = NDg[8 * KB + (lane & 7) * 8 + v];
+                const double* Lr = Lg + (size_t)(KB + v) * LH_LBW + LH_LBW - KB - v;   // + r: L[KB+v][r]
+                l0[v] = (r0 < KB) ? Lr[r0] : 0.0;
+                l1[v] = (r1 < KB) ? Lr[r1] : 0.0;
             }
         };
-        load_blk(nb - 8, la, lb, nd);
-        for (int KB = nb - 8; KB >= 0; KB -= 8) {
+        int KB = nb - 8;
+        double y0, y1;
+        {
+            const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
+            y0 = (r0 >= 0) ? z[r0] : 0.0;
+            y1 = (r1 >= 0) ? z[r1] : 0.0;
+        }
+        double la[8], lb[8];
+        load_blk(KB, la, lb);
+        for (; KB >= 0; KB -= 8) {
             double ca[8], cb[8], cn[8];
 #pragma unroll
-            for (int v = 0; v < 8; ++v) { ca[v] = la[v]; cb[v] = lb[v]; cn[v] = nd[v]; }
-            if (KB >= 8) load_blk(KB - 8, la, lb, nd);
+            for (int v = 0; v < 8; ++v) { ca[v] = la[v]; cb[v] = lb[v]; cn[v] = NDs[8 * KB + (lane & 7) * 8 + v]; }
+            if (KB >= 8) load_blk(KB - 8, la, lb);
+            const int sb_ = (KB >> 6) & 1, kl = KB & 63;
+            const bool mine = lane >= kl && lane < kl + 8;
+            const int re = KB - 128 + (lane - kl);                       // the row entering this lane's slot
+            const double zin = (mine && re >= 0) ? z[re] : 0.0;
+            const double ys = sb_ ? y1 : y0;
             double yb[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) yb[w] = y[KB + w];
+            if (KB & 8) {
+                yb[0] = bcast16<8>(ys); yb[1] = bcast16<9>(ys); yb[2] = bcast16<10>(ys); yb[3] = bcast16<11>(ys);
+                yb[4] = bcast16<12>(ys); yb[5] = bcast16<13>(ys); yb[6] = bcast16<14>(ys); yb[7] = bcast16<15>(ys);
+            } else {
+                yb[0] = bcast16<0>(ys); yb[1] = bcast16<1>(ys); yb[2] = bcast16<2>(ys); yb[3] = bcast16<3>(ys);
+                yb[4] = bcast16<4>(ys); yb[5] = bcast16<5>(ys); yb[6] = bcast16<6>(ys); yb[7] = bcast16<7>(ys);
+            }
             const double xv = ((cn[0] * yb[0] + cn[1] * yb[1]) + (cn[2] * yb[2] + cn[3] * yb[3])) +
                               ((cn[4] * yb[4] + cn[5] * yb[5]) + (cn[6] * yb[6] + cn[7] * yb[7]));
             double xb[8];
 #pragma unroll
-            for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, v);
-            const int ra = KB - 128 + lane, rb = KB - 64 + lane;
+            for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, kl + v);
             const double sa = ((ca[0] * xb[0] + ca[1] * xb[1]) + (ca[2] * xb[2] + ca[3] * xb[3])) +
                               ((ca[4] * xb[4] + ca[5] * xb[5]) + (ca[6] * xb[6] + ca[7] * xb[7]));
-            const double sb = ((cb[0] * xb[0] + cb[1] * xb[1]) + (cb[2] * xb[2] + cb[3] * xb[3])) +
-                              ((cb[4] * xb[4] + cb[5] * xb[5]) + (cb[6] * xb[6] + cb[7] * xb[7]));
-            if (ra >= 0) y[ra] -= sa;
-            if (rb >= 0) y[rb] -= sb;
-            if (lane < 8) y[KB + lane] = xv;
-            wave_sync();
+            const double sbb = ((cb[0] * xb[0] + cb[1] * xb[1]) + (cb[2] * xb[2] + cb[3] * xb[3])) +
+                               ((cb[4] * xb[4] + cb[5] * xb[5]) + (cb[6] * xb[6] + cb[7] * xb[7]));
+            y0 -= sa;   // zero L where the held row is this block's own or past the band
+            y1 -= sbb;
+            if (mine) {
+                y[KB + (lane - kl)] = xv;                                // the solution, natural order
+                if (sb_) y1 = zin; else y0 = zin;
+            }
         }
     }
     __syncthreads();

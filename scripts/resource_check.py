@@ -35,10 +35,9 @@ def parse(path):
     return kernels
 
 
-# Kernels allowed a small spill: k_ctrl_g (and its probe) at 512 threads keep a few loop-invariant
-# registers in scratch, stored once before the panel loop and reloaded once after it (measured: 512
-# threads with those bytes run a P = 64 trial in ~650 us, 256 spill-free threads in ~810 us).
-SPILL_ALLOWED = {"k_ctrl_g": 64, "k_ldlt_g_probe": 64}
+# No kernel may spill (round 4: k_ctrl_g's rows-below loop addresses its LDS operands off one base
+# register instead of ~160 constant-address VGPRs, which had pushed it 3 registers over its budget).
+SPILL_ALLOWED = {}
 
 
 def main():
