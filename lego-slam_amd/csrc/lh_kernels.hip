@@ -1514,7 +1514,10 @@ struct LdsSys {
     __device__ __forceinline__ double& at(int r, int c) const { return A[r * AS + c]; }
     __device__ __forceinline__ double& rhs(int r) const { return A[NP * AS + r]; }
     __device__ __forceinline__ void store_l(int r, int c, double v) const { A[c * AS + r] = v; }
-    __device__ __forceinline__ void store_nd(int, int, double2) const {}   // ND stays in LDS (LdltBlockLds)
+    // indices as stored: a 16-row tile row or 8-column block starts at a multiple of 8, so wrapping its
+    // base once wraps every row / column of it (no carry into the base)
+    __device__ __forceinline__ int wrap(int x) const { return x; }
+    __device__ __forceinline__ double& atw(int r, int c) const { return A[r * AS + c]; }
 };
 #define LH_LBW 128   // k_ctrl_b: L entries kept per row (columns r - 128 .. r - 1)
 struct BandSys {
@@ -1523,11 +1526,9 @@ struct BandSys {
     double* Lg;  // global, LH_LBW per row
     __device__ __forceinline__ double& at(int r, int c) const { return A[(r & 127) * AS + (c & 127)]; }
     __device__ __forceinline__ double& rhs(int r) const { return y[r]; }
-    double* NDg; // global, 64 per 8-column block: the back substitution's block solves
     __device__ __forceinline__ void store_l(int r, int c, double v) const { Lg[(size_t)r * LH_LBW + (c - r + LH_LBW)] = v; }
-    __device__ __forceinline__ void store_nd(int k0, int i2, double2 v) const {
-        reinterpret_cast<double2*>(NDg + 8 * k0)[i2] = v;
-    }
+    __device__ __forceinline__ int wrap(int x) const { return x & 127; }
+    __device__ __forceinline__ double& atw(int r, int c) const { return A[r * AS + c]; }
 };
 
 // LDL^T of the 8x8 diagonal block at (k0, k0) of A by one wave, Eigen ldlt_inplace order (L = W
@@ -1546,8 +1547,9 @@ __device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ N
     const bool ident = p >= 8;
     double R[8], dl[8];
     double v[8];
+    const int kw = A.wrap(k0);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = A.at(k0 + r, k0 + q);   // upper entries: garbage confined to this lane's upper part
+    for (int q = 0; q < 8; ++q) v[q] = A.atw(kw + r, kw + q);   // upper entries: garbage confined to this lane's upper part
 #pragma unroll
     for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
     factor_column<0>(R, dl);
@@ -1561,7 +1563,7 @@ __device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ N
     if (lane < 8) {
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-            if (q <= r) A.at(k0 + q, k0 + r) = (q == r) ? dl[q] : R[q];
+            if (q <= r) A.atw(kw + q, kw + r) = (q == r) ? dl[q] : R[q];
     } else if (lane < 16) {
         double2* n2 = reinterpret_cast<double2*>(No + 8 * r);
         double2* d2 = reinterpret_cast<double2*>(NDo + 8 * r);
@@ -1569,7 +1571,6 @@ __device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ N
         for (int q = 0; q < 4; ++q) {
             n2[q] = double2{R[2 * q], R[2 * q + 1]};
             d2[q] = double2{R[2 * q] * dl[2 * q], R[2 * q + 1] * dl[2 * q + 1]};
-            A.store_nd(k0, 4 * r + q, d2[q]);
         }
     }
 }
@@ -1587,19 +1588,21 @@ template <class S>
 __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restrict__ N, const double* __restrict__ ND,
                                               int k0, int rb, int jb0, int jb1, int skip_cb, bool store_l, int lane) {
     const int li = lane & 15, lk = lane >> 4, m0 = k0 + 8;
+    const int rbw = A.wrap(rb), kw = A.wrap(k0);
     const bool lo = li < 8;
     // every LDS read of this tile row is issued up front (tiles are disjoint and this step's
     // writes never touch block column k0, so no read here can see a write of this step)
     const double na0 = lo ? N[lk * 8 + li] : 0.0, na1 = lo ? N[(lk + 4) * 8 + li] : 0.0;
     const double da0 = lo ? ND[li * 8 + lk] : 0.0, da1 = lo ? ND[li * 8 + 4 + lk] : 0.0;
-    const double a0 = A.at(rb + li, k0 + lk), a1 = A.at(rb + li, k0 + 4 + lk);
+    const double a0 = A.atw(rbw + li, kw + lk), a1 = A.atw(rbw + li, kw + 4 + lk);
     int cb = (jb0 == skip_cb) ? jb0 + 16 : jb0;
     double b0 = 0.0, b1 = 0.0, old[4] = {0.0, 0.0, 0.0, 0.0};
     if (cb < jb1) {
-        b0 = A.at(cb + li, k0 + lk);
-        b1 = A.at(cb + li, k0 + 4 + lk);
+        const int cbw = A.wrap(cb);
+        b0 = A.atw(cbw + li, kw + lk);
+        b1 = A.atw(cbw + li, kw + 4 + lk);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) old[q] = A.at(rb + lk + 4 * q, cb + li);
+        for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + lk + 4 * q, cbw + li);
     }
     v4d l = {0.0, 0.0, 0.0, 0.0};
     l = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, a0, l, 0, 0, 0);
@@ -1632,14 +1635,16 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
     }
     // trailing tiles, software-pipelined: the next tile's operands are in flight during this one's MFMAs
     while (cb < jb1) {
+        const int cbw_cur = A.wrap(cb);
         int nc = cb + 16;
         if (nc == skip_cb) nc += 16;
         double nb0 = 0.0, nb1 = 0.0, nold[4] = {0.0, 0.0, 0.0, 0.0};
         if (nc < jb1) {
-            nb0 = A.at(nc + li, k0 + lk);
-            nb1 = A.at(nc + li, k0 + 4 + lk);
+            const int ncw = A.wrap(nc);
+            nb0 = A.atw(ncw + li, kw + lk);
+            nb1 = A.atw(ncw + li, kw + 4 + lk);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) nold[q] = A.at(rb + lk + 4 * q, nc + li);
+            for (int q = 0; q < 4; ++q) nold[q] = A.atw(rbw + lk + 4 * q, ncw + li);
         }
         v4d acc = {0.0, 0.0, 0.0, 0.0};
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], b0, acc, 0, 0, 0);
@@ -1648,7 +1653,7 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = rb + lk + 4 * q;
-            if (row >= m0 && col >= m0 && col <= row) A.at(row, col) = old[q] - acc[q];
+            if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + lk + 4 * q, cbw_cur + li) = old[q] - acc[q];
         }
         cb = nc;
         b0 = nb0; b1 = nb1;
@@ -2709,7 +2714,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     lds_barrier();
     CSTAMP(4);
 
-    const BandSys SY{A, y, Lg, NDg};
+    const BandSys SY{A, y, Lg};
     if (wv == 0) factor_block8(SY, Nl[0], NDl[0], 0, lane);
     lds_barrier();
     CSTAMP(5);
@@ -2720,12 +2725,15 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         const int k0 = 8 * t, par = t & 1, m0 = k0 + 8;
         const double* N = Nl[par];
         const double* ND = NDl[par];
-        if (wv == BLOAD && lane < 8) {   // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
-            double zz = 0.0;
+        if (wv == BLOAD) {
+            if (lane < 8) {   // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
+                double zz = 0.0;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) zz += y[k0 + q] * N[q * 8 + lane];
-            const double d = SY.at(k0 + lane, k0 + lane);
-            z[k0 + lane] = fabs(d) > 2.2250738585072014e-308 ? zz : 0.0;
+                for (int q = 0; q < 8; ++q) zz += y[k0 + q] * N[q * 8 + lane];
+                const double d = SY.at(k0 + lane, k0 + lane);
+                z[k0 + lane] = fabs(d) > 2.2250738585072014e-308 ? zz : 0.0;
+            }
+            NDg[64 * t + lane] = ND[lane];   // the back substitution's copy, off wave 0's chain
         }
         if (m0 < nb) {
             const int g0 = m0 >> 4;
@@ -2747,6 +2755,8 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         if (wv >= BLOAD) {
             // tile row I enters the window at step 2 I - 14, into the slots of tile row I - 8 (retired
             // after step 2 I - 15); its block indices are loaded at step 2 I - 16, its values at 2 I - 15
+            // Every load is unconditional (clamped index): a conditional load becomes a branch whose join
+            // waits for it.  Selections and the diagonal's lambda wait until the values are written.
             if ((t & 1) == 0) {
                 const int Iw = t / 2 + 7;
                 if (Iw >= 8 && Iw < NT) {
@@ -2754,14 +2764,20 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int c = 16 * (Iw - 7) + lcol + k;
-                        SY.at(r, c) = (c <= r) ? lval[k] : 0.0;
+                        double v = (lbk[k] >= 0) ? lval[k] : 0.0;
+                        if (r == c) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
+                        SY.at(r, c) = (c <= r) ? v : 0.0;
                     }
                 }
                 const int Ia = t / 2 + 8;
                 if (Ia < NT) {
-                    const int r = 16 * Ia + lrow;
+                    const int r = 16 * Ia + lrow, pr = r / 6;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) lbk[k] = band_block(bblk, r, 16 * (Ia - 7) + lcol + k, n);
+                    for (int k = 0; k < 8; ++k) {
+                        const int c = 16 * (Ia - 7) + lcol + k, pc = c / 6, d = pr - pc;
+                        lbk[k] = bblk[min(max(pc, 0), P - 1) * 64 + min(max(d, 0), 63)];
+                        if (!(c <= r && r < n && d < 64)) lbk[k] = -1;
+                    }
                 }
             } else {
                 const int Ib = (t - 1) / 2 + 8;
@@ -2770,7 +2786,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int c = 16 * (Ib - 7) + lcol + k;
-                        lval[k] = (c <= r && r < NE) ? band_value(src, lbk[k], r, c, lambda, prm.strategy, n) : 0.0;
+                        lval[k] = src[(size_t)max(lbk[k], 0) * 36 + (c % 6) * 6 + (r % 6)];
                     }
                 }
             }
@@ -2810,10 +2826,10 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         auto load_blk = [&](int KB, double (&l0)[8], double (&l1)[8]) {
             const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
 #pragma unroll
-            for (int v = 0; v < 8; ++v) {
+            for (int v = 0; v < 8; ++v) {   // unconditional loads (clamped), the own block's rows selected to 0 later
                 const double* Lr = Lg + (size_t)(KB + v) * LH_LBW + LH_LBW - KB - v;   // + r: L[KB+v][r]
-                l0[v] = (r0 < KB) ? Lr[r0] : 0.0;
-                l1[v] = (r1 < KB) ? Lr[r1] : 0.0;
+                l0[v] = Lr[min(r0, KB - 1)];
+                l1[v] = Lr[min(r1, KB - 1)];
             }
         };
         int KB = nb - 8;
@@ -2852,8 +2868,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                               ((ca[4] * xb[4] + ca[5] * xb[5]) + (ca[6] * xb[6] + ca[7] * xb[7]));
             const double sbb = ((cb[0] * xb[0] + cb[1] * xb[1]) + (cb[2] * xb[2] + cb[3] * xb[3])) +
                                ((cb[4] * xb[4] + cb[5] * xb[5]) + (cb[6] * xb[6] + cb[7] * xb[7]));
-            y0 -= sa;   // zero L where the held row is this block's own or past the band
-            y1 -= sbb;
+            // rows past the band have zero L; the block's own rows (r >= KB) take no update
+            if (row_of(KB, 0) < KB) y0 -= sa;
+            if (row_of(KB, 1) < KB) y1 -= sbb;
             if (mine) {
                 y[KB + (lane - kl)] = xv;                                // the solution, natural order
                 if (sb_) y1 = zin; else y0 = zin;
