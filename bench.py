@@ -136,10 +136,11 @@ def native_oracle():
         return None, "-O3 -ffp-contract=off -fopenmp (parity build; native build failed)"
 
 
-def cxx_caller_ms(w, reps):
+def cxx_caller_ms(w, reps, exe=None, line=False, env=None):
     """Median wall time of lh_solve on this window from the compiled C++ caller (tests/abi_caller.cpp,
-    window file format there), or None when the binary is missing or fails."""
-    exe = os.path.join(ROOT, "lego-slam_amd", "lib", "abi_caller")
+    window file format there), or None when the binary is missing or fails.  line: return the caller's
+    whole timing line (prep / upload / solve / download of the last call) instead."""
+    exe = exe or os.path.join(ROOT, "lego-slam_amd", "lib", "abi_caller")
     if not os.path.exists(exe):
         return None
     O = len(w["obs_pose"])
@@ -163,12 +164,13 @@ def cxx_caller_ms(w, reps):
             if ext is not None:
                 np.asarray(ext, np.float64).tofile(f)
         try:
-            r = subprocess.run([exe, win, res, str(reps)], capture_output=True, text=True, timeout=120)
+            r = subprocess.run([exe, win, res, str(reps)], capture_output=True, text=True, timeout=120,
+                               env=None if env is None else {**os.environ, **env})
         except subprocess.TimeoutExpired:
             return None
-        for line in r.stdout.splitlines():
-            if "lh_solve median" in line:
-                return round(float(line.split("lh_solve median")[1].split()[0]), 3)
+        for ln in r.stdout.splitlines():
+            if "lh_solve median" in ln:
+                return ln if line else round(float(ln.split("lh_solve median")[1].split()[0]), 3)
     return None
 
 

@@ -133,6 +133,7 @@ struct lh_params {
     int32_t pcg_max_it;     // PCG cap (<= 0: 2 * rows, problem.cpp:422)
     int32_t precision;      // lh_precision: 0 fp64 throughout, 1 fp32 per-edge residual/Jacobians (k_lin<T, TRIAL, true>)
     int32_t dec_in_reduce;  // 1: k_reduce's scalar block takes the LM decision (one rank; k_ctrl, k_ctrl_b)
+    int32_t nd_a, nd_s, nd_long_first, nd_steps;   // k_ctrl's two-chain split (lh_ctrl_nd_plan; nd_steps 0: off)
     int32_t commit_in_reduce;   // 1: k_reduce copies an accepted trial's staged blocks to the committed system
                                 //    before it overwrites them (k_ctrl_b: no one-CU copy of a large system)
     double K[4];
@@ -219,3 +220,163 @@ struct lh_band_args {
     double* Lg;              // [ceil16(6P)][128] L rows
     double* NDg;             // [steps][64] ND per block
 };
+
+// the two-chain order of lh_ctrl_nd_plan as arithmetic (k_ctrl: no tables): the position of pose p, and
+// the pose at position x
+LH_HD static inline int lh_nd_pos(int p, int P, int a, int s, int long_first) {
+    const int b = P - a - s, nlong = long_first ? a : b, nshort = long_first ? b : a;
+    const bool inA = p < a, inB = p >= a + s;
+    const bool inLong = long_first ? inA : inB, inShort = long_first ? inB : inA;
+    const int first = inA ? 0 : (inB ? a + s : a);
+    return inLong ? p - first : (inShort ? nlong + (p - first) : nlong + nshort + (p - a));
+}
+LH_HD static inline int lh_nd_nat(int x, int P, int a, int s, int long_first) {
+    const int b = P - a - s, nlong = long_first ? a : b, nshort = long_first ? b : a;
+    if (x < nlong) return long_first ? x : a + s + x;
+    if (x < nlong + nshort) return long_first ? a + s + (x - nlong) : x - nlong;
+    return a + (x - nlong - nshort);
+}
+
+// ---- k_ctrl's two-chain schedule (nested dissection of a banded S) ------------------
+// Poses split as [A | S | B] in natural order, A and B decoupled (no chunk window holds poses of both:
+// every B pose's envelope starts at or after A's end).  In the order [long part, short part, S] the
+// LDL^T of the two parts are independent chains (chain 0: the long part's blocks then S's; chain 1:
+// the short part's), run concurrently by wave 0 and wave 1, one barrier per step; both update S.
+// A step's work units may then apply both chains' current blocks (sources): unit word bits 0-2 tile row,
+// 3-5 first tile column, 6-9 end tile column (absolute tiles), 10-11 source mask, 12-13 store mask
+// (L^T and the rhs row), 15 valid.  Wave 0's / wave 1's word: the sources of its next block's diagonal
+// tile.  chain[c][t]: the block chain c eliminates at step t (-1: none).
+#define LH_ND_SRC0 0x0400u
+#define LH_ND_STORE0 0x1000u
+struct lh_ctrl_nd {
+    int nsteps;                       // 0: no worthwhile split (run the one-chain schedule)
+    int a, s, long_first;             // [A | S | B]: A = poses [0, a), S = [a, a + s); the long part first
+    int8_t chain[2][LH_NSTEP + 1];
+    uint8_t pos[LH_PMAX];             // natural pose -> position in the factor order
+    uint16_t units[16 * LH_NSTEP];
+};
+LH_HD static inline uint16_t lh_nd_unit(int I, int jb0, int jb1, int src, int store) {
+    return (uint16_t)(LH_UNIT_VALID | (uint32_t)I | ((uint32_t)jb0 << 3) | ((uint32_t)jb1 << 6) | ((uint32_t)src << 10) |
+                      ((uint32_t)store << 12));
+}
+// pf[p]: the first pose coupled with pose p (p's envelope).  Fills nd; returns nd.nsteps.
+static inline int lh_ctrl_nd_plan(int P, const int* pf, lh_ctrl_nd& nd) {
+    nd.nsteps = 0;
+    const int n = 6 * P, NE = (n + 15) & ~15, NB = ((n + 7) & ~7) / 8, NT = NE / 16;
+    if (P < 12 || P > LH_PMAX) return 0;
+    int best = NB - 2, ba = -1, bs = -1, blong_first = 1;
+    for (int a = 4; a < P; a += 4)
+        for (int b = 4; a + b < P; b += 4) {
+            const int s = P - a - b;
+            bool dec = true;                              // B's envelope must not reach A
+            for (int q = a + s; q < P && dec; ++q) dec = pf[q] >= a;
+            if (!dec) continue;
+            const int nl = 6 * (a > b ? a : b) / 8, ns = 6 * (a > b ? b : a) / 8, nS = NB - nl - ns;
+            if (ns >= nl || nS < 1) continue;
+            if (nl + nS < best) { best = nl + nS; ba = a; bs = s; blong_first = a > b; }
+        }
+    if (ba < 0) return 0;
+    const int a = ba, s = bs, b = P - a - s;
+    const int nlong = blong_first ? a : b, nshort = blong_first ? b : a;
+    nd.a = a; nd.s = s; nd.long_first = blong_first;
+    for (int p = 0; p < P; ++p) nd.pos[p] = (uint8_t)lh_nd_pos(p, P, a, s, blong_first);
+    int nat[LH_PMAX];                                     // position -> natural pose
+    for (int p = 0; p < P; ++p) nat[nd.pos[p]] = p;
+    // block-level structure in the factor order, then the symbolic fill of the elimination
+    bool nz[LH_NSTEP][LH_NSTEP];
+    for (int i = 0; i < NB; ++i)
+        for (int k = 0; k < NB; ++k) {
+            bool v = false;
+            for (int r = 8 * i; r < 8 * i + 8 && r < n && !v; ++r)
+                for (int c = 8 * k; c < 8 * k + 8 && c < n && !v; ++c) {
+                    const int p = nat[r / 6], q = nat[c / 6], hi = p > q ? p : q, lo = p > q ? q : p;
+                    v = lo >= pf[hi];
+                }
+            nz[i][k] = v && i > k;
+        }
+    for (int k = 0; k < NB; ++k)
+        for (int i = k + 1; i < NB; ++i)
+            if (nz[i][k])
+                for (int j = k + 1; j < i; ++j)
+                    if (nz[j][k]) nz[i][j] = true;
+    auto tnz = [&](int I, int k) {
+        return (2 * I > k && 2 * I < NB && nz[2 * I][k]) || (2 * I + 1 > k && 2 * I + 1 < NB && nz[2 * I + 1][k]);
+    };
+    const int nl_blk = 6 * nlong / 8, ns_blk = 6 * nshort / 8;
+    for (int c = 0; c < 2; ++c)
+        for (int t = 0; t <= LH_NSTEP; ++t) nd.chain[c][t] = -1;
+    int T = 0;
+    for (int k = 0; k < nl_blk; ++k) nd.chain[0][T++] = (int8_t)k;
+    for (int k = nl_blk + ns_blk; k < NB; ++k) nd.chain[0][T++] = (int8_t)k;
+    for (int k = 0; k < ns_blk; ++k) nd.chain[1][k] = (int8_t)(nl_blk + k);
+    for (int i = 0; i < 16 * LH_NSTEP; ++i) nd.units[i] = 0;
+    const int order[14] = {2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12};
+    for (int t = 0; t < T; ++t) {
+        int src_blk[2] = {nd.chain[0][t], nd.chain[1][t]};
+        // the chains' next diagonal tiles
+        int dg[2] = {-1, -1};
+        for (int c = 0; c < 2; ++c) {
+            const int nx = nd.chain[c][t + 1];
+            if (nx < 0 || src_blk[c] < 0) continue;
+            dg[c] = nx >> 1;
+            if (c == 1 && dg[0] == dg[1]) return 0;   // waves 0 and 1 would update one tile
+            int m = 0;
+            for (int q = 0; q < 2; ++q)
+                if (src_blk[q] >= 0 && tnz(dg[c], src_blk[q])) m |= 1 << q;
+            nd.units[(c == 0 ? 0 : 1) * LH_NSTEP + t] = m ? lh_nd_unit(dg[c], dg[c], dg[c] + 1, m, 0) : 0;
+        }
+        uint16_t item[64];
+        int ni = 0;
+        auto mask_of = [&](int I, int J) {
+            int m = 0;
+            for (int q = 0; q < 2; ++q) {
+                const int k = src_blk[q];
+                if (k >= 0 && tnz(I, k) && tnz(J, k)) m |= 1 << q;
+            }
+            return m;
+        };
+        auto store_of = [&](int I) {
+            int m = 0;
+            for (int q = 0; q < 2; ++q) {
+                const int k = src_blk[q];
+                if (k >= 0 && tnz(I, k)) m |= 1 << q;
+            }
+            return m;
+        };
+        for (int gran = 0; gran < 3; ++gran) {   // one tile per unit, one row per unit, stores merged in
+            ni = 0;
+            for (int I = 0; I < NT; ++I) {
+                const int st = store_of(I);
+                int j0 = -1, jm = 0, jl = -1;
+                bool stored = false;
+                for (int J = 0; J <= I; ++J) {
+                    const bool diag = (J == I) && (I == dg[0] || I == dg[1]);
+                    const int m = diag ? 0 : mask_of(I, J);
+                    if (!m) continue;
+                    if (gran == 0) {
+                        item[ni++] = lh_nd_unit(I, J, J + 1, m, 0);
+                    } else {
+                        if (j0 < 0) j0 = J;
+                        if (jl >= 0 && jl != J - 1) {   // a gap (a chain's diagonal tile): close the range
+                            item[ni++] = lh_nd_unit(I, j0, jl + 1, jm, (gran == 2 && !stored) ? st : 0);
+                            stored = stored || gran == 2;
+                            j0 = J; jm = 0;
+                        }
+                        jm |= m; jl = J;
+                    }
+                    if (ni > 60) return 0;
+                }
+                if (gran > 0 && j0 >= 0) {
+                    item[ni++] = lh_nd_unit(I, j0, jl + 1, jm, (gran == 2 && !stored) ? st : 0);
+                    stored = stored || gran == 2;
+                }
+                if (st && !(gran == 2 && stored)) item[ni++] = lh_nd_unit(I, 0, 0, st, st);
+            }
+            if (ni <= 14) break;
+        }
+        if (ni > 14) return 0;
+        for (int i = 0; i < ni; ++i) nd.units[order[i] * LH_NSTEP + t] = item[i];
+    }
+    nd.nsteps = T;
+    return T;
+}

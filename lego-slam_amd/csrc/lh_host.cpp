@@ -280,6 +280,7 @@ struct lh_handle {
     View<int32_t> d_bblk;
     DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64)
     bool band = false;            // this window's LDL^T runs in k_ctrl_b
+    lh_ctrl_nd nd{};              // k_ctrl's two-chain schedule (nd.nsteps 0: the one-chain one)
     View<int32_t> d_lm_perm;
     View<double> d_ptab_init, d_qt_init, d_ext;
     DevBuf<uint8_t> d_arena;
@@ -686,9 +687,18 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
                 for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
                 fcb[I] = f >> 3;
             }
+            // the two-chain schedule when the window splits into decoupled parts (fewer steps)
+            h->nd.nsteps = 0;
+            if (h->opt.linear_solver == LH_SOLVER_LDLT && !getenv("LH_NO_ND")) lh_ctrl_nd_plan(P, pf.data(), h->nd);
         }
-        const int order[15] = LH_ORDER_CTRL;
-        lh_ctrl_units(6 * P, fcb, order, 15, LH_NSTEP, h->s_units.p);
+        if (h->nd.nsteps > 0) {
+            std::memcpy(h->s_units.p, h->nd.units, sizeof(h->nd.units));
+        } else {
+            const int order[15] = LH_ORDER_CTRL;
+            lh_ctrl_units(6 * P, fcb, order, 15, LH_NSTEP, h->s_units.p);
+        }
+    } else {
+        h->nd.nsteps = 0;
     }
 
     if (h->band) {
@@ -727,6 +737,10 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.no_evo = getenv("LH_NO_EVO") != nullptr;
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
+    prm.nd_steps = h->nd.nsteps;
+    prm.nd_a = h->nd.a;
+    prm.nd_s = h->nd.s;
+    prm.nd_long_first = h->nd.long_first;
     for (int i = 0; i < 4; ++i) prm.K[i] = w->K[i];
     const double t1 = now_ms();
 

@@ -1465,11 +1465,17 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
 
 // Per-block products of the 8x8 diagonal-block factor (LDS, shared by all waves).
 struct LdltBlockLds {
-    double N[2][64];          // N = (Delta L^T)^-1 of the block being eliminated (row-major), by step parity
+    double N[4][64];          // N = (Delta L^T)^-1 of the block being eliminated (row-major), by step parity
+                              // (the two-chain schedule: chain c uses N[2c + parity])
     double ND[NBLK][64];      // N Delta = L_bb^-T of every block (row-major): trailing-update operand
                               // and the back substitution's block solve
     double z[NP];             // z = D^-1 L^-1 b (zero where |D| <= DBL_MIN)
 };
+// one instance per kernel, whichever schedule runs
+__device__ __forceinline__ LdltBlockLds& ldlt_lds() {
+    __shared__ __attribute__((aligned(16))) LdltBlockLds F;
+    return F;
+}
 
 // 64-bit broadcast of lane L of each 16-lane row (DPP row_newbcast, two 32-bit moves): a few
 // cycles, where a readlane round trip through an SGPR costs ~45 on a dependent chain.  (A single
@@ -1482,12 +1488,20 @@ __device__ __forceinline__ double bcast16(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Column Q of the 8x8 factor.  Its pivot d is on the step's critical chain (the next pivot needs coef),
+// so the reciprocal takes one cubic correction folded into the quotient: r0 = v_rcp_f64(d),
+// e = 1 - d r0, coef = a (1 + e + e^2) with a = R[Q] r0 -- three dependent FMAs after the rcp (two
+// Newton steps and a multiply were five), the relative error O(e^3) below rounding.  The zero-pivot
+// select (Eigen's pivot_is_valid: no scaling) comes last, off the chain.
 template <int Q>
 __device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
     const double d = bcast16<Q>(R[Q]);
-    dl[Q] = fabs(d) > 0.0 ? d : 1.0;          // Eigen ldlt_inplace: no scaling where !pivot_is_valid
-    const double inv = fast_rcp(dl[Q]);
-    const double coef = R[Q] * inv;
+    const bool ok = fabs(d) > 0.0;
+    dl[Q] = ok ? d : 1.0;
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double e = fma(-d, r0, 1.0);
+    const double a = R[Q] * r0;
+    const double coef = ok ? fma(a, fma(e, e, e), a) : R[Q];
     double u[8];
     // W[j][Q] = lane j's R[Q], read before R[Q] becomes coef
     if (Q < 1) u[1] = bcast16<1>(R[Q]);
@@ -1592,9 +1606,11 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
     const bool lo = li < 8;
     // every LDS read of this tile row is issued up front (tiles are disjoint and this step's
     // writes never touch block column k0, so no read here can see a write of this step)
-    const double na0 = lo ? N[lk * 8 + li] : 0.0, na1 = lo ? N[(lk + 4) * 8 + li] : 0.0;
-    const double da0 = lo ? ND[li * 8 + lk] : 0.0, da1 = lo ? ND[li * 8 + 4 + lk] : 0.0;
+    // (unconditional reads, selected after: no exec-masked branches between the loads)
+    const double n0 = N[lk * 8 + (li & 7)], n1 = N[(lk + 4) * 8 + (li & 7)];
+    const double d0 = ND[(li & 7) * 8 + lk], d1 = ND[(li & 7) * 8 + 4 + lk];
     const double a0 = A.atw(rbw + li, kw + lk), a1 = A.atw(rbw + li, kw + 4 + lk);
+    const double na0 = lo ? n0 : 0.0, na1 = lo ? n1 : 0.0, da0 = lo ? d0 : 0.0, da1 = lo ? d1 : 0.0;
     int cb = (jb0 == skip_cb) ? jb0 + 16 : jb0;
     double b0 = 0.0, b1 = 0.0, old[4] = {0.0, 0.0, 0.0, 0.0};
     if (cb < jb1) {
@@ -1604,6 +1620,7 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
 #pragma unroll
         for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + lk + 4 * q, cbw + li);
     }
+    __builtin_amdgcn_sched_barrier(0);   // every load above is in flight before the first wait
     v4d l = {0.0, 0.0, 0.0, 0.0};
     l = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, a0, l, 0, 0, 0);
     l = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, a1, l, 0, 0, 0);
@@ -1659,6 +1676,122 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
         b0 = nb0; b1 = nb1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) old[q] = nold[q];
+    }
+}
+
+// Wave 0's share of step k0: the trailing update of the diagonal tile at rb (the one holding block
+// k0 + 8), the head of every step's critical chain (this, then the next block's factor).  The
+// operands are ldlt_tile_row's with a_J = a_I (the tile is its own column), so the eight LDS reads go
+// out in one batch, unconditionally (N / ND rows past 7 read the neighbouring in-bounds LDS and are
+// dropped by the select), and the only waits are the one round trip and the MFMA chain.
+template <class S>
+__device__ __forceinline__ void diag_tile(const S& A, const double* __restrict__ N, const double* __restrict__ ND,
+                                          int k0, int rb, int lane) {
+    const int li = lane & 15, lk = lane >> 4, m0 = k0 + 8;
+    const int rbw = A.wrap(rb), kw = A.wrap(k0);
+    const bool lo = li < 8;
+    const double n0 = N[lk * 8 + (li & 7)], n1 = N[(lk + 4) * 8 + (li & 7)];
+    const double d0 = ND[(li & 7) * 8 + lk], d1 = ND[(li & 7) * 8 + 4 + lk];
+    const double a0 = A.atw(rbw + li, kw + lk), a1 = A.atw(rbw + li, kw + 4 + lk);
+    double old[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + lk + 4 * q, rbw + li);
+    __builtin_amdgcn_sched_barrier(0);   // the scheduler otherwise sinks the loads between the MFMAs
+    v4d l = {0.0, 0.0, 0.0, 0.0};
+    l = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? n0 : 0.0, a0, l, 0, 0, 0);
+    l = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? n1 : 0.0, a1, l, 0, 0, 0);
+    v4d t = {0.0, 0.0, 0.0, 0.0};
+    t = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? d0 : 0.0, l[0], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? d1 : 0.0, l[1], t, 0, 0, 0);
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], a0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[1], a1, acc, 0, 0, 0);
+    const int col = rb + li;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = rb + lk + 4 * q;
+        if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + lk + 4 * q, rbw + li) = old[q] - acc[q];
+    }
+}
+
+// k_ctrl's two-chain steps (lh_ctrl_nd_plan): one tile row's unit applying up to two sources, the blocks
+// the two chains eliminate this step.  For each source s in smask | stmask: L_s = a_s N_s, T_s = L_s ND_s^T
+// with the rows above its block (< m0_s) zeroed, so they contribute nothing; stmask: L_s^T stored for the
+// tile row and the rhs row updated by every stored source at once (two units never update one rhs row
+// in a step); then A_IJ -= sum_{s in smask} T_s a_{s,J}^T over the tiles [jb0, jb1), a_{s,J}'s rows above
+// the block zeroed likewise.  Entries above every applied source's block are left alone.
+struct NdSrc {
+    const double* N;
+    const double* ND;
+    int k0;
+};
+__device__ __forceinline__ void nd_tile_row(double* __restrict__ A, const NdSrc (&src)[2], int smask, int stmask, int rb,
+                                            int jb0, int jb1, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    const bool lo = li < 8;
+    double t0[2], t1[2];
+    int mm = 1 << 20;
+    double ru[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        t0[q] = 0.0; t1[q] = 0.0;
+        if (!(((smask | stmask) >> q) & 1)) continue;   // a stored source need not reach the unit's tiles
+        const int k0 = src[q].k0, m0 = k0 + 8;
+        mm = min(mm, m0);
+        const double* N = src[q].N;
+        const double* ND = src[q].ND;
+        const double na0 = lo ? N[lk * 8 + li] : 0.0, na1 = lo ? N[(lk + 4) * 8 + li] : 0.0;
+        const double da0 = lo ? ND[li * 8 + lk] : 0.0, da1 = lo ? ND[li * 8 + 4 + lk] : 0.0;
+        const double a0 = A[(rb + li) * AS + k0 + lk], a1 = A[(rb + li) * AS + k0 + 4 + lk];
+        v4d l = {0.0, 0.0, 0.0, 0.0};
+        l = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, a0, l, 0, 0, 0);
+        l = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, a1, l, 0, 0, 0);
+        v4d t = {0.0, 0.0, 0.0, 0.0};
+        t = __builtin_amdgcn_mfma_f64_16x16x4f64(da0, l[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f64_16x16x4f64(da1, l[1], t, 0, 0, 0);
+        const bool below = rb + li >= m0;
+        t0[q] = below ? t[0] : 0.0;
+        t1[q] = below ? t[1] : 0.0;
+        if ((stmask >> q) & 1) {
+            if (below) {
+                A[(k0 + lk) * AS + rb + li] = l[0];
+                A[(k0 + 4 + lk) * AS + rb + li] = l[1];
+            }
+            const double rb0 = (li == 0) ? A[NP * AS + k0 + lk] : 0.0, rb1 = (li == 0) ? A[NP * AS + k0 + 4 + lk] : 0.0;
+            v4d u = {0.0, 0.0, 0.0, 0.0};
+            u = __builtin_amdgcn_mfma_f64_16x16x4f64(t0[q], rb0, u, 0, 0, 0);
+            u = __builtin_amdgcn_mfma_f64_16x16x4f64(t1[q], rb1, u, 0, 0, 0);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) ru[w] += u[w];
+        }
+    }
+    if (stmask && li == 0) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int row = rb + lk + 4 * w;
+            if (row >= mm) A[NP * AS + row] -= ru[w];
+        }
+    }
+    for (int cb = jb0; cb < jb1; cb += 16) {
+        double old[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) old[w] = A[(rb + lk + 4 * w) * AS + cb + li];
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (!((smask >> q) & 1)) continue;
+            const int k0 = src[q].k0, m0 = k0 + 8;
+            const bool cin = cb + li >= m0;
+            const double b0 = cin ? A[(cb + li) * AS + k0 + lk] : 0.0, b1 = cin ? A[(cb + li) * AS + k0 + 4 + lk] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t0[q], b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t1[q], b1, acc, 0, 0, 0);
+        }
+        const int col = cb + li;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int row = rb + lk + 4 * w;
+            if (row >= mm && col >= mm && col <= row) A[row * AS + col] = old[w] - acc[w];
+        }
     }
 }
 
@@ -1720,6 +1853,45 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
     }
 }
 
+// Phase 4 of both LDL^T schedules: x = L^-T z over every block, descending, one wave (y0 / y1: rows
+// lane / lane + 64 of z in, of x out, in the factor's order).
+__device__ __forceinline__ void ldlt_backsub(const double* __restrict__ A, const LdltBlockLds& F, int nb, int lane,
+                                             double& y0, double& y1) {
+    double nda[8], ndb[8];
+    backsub_load_nd<120>(F, lane, nda);
+    backsub_load_nd<112>(F, lane, ndb);
+    backsub_block<120>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<104>(F, lane, nda);
+    backsub_block<112>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<96>(F, lane, ndb);
+    backsub_block<104>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<88>(F, lane, nda);
+    backsub_block<96>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<80>(F, lane, ndb);
+    backsub_block<88>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<72>(F, lane, nda);
+    backsub_block<80>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<64>(F, lane, ndb);
+    backsub_block<72>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<56>(F, lane, nda);
+    backsub_block<64>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<48>(F, lane, ndb);
+    backsub_block<56>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<40>(F, lane, nda);
+    backsub_block<48>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<32>(F, lane, ndb);
+    backsub_block<40>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<24>(F, lane, nda);
+    backsub_block<32>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<16>(F, lane, ndb);
+    backsub_block<24>(A, nda, nb, lane, y0, y1);
+    backsub_load_nd<8>(F, lane, nda);
+    backsub_block<16>(A, ndb, nb, lane, y0, y1);
+    backsub_load_nd<0>(F, lane, ndb);
+    backsub_block<8>(A, nda, nb, lane, y0, y1);
+    backsub_block<0>(A, ndb, nb, lane, y0, y1);
+}
+
 // Phases 3-4 of k_ctrl on a padded system already in LDS (A lower + rhs row NP, zeros in the upper
 // triangle): blocked LDL^T with the forward substitution, then the back substitution; xsol[perm[r]] =
 // the solution's entry r < n (perm == nullptr: xsol[r]).  units: the per-step work units in LDS
@@ -1736,7 +1908,7 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid,
                                                const int* __restrict__ perm, const uint16_t* __restrict__ units) {
     const int lane = tid & 63, wave = tid >> 6;
-    __shared__ __attribute__((aligned(16))) LdltBlockLds F;
+    LdltBlockLds& F = ldlt_lds();
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const LdsSys SY{A};
@@ -1775,7 +1947,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
             const uint32_t uw = __builtin_amdgcn_readfirstlane(units[wv * LH_NSTEP + t]);
             if (wv == 0) {
                 if (uw & LH_UNIT_VALID) {
-                    ldlt_tile_row(SY, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
+                    diag_tile(SY, N, ND, k0, 16 * g0, lane);
                     wave_sync();
                 }
                 LDLT_SSTAMP(0);
@@ -1808,39 +1980,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
     if (wv == 0) {
         double y0 = (lane < nb) ? F.z[lane] : 0.0, y1 = (lane + 64 < nb) ? F.z[lane + 64] : 0.0;
-        double nda[8], ndb[8];
-        backsub_load_nd<120>(F, lane, nda);
-        backsub_load_nd<112>(F, lane, ndb);
-        backsub_block<120>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<104>(F, lane, nda);
-        backsub_block<112>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<96>(F, lane, ndb);
-        backsub_block<104>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<88>(F, lane, nda);
-        backsub_block<96>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<80>(F, lane, ndb);
-        backsub_block<88>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<72>(F, lane, nda);
-        backsub_block<80>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<64>(F, lane, ndb);
-        backsub_block<72>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<56>(F, lane, nda);
-        backsub_block<64>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<48>(F, lane, ndb);
-        backsub_block<56>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<40>(F, lane, nda);
-        backsub_block<48>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<32>(F, lane, ndb);
-        backsub_block<40>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<24>(F, lane, nda);
-        backsub_block<32>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<16>(F, lane, ndb);
-        backsub_block<24>(A, nda, nb, lane, y0, y1);
-        backsub_load_nd<8>(F, lane, nda);
-        backsub_block<16>(A, ndb, nb, lane, y0, y1);
-        backsub_load_nd<0>(F, lane, ndb);
-        backsub_block<8>(A, nda, nb, lane, y0, y1);
-        backsub_block<0>(A, ndb, nb, lane, y0, y1);
+        ldlt_backsub(A, F, nb, lane, y0, y1);
         if (perm) {
             if (lane < n) xsol[perm[lane]] = y0;
             if (lane + 64 < n) xsol[perm[lane + 64]] = y1;
@@ -1848,6 +1988,72 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
             if (lane < NE) xsol[lane] = y0;
             if (lane + 64 < NE) xsol[lane + 64] = y1;
         }
+    }
+    lds_barrier();
+    CSTAMP(7);
+}
+
+// Phases 3-4 of k_ctrl, two-chain schedule (lh_ctrl_nd_plan): the system is in LDS in
+// the order [long part | short part | separator] (lh_nd_pos), the two parts decoupled, so their LDL^T
+// are independent chains.  Step t eliminates chain 0's block c0(t) (the long part's blocks, then the
+// separator's) and chain 1's block c1(t) (the short part's, while they last); one barrier per step.
+//   wave 0 / wave 1: the next diagonal tile of chain 0 / 1 (every source of the step reaching it), then
+//                    that chain's next factor (N by chain and step parity, ND per block);
+//   other waves:     their unit (nd_tile_row: up to both sources per tile, tile rows and columns absolute);
+//   wave 12 / 13:    z of chain 0's / 1's block first.
+// The back substitution is the one-chain one over the factor order; x goes out in natural order.
+__device__ __forceinline__ void lds_ldlt_solve_nd(double* __restrict__ A, double* __restrict__ xsol, int n, int tid,
+                                                  const uint16_t* __restrict__ units, const lh_params& prm) {
+    const int lane = tid & 63, wave = tid >> 6;
+    LdltBlockLds& F = ldlt_lds();
+    const int nb = (n + 7) & ~7;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int P = prm.P, a = prm.nd_a, sep = prm.nd_s, lf = prm.nd_long_first, T = prm.nd_steps;
+    const int b = P - a - sep;
+    const int nl_blk = 6 * (lf ? a : b) / 8, ns_blk = 6 * (lf ? b : a) / 8;
+    auto c0 = [&](int t) { return t < nl_blk ? t : t + ns_blk; };          // chain 0's block at step t
+    auto c1 = [&](int t) { return t < ns_blk ? nl_blk + t : -1; };        // chain 1's (-1: done)
+    const LdsSys SY{A};
+    if (wv == 0) factor_block8(SY, F.N[0], F.ND[c0(0)], 8 * c0(0), lane);
+    if (wv == 1 && ns_blk > 0) factor_block8(SY, F.N[2], F.ND[c1(0)], 8 * c1(0), lane);
+    lds_barrier();
+    CSTAMP(5);
+    for (int t = 0; t < T; ++t) {
+        const int par = t & 1, ka = c0(t), kb = c1(t);
+        const NdSrc src[2] = {{F.N[par], F.ND[ka], 8 * ka}, {F.N[2 + par], F.ND[kb < 0 ? 0 : kb], 8 * kb}};
+        if ((wv == 12 || (wv == 13 && kb >= 0)) && lane < 8) {   // z of the step's blocks (LDLT::_solve_impl)
+            const int q0 = wv == 12 ? 0 : 1, k0 = src[q0].k0;
+            const double* N = src[q0].N;
+            double z = 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) z += A[NP * AS + k0 + q] * N[q * 8 + lane];
+            const double d = A[(k0 + lane) * AS + k0 + lane];
+            F.z[k0 + lane] = fabs(d) > 2.2250738585072014e-308 ? z : 0.0;
+        }
+        const uint32_t uw = __builtin_amdgcn_readfirstlane(units[wv * LH_NSTEP + t]);
+        const int smask = (uw >> 10) & 3, stmask = (uw >> 12) & 3;
+        if (wv < 2) {
+            const int nx = wv == 0 ? c0(t + 1) : c1(t + 1);
+            const bool live = wv == 0 ? (t + 1 < T) : (kb >= 0 && nx >= 0);
+            if (uw & LH_UNIT_VALID) {
+                const int I = uw & 7;
+                nd_tile_row(A, src, smask, 0, 16 * I, 16 * I, 16 * I + 16, lane);
+                wave_sync();
+            }
+            if (live) factor_block8(SY, F.N[2 * wv + (par ^ 1)], F.ND[nx], 8 * nx, lane);
+        } else if (uw & LH_UNIT_VALID) {
+            const int I = uw & 7, jb0 = (uw >> 3) & 7, jb1 = (uw >> 6) & 15;
+            nd_tile_row(A, src, smask, stmask, 16 * I, 16 * jb0, 16 * jb1, lane);
+        }
+        lds_barrier();
+    }
+    CSTAMP(6);
+    if (wv == 0) {
+        double y0 = (lane < nb) ? F.z[lane] : 0.0, y1 = (lane + 64 < nb) ? F.z[lane + 64] : 0.0;
+        ldlt_backsub(A, F, nb, lane, y0, y1);
+        // factor row r -> natural row 6 nat(r / 6) + r mod 6
+        if (lane < n) xsol[6 * lh_nd_nat(lane / 6, P, a, sep, lf) + lane % 6] = y0;
+        if (lane + 64 < n) xsol[6 * lh_nd_nat((lane + 64) / 6, P, a, sep, lf) + (lane + 64) % 6] = y1;
     }
     lds_barrier();
     CSTAMP(7);
@@ -2015,6 +2221,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
     const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
     const bool decided = mode != 0 && prm.dec_in_reduce;   // k_reduce took this trial's LM decision
+    const bool nd = SOLVER == 0 && prm.nd_steps > 0;        // the two-chain LDL^T schedule
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2113,7 +2320,11 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             // S element i: pose pair (p, q), p <= q, entry (ea, eb) -> rows 6 p + ea, 6 q + eb.  The
             // upper slot of every off-diagonal entry is zeroed: the factor stores L^T there where the
             // envelope reaches, and the back substitution reads zeros elsewhere.
-            const int pp = (int)(mp[u] & 0xffffu), qq = (int)(mp[u] >> 16);
+            int pp = (int)(mp[u] & 0xffffu), qq = (int)(mp[u] >> 16);
+            if (nd) {
+                pp = lh_nd_pos(pp, P, prm.nd_a, prm.nd_s, prm.nd_long_first);
+                qq = lh_nd_pos(qq, P, prm.nd_a, prm.nd_s, prm.nd_long_first);
+            }
             const int gi = 6 * pp + ea, gj = 6 * qq + eb;
             const int hi = max(gi, gj), lo = min(gi, gj);
             if (gi == gj) {
@@ -2123,7 +2334,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
                 A[lo * AS + hi] = 0.0;
             }
         } else if (i < LY.off_bp) {
-            A[NP * AS + (i - LY.off_bs)] = v;
+            int r = i - LY.off_bs;
+            if (nd) r = 6 * lh_nd_pos(r / 6, P, prm.nd_a, prm.nd_s, prm.nd_long_first) + r % 6;
+            A[NP * AS + r] = v;
         } else if (i < LY.off_hd) {
             bpv[i - LY.off_bp] = v;
         } else if (i < LY.off_hd + n) {
@@ -2150,7 +2363,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         const int its = lds_pcg_solve(A, xs, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
         if (tid == 0) ctrl->pcg_iters += its;
     } else {
-        lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units);
+        if (nd) lds_ldlt_solve_nd(A, xs, n, tid, s_units, prm);
+        else lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units);
     }
     CSTAMP(8);
 
@@ -2611,7 +2825,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                                                const int32_t* __restrict__ bblk, const uint16_t* __restrict__ bunits,
                                                double* __restrict__ Lg, double* __restrict__ NDg, double* __restrict__ dxp,
                                                lh_params prm, int mode, volatile int* __restrict__ host_done, int seq) {
-    __shared__ double A[128 * AS];                          // the circular window of the lower band
+    __shared__ __attribute__((aligned(16))) double A[128 * AS];   // the circular window of the lower band
     __shared__ __attribute__((aligned(16))) double y[BNMAX];   // rhs (forward substitution), then x
     __shared__ double z[BNMAX];                             // D^-1 L^-1 b
     __shared__ __attribute__((aligned(16))) double Nl[2][64], NDl[2][64];
@@ -2740,7 +2954,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             const uint32_t uw = unit_word(t);
             if (wv == 0) {
                 if (uw & LH_UNIT_VALID) {
-                    ldlt_tile_row(SY, N, ND, k0, 16 * g0, 16 * g0, 16 * g0 + 16, -1, false, lane);
+                    diag_tile(SY, N, ND, k0, 16 * g0, lane);
                     wave_sync();
                 }
                 LDLT_SSTAMP(0);
@@ -2817,19 +3031,54 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     // and once solved their lanes take the rows 128 below, which enter the window for the next block.
     // Per block: x_b = ND_b y_b, then every other held row takes y_r -= sum_v L[KB+v][r] x_b[v]; the
     // next block's L rows and ND are loaded while this one computes.
-    // every block's ND into the (now free) window's LDS first
-    double* NDs = A;
-    for (int i = tid; i < 8 * nb; i += CT) NDs[i] = NDg[i];
+    // The L rows and ND come from global memory through an LDS ring the other 15 waves fill ahead of
+    // wave 0 (the window's LDS is free now): block j of the descent (KB = nb - 8 - 8 j) goes to slot
+    // j mod BRING, loaded by wave 1 + j mod 15 once wave 0 has read block j - BRING, and published by
+    // a workgroup-scope release of bring_ready[slot] = j + 1.  Wave 0 then reads each block's L from LDS
+    // one block ahead (its ND when it starts the block), and frees the slot of the block before: a
+    // one-block-ahead global prefetch left ~0.65 us of HBM latency per block on its chain (P = 128:
+    // 63 us of back substitution).
+    constexpr int BSLOT = 8 * LH_LBW + 64;   // one block: its 8 L rows as stored, then its ND
+    constexpr int BRING = (128 * AS) / BSLOT;
+    static_assert(BRING >= 15, "ring deeper than the producer count");
+    __shared__ int bring_ready[BRING], bring_used;
+    const int nblk = nb / 8;
+    if (tid < BRING) bring_ready[tid] = 0;
+    if (tid == 0) bring_used = 0;
     lds_barrier();
-    if (wv == 0) {
+    if (wv > 0) {   // producers
+        for (int j = wv - 1; j < nblk; j += 15) {
+            if (j >= BRING)
+                while (__hip_atomic_load(&bring_used, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < j - BRING + 1)
+                    __builtin_amdgcn_s_sleep(1);
+            const int KB = nb - 8 - 8 * j;
+            const double2* gl = reinterpret_cast<const double2*>(Lg + (size_t)KB * LH_LBW);
+            const double2* gn = reinterpret_cast<const double2*>(NDg + (size_t)8 * KB);
+            double2 v[8], vn = double2{0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = gl[k * 64 + lane];
+            if (lane < 32) vn = gn[lane];
+            double2* dst = reinterpret_cast<double2*>(A + (j % BRING) * BSLOT);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dst[k * 64 + lane] = v[k];
+            if (lane < 32) dst[8 * 64 + lane] = vn;
+            __hip_atomic_store(&bring_ready[j % BRING], j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else {
         auto row_of = [&](int KB, int sl) { const int lo = KB - 120; return lo + ((lane + 64 * sl - lo) & 127); };
-        auto load_blk = [&](int KB, double (&l0)[8], double (&l1)[8]) {
+        // block j's operands from its slot: L[KB+v][r] of this lane's two rows (clamped: the own block's
+        // rows and rows past the band read in-bounds values never used) and its ND row
+        auto load_blk = [&](int j, double (&l0)[8], double (&l1)[8]) {
+            while (__hip_atomic_load(&bring_ready[j % BRING], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != j + 1)
+                __builtin_amdgcn_s_sleep(1);
+            const int KB = nb - 8 - 8 * j;
+            const double* sl = A + (j % BRING) * BSLOT;
             const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
 #pragma unroll
-            for (int v = 0; v < 8; ++v) {   // unconditional loads (clamped), the own block's rows selected to 0 later
-                const double* Lr = Lg + (size_t)(KB + v) * LH_LBW + LH_LBW - KB - v;   // + r: L[KB+v][r]
-                l0[v] = Lr[min(r0, KB - 1)];
-                l1[v] = Lr[min(r1, KB - 1)];
+            for (int v = 0; v < 8; ++v) {
+                const double* Lr = sl + v * LH_LBW + LH_LBW - KB - v;   // + r: L[KB+v][r]
+                l0[v] = Lr[max(min(r0, KB - 1), KB + v - LH_LBW)];
+                l1[v] = Lr[max(min(r1, KB - 1), KB + v - LH_LBW)];
             }
         };
         int KB = nb - 8;
@@ -2840,12 +3089,17 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             y1 = (r1 >= 0) ? z[r1] : 0.0;
         }
         double la[8], lb[8];
-        load_blk(KB, la, lb);
-        for (; KB >= 0; KB -= 8) {
+        load_blk(0, la, lb);
+        for (int j = 0; j < nblk; ++j, KB -= 8) {
             double ca[8], cb[8], cn[8];
 #pragma unroll
-            for (int v = 0; v < 8; ++v) { ca[v] = la[v]; cb[v] = lb[v]; cn[v] = NDs[8 * KB + (lane & 7) * 8 + v]; }
-            if (KB >= 8) load_blk(KB - 8, la, lb);
+            for (int v = 0; v < 8; ++v) { ca[v] = la[v]; cb[v] = lb[v]; }
+            // block j - 1's slot is fully read: free it (block j's L is in registers, its ND read now), then
+            // fetch block j + 1's L
+            if (j > 0 && lane == 0) __hip_atomic_store(&bring_used, j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+            for (int v = 0; v < 8; ++v) cn[v] = A[(j % BRING) * BSLOT + 8 * LH_LBW + (lane & 7) * 8 + v];
+            if (j + 1 < nblk) load_blk(j + 1, la, lb);
             const int sb_ = (KB >> 6) & 1, kl = KB & 63;
             const bool mine = lane >= kl && lane < kl + 8;
             const int re = KB - 128 + (lane - kl);                       // the row entering this lane's slot

@@ -50,28 +50,39 @@ std::vector<int> llc_cpus() {
 // Workers are pinned to the CPUs sharing the caller's last-level cache (LH_HOST_PIN=0 leaves them to
 // the scheduler): a GPU box exposes every host core to a process with a share of them, and a worker
 // the scheduler puts on the other socket runs a pass's block at a fraction of the others' speed.
-// Only one live pool per process pins (a second handle's pool would stack its workers on the same
-// cores), and rank processes of one box (LOCAL_RANK) start at disjoint offsets into the LLC's list.
+// Pools of one process never stack their workers: each worker takes the least-used CPU of the LLC's
+// list (a process-wide count, released when the pool goes), so a second live handle's pool gets the
+// next free cores, and rank processes of one box (LOCAL_RANK) break ties from disjoint offsets.
 namespace {
-std::atomic<int> g_pinned_pools{0};
+std::mutex g_pin_mu;
+std::vector<int> g_pin_use;   // per index into llc_cpus(): workers of live pools pinned there
 }
 
 Pool::Pool(int threads) {
     const char* pin_env = std::getenv("LH_HOST_PIN");
     const bool want_pin = !(pin_env && pin_env[0] == '0');
-    int expected = 0;
-    pinned_ = want_pin && g_pinned_pools.compare_exchange_strong(expected, 1);
-    const std::vector<int> cpus = pinned_ ? llc_cpus() : std::vector<int>();
+    const std::vector<int> cpus = want_pin ? llc_cpus() : std::vector<int>();
     int offset = 0;
     if (const char* lr = std::getenv("LOCAL_RANK")) offset = std::max(0, std::atoi(lr)) * std::max(threads - 1, 1);
+    const int nc = (int)cpus.size();
     for (int i = 1; i < threads; ++i) {
         workers_.emplace_back([this] { loop(); });
-        if (!cpus.empty() && (offset + i - 1) < 4 * (int)cpus.size()) {
-            cpu_set_t one;
-            CPU_ZERO(&one);
-            CPU_SET(cpus[(offset + i - 1) % cpus.size()], &one);
-            pthread_setaffinity_np(workers_.back().native_handle(), sizeof(one), &one);   // best effort
+        if (nc == 0) continue;
+        int pick = -1;
+        {
+            std::lock_guard<std::mutex> g(g_pin_mu);
+            if ((int)g_pin_use.size() < nc) g_pin_use.resize(nc, 0);
+            for (int k = 0; k < nc; ++k) {
+                const int c = (offset + k) % nc;
+                if (pick < 0 || g_pin_use[c] < g_pin_use[pick]) pick = c;
+            }
+            ++g_pin_use[pick];
         }
+        pinned_.push_back(pick);
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpus[pick], &one);
+        pthread_setaffinity_np(workers_.back().native_handle(), sizeof(one), &one);   // best effort
     }
 }
 
@@ -82,7 +93,9 @@ Pool::~Pool() {
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
-    if (pinned_) g_pinned_pools.store(0);
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    for (const int c : pinned_)
+        if (c < (int)g_pin_use.size()) --g_pin_use[c];
 }
 
 // Hand-off protocol (every atomic seq_cst).  A worker counts itself in active_ *before* it loads

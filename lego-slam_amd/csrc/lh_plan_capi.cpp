@@ -115,6 +115,18 @@ int lhp_ctrl_units(int n, const int32_t* fcb, int band, uint16_t* units) {
     return lh_ctrl_units(n, fcb, order, 15, LH_NSTEP, units);
 }
 
+// k_ctrl's two-chain schedule (lh_ctrl_nd_plan) for tests: info = {nsteps, a, s, long_first}, units
+// [16 * LH_NSTEP], pos [P]
+int lhp_ctrl_nd(int P, const int32_t* pf, int32_t* info, uint16_t* units, uint8_t* pos) {
+    lh_ctrl_nd nd{};
+    std::vector<int> f(pf, pf + P);
+    lh_ctrl_nd_plan(P, f.data(), nd);
+    info[0] = nd.nsteps; info[1] = nd.a; info[2] = nd.s; info[3] = nd.long_first;
+    std::memcpy(units, nd.units, sizeof(nd.units));
+    for (int p = 0; p < P && p < LH_PMAX; ++p) pos[p] = nd.pos[p];
+    return nd.nsteps;
+}
+
 int64_t lhp_pool_stress(int threads, int runs, int n) {
     lh::Pool pool(threads > 0 ? threads : 1);
     std::atomic<int64_t> s{0};

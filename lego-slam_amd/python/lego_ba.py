@@ -520,6 +520,7 @@ def _pl():
             lib.lhp_plan_stages.argtypes = [C.POINTER(LhWindow), C.c_int, C.c_int, vp]
         lib.lhp_pool_stress.argtypes = [C.c_int, C.c_int, C.c_int]
         lib.lhp_ctrl_units.argtypes = [C.c_int, vp, C.c_int, vp]
+        lib.lhp_ctrl_nd.argtypes = [C.c_int, vp, vp, vp, vp]
         lib.lhp_pool_stress.restype = C.c_int64
         _planlib = lib
     return _planlib
@@ -554,6 +555,19 @@ def ctrl_units(n, fcb, band=False):
     u = np.zeros(16 * steps, np.uint16)
     worst = _pl().lhp_ctrl_units(int(n), _ptr(f), int(bool(band)), _ptr(u))
     return u.reshape(16, steps), worst
+
+
+def ctrl_nd(pf):
+    """k_ctrl's two-chain schedule (lh_ctrl_nd_plan) for a window whose pose p first couples pose pf[p]:
+    dict(nsteps, a, s, long_first, units[16][16] uint16, pos[P]); nsteps 0 = no split."""
+    P = len(pf)
+    f = np.ascontiguousarray(pf, np.int32)
+    info = np.zeros(4, np.int32)
+    u = np.zeros(16 * 16, np.uint16)
+    pos = np.zeros(max(P, 1), np.uint8)
+    _pl().lhp_ctrl_nd(int(P), _ptr(f), _ptr(info), _ptr(u), _ptr(pos))
+    return {"nsteps": int(info[0]), "a": int(info[1]), "s": int(info[2]), "long_first": int(info[3]),
+            "units": u.reshape(16, 16), "pos": pos[:P].astype(np.int64)}
 
 
 def pool_stress(threads, runs, n):

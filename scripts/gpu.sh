@@ -10,6 +10,7 @@
 #   trace              rocprofv3 --kernel-trace --stats of the quick bench (per-kernel averages)
 #   pmc                the PMC passes over the quick bench (one counter group per run)
 #   stamps=CFG         k_ctrl phase stamps (diagnostic -DLH_STAMPS library) on window CFG (C3, P64, ...)
+#   linstamps=CFG      k_lin / k_reduce per-phase wave-cycle shares (the same diagnostic library)
 #   ab=LIB             rocprofv3 A/B of the current library against LIB, alternated twice (k_lin, k_reduce,
 #                      k_ctrl* averages and the bench line of each)
 #   py=SCRIPT[,ARGS]   python3 SCRIPT ARGS (a measurement script under scripts/)
@@ -71,6 +72,10 @@ for step in "$@"; do
         LH_LIB=lego-slam_amd/lib/liblego_ba_stamps.so timeout -k 10 200 python3 scripts/ctrl_stamps.py ${arg:-C3} \
             > "$OUT/stamps_${arg:-C3}.log" 2>&1 || { cat "$OUT/stamps_${arg:-C3}.log"; exit 1; }
         cat "$OUT/stamps_${arg:-C3}.log" ;;
+    linstamps)
+        LH_LIB=lego-slam_amd/lib/liblego_ba_stamps.so timeout -k 10 200 python3 scripts/stamps.py ${arg:-C3} \
+            > "$OUT/linstamps_${arg:-C3}.log" 2>&1 || { cat "$OUT/linstamps_${arg:-C3}.log"; exit 1; }
+        cat "$OUT/linstamps_${arg:-C3}.log" ;;
     ab)
         : > "$OUT/ab_summary.txt"
         for r in 1 2; do

@@ -182,3 +182,168 @@ def test_k_ctrl_b_units_solve_and_window(P, span, seed):
     x = replay(S, b, units, units.shape[1], band=True)
     xr = np.linalg.solve(S, b)
     assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
+
+
+# ---- the two-chain schedule (lh_ctrl_nd_plan): k_ctrl's LDL^T as two concurrent chains ----
+SRC0, STORE0 = 0x0400, 0x1000
+
+
+def replay_nd(S, b, nd, debug=False):
+    """k_ctrl's two-chain LDL^T (lds_ldlt_solve_nd) driven by the plan's unit words, at tile granularity with
+    the kernel's operand algebra (every unit reads the operands as they were before the step); returns x
+    in natural order."""
+    n = len(b)
+    P = n // 6
+    NE, nb = (n + 15) & ~15, (n + 7) & ~7
+    pos = nd["pos"]
+    fr = np.array([6 * pos[r // 6] + r % 6 for r in range(n)])   # natural row -> factor row
+    Sp = np.zeros((n, n))
+    Sp[np.ix_(fr, fr)] = S
+    A = np.eye(NE)
+    A[:n, :n] = np.tril(Sp)
+    rhs = np.zeros(NE)
+    rhs[fr] = b
+    L = np.zeros((NE, NE))
+    a, sep, lf, T = nd["a"], nd["s"], nd["long_first"], nd["nsteps"]
+    bb = P - a - sep
+    nl_blk, ns_blk = 6 * (a if lf else bb) // 8, 6 * (bb if lf else a) // 8
+    c0 = lambda t: t if t < nl_blk else t + ns_blk          # noqa: E731
+    c1 = lambda t: nl_blk + t if t < ns_blk else -1         # noqa: E731
+    fac = {}
+
+    def factor(k):
+        k0 = 8 * k
+        M = np.tril(A[k0:k0 + 8, k0:k0 + 8])
+        M = M + np.tril(M, -1).T
+        Lb, D, W = np.eye(8), np.zeros(8), M.copy()
+        for q in range(8):
+            D[q] = W[q, q]
+            dl = D[q] if D[q] != 0 else 1.0
+            Lb[q + 1:, q] = W[q + 1:, q] / dl
+            W[q + 1:, q + 1:] -= np.outer(Lb[q + 1:, q], W[q, q + 1:])
+        dl = np.where(D != 0, D, 1.0)
+        N = np.linalg.inv(np.diag(dl) @ Lb.T)
+        fac[k] = (N, N @ np.diag(dl), D)
+
+    def unit(A, rhs, srcs, smask, stmask, rb, jb0, jb1):
+        Ts, mm, ru = {}, 1 << 20, np.zeros(16)
+        rows = np.arange(rb, rb + 16)
+        for q in (0, 1):
+            if not ((smask | stmask) >> q) & 1:   # a stored source need not reach the unit's tiles
+                continue
+            k = srcs[q]
+            k0, m0 = 8 * k, 8 * k + 8
+            mm = min(mm, m0)
+            N, ND, _ = fac[k]
+            Li = A[rb:rb + 16, k0:k0 + 8] @ N
+            Ti = Li @ ND.T
+            Ti[rows < m0] = 0.0
+            Ts[q] = Ti
+            if (stmask >> q) & 1:
+                keep = rows >= m0
+                L[rows[keep], k0:k0 + 8] = Li[keep]
+                ru += Ti @ rhs[k0:k0 + 8]
+        if stmask:
+            keep = rows >= mm
+            rhs[rows[keep]] -= ru[keep]
+        for cb in range(jb0, jb1, 16):
+            acc = np.zeros((16, 16))
+            cols = np.arange(cb, cb + 16)
+            for q, Ti in Ts.items():
+                if not (smask >> q) & 1:
+                    continue
+                k0 = 8 * srcs[q]
+                aj = A[cb:cb + 16, k0:k0 + 8].copy()
+                aj[cols < k0 + 8] = 0.0
+                acc += Ti @ aj.T
+            for i in range(16):
+                for j in range(16):
+                    r, c = rb + i, cb + j
+                    if r >= mm and c >= mm and c <= r:
+                        A[r, c] -= acc[i, j]
+
+    factor(c0(0))
+    if ns_blk > 0:
+        factor(c1(0))
+    z = np.zeros(NE)
+    units = nd["units"]
+    touched = []
+    for t in range(T):
+        srcs = (c0(t), c1(t))
+        for k in srcs:
+            if k >= 0:
+                k0 = 8 * k
+                zz = rhs[k0:k0 + 8] @ fac[k][0]
+                z[k0:k0 + 8] = np.where(np.abs(fac[k][2]) > 2.2250738585072014e-308, zz, 0.0)
+        pend = []
+        for w in range(16):
+            u = int(units[w, t])
+            if not u & VALID:
+                continue
+            I = u & 7
+            sm, st = (u >> 10) & 3, (u >> 12) & 3
+            if w < 2:
+                pend.append((sm, 0, 16 * I, 16 * I, 16 * I + 16))
+            else:
+                pend.append((sm, st, 16 * I, 16 * ((u >> 3) & 7), 16 * ((u >> 6) & 15)))
+        owned, rhs_rows = set(), set()   # each tile and each rhs tile row has one owner per step
+        for sm, st, rb, j0, j1 in pend:
+            for cb in range(j0, j1, 16):
+                assert (rb, cb) not in owned
+                owned.add((rb, cb))
+            if st:
+                assert rb not in rhs_rows
+                rhs_rows.add(rb)
+        snapA, snapR = A.copy(), rhs.copy()
+        dA, dR = np.zeros_like(A), np.zeros_like(rhs)
+        cells = set()
+        for sm, st, rb, j0, j1 in pend:
+            A2, R2 = snapA.copy(), snapR.copy()
+            unit(A2, R2, srcs, sm, st, rb, j0, j1)
+            ch = np.argwhere(A2 != snapA)
+            for r, c in ch:            # no two units of a step write one entry
+                assert (r, c) not in cells
+                cells.add((r, c))
+            dA += A2 - snapA
+            dR += R2 - snapR
+        A, rhs = snapA + dA, snapR + dR
+        touched.append(len(pend))
+        if t + 1 < T:
+            factor(c0(t + 1))
+        if srcs[1] >= 0 and c1(t + 1) >= 0:
+            factor(c1(t + 1))
+    assert len(fac) == nb // 8   # every block factored once
+    y = z.copy()
+    for KB in range(nb - 8, -1, -8):
+        xb = fac[KB // 8][1] @ y[KB:KB + 8]
+        y[:KB] -= L[KB:KB + 8, :KB].T @ xb
+        y[KB:KB + 8] = xb
+    if debug:
+        return y[fr], L, fac, z
+    return y[fr]
+
+
+@pytest.mark.parametrize("P,span,seed", [(20, 7, 0), (20, 5, 1), (21, 7, 2), (21, 3, 3), (20, 3, 4), (18, 4, 5)])
+def test_k_ctrl_two_chain_schedule_solves(P, span, seed):
+    rng = np.random.default_rng(seed)
+    S, pf = banded_system(P, span, rng)
+    nd = lego_ba.ctrl_nd(pf)
+    NB = (6 * P + 7) // 8
+    if nd["nsteps"] == 0:
+        pytest.skip("no split for this window")
+    assert nd["nsteps"] < NB - 1
+    assert sorted(nd["pos"]) == list(range(P))
+    b = rng.standard_normal(6 * P)
+    x = replay_nd(S, b, nd)
+    xr = np.linalg.solve(S, b)
+    assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
+
+
+def test_k_ctrl_two_chain_schedule_on_c3():
+    """C3's window (20 keyframes, chunk windows of 8 consecutive poses): 12 steps instead of 15."""
+    pf = [max(0, p - 7) for p in range(20)]
+    nd = lego_ba.ctrl_nd(pf)
+    assert nd["nsteps"] == 12
+    # a separator wide enough to decouple the two parts: no pose past it reaches the part before it
+    a, s = nd["a"], nd["s"]
+    assert all(pf[q] >= a for q in range(a + s, 20))
