@@ -310,7 +310,8 @@ static inline int lh_ctrl_nd_plan(int P, const int* pf, lh_ctrl_nd& nd) {
     for (int k = nl_blk + ns_blk; k < NB; ++k) nd.chain[0][T++] = (int8_t)k;
     for (int k = 0; k < ns_blk; ++k) nd.chain[1][k] = (int8_t)(nl_blk + k);
     for (int i = 0; i < 16 * LH_NSTEP; ++i) nd.units[i] = 0;
-    const int order[14] = {2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12};
+    // SIMD 2 and 3's waves first, then wave 1's SIMD-mates, then wave 0's
+    const int order[14] = {2, 3, 6, 7, 10, 11, 14, 15, 5, 9, 13, 4, 8, 12};
     for (int t = 0; t < T; ++t) {
         int src_blk[2] = {nd.chain[0][t], nd.chain[1][t]};
         // the chains' next diagonal tiles
@@ -343,38 +344,52 @@ static inline int lh_ctrl_nd_plan(int P, const int* pf, lh_ctrl_nd& nd) {
             }
             return m;
         };
-        for (int gran = 0; gran < 3; ++gran) {   // one tile per unit, one row per unit, stores merged in
-            ni = 0;
-            for (int I = 0; I < NT; ++I) {
-                const int st = store_of(I);
-                int j0 = -1, jm = 0, jl = -1;
-                bool stored = false;
-                for (int J = 0; J <= I; ++J) {
-                    const bool diag = (J == I) && (I == dg[0] || I == dg[1]);
-                    const int m = diag ? 0 : mask_of(I, J);
-                    if (!m) continue;
-                    if (gran == 0) {
-                        item[ni++] = lh_nd_unit(I, J, J + 1, m, 0);
-                    } else {
+        // the step's tiles in pieces of at most L consecutive tiles of one tile row (a chain's diagonal tile
+        // breaks a run), the row's L^T / rhs store a unit of its own or (merge) riding on the row's first
+        // piece: the smallest L (stores separate first) whose units fit the 14 unit waves
+        int cost[64];
+        bool fit = false;
+        for (int L = 1; L <= 8 && !fit; ++L)
+            for (int merge = 0; merge < 2 && !fit; ++merge) {
+                ni = 0;
+                bool over = false;
+                for (int I = 0; I < NT && !over; ++I) {
+                    const int st = store_of(I);
+                    bool stored = false;
+                    int j0 = -1, jm = 0, jl = -1;
+                    auto close = [&]() {
+                        if (j0 < 0) return;
+                        const int stm = (merge && !stored) ? st : 0;
+                        stored = stored || (merge && st);
+                        const int ns = (jm & 1) + (jm >> 1), nst = ((jm | stm) & 1) + ((jm | stm) >> 1);
+                        if (ni >= 60) { over = true; return; }
+                        cost[ni] = 4 * nst + 2 * ns * (jl + 1 - j0) + (stm ? 2 : 0);
+                        item[ni++] = lh_nd_unit(I, j0, jl + 1, jm, stm);
+                        j0 = -1; jm = 0;
+                    };
+                    for (int J = 0; J <= I; ++J) {
+                        const bool diag = (J == I) && (I == dg[0] || I == dg[1]);
+                        const int m = diag ? 0 : mask_of(I, J);
+                        if (!m) { close(); continue; }
+                        if (j0 >= 0 && (jl != J - 1 || J - j0 >= L)) close();
                         if (j0 < 0) j0 = J;
-                        if (jl >= 0 && jl != J - 1) {   // a gap (a chain's diagonal tile): close the range
-                            item[ni++] = lh_nd_unit(I, j0, jl + 1, jm, (gran == 2 && !stored) ? st : 0);
-                            stored = stored || gran == 2;
-                            j0 = J; jm = 0;
-                        }
                         jm |= m; jl = J;
                     }
-                    if (ni > 60) return 0;
+                    close();
+                    if (st && !stored) {
+                        if (ni >= 60) { over = true; break; }
+                        cost[ni] = 4 * ((st & 1) + (st >> 1)) + 2;
+                        item[ni++] = lh_nd_unit(I, 0, 0, st, st);
+                    }
                 }
-                if (gran > 0 && j0 >= 0) {
-                    item[ni++] = lh_nd_unit(I, j0, jl + 1, jm, (gran == 2 && !stored) ? st : 0);
-                    stored = stored || gran == 2;
-                }
-                if (st && !(gran == 2 && stored)) item[ni++] = lh_nd_unit(I, 0, 0, st, st);
+                fit = !over && ni <= 14;
             }
-            if (ni <= 14) break;
-        }
-        if (ni > 14) return 0;
+        if (!fit) return 0;
+        for (int a = 1; a < ni; ++a)   // stable insertion sort, cost descending: the heaviest on the freest SIMDs
+            for (int b = a; b > 0 && cost[b] > cost[b - 1]; --b) {
+                const int c = cost[b]; cost[b] = cost[b - 1]; cost[b - 1] = c;
+                const uint16_t u = item[b]; item[b] = item[b - 1]; item[b - 1] = u;
+            }
         for (int i = 0; i < ni; ++i) nd.units[order[i] * LH_NSTEP + t] = item[i];
     }
     nd.nsteps = T;

@@ -687,9 +687,12 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
                 for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
                 fcb[I] = f >> 3;
             }
-            // the two-chain schedule when the window splits into decoupled parts (fewer steps)
+            // the two-chain schedule (opt-in, LH_ND=1): fewer steps where the window splits into decoupled
+            // parts, but the separator's fill makes the early steps heavier; on C3 it measured slower than
+            // the one-chain schedule
             h->nd.nsteps = 0;
-            if (h->opt.linear_solver == LH_SOLVER_LDLT && !getenv("LH_NO_ND")) lh_ctrl_nd_plan(P, pf.data(), h->nd);
+            const char* nd_env = getenv("LH_ND");
+            if (h->opt.linear_solver == LH_SOLVER_LDLT && nd_env && nd_env[0] == '1') lh_ctrl_nd_plan(P, pf.data(), h->nd);
         }
         if (h->nd.nsteps > 0) {
             std::memcpy(h->s_units.p, h->nd.units, sizeof(h->nd.units));

@@ -1477,31 +1477,25 @@ __device__ __forceinline__ LdltBlockLds& ldlt_lds() {
     return F;
 }
 
-// 64-bit broadcast of lane L of each 16-lane row (DPP row_newbcast, two 32-bit moves): a few
-// cycles, where a readlane round trip through an SGPR costs ~45 on a dependent chain.  (A single
-// v_fmac_f64_dpp from inline asm measured 10% faster but lost precision: not used.)
+// 64-bit broadcast of lane L of each 16-lane row: one v_mov_b64_dpp row_newbcast (gfx950 allows 64-bit DPP
+// for row_newbcast).  The factor and the back substitution are issue-bound chains of these (a lone wave
+// issues a dependent f64 op every ~7-10 cycles), so one move instead of two 32-bit halves is what counts.
 template <int L>
 __device__ __forceinline__ double bcast16(double v) {
-    const long long x = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)x, 0x150 + L, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), 0x150 + L, 0xf, 0xf, true);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    const long long x = __builtin_amdgcn_update_dpp((long long)0, __double_as_longlong(v), 0x150 + L, 0xf, 0xf, true);
+    return __longlong_as_double(x);
 }
 
-// Column Q of the 8x8 factor.  Its pivot d is on the step's critical chain (the next pivot needs coef),
-// so the reciprocal takes one cubic correction folded into the quotient: r0 = v_rcp_f64(d),
-// e = 1 - d r0, coef = a (1 + e + e^2) with a = R[Q] r0 -- three dependent FMAs after the rcp (two
-// Newton steps and a multiply were five), the relative error O(e^3) below rounding.  The zero-pivot
-// select (Eigen's pivot_is_valid: no scaling) comes last, off the chain.
+// Column Q of the 8x8 factor: the pivot from lane Q by broadcast, its reciprocal (v_rcp_f64 and two
+// Newton steps), the column's entries and the trailing updates of the lane's row.  (A cubic correction
+// folded into the quotient, three dependent FMAs instead of five, measured the same ~1.8k cycles per
+// block alone, tools/ubench_ctrl_chain.hip: the chain is bound by issue, not by this latency.)
 template <int Q>
 __device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
     const double d = bcast16<Q>(R[Q]);
-    const bool ok = fabs(d) > 0.0;
-    dl[Q] = ok ? d : 1.0;
-    const double r0 = __builtin_amdgcn_rcp(d);
-    const double e = fma(-d, r0, 1.0);
-    const double a = R[Q] * r0;
-    const double coef = ok ? fma(a, fma(e, e, e), a) : R[Q];
+    dl[Q] = fabs(d) > 0.0 ? d : 1.0;          // Eigen ldlt_inplace: no scaling where !pivot_is_valid
+    const double inv = fast_rcp(dl[Q]);
+    const double coef = R[Q] * inv;
     double u[8];
     // W[j][Q] = lane j's R[Q], read before R[Q] becomes coef
     if (Q < 1) u[1] = bcast16<1>(R[Q]);
@@ -1912,6 +1906,9 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const LdsSys SY{A};
+#ifdef LH_PRIO
+    if (wv == 0) __builtin_amdgcn_s_setprio(3);   // A/B variant: wave 0's chain first in issue arbitration
+#endif
     if (wv == 0) factor_block8(SY, F.N[0], F.ND[0], 0, lane);
     lds_barrier();
     CSTAMP(5);
@@ -1976,6 +1973,9 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     }
 #endif
     CSTAMP(6);
+#ifdef LH_PRIO
+    if (wv == 0) __builtin_amdgcn_s_setprio(0);
+#endif
 
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
     if (wv == 0) {
@@ -3034,10 +3034,8 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     // The L rows and ND come from global memory through an LDS ring the other 15 waves fill ahead of
     // wave 0 (the window's LDS is free now): block j of the descent (KB = nb - 8 - 8 j) goes to slot
     // j mod BRING, loaded by wave 1 + j mod 15 once wave 0 has read block j - BRING, and published by
-    // a workgroup-scope release of bring_ready[slot] = j + 1.  Wave 0 then reads each block's L from LDS
-    // one block ahead (its ND when it starts the block), and frees the slot of the block before: a
-    // one-block-ahead global prefetch left ~0.65 us of HBM latency per block on its chain (P = 128:
-    // 63 us of back substitution).
+    // a workgroup-scope release of bring_ready[slot] = j + 1.  Wave 0 reads each block's L from LDS one
+    // block ahead (its ND when it starts the block).
     constexpr int BSLOT = 8 * LH_LBW + 64;   // one block: its 8 L rows as stored, then its ND
     constexpr int BRING = (128 * AS) / BSLOT;
     static_assert(BRING >= 15, "ring deeper than the producer count");
@@ -3066,11 +3064,19 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         }
     } else {
         auto row_of = [&](int KB, int sl) { const int lo = KB - 120; return lo + ((lane + 64 * sl - lo) & 127); };
-        // block j's operands from its slot: L[KB+v][r] of this lane's two rows (clamped: the own block's
-        // rows and rows past the band read in-bounds values never used) and its ND row
-        auto load_blk = [&](int j, double (&l0)[8], double (&l1)[8]) {
-            while (__hip_atomic_load(&bring_ready[j % BRING], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != j + 1)
+        // every block in [j0, j1] published (one round trip for the batch; producers run far ahead)
+        auto wait_ready = [&](int j0, int j1) {
+            for (;;) {
+                bool all = true;
+                for (int j = j0; j <= j1; ++j)
+                    all = all && __hip_atomic_load(&bring_ready[j % BRING], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == j + 1;
+                if (all) return;
                 __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        // block j's L entries of this lane's two rows from its slot (clamped: the own block's rows and rows
+        // past the band read in-bounds values never used)
+        auto load_blk = [&](int j, double (&l0)[8], double (&l1)[8]) {
             const int KB = nb - 8 - 8 * j;
             const double* sl = A + (j % BRING) * BSLOT;
             const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
@@ -3081,29 +3087,22 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 l1[v] = Lr[max(min(r1, KB - 1), KB + v - LH_LBW)];
             }
         };
-        int KB = nb - 8;
         double y0, y1;
         {
-            const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
+            const int r0 = row_of(nb - 8, 0), r1 = row_of(nb - 8, 1);
             y0 = (r0 >= 0) ? z[r0] : 0.0;
             y1 = (r1 >= 0) ? z[r1] : 0.0;
         }
-        double la[8], lb[8];
-        load_blk(0, la, lb);
-        for (int j = 0; j < nblk; ++j, KB -= 8) {
-            double ca[8], cb[8], cn[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) { ca[v] = la[v]; cb[v] = lb[v]; }
-            // block j - 1's slot is fully read: free it (block j's L is in registers, its ND read now), then
-            // fetch block j + 1's L
-            if (j > 0 && lane == 0) __hip_atomic_store(&bring_used, j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // block j with its L entries ca / cb: x_b = ND_b y_b, then the held rows' updates
+        auto solve_blk = [&](int j, const double (&ca)[8], const double (&cb)[8]) {
+            const int KB = nb - 8 - 8 * j;
+            double cn[8];
 #pragma unroll
             for (int v = 0; v < 8; ++v) cn[v] = A[(j % BRING) * BSLOT + 8 * LH_LBW + (lane & 7) * 8 + v];
-            if (j + 1 < nblk) load_blk(j + 1, la, lb);
             const int sb_ = (KB >> 6) & 1, kl = KB & 63;
             const bool mine = lane >= kl && lane < kl + 8;
             const int re = KB - 128 + (lane - kl);                       // the row entering this lane's slot
-            const double zin = (mine && re >= 0) ? z[re] : 0.0;
+            const double zin = z[max(re, 0)];
             const double ys = sb_ ? y1 : y0;
             double yb[8];
             if (KB & 8) {
@@ -3127,8 +3126,25 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             if (row_of(KB, 1) < KB) y1 -= sbb;
             if (mine) {
                 y[KB + (lane - kl)] = xv;                                // the solution, natural order
-                if (sb_) y1 = zin; else y0 = zin;
+                const double zi = re >= 0 ? zin : 0.0;
+                if (sb_) y1 = zi; else y0 = zi;
             }
+        };
+        // two register sets in turn (no copies between blocks); every 4 blocks one batched readiness check
+        // for the next 4 and one release of the slots read so far (the release waits for this wave's
+        // outstanding LDS reads, so no producer rewrites a slot still being read)
+        double la[8], lb[8], ma[8], mb[8];
+        wait_ready(0, min(3, nblk - 1));
+        load_blk(0, la, lb);
+        for (int j = 0; j < nblk; j += 2) {
+            if ((j & 3) == 0 && j + 4 < nblk) wait_ready(j + 4, min(j + 7, nblk - 1));
+            load_blk(min(j + 1, nblk - 1), ma, mb);
+            solve_blk(j, la, lb);
+            if (j + 1 >= nblk) break;
+            load_blk(min(j + 2, nblk - 1), la, lb);
+            solve_blk(j + 1, ma, mb);
+            if ((j & 3) == 2 && lane == 0)
+                __hip_atomic_store(&bring_used, j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();

@@ -14,12 +14,15 @@
 #   ab=LIB             rocprofv3 A/B of the current library against LIB, alternated twice (k_lin, k_reduce,
 #                      k_ctrl* averages and the bench line of each)
 #   py=SCRIPT[,ARGS]   python3 SCRIPT ARGS (a measurement script under scripts/)
+#   bin=PATH           a diagnostic binary built in-tree (lego-slam_amd/lib/ubench_*)
+#   env=VAR=VALUE      export VAR for the steps after it (their outputs get a _VAR_VALUE suffix); unenv=VAR
 set -u
 TAG=${TAG:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 QUICK="bench.py --steps 200 --warmup 3 --no-cpu --no-extras"
+SFX=""
 
 kstats() {   # label, rocprof output dir -> one summary line per kernel of interest
     for f in $(find "$2" -name '*kernel_stats.csv'); do
@@ -50,8 +53,8 @@ for step in "$@"; do
         timeout -k 10 600 python3 bench.py $arg > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
         tail -c 600 "$OUT/bench.json" ;;
     quick)
-        timeout -k 10 300 python3 $QUICK > "$OUT/quick.json" 2> "$OUT/quick.err" || { tail -20 "$OUT/quick.err"; exit 1; }
-        cat "$OUT/quick.json" ;;
+        timeout -k 10 300 python3 $QUICK > "$OUT/quick$SFX.json" 2> "$OUT/quick$SFX.err" || { tail -20 "$OUT/quick$SFX.err"; exit 1; }
+        cat "$OUT/quick$SFX.json" ;;
     trace)
         rm -rf "$OUT/trace"
         timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $QUICK \
@@ -70,8 +73,8 @@ for step in "$@"; do
         pass write WRITE_SIZE || exit 1 ;;
     stamps)
         LH_LIB=lego-slam_amd/lib/liblego_ba_stamps.so timeout -k 10 200 python3 scripts/ctrl_stamps.py ${arg:-C3} \
-            > "$OUT/stamps_${arg:-C3}.log" 2>&1 || { cat "$OUT/stamps_${arg:-C3}.log"; exit 1; }
-        cat "$OUT/stamps_${arg:-C3}.log" ;;
+            > "$OUT/stamps_${arg:-C3}$SFX.log" 2>&1 || { cat "$OUT/stamps_${arg:-C3}$SFX.log"; exit 1; }
+        cat "$OUT/stamps_${arg:-C3}$SFX.log" ;;
     linstamps)
         LH_LIB=lego-slam_amd/lib/liblego_ba_stamps.so timeout -k 10 200 python3 scripts/stamps.py ${arg:-C3} \
             > "$OUT/linstamps_${arg:-C3}.log" 2>&1 || { cat "$OUT/linstamps_${arg:-C3}.log"; exit 1; }
@@ -95,6 +98,15 @@ for step in "$@"; do
         [ "$scr" != "$arg" ] && rest=${arg#*,}
         timeout -k 10 600 python3 $scr ${rest//,/ } > "$OUT/$(basename $scr .py).log" 2>&1 || { tail -30 "$OUT/$(basename $scr .py).log"; exit 1; }
         tail -30 "$OUT/$(basename $scr .py).log" ;;
+    env)
+        export "$arg"
+        SFX="_${arg//[^A-Za-z0-9]/_}" ;;
+    unenv)
+        unset "$arg"
+        SFX="" ;;
+    bin)
+        timeout -k 10 120 "$arg" > "$OUT/$(basename $arg).log" 2>&1 || { tail -30 "$OUT/$(basename $arg).log"; exit 1; }
+        cat "$OUT/$(basename $arg).log" ;;
     *)
         echo "unknown step $step"; exit 2 ;;
     esac

@@ -675,3 +675,21 @@ def test_five_cameras_are_unsupported():
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.Solver().solve(w)
     assert e.value.status == lego_ba.LH_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("cfg,seed,family", [("C3", 0, "stable_noout"), ("C3", 1, "stable_noout")])
+def test_two_chain_schedule_matches_the_one_chain_solve(monkeypatch, cfg, seed, family):
+    """k_ctrl's two-chain LDL^T (opt-in LH_ND=1, lh_ctrl_nd_plan) on windows that split (C3: A = 4, S = 8,
+    B = 8 poses): a different elimination order, so the same LM path and the final chi2 to rounding."""
+    w = window(cfg, seed=seed, family=family)
+    s0 = lego_ba.Solver()
+    a = s0.solve(w)
+    s0.close()
+    monkeypatch.setenv("LH_ND", "1")
+    s1 = lego_ba.Solver()
+    b = s1.solve(w)
+    assert s1.controller() == "k_ctrl"
+    s1.close()
+    assert (b["iterations"], b["trials"]) == (a["iterations"], a["trials"])
+    assert rel(b["chi2_final"], a["chi2_final"]) <= 1e-9
+    assert np.allclose(b["pose_Tcw"], a["pose_Tcw"], atol=1e-7)
