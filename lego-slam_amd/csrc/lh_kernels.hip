@@ -1548,16 +1548,14 @@ struct BandSys {
 // For a row a below the block, l = a N is its forward substitution through the block and
 // l Delta its partially eliminated entries, so the trailing update of rows i, j is
 // L_i Delta L_j^T = T_i a_j^T with T_i = L_i ND^T.
+// v: row r = lane & 7 of the block (entries past the diagonal unused)
 template <class S>
-__device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ No, double* __restrict__ NDo, int k0,
-                                              int lane) {
+__device__ __forceinline__ void factor_block8_v(const S& A, const double (&v)[8], double* __restrict__ No,
+                                                double* __restrict__ NDo, int k0, int lane) {
     const int p = lane & 15, r = p & 7;
     const bool ident = p >= 8;
     double R[8], dl[8];
-    double v[8];
     const int kw = A.wrap(k0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = A.atw(kw + r, kw + q);   // upper entries: garbage confined to this lane's upper part
 #pragma unroll
     for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
     factor_column<0>(R, dl);
@@ -1581,6 +1579,15 @@ __device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ N
             d2[q] = double2{R[2 * q] * dl[2 * q], R[2 * q + 1] * dl[2 * q + 1]};
         }
     }
+}
+template <class S>
+__device__ __forceinline__ void factor_block8(const S& A, double* __restrict__ No, double* __restrict__ NDo, int k0,
+                                              int lane) {
+    const int r = lane & 7, kw = A.wrap(k0);
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = A.atw(kw + r, kw + q);   // upper entries: garbage confined to this lane's upper part
+    factor_block8_v(A, v, No, NDo, k0, lane);
 }
 
 // Step k0 of the elimination for the 16-row tile row at rb (one wave): with the raw block column
@@ -1886,6 +1893,29 @@ __device__ __forceinline__ void ldlt_backsub(const double* __restrict__ A, const
     backsub_block<0>(A, ndb, nb, lane, y0, y1);
 }
 
+// The controller's step tail taken by the back-substitution wave from its registers (k_ctrl, LDL^T): the
+// pose part of the gain denominator (isGoodStepInLM's scale, problem.cpp:528-533) summed over the wave
+// (rows lane and lane + 64 of one lane first), the step stored for k_lin.  ctrl null: no tail (the probe).
+struct LdltTail {
+    lh_ctrl* ctrl;
+    double* dxp;
+    const double* bpv;
+    const double* hdv;
+    double lambda;
+    int strategy;
+};
+__device__ __forceinline__ void ldlt_tail(const LdltTail& tl, int n, int lane, double y0, double y1) {
+    auto term = [&](int r, double d) {
+        if (r >= n) return 0.0;
+        if (tl.dxp) tl.dxp[r] = d;
+        const double b = tl.bpv[r];
+        return (tl.strategy == 0) ? d * (tl.lambda * d + b) : d * (tl.lambda * tl.hdv[r] * d + b);
+    };
+    double sp[1] = {term(lane, y0) + term(lane + 64, y1)};
+    group_sum(sp, 6);
+    if (lane == 0) tl.ctrl->spose = sp[0];
+}
+
 // Phases 3-4 of k_ctrl on a padded system already in LDS (A lower + rhs row NP, zeros in the upper
 // triangle): blocked LDL^T with the forward substitution, then the back substitution; xsol[perm[r]] =
 // the solution's entry r < n (perm == nullptr: xsol[r]).  units: the per-step work units in LDS
@@ -1900,7 +1930,8 @@ __device__ __forceinline__ void ldlt_backsub(const double* __restrict__ A, const
 //   wave 12 first: z_t = b_t N_t (Eigen's solve tolerance applied).
 // L lives in the upper triangle, so the raw block columns stay readable for the whole step.
 __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* __restrict__ xsol, int n, int NE, int tid,
-                                               const int* __restrict__ perm, const uint16_t* __restrict__ units) {
+                                               const int* __restrict__ perm, const uint16_t* __restrict__ units,
+                                               const LdltTail& tl = LdltTail{}, bool factored0 = false) {
     const int lane = tid & 63, wave = tid >> 6;
     LdltBlockLds& F = ldlt_lds();
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
@@ -1909,8 +1940,10 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
 #ifdef LH_PRIO
     if (wv == 0) __builtin_amdgcn_s_setprio(3);   // A/B variant: wave 0's chain first in issue arbitration
 #endif
-    if (wv == 0) factor_block8(SY, F.N[0], F.ND[0], 0, lane);
-    lds_barrier();
+    if (!factored0) {   // (k_ctrl factors block 0 during its scatter)
+        if (wv == 0) factor_block8(SY, F.N[0], F.ND[0], 0, lane);
+        lds_barrier();
+    }
     CSTAMP(5);
 #ifdef LH_STAMPS
     // per-step split (diagnostic): wave 0's diagonal tile, its factor and its wait at the barrier;
@@ -1988,6 +2021,7 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
             if (lane < NE) xsol[lane] = y0;
             if (lane + 64 < NE) xsol[lane + 64] = y1;
         }
+        if (tl.ctrl) ldlt_tail(tl, n, lane, y0, y1);
     }
     lds_barrier();
     CSTAMP(7);
@@ -2261,6 +2295,25 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     uint32_t unit2 = 0;   // two unit words per thread (SOLVER 0)
     if (SOLVER == 0 && tid < 8 * LH_NSTEP) unit2 = reinterpret_cast<const uint32_t*>(units)[tid];
+    // The one-chain LDL^T's first block (rows 0-7: pose 0 and two rows of pose 1) is factored by wave 0
+    // while the other waves scatter: its row r = lane & 7 comes straight from the packed pair blocks
+    // (pairs (0, 0), (0, 1), (1, 1) at indices 0, 1, P: every pair is listed for P <= LH_PMAX), staged
+    // and committed, selected once the decision is known; the scatter leaves block 0 alone.
+    const bool early0 = SOLVER == 0 && !(prm.nd_steps > 0) && n >= 8;
+    double b0s[8], b0c[8];
+    if (early0 && wave == 0) {
+        const int r = lane & 7;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            int i;
+            if (r < 6 && q < 6) i = 6 * r + q;                           // pair (0, 0)
+            else if (r >= 6 && q < 6) i = 36 + 6 * q + (r - 6);           // pair (0, 1): S(6 + eb, ea)
+            else if (r < 6) i = 36 + 6 * r + (q - 6);                    // (upper, unused)
+            else i = 36 * P + 6 * (r - 6) + (q - 6);                     // pair (1, 1)
+            b0s[q] = rs_stage[i];
+            b0c[q] = rs_commit[i];
+        }
+    }
 
     if (!decided) {
         if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
@@ -2327,7 +2380,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             }
             const int gi = 6 * pp + ea, gj = 6 * qq + eb;
             const int hi = max(gi, gj), lo = min(gi, gj);
-            if (gi == gj) {
+            if (early0 && hi < 8) {
+                // block 0: wave 0's
+            } else if (gi == gj) {
                 A[gi * AS + gi] = (prm.strategy == 0) ? v + lambda : v + lambda * v;
             } else if (pp != qq || gi > gj) {
                 A[hi * AS + lo] = v;
@@ -2355,6 +2410,18 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
     }
     if (SOLVER == 0 && tid < 8 * LH_NSTEP) reinterpret_cast<uint32_t*>(s_units)[tid] = unit2;
+    if (early0 && wave == 0) {
+        const int r = lane & 7;
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            double x = accept ? b0s[q] : b0c[q];
+            if (q == r) x = (prm.strategy == 0) ? x + lambda : x + lambda * x;
+            v[q] = x;
+        }
+        LdltBlockLds& F = ldlt_lds();
+        factor_block8_v(LdsSys{A}, v, F.N[0], F.ND[0], 0, lane);
+    }
     lds_barrier();
     CSTAMP(4);
 
@@ -2364,11 +2431,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         if (tid == 0) ctrl->pcg_iters += its;
     } else {
         if (nd) lds_ldlt_solve_nd(A, xs, n, tid, s_units, prm);
-        else lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units);
+        else lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units, LdltTail{ctrl, dxp, bpv, hdv, lambda, prm.strategy}, early0);
     }
     CSTAMP(8);
 
-    ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, dxp);
+    // the one-chain LDL^T took the tail in its back-substitution wave
+    if (SOLVER == 1 || nd) ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, dxp);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -2975,6 +3043,14 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 const int Iw = t / 2 + 7;
                 if (Iw >= 8 && Iw < NT) {
                     const int r = 16 * Iw + lrow;
+#ifdef LH_STAMPS
+                    // (diagnostic) loader wave 12: the wait for its value loads, then the window writes
+                    unsigned long long lt0_ = __builtin_amdgcn_s_memtime();
+                    __builtin_amdgcn_s_waitcnt(0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    unsigned long long lt1_ = __builtin_amdgcn_s_memtime();
+                    if (wv == BLOAD && lane == 0) atomicAdd(&lh_stamps[56], lt1_ - lt0_);
+#endif
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int c = 16 * (Iw - 7) + lcol + k;
@@ -2982,6 +3058,14 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                         if (r == c) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
                         SY.at(r, c) = (c <= r) ? v : 0.0;
                     }
+#ifdef LH_STAMPS
+                    __builtin_amdgcn_s_waitcnt(0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (wv == BLOAD && lane == 0) {
+                        atomicAdd(&lh_stamps[57], __builtin_amdgcn_s_memtime() - lt1_);
+                        atomicAdd(&lh_stamps[58], 1ull);
+                    }
+#endif
                 }
                 const int Ia = t / 2 + 8;
                 if (Ia < NT) {
@@ -3067,10 +3151,13 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         // every block in [j0, j1] published (one round trip for the batch; producers run far ahead)
         auto wait_ready = [&](int j0, int j1) {
             for (;;) {
-                bool all = true;
+                int miss = 0;   // every flag read in one round trip (no short circuit)
                 for (int j = j0; j <= j1; ++j)
-                    all = all && __hip_atomic_load(&bring_ready[j % BRING], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == j + 1;
-                if (all) return;
+                    miss |= __hip_atomic_load(&bring_ready[j % BRING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != j + 1;
+                if (!miss) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // orders the slot reads after
+                    return;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
         };
@@ -3094,7 +3181,15 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             y1 = (r1 >= 0) ? z[r1] : 0.0;
         }
         // block j with its L entries ca / cb: x_b = ND_b y_b, then the held rows' updates
+#ifdef LH_STAMPS
+        unsigned long long bs_[3] = {0, 0, 0}, ba_ = 0, bb_ = 0;
+#define BSUB_STAMP(i) do { __builtin_amdgcn_sched_barrier(0); bb_ = __builtin_amdgcn_s_memtime(); \
+        if ((i) >= 0) bs_[i] += bb_ - ba_; ba_ = bb_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define BSUB_STAMP(i)
+#endif
         auto solve_blk = [&](int j, const double (&ca)[8], const double (&cb)[8]) {
+            BSUB_STAMP(-1);
             const int KB = nb - 8 - 8 * j;
             double cn[8];
 #pragma unroll
@@ -3114,6 +3209,11 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             }
             const double xv = ((cn[0] * yb[0] + cn[1] * yb[1]) + (cn[2] * yb[2] + cn[3] * yb[3])) +
                               ((cn[4] * yb[4] + cn[5] * yb[5]) + (cn[6] * yb[6] + cn[7] * yb[7]));
+#ifdef LH_STAMPS
+            double xvs = xv;
+            asm volatile("" : "+v"(xvs));
+#endif
+            BSUB_STAMP(0);
             double xb[8];
 #pragma unroll
             for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, kl + v);
@@ -3129,6 +3229,10 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 const double zi = re >= 0 ? zin : 0.0;
                 if (sb_) y1 = zi; else y0 = zi;
             }
+#ifdef LH_STAMPS
+            asm volatile("" : "+v"(y0), "+v"(y1));
+#endif
+            BSUB_STAMP(1);
         };
         // two register sets in turn (no copies between blocks); every 4 blocks one batched readiness check
         // for the next 4 and one release of the slots read so far (the release waits for this wave's
@@ -3137,7 +3241,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         wait_ready(0, min(3, nblk - 1));
         load_blk(0, la, lb);
         for (int j = 0; j < nblk; j += 2) {
+            BSUB_STAMP(-1);
             if ((j & 3) == 0 && j + 4 < nblk) wait_ready(j + 4, min(j + 7, nblk - 1));
+            BSUB_STAMP(2);
             load_blk(min(j + 1, nblk - 1), ma, mb);
             solve_blk(j, la, lb);
             if (j + 1 >= nblk) break;
@@ -3146,6 +3252,15 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             if ((j & 3) == 2 && lane == 0)
                 __hip_atomic_store(&bring_used, j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+#ifdef LH_STAMPS
+        if (lane == 0) {
+            atomicAdd(&lh_stamps[52], bs_[0]);
+            atomicAdd(&lh_stamps[53], bs_[1]);
+            atomicAdd(&lh_stamps[54], bs_[2]);
+            atomicAdd(&lh_stamps[55], (unsigned long long)nblk);
+        }
+#endif
+#undef BSUB_STAMP
     }
     __syncthreads();
     CSTAMP(8);

@@ -64,3 +64,12 @@ if len(st) >= 128 and st[51]:
         a, b, c, m = st[64 + t] / nl, st[80 + t] / nl, st[96 + t] / nl, st[112 + t]
         if a or b or c or m:
             print(f"  {t:4d} {a:8.0f} {b:10.0f} {c:8.0f} {m:11d}")
+# k_ctrl_b's back substitution (stamps 52-55): per block, wave 0's x_b = ND_b y_b (ND read, broadcasts, dot)
+# and its row updates (readlanes, dots, the entering row), and its ring readiness checks
+if st[55]:
+    nb_ = st[55]
+    print(f"  back substitution per block: x_b {st[52] / nb_:.0f}, row updates {st[53] / nb_:.0f}, "
+          f"ring checks {st[54] / nb_:.0f} cycles ({nb_ // max(n, 1)} blocks per launch)")
+# k_ctrl_b's loader wave 12 at the tile-row writes (stamps 56-58): the wait for its value loads, the writes
+if st[58]:
+    print(f"  loader per tile row: value-load wait {st[56] / st[58]:.0f}, window writes {st[57] / st[58]:.0f} cycles")
