@@ -1457,7 +1457,10 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
 // ============================================================================
 #define CT 1024
 #define NP LH_NPAD            // padded system size; row NP of A holds the right-hand side
-#define AS (LH_NPAD + 1)      // LDS row stride (odd: row-per-lane access is conflict-free)
+#define AS (LH_NPAD + 2)      // LDS row stride, = 2 mod 32 doubles: a 16x4 tile fragment (lane (i, k) at row i,
+                              // column k) hits 32 distinct 8-byte bank pairs per half-wave (ds_read_b64 banks
+                              // (a/4) mod 64 over lanes 0-31 / 32-63); the odd stride 129 put rows i and i + 1 at
+                              // columns k + 1 and k on one pair (two-way conflicts on every tile read)
 #define RS_MAX (LH_PMAX * (LH_PMAX + 1) / 2 * 36 + 18 * LH_PMAX + 8)
 #define ER 1008               // reduced-system elements per prefetch round: 28 whole 6x6 S blocks
 #define NLD ((RS_MAX + ER - 1) / ER)
@@ -1619,7 +1622,7 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
         b0 = A.atw(cbw + li, kw + lk);
         b1 = A.atw(cbw + li, kw + 4 + lk);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + lk + 4 * q, cbw + li);
+        for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + li, cbw + lk + 4 * q);
     }
     __builtin_amdgcn_sched_barrier(0);   // every load above is in flight before the first wait
     v4d l = {0.0, 0.0, 0.0, 0.0};
@@ -1662,16 +1665,19 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
             nb0 = A.atw(ncw + li, kw + lk);
             nb1 = A.atw(ncw + li, kw + 4 + lk);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) nold[q] = A.atw(rbw + lk + 4 * q, ncw + li);
+            for (int q = 0; q < 4; ++q) nold[q] = A.atw(rbw + li, ncw + lk + 4 * q);
         }
+        // the update transposed, (a_J T_I^T)^T: lane (li, lk) gets row li, columns lk + 4q of the tile, the
+        // same fragment shape as the operand reads (conflict-free at this stride); the products are the
+        // same, so are the bits
         v4d acc = {0.0, 0.0, 0.0, 0.0};
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], b0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[1], b1, acc, 0, 0, 0);
-        const int col = cb + li;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b0, t[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b1, t[1], acc, 0, 0, 0);
+        const int row = rb + li;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int row = rb + lk + 4 * q;
-            if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + lk + 4 * q, cbw_cur + li) = old[q] - acc[q];
+            const int col = cb + lk + 4 * q;
+            if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + li, cbw_cur + lk + 4 * q) = old[q] - acc[q];
         }
         cb = nc;
         b0 = nb0; b1 = nb1;
@@ -1696,7 +1702,7 @@ __device__ __forceinline__ void diag_tile(const S& A, const double* __restrict__
     const double a0 = A.atw(rbw + li, kw + lk), a1 = A.atw(rbw + li, kw + 4 + lk);
     double old[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + lk + 4 * q, rbw + li);
+    for (int q = 0; q < 4; ++q) old[q] = A.atw(rbw + li, rbw + lk + 4 * q);
     __builtin_amdgcn_sched_barrier(0);   // the scheduler otherwise sinks the loads between the MFMAs
     v4d l = {0.0, 0.0, 0.0, 0.0};
     l = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? n0 : 0.0, a0, l, 0, 0, 0);
@@ -1704,14 +1710,14 @@ __device__ __forceinline__ void diag_tile(const S& A, const double* __restrict__
     v4d t = {0.0, 0.0, 0.0, 0.0};
     t = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? d0 : 0.0, l[0], t, 0, 0, 0);
     t = __builtin_amdgcn_mfma_f64_16x16x4f64(lo ? d1 : 0.0, l[1], t, 0, 0, 0);
-    v4d acc = {0.0, 0.0, 0.0, 0.0};
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[0], a0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t[1], a1, acc, 0, 0, 0);
-    const int col = rb + li;
+    v4d acc = {0.0, 0.0, 0.0, 0.0};   // transposed, as in ldlt_tile_row
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, t[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, t[1], acc, 0, 0, 0);
+    const int row = rb + li;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int row = rb + lk + 4 * q;
-        if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + lk + 4 * q, rbw + li) = old[q] - acc[q];
+        const int col = rb + lk + 4 * q;
+        if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + li, rbw + lk + 4 * q) = old[q] - acc[q];
     }
 }
 
@@ -1776,7 +1782,7 @@ __device__ __forceinline__ void nd_tile_row(double* __restrict__ A, const NdSrc 
     for (int cb = jb0; cb < jb1; cb += 16) {
         double old[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) old[w] = A[(rb + lk + 4 * w) * AS + cb + li];
+        for (int w = 0; w < 4; ++w) old[w] = A[(rb + li) * AS + cb + lk + 4 * w];
         v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -1784,13 +1790,13 @@ __device__ __forceinline__ void nd_tile_row(double* __restrict__ A, const NdSrc 
             const int k0 = src[q].k0, m0 = k0 + 8;
             const bool cin = cb + li >= m0;
             const double b0 = cin ? A[(cb + li) * AS + k0 + lk] : 0.0, b1 = cin ? A[(cb + li) * AS + k0 + 4 + lk] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t0[q], b0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(t1[q], b1, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b0, t0[q], acc, 0, 0, 0);   // transposed
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b1, t1[q], acc, 0, 0, 0);
         }
-        const int col = cb + li;
+        const int row = rb + li;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            const int row = rb + lk + 4 * w;
+            const int col = cb + lk + 4 * w;
             if (row >= mm && col >= mm && col <= row) A[row * AS + col] = old[w] - acc[w];
         }
     }
@@ -1985,6 +1991,9 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 LDLT_SSTAMP(1);
             } else if (uw & LH_UNIT_VALID) {
                 const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
+#ifdef LH_UNIT_DELAY
+                __builtin_amdgcn_s_sleep(LH_UNIT_DELAY);   // A/B variant: wave 0's tile reads reach the LDS first
+#endif
                 ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
             if (wv != 0) LDLT_SSTAMP(3);
@@ -2965,15 +2974,18 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         z[i] = 0.0;
     }
     {
-        constexpr int PER = 128 * 128 / CT;   // 16 elements of the first window per thread
-        const int r0 = tid >> 3, cseg = (tid & 7) * 16;
+        // 16 elements of the first window per thread: element k at row 8 k + tid / 128, column tid mod 128, so a
+        // wave's writes go to consecutive columns (one row of 16-column stripes per thread put 8 lanes of a
+        // 16-lane write group on one bank pair)
+        constexpr int PER = 128 * 128 / CT;
+        const int c0 = tid & 127, rr = tid >> 7;
         int bk[PER];
 #pragma unroll
-        for (int k = 0; k < PER; ++k) bk[k] = band_block(bblk, r0, cseg + k, n);
+        for (int k = 0; k < PER; ++k) bk[k] = band_block(bblk, 8 * k + rr, c0, n);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int c = cseg + k;
-            A[r0 * AS + c] = (r0 < NE && c <= r0) ? band_value(src, bk[k], r0, c, lambda, prm.strategy, n) : 0.0;
+            const int r = 8 * k + rr;
+            A[r * AS + c0] = (r < NE && c0 <= r) ? band_value(src, bk[k], r, c0, lambda, prm.strategy, n) : 0.0;
         }
     }
     uint32_t uwa = 0, uwb = 0;   // this wave's unit words: steps 2j, 2j + 1 in u32 j (lane j, lane j + 64)
@@ -2987,9 +2999,12 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         const uint32_t w = (j < 64) ? __builtin_amdgcn_readlane(uwa, j & 63) : __builtin_amdgcn_readlane(uwb, j & 63);
         return (t & 1) ? (w >> 16) : (w & 0xffffu);
     };
-    // loader state (waves 12-15): lane q of 256 owns row 16 I + (q >> 4), columns 16 (I - 7) + 8 (q & 15) + k
-    const int lq = tid - 64 * BLOAD, lrow = lq >> 4, lcol = (lq & 15) * 8;
+    // loader lane lq of 256 owns the elements k = 0..7 at row 16 I + 2 k + lq / 128, column 16 (I - 7) + lq mod 128
+    // (consecutive lanes, consecutive columns: conflict-free window writes)
+    const int lq = tid - 64 * BLOAD, lrow = lq >> 7, lcol = lq & 127;
     int lbk[8];
+    uint32_t lok = 0;   // bit k: element k is a stored entry (kept apart from lbk: overwriting a register with a
+                        // load in flight waits for the load, which put the block-index latency on the step)
     double lval[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { lbk[k] = -1; lval[k] = 0.0; }
@@ -3042,7 +3057,6 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             if ((t & 1) == 0) {
                 const int Iw = t / 2 + 7;
                 if (Iw >= 8 && Iw < NT) {
-                    const int r = 16 * Iw + lrow;
 #ifdef LH_STAMPS
                     // (diagnostic) loader wave 12: the wait for its value loads, then the window writes
                     unsigned long long lt0_ = __builtin_amdgcn_s_memtime();
@@ -3053,8 +3067,8 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #endif
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const int c = 16 * (Iw - 7) + lcol + k;
-                        double v = (lbk[k] >= 0) ? lval[k] : 0.0;
+                        const int r = 16 * Iw + 2 * k + lrow, c = 16 * (Iw - 7) + lcol;
+                        double v = ((lok >> k) & 1) ? lval[k] : 0.0;
                         if (r == c) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
                         SY.at(r, c) = (c <= r) ? v : 0.0;
                     }
@@ -3069,22 +3083,24 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 }
                 const int Ia = t / 2 + 8;
                 if (Ia < NT) {
-                    const int r = 16 * Ia + lrow, pr = r / 6;
+                    const int c = 16 * (Ia - 7) + lcol, pc = c / 6;
+                    lok = 0;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const int c = 16 * (Ia - 7) + lcol + k, pc = c / 6, d = pr - pc;
+                        const int r = 16 * Ia + 2 * k + lrow, pr = r / 6, d = pr - pc;
                         lbk[k] = bblk[min(max(pc, 0), P - 1) * 64 + min(max(d, 0), 63)];
-                        if (!(c <= r && r < n && d < 64)) lbk[k] = -1;
+                        lok |= (c <= r && r < n && d < 64) ? (1u << k) : 0u;
                     }
                 }
             } else {
                 const int Ib = (t - 1) / 2 + 8;
                 if (Ib < NT) {
-                    const int r = 16 * Ib + lrow;
+                    const int c = 16 * (Ib - 7) + lcol;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const int c = 16 * (Ib - 7) + lcol + k;
+                        const int r = 16 * Ib + 2 * k + lrow;
                         lval[k] = src[(size_t)max(lbk[k], 0) * 36 + (c % 6) * 6 + (r % 6)];
+                        if (lbk[k] < 0) lok &= ~(1u << k);   // a pair no chunk couples
                     }
                 }
             }
@@ -3163,15 +3179,17 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         };
         // block j's L entries of this lane's two rows from its slot (clamped: the own block's rows and rows
         // past the band read in-bounds values never used)
+        // (a held row is >= KB - 120 >= KB + v - LH_LBW, inside every stored L row: one clamp, and the 8 reads
+        // of a row share one address, v (LH_LBW - 1) doubles apart as immediate offsets)
         auto load_blk = [&](int j, double (&l0)[8], double (&l1)[8]) {
             const int KB = nb - 8 - 8 * j;
-            const double* sl = A + (j % BRING) * BSLOT;
-            const int r0 = row_of(KB, 0), r1 = row_of(KB, 1);
+            const double* sl = A + (j % BRING) * BSLOT + LH_LBW - KB;   // + v (LH_LBW - 1) + r: L[KB+v][r]
+            const double* p0 = sl + min(row_of(KB, 0), KB - 1);
+            const double* p1 = sl + min(row_of(KB, 1), KB - 1);
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
-                const double* Lr = sl + v * LH_LBW + LH_LBW - KB - v;   // + r: L[KB+v][r]
-                l0[v] = Lr[max(min(r0, KB - 1), KB + v - LH_LBW)];
-                l1[v] = Lr[max(min(r1, KB - 1), KB + v - LH_LBW)];
+                l0[v] = p0[v * (LH_LBW - 1)];
+                l1[v] = p1[v * (LH_LBW - 1)];
             }
         };
         double y0, y1;
@@ -3188,12 +3206,16 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #else
 #define BSUB_STAMP(i)
 #endif
+        // block j's ND row (lane & 7) from its slot
+        auto load_nd = [&](int j, double (&cn)[8]) {
+            const double* p = A + (j % BRING) * BSLOT + 8 * LH_LBW + (lane & 7) * 8;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) cn[v] = p[v];
+        };
+        double cn[8];   // block j's ND row on entry; block j + 1's, loaded once x_b is formed, on exit
         auto solve_blk = [&](int j, const double (&ca)[8], const double (&cb)[8]) {
             BSUB_STAMP(-1);
             const int KB = nb - 8 - 8 * j;
-            double cn[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) cn[v] = A[(j % BRING) * BSLOT + 8 * LH_LBW + (lane & 7) * 8 + v];
             const int sb_ = (KB >> 6) & 1, kl = KB & 63;
             const bool mine = lane >= kl && lane < kl + 8;
             const int re = KB - 128 + (lane - kl);                       // the row entering this lane's slot
@@ -3209,6 +3231,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             }
             const double xv = ((cn[0] * yb[0] + cn[1] * yb[1]) + (cn[2] * yb[2] + cn[3] * yb[3])) +
                               ((cn[4] * yb[4] + cn[5] * yb[5]) + (cn[6] * yb[6] + cn[7] * yb[7]));
+            load_nd(min(j + 1, nblk - 1), cn);   // published: j + 1 < j + 4, checked an iteration before
 #ifdef LH_STAMPS
             double xvs = xv;
             asm volatile("" : "+v"(xvs));
@@ -3240,12 +3263,23 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         double la[8], lb[8], ma[8], mb[8];
         wait_ready(0, min(3, nblk - 1));
         load_blk(0, la, lb);
+        load_nd(0, cn);
         for (int j = 0; j < nblk; j += 2) {
-            BSUB_STAMP(-1);
-            if ((j & 3) == 0 && j + 4 < nblk) wait_ready(j + 4, min(j + 7, nblk - 1));
-            BSUB_STAMP(2);
+            // the flags of blocks j + 4 .. j + 7 (first loaded at iteration j + 2) are read now and checked
+            // after block j, so the read's round trip overlaps the block instead of preceding it
+            const bool chk = (j & 3) == 0 && j + 4 < nblk;
+            int miss = 0;
+            if (chk)
+                for (int q = j + 4; q <= min(j + 7, nblk - 1); ++q)
+                    miss |= __hip_atomic_load(&bring_ready[q % BRING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != q + 1;
             load_blk(min(j + 1, nblk - 1), ma, mb);
             solve_blk(j, la, lb);
+            BSUB_STAMP(-1);
+            if (chk) {
+                if (miss) wait_ready(j + 4, min(j + 7, nblk - 1));
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+            BSUB_STAMP(2);
             if (j + 1 >= nblk) break;
             load_blk(min(j + 2, nblk - 1), la, lb);
             solve_blk(j + 1, ma, mb);
