@@ -26,7 +26,8 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // summed over all waves into lh_stamps[] (cdna_hip_programming.md §7 "In-kernel
 // stamps").  The product build compiles these to nothing.
 #ifdef LH_STAMPS
-__device__ unsigned long long lh_stamps[128];   // [64, 128): k_ctrl's LDL^T steps, per step (lds_ldlt_solve)
+__device__ unsigned long long lh_stamps[256];   // [64, 128): k_ctrl's LDL^T steps, per step (lds_ldlt_solve);
+                                                // [128, 160): k_ctrl_b's barrier arrival per wave, even / odd steps
 #define STAMP_DECL unsigned long long st0_ = __builtin_amdgcn_s_memtime(), st1_, sacc_[24] = {0};
 #define STAMP(i)                                                                   \
     do {                                                                           \
@@ -1943,9 +1944,6 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const LdsSys SY{A};
-#ifdef LH_PRIO
-    if (wv == 0) __builtin_amdgcn_s_setprio(3);   // A/B variant: wave 0's chain first in issue arbitration
-#endif
     if (!factored0) {   // (k_ctrl factors block 0 during its scatter)
         if (wv == 0) factor_block8(SY, F.N[0], F.ND[0], 0, lane);
         lds_barrier();
@@ -1991,9 +1989,6 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
                 LDLT_SSTAMP(1);
             } else if (uw & LH_UNIT_VALID) {
                 const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
-#ifdef LH_UNIT_DELAY
-                __builtin_amdgcn_s_sleep(LH_UNIT_DELAY);   // A/B variant: wave 0's tile reads reach the LDS first
-#endif
                 ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
             if (wv != 0) LDLT_SSTAMP(3);
@@ -2015,9 +2010,6 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     }
 #endif
     CSTAMP(6);
-#ifdef LH_PRIO
-    if (wv == 0) __builtin_amdgcn_s_setprio(0);
-#endif
 
     // ---------------- 4. back substitution x = L^-T z, blocks descending, one wave ----------------
     if (wv == 0) {
@@ -2870,7 +2862,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 // of keyframes, so row r's nonzeros start at its envelope fc(r) >= r - 104 (the host checks this per
 // window, lh_host.cpp; other windows go to k_ctrl_g or PCG).  The blocked LDL^T of k_ctrl then needs
 // only 8 tile rows (128 rows) of S at a time: the window holds them in one CU's LDS as a circular
-// buffer (BandSys), and waves 12-15 stream the next tile row in (its block-index loads two steps
+// buffer (BandSys), and waves 11, 13-15 stream the next tile row in (its block-index loads two steps
 // ahead, its values one step ahead, written into the slots of the tile row that just retired).  L goes
 // to global memory row by row, ND per block; the back substitution (one wave) reads them back.  The
 // per-step work units come from the same envelope (lh_ctrl_units over 11 unit waves).  One 1024-thread
@@ -2879,7 +2871,11 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 // ============================================================================
 #define BNMAX (6 * LH_PMAX_ANY)         // largest reduced system (1536 rows)
 #define BSTEP_MAX (BNMAX / 8)           // LDL^T steps
-#define BLOAD 12                        // first loader wave
+// the stream loaders: waves 11, 13, 14, 15 (none on wave 0's SIMD, where a loader's per-step work competed
+// with the factor for issue); wave 13 also forms z and copies ND out
+__device__ __forceinline__ bool band_loader(int w) { return w == 11 || w >= 13; }
+__device__ __forceinline__ int band_loader_slot(int w) { return w == 11 ? 0 : w - 12; }
+#define BZW 13
 
 // S(r, c), c <= r < n, of the packed system: block (pose(c), pose(r)) through the per-window table
 // bblk[p * 64 + d] (the block of pose pair (p, p + d), -1 where no chunk couples them)
@@ -3001,7 +2997,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     };
     // loader lane lq of 256 owns the elements k = 0..7 at row 16 I + 2 k + lq / 128, column 16 (I - 7) + lq mod 128
     // (consecutive lanes, consecutive columns: conflict-free window writes)
-    const int lq = tid - 64 * BLOAD, lrow = lq >> 7, lcol = lq & 127;
+    const int lq = 64 * band_loader_slot(wv) + lane, lrow = lq >> 7, lcol = lq & 127;
     int lbk[8];
     uint32_t lok = 0;   // bit k: element k is a stored entry (kept apart from lbk: overwriting a register with a
                         // load in flight waits for the load, which put the block-index latency on the step)
@@ -3016,13 +3012,13 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     lds_barrier();
     CSTAMP(5);
 #ifdef LH_STAMPS
-    unsigned long long ss_[5] = {0, 0, 0, 0, 0}, sa_ = __builtin_amdgcn_s_memtime(), sb_;
+    unsigned long long ss_[5] = {0, 0, 0, 0, 0}, sa_ = __builtin_amdgcn_s_memtime(), sb_, bst_ = sa_;
 #endif
     for (int t = 0; t < nstep; ++t) {
         const int k0 = 8 * t, par = t & 1, m0 = k0 + 8;
         const double* N = Nl[par];
         const double* ND = NDl[par];
-        if (wv == BLOAD) {
+        if (wv == BZW) {
             if (lane < 8) {   // z_t = b_t N_t, zeroed where |D| <= DBL_MIN (LDLT::_solve_impl)
                 double zz = 0.0;
 #pragma unroll
@@ -3043,13 +3039,13 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 LDLT_SSTAMP(0);
                 factor_block8(SY, Nl[par ^ 1], NDl[par ^ 1], m0, lane);
                 LDLT_SSTAMP(1);
-            } else if (wv < BLOAD && (uw & LH_UNIT_VALID)) {
+            } else if (!band_loader(wv) && (uw & LH_UNIT_VALID)) {
                 const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
                 ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
             if (wv != 0) LDLT_SSTAMP(3);
         }
-        if (wv >= BLOAD) {
+        if (band_loader(wv)) {
             // tile row I enters the window at step 2 I - 14, into the slots of tile row I - 8 (retired
             // after step 2 I - 15); its block indices are loaded at step 2 I - 16, its values at 2 I - 15
             // Every load is unconditional (clamped index): a conditional load becomes a branch whose join
@@ -3058,12 +3054,12 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 const int Iw = t / 2 + 7;
                 if (Iw >= 8 && Iw < NT) {
 #ifdef LH_STAMPS
-                    // (diagnostic) loader wave 12: the wait for its value loads, then the window writes
+                    // (diagnostic) loader wave 13: the wait for its value loads, then the window writes
                     unsigned long long lt0_ = __builtin_amdgcn_s_memtime();
                     __builtin_amdgcn_s_waitcnt(0);
                     __builtin_amdgcn_sched_barrier(0);
                     unsigned long long lt1_ = __builtin_amdgcn_s_memtime();
-                    if (wv == BLOAD && lane == 0) atomicAdd(&lh_stamps[56], lt1_ - lt0_);
+                    if (wv == BZW && lane == 0) atomicAdd(&lh_stamps[56], lt1_ - lt0_);
 #endif
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -3075,7 +3071,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #ifdef LH_STAMPS
                     __builtin_amdgcn_s_waitcnt(0);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (wv == BLOAD && lane == 0) {
+                    if (wv == BZW && lane == 0) {
                         atomicAdd(&lh_stamps[57], __builtin_amdgcn_s_memtime() - lt1_);
                         atomicAdd(&lh_stamps[58], 1ull);
                     }
@@ -3105,7 +3101,14 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 }
             }
         }
+#ifdef LH_STAMPS
+        // (diagnostic) each wave's arrival at the step barrier, from its own exit of the previous one
+        if (lane == 0) atomicAdd(&lh_stamps[128 + 16 * (t & 1) + wv], __builtin_amdgcn_s_memtime() - bst_);
+#endif
         lds_barrier();
+#ifdef LH_STAMPS
+        bst_ = __builtin_amdgcn_s_memtime();
+#endif
         if (wv == 0) LDLT_SSTAMP(2); else LDLT_SSTAMP(4);
     }
 #ifdef LH_STAMPS
@@ -4335,10 +4338,10 @@ __global__ void k_mfma_probe(const double* A, const double* B, double* D) {
 
 hipError_t lh_read_stamps(unsigned long long* out, int n, int reset) {
 #ifdef LH_STAMPS
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lh_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128));
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lh_stamps), sizeof(unsigned long long) * (n < 256 ? n : 256));
     if (e != hipSuccess) return e;
     if (reset) {
-        unsigned long long z[128] = {0};
+        unsigned long long z[256] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(lh_stamps), z, sizeof(z));
     }
     return e;

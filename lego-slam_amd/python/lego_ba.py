@@ -471,8 +471,8 @@ def debug_stamps(reset=True):
     """Per-phase wave-cycle totals from the LH_STAMPS diagnostic build (zeros otherwise)."""
     lib = ba_lib()
     lib.lh_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
-    out = (C.c_ulonglong * 128)()
-    _check(lib.lh_debug_stamps(out, 128, int(reset)), "lh_debug_stamps")
+    out = (C.c_ulonglong * 256)()
+    _check(lib.lh_debug_stamps(out, 256, int(reset)), "lh_debug_stamps")
     return np.array(out[:], dtype=np.uint64)
 
 

@@ -73,3 +73,9 @@ if st[55]:
 # k_ctrl_b's loader wave 12 at the tile-row writes (stamps 56-58): the wait for its value loads, the writes
 if st[58]:
     print(f"  loader per tile row: value-load wait {st[56] / st[58]:.0f}, window writes {st[57] / st[58]:.0f} cycles")
+# k_ctrl_b's barrier arrival per wave (stamps 128-159), mean per step, even and odd steps
+if len(st) >= 160 and any(st[128:160]):
+    ns = max(nl, 1) * 48   # 96 steps per launch at P = 128: an approximate per-step mean
+    for par, nm in ((0, "even"), (1, "odd")):
+        print(f"  barrier arrival, {nm} steps (sum over launches / launches / half the steps, per wave):",
+              " ".join(f"{st[128 + 16 * par + w] / max(n, 1) / max(1, (st[51] and 48)):.0f}" for w in range(16)))
