@@ -210,8 +210,8 @@ LH_HD static inline int lh_ctrl_units(int n, const int32_t* tile_fcb, const int*
 }
 // k_ctrl: all 15 waves take units, wave 0's SIMD-mates (4, 8, 12) last
 #define LH_ORDER_CTRL {1, 2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12}
-// k_ctrl_b: waves 11, 13, 14, 15 stream tile rows into the window instead; wave 0's SIMD-mates last
-#define LH_ORDER_BAND {1, 2, 3, 5, 6, 7, 9, 10, 4, 8, 12}
+// k_ctrl_b: waves 12-15 stream tile rows into the window instead
+#define LH_ORDER_BAND {1, 2, 3, 5, 6, 7, 9, 10, 11, 4, 8}
 
 // k_ctrl_b's per-window tables (bblk null: no banded controller for this window)
 struct lh_band_args {
