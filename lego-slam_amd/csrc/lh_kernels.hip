@@ -2998,26 +2998,12 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     // loader lane lq of 256 owns the elements k = 0..7 at row 16 I + 2 k + lq / 128, column 16 (I - 7) + lq mod 128
     // (consecutive lanes, consecutive columns: conflict-free window writes)
     const int lq = 64 * band_loader_slot(wv) + lane, lrow = lq >> 7, lcol = lq & 127;
-    // Block indices two tile rows ahead (two sets, by row parity), values one step ahead: a block index
-    // loaded at the step before its value loads put the index's latency on every odd step.
-    int lbk[2][8];
-    uint32_t lok[2] = {0, 0};   // bit k: element k is a stored entry (kept apart from lbk: overwriting a register
-                                // with a load in flight waits for the load)
+    int lbk[8];
+    uint32_t lok = 0;   // bit k: element k is a stored entry (kept apart from lbk: overwriting a register with a
+                        // load in flight waits for the load, which put the block-index latency on the step)
     double lval[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { lbk[0][k] = -1; lbk[1][k] = -1; lval[k] = 0.0; }
-    auto load_idx = [&](int I) {   // tile row I's block indices and entry-valid bits into set I & 1
-        const int sI = I & 1, c = 16 * (I - 7) + lcol, pc = c / 6;
-        uint32_t m = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int r = 16 * I + 2 * k + lrow, pr = r / 6, d = pr - pc;
-            lbk[sI][k] = bblk[min(max(pc, 0), P - 1) * 64 + min(max(d, 0), 63)];
-            m |= (c <= r && r < n && d < 64) ? (1u << k) : 0u;
-        }
-        lok[sI] = m;
-    };
-    if (band_loader(wv) && 8 < NT) load_idx(8);
+    for (int k = 0; k < 8; ++k) { lbk[k] = -1; lval[k] = 0.0; }
     lds_barrier();
     CSTAMP(4);
 
@@ -3061,7 +3047,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         }
         if (band_loader(wv)) {
             // tile row I enters the window at step 2 I - 14, into the slots of tile row I - 8 (retired
-            // after step 2 I - 15); its block indices are loaded at step 2 I - 18, its values at 2 I - 15
+            // after step 2 I - 15); its block indices are loaded at step 2 I - 16, its values at 2 I - 15
             // Every load is unconditional (clamped index): a conditional load becomes a branch whose join
             // waits for it.  Selections and the diagonal's lambda wait until the values are written.
             if ((t & 1) == 0) {
@@ -3078,7 +3064,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int r = 16 * Iw + 2 * k + lrow, c = 16 * (Iw - 7) + lcol;
-                        double v = ((lok[Iw & 1] >> k) & 1) ? lval[k] : 0.0;
+                        double v = ((lok >> k) & 1) ? lval[k] : 0.0;
                         if (r == c) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
                         SY.at(r, c) = (c <= r) ? v : 0.0;
                     }
@@ -3091,16 +3077,26 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                     }
 #endif
                 }
-                if (t / 2 + 9 < NT) load_idx(t / 2 + 9);
+                const int Ia = t / 2 + 8;
+                if (Ia < NT) {
+                    const int c = 16 * (Ia - 7) + lcol, pc = c / 6;
+                    lok = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int r = 16 * Ia + 2 * k + lrow, pr = r / 6, d = pr - pc;
+                        lbk[k] = bblk[min(max(pc, 0), P - 1) * 64 + min(max(d, 0), 63)];
+                        lok |= (c <= r && r < n && d < 64) ? (1u << k) : 0u;
+                    }
+                }
             } else {
                 const int Ib = (t - 1) / 2 + 8;
                 if (Ib < NT) {
-                    const int c = 16 * (Ib - 7) + lcol, sI = Ib & 1;
+                    const int c = 16 * (Ib - 7) + lcol;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int r = 16 * Ib + 2 * k + lrow;
-                        lval[k] = src[(size_t)max(lbk[sI][k], 0) * 36 + (c % 6) * 6 + (r % 6)];
-                        if (lbk[sI][k] < 0) lok[sI] &= ~(1u << k);   // a pair no chunk couples
+                        lval[k] = src[(size_t)max(lbk[k], 0) * 36 + (c % 6) * 6 + (r % 6)];
+                        if (lbk[k] < 0) lok &= ~(1u << k);   // a pair no chunk couples
                     }
                 }
             }
