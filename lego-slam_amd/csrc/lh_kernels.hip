@@ -1494,10 +1494,14 @@ __device__ __forceinline__ double bcast16(double v) {
 // Newton steps), the column's entries and the trailing updates of the lane's row.  (A cubic correction
 // folded into the quotient, three dependent FMAs instead of five, measured the same ~1.8k cycles per
 // block alone, tools/ubench_ctrl_chain.hip: the chain is bound by issue, not by this latency.)
-template <int Q>
+// SAFE: Eigen ldlt_inplace's zero-pivot rule (no scaling where !pivot_is_valid: Delta = 1) on the chain;
+// the fast form takes every pivot as valid and factor_block8_v redoes the block in the safe form when one
+// was not (a fixed pose under STRATEGY1), so valid blocks get the same bits with three fewer dependent
+// instructions per column.
+template <int Q, bool SAFE>
 __device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
     const double d = bcast16<Q>(R[Q]);
-    dl[Q] = fabs(d) > 0.0 ? d : 1.0;          // Eigen ldlt_inplace: no scaling where !pivot_is_valid
+    dl[Q] = SAFE ? (fabs(d) > 0.0 ? d : 1.0) : d;
     const double inv = fast_rcp(dl[Q]);
     const double coef = R[Q] * inv;
     double u[8];
@@ -1562,14 +1566,29 @@ __device__ __forceinline__ void factor_block8_v(const S& A, const double (&v)[8]
     const int kw = A.wrap(k0);
 #pragma unroll
     for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
-    factor_column<0>(R, dl);
-    factor_column<1>(R, dl);
-    factor_column<2>(R, dl);
-    factor_column<3>(R, dl);
-    factor_column<4>(R, dl);
-    factor_column<5>(R, dl);
-    factor_column<6>(R, dl);
-    factor_column<7>(R, dl);
+    factor_column<0, false>(R, dl);
+    factor_column<1, false>(R, dl);
+    factor_column<2, false>(R, dl);
+    factor_column<3, false>(R, dl);
+    factor_column<4, false>(R, dl);
+    factor_column<5, false>(R, dl);
+    factor_column<6, false>(R, dl);
+    factor_column<7, false>(R, dl);
+    bool ok = true;   // every pivot valid (the pivots are the same in every lane)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ok = ok && fabs(dl[q]) > 0.0;
+    if (!__builtin_amdgcn_readfirstlane(ok)) {   // rare: redo the block with the zero-pivot rule
+#pragma unroll
+        for (int q = 0; q < 8; ++q) R[q] = ident ? (q == r ? 1.0 : 0.0) : v[q];
+        factor_column<0, true>(R, dl);
+        factor_column<1, true>(R, dl);
+        factor_column<2, true>(R, dl);
+        factor_column<3, true>(R, dl);
+        factor_column<4, true>(R, dl);
+        factor_column<5, true>(R, dl);
+        factor_column<6, true>(R, dl);
+        factor_column<7, true>(R, dl);
+    }
     if (lane < 8) {
 #pragma unroll
         for (int q = 0; q < 8; ++q)
