@@ -1361,6 +1361,10 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     // them with the controller's instead of sinking them below the branch, a second round trip)
     if ((done != 0) | ((evo != 0) & (b < LY.npairs)) | (p > q) | (ib > ie)) return;   // no short-circuit: one test
     if (b == LY.npairs) {
+        // the LM decision's controller words go out with the chunk scalars (one round trip, not a third
+        // after the sums; only this block's thread 0 writes them in this kernel)
+        CtrlWords cw0{};
+        if (prm.dec_in_reduce && mode != 0 && tid == 0) cw0 = ctrl_load(ctrl);
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
         for (int c = tid; c < n_chunks; c += RT) {
             const double* sc = csc + (size_t)c * 4;
@@ -1381,10 +1385,9 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
             rs[LY.off_sc + LH_SC_MAXD] = m;
             *maxd_out = m;
             if (prm.dec_in_reduce && mode != 0) {
-                const CtrlWords cw = ctrl_load(ctrl);
                 int d_o, a_o, c_o;
                 double l_o;
-                ctrl_lm_step(ctrl, cw, prm, 1, 0.0, 0.5 * a0, a1, a2, host_done, seq, d_o, a_o, c_o, l_o);
+                ctrl_lm_step(ctrl, cw0, prm, 1, 0.0, 0.5 * a0, a1, a2, host_done, seq, d_o, a_o, c_o, l_o);
             }
         }
         return;
