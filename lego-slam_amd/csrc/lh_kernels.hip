@@ -1861,6 +1861,9 @@ __device__ __forceinline__ void backsub_block(const double* __restrict__ A, cons
 #pragma unroll
         for (int v = 0; v < 8; ++v) l1[v] = A[(lane + 64) * AS + KB + v];
     }
+    // the loads stay ahead of the broadcasts (left alone, the scheduler sinks them past the nb branch to
+    // their first use, after x_b, and the LDS round trip lands on the chain)
+    __builtin_amdgcn_sched_barrier(0);
     if (KB >= nb) return;
     const double ys = HI ? y1 : y0;
     double yb[8];
@@ -1966,6 +1969,8 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     const int nb = (n + 7) & ~7;          // blocks past the last real row are identity: never eliminated
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const LdsSys SY{A};
+    // this wave's unit words, lane t holding step t's: read once, so no step starts with an LDS round trip
+    const uint32_t uwv = (lane < LH_NSTEP) ? units[wv * LH_NSTEP + lane] : 0u;
     if (!factored0) {   // (k_ctrl factors block 0 during its scatter)
         if (wv == 0) factor_block8(SY, F.N[0], F.ND[0], 0, lane);
         lds_barrier();
@@ -1976,12 +1981,14 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
     // the other waves' unit time and barrier wait (wave-cycles summed over waves)
     unsigned long long ss_[5] = {0, 0, 0, 0, 0}, sa_ = __builtin_amdgcn_s_memtime(), sb_;
     // per step t: [64 + t] wave 0's diagonal tile, [80 + t] its factor, [96 + t] its barrier wait
-    // (sums over launches), [112 + t] the slowest other wave's unit in the worst launch (atomicMax)
+    // (sums over launches), [112 + t] the slowest other wave's unit in the worst launch (atomicMax of
+    // cycles << 24 | unit word << 4 | wave)
+    uint32_t su_ = 0;
 #define LDLT_SSTAMP(i) do { __builtin_amdgcn_sched_barrier(0); sb_ = __builtin_amdgcn_s_memtime(); \
         ss_[i] += sb_ - sa_; \
         if (lane == 0 && (i) != 4) { \
             const int ti_ = min(k0 >> 3, 15); \
-            if ((i) == 3) atomicMax(&lh_stamps[112 + ti_], sb_ - sa_); \
+            if ((i) == 3) atomicMax(&lh_stamps[112 + ti_], ((sb_ - sa_) << 24) | ((unsigned long long)(su_ & 0xffffu) << 4) | (unsigned)wv); \
             else atomicAdd(&lh_stamps[64 + 16 * ((i) == 0 ? 0 : (i) == 1 ? 1 : 2) + ti_], sb_ - sa_); } \
         sa_ = sb_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
@@ -2000,7 +2007,10 @@ __device__ __forceinline__ void lds_ldlt_solve(double* __restrict__ A, double* _
         }
         if (m0 < nb) {
             const int g0 = m0 >> 4;               // tile row/col of the next diagonal block
-            const uint32_t uw = __builtin_amdgcn_readfirstlane(units[wv * LH_NSTEP + t]);
+            const uint32_t uw = __builtin_amdgcn_readlane(uwv, t);
+#ifdef LH_STAMPS
+            su_ = uw;
+#endif
             if (wv == 0) {
                 if (uw & LH_UNIT_VALID) {
                     diag_tile(SY, N, ND, k0, 16 * g0, lane);
@@ -2071,6 +2081,7 @@ __device__ __forceinline__ void lds_ldlt_solve_nd(double* __restrict__ A, double
     auto c0 = [&](int t) { return t < nl_blk ? t : t + ns_blk; };          // chain 0's block at step t
     auto c1 = [&](int t) { return t < ns_blk ? nl_blk + t : -1; };        // chain 1's (-1: done)
     const LdsSys SY{A};
+    const uint32_t uwv = (lane < LH_NSTEP) ? units[wv * LH_NSTEP + lane] : 0u;   // lane t: step t's unit word
     if (wv == 0) factor_block8(SY, F.N[0], F.ND[c0(0)], 8 * c0(0), lane);
     if (wv == 1 && ns_blk > 0) factor_block8(SY, F.N[2], F.ND[c1(0)], 8 * c1(0), lane);
     lds_barrier();
@@ -2087,7 +2098,7 @@ __device__ __forceinline__ void lds_ldlt_solve_nd(double* __restrict__ A, double
             const double d = A[(k0 + lane) * AS + k0 + lane];
             F.z[k0 + lane] = fabs(d) > 2.2250738585072014e-308 ? z : 0.0;
         }
-        const uint32_t uw = __builtin_amdgcn_readfirstlane(units[wv * LH_NSTEP + t]);
+        const uint32_t uw = __builtin_amdgcn_readlane(uwv, t);
         const int smask = (uw >> 10) & 3, stmask = (uw >> 12) & 3;
         if (wv < 2) {
             const int nx = wv == 0 ? c0(t + 1) : c1(t + 1);
@@ -3035,6 +3046,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     CSTAMP(5);
 #ifdef LH_STAMPS
     unsigned long long ss_[5] = {0, 0, 0, 0, 0}, sa_ = __builtin_amdgcn_s_memtime(), sb_, bst_ = sa_;
+    uint32_t su_ = 0;
 #endif
     for (int t = 0; t < nstep; ++t) {
         const int k0 = 8 * t, par = t & 1, m0 = k0 + 8;
@@ -3053,6 +3065,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         if (m0 < nb) {
             const int g0 = m0 >> 4;
             const uint32_t uw = unit_word(t);
+#ifdef LH_STAMPS
+            su_ = uw;
+#endif
             if (wv == 0) {
                 if (uw & LH_UNIT_VALID) {
                     diag_tile(SY, N, ND, k0, 16 * g0, lane);

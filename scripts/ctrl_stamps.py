@@ -59,11 +59,14 @@ if st[51]:
 # per step t of the LDL^T loop (stamps 64-127): wave 0's diagonal tile, factor and barrier wait (mean
 # per launch) and the slowest other wave's unit (the worst launch)
 if len(st) >= 128 and st[51]:
-    print("  step  w0 tile  w0 factor  w0 wait  worst unit")
+    # the worst unit's stamp: cycles << 24 | its unit word << 4 | its wave
+    print("  step  w0 tile  w0 factor  w0 wait  worst unit  (wave: tile row I, tile columns [j0, j1), S = stores L)")
     for t in range(16):
         a, b, c, m = st[64 + t] / nl, st[80 + t] / nl, st[96 + t] / nl, st[112 + t]
         if a or b or c or m:
-            print(f"  {t:4d} {a:8.0f} {b:10.0f} {c:8.0f} {m:11d}")
+            cyc, uw, wv = m >> 24, (m >> 4) & 0xffff, m & 15
+            desc = f"w{wv}: I+{uw & 7} [{(uw >> 3) & 7}, {(uw >> 6) & 15}){' S' if uw & 0x4000 else ''}" if uw & 0x8000 else ""
+            print(f"  {t:4d} {a:8.0f} {b:10.0f} {c:8.0f} {cyc:11d}  {desc}")
 # k_ctrl_b's back substitution (stamps 52-55): per block, wave 0's x_b = ND_b y_b (ND read, broadcasts, dot)
 # and its row updates (readlanes, dots, the entering row), and its ring readiness checks
 if st[55]:
