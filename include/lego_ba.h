@@ -157,7 +157,8 @@ typedef struct lh_result {
     double chi2_initial;       /* 0.5 * sum rho0 at the input state (problem.cpp:475-479)          */
     double chi2_final;         /* currentChi_ at exit                                              */
     double lambda_final;
-    double time_ms;            /* wall time of the LM solve on the device (excludes upload)        */
+    double time_ms;            /* wall time of the LM solve on the device (excludes upload); host
+                                  clock from the first launch to the stop when no array is requested */
     int32_t pcg_iterations;    /* PCG iterations summed over all trials (0 with LH_SOLVER_LDLT)    */
     int32_t degenerate;        /* landmarks with a rank-deficient H_ll at the initial linearisation */
     double time_prep_ms;       /* lh_solve / lh_upload: host preprocessing of the window           */
@@ -186,7 +187,11 @@ void lh_destroy(lh_handle *h);
 int lh_solve(lh_handle *h, const lh_window *in, lh_result *out);
 
 /* Device-resident path (bench): lh_upload preprocesses and copies the window
-   once; every lh_solve_resident restarts from the uploaded initial state. */
+   once; every lh_solve_resident restarts from the uploaded initial state.
+   A solve that requests no array (pose_Tcw, lm_xyz, edge_robust_chi2 all NULL) returns as soon as
+   the device has stopped the LM loop: its scalars and trace come with the stop flag in mapped
+   host memory, and the kernels still draining are stream-ordered before any later call on the
+   handle (lh_destroy synchronises). */
 int lh_upload(lh_handle *h, const lh_window *in);
 int lh_solve_resident(lh_handle *h, lh_result *out);
 

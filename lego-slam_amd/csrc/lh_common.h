@@ -117,6 +117,17 @@ struct lh_ctrl {
     int32_t evo;               // the next trial is in the final LM iteration: k_lin evaluates only
     int32_t acc_hist[2];       // trial seq's LM decision (accepted) at [seq & 1]: read by its controller, and by
                                // the next trial's k_reduce when it commits the staged system (commit_in_reduce)
+    int32_t done_seq;          // the trial whose decision stopped the loop (its controller raises the host's done)
+    double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
+};
+
+// The host-visible words (pinned, mapped; written by ctrl_lm_step): done (the LM loop stopped), the
+// progress word, and the solve's summary, written before done is raised, so a solve that returns no
+// arrays ends when the host sees done: no copy of lh_ctrl behind the last kernel, no stream sync.
+struct lh_host_words {
+    int32_t done, progress;
+    int32_t iter, trials, accepted, trace_len, nonpd, pcg_iters;
+    double chi2_initial, chi, lambda;
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
 };
 

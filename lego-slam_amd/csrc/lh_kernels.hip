@@ -1214,7 +1214,7 @@ __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl)
 __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
                                              volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
-                                             int& cur_o, double& lam_o) {
+                                             int& cur_o, double& lam_o, bool raise_done = true) {
     double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
     int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
     int done = w.done, cur = w.cur;
@@ -1285,7 +1285,13 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
             }
         }
         if (trace) {
-            if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
+            if (tl < LH_TRACE) {
+                ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam;
+                if (host_done) {   // the host's copy as it grows (posted stores: nothing waits here)
+                    volatile lh_host_words* hw = reinterpret_cast<volatile lh_host_words*>(host_done);
+                    hw->trace_chi[tl] = chi; hw->trace_lambda[tl] = lam;
+                }
+            }
             tl += 1;
         }
         ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
@@ -1304,8 +1310,22 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         // advances past the stop trial, which bounds how many trials (and all-reduces) any rank
         // can have enqueued.  One 32-bit store: the host never sees a torn pair.
         if (host_done) {
-            if (done) host_done[0] = 1;
-            else host_done[1] = 2 * seq + near;
+            if (done) {   // the summary (the trace is there already), then done, released to the host
+                const int nonpd = ctrl->nonpd, pcg = ctrl->pcg_iters;
+                volatile lh_host_words* hw = reinterpret_cast<volatile lh_host_words*>(host_done);
+                hw->iter = iter; hw->trials = trials; hw->accepted = nacc; hw->trace_len = tl;
+                hw->nonpd = nonpd; hw->pcg_iters = pcg;
+                hw->chi2_initial = chi0; hw->chi = chi; hw->lambda = lam;
+                ctrl->done_seq = seq;
+                if (raise_done) {
+                    __threadfence_system();
+                    host_done[0] = 1;
+                }
+                // else the same trial's controller raises it as it starts: its kernel begins after this
+                // one's stores are complete, so the summary needs no fence here (one that drained the L2)
+            } else {
+                host_done[1] = 2 * seq + near;
+            }
         }
     }
     done_o = done;
@@ -1387,7 +1407,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
             if (prm.dec_in_reduce && mode != 0) {
                 int d_o, a_o, c_o;
                 double l_o;
-                ctrl_lm_step(ctrl, cw0, prm, 1, 0.0, 0.5 * a0, a1, a2, host_done, seq, d_o, a_o, c_o, l_o);
+                ctrl_lm_step(ctrl, cw0, prm, 1, 0.0, 0.5 * a0, a1, a2, host_done, seq, d_o, a_o, c_o, l_o, false);
             }
         }
         return;
@@ -2292,6 +2312,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const bool nd = SOLVER == 0 && prm.nd_steps > 0;        // the two-chain LDL^T schedule
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
+    // [160 + wave]: the wave's HW_ID word (SIMD in bits 5:4): which waves share wave 0's SIMD
+    if (lane == 0) lh_stamps[160 + wave] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (1ull << 32);
 #endif
 
     // ---------------- 1. prefetch (one round trip) ----------------
@@ -2306,10 +2328,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // the decision's words: uniform loads in the same round trip as the system
     int done = 0, accept = 0;
     double lambda = 0.0;
+    int dseq = -1;
     if (decided) {
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
+        dseq = __builtin_amdgcn_readfirstlane(ctrl->done_seq);
     }
     // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
@@ -2380,6 +2404,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         accept = s_flags[1];
         lambda = s_lam;
     }
+    // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
+    if (decided && done && dseq == seq && tid == 0 && host_done) host_done[0] = 1;
     if (done) return;
 #ifdef LH_STAMPS
     if (tid == 0) {
@@ -2953,6 +2979,8 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
+        // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
+        if (done && tid == 0 && host_done && ctrl->done_seq == seq) host_done[0] = 1;
     } else {
         double tchi = 0.0, sl = 0.0, ndg = 0.0;
         CtrlWords cw{};

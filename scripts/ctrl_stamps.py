@@ -67,6 +67,9 @@ if len(st) >= 128 and st[51]:
             cyc, uw, wv = m >> 24, (m >> 4) & 0xffff, m & 15
             desc = f"w{wv}: I+{uw & 7} [{(uw >> 3) & 7}, {(uw >> 6) & 15}){' S' if uw & 0x4000 else ''}" if uw & 0x8000 else ""
             print(f"  {t:4d} {a:8.0f} {b:10.0f} {c:8.0f} {cyc:11d}  {desc}")
+# the waves' SIMDs (stamps 160-175: HW_ID, SIMD_ID in bits 5:4, bit 32 set once written)
+if len(st) >= 176 and any(st[160 + w] >> 32 for w in range(16)):
+    print("  wave -> SIMD: " + " ".join(f"{w}:{(st[160 + w] >> 4) & 3}" for w in range(16) if st[160 + w] >> 32))
 # k_ctrl_b's back substitution (stamps 52-55): per block, wave 0's x_b = ND_b y_b (ND read, broadcasts, dot)
 # and its row updates (readlanes, dots, the entering row), and its ring readiness checks
 if st[55]:
