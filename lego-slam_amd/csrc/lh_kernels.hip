@@ -1549,6 +1549,10 @@ __device__ __forceinline__ void factor_column(double (&R)[8], double (&dl)[8]) {
 //          than the window share a slot), the rhs in its own LDS array, L rows to global memory
 //          (L[r][c] at Lg[r * LH_LBW + c - r + LH_LBW], c in [r - LH_LBW, r)).
 struct LdsSys {
+    // the trailing stores rewrite the entries outside the update with their own value (one exec mask
+    // for the four stores; k_ctrl 28.09 / 28.04 -> 27.46 / 27.54 us); in k_ctrl_b's busier LDS (the
+    // stream loaders' writes) the extra stores measured slower, so BandSys keeps the per-entry masks
+    static constexpr bool rewrite_masked = true;
     double* A;
     __device__ __forceinline__ double& at(int r, int c) const { return A[r * AS + c]; }
     __device__ __forceinline__ double& rhs(int r) const { return A[NP * AS + r]; }
@@ -1560,6 +1564,7 @@ struct LdsSys {
 };
 #define LH_LBW 128   // k_ctrl_b: L entries kept per row (columns r - 128 .. r - 1)
 struct BandSys {
+    static constexpr bool rewrite_masked = false;
     double* A;   // LDS, 128 rows of stride AS
     double* y;   // LDS rhs
     double* Lg;  // global, LH_LBW per row
@@ -1717,10 +1722,22 @@ __device__ __forceinline__ void ldlt_tile_row(const S& A, const double* __restri
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b0, t[0], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b1, t[1], acc, 0, 0, 0);
         const int row = rb + li;
+        // entries outside the update (left of m0, above the diagonal) get their own value back: no other
+        // wave writes them this step, and the four stores share one exec mask instead of four branches
+        if constexpr (S::rewrite_masked) {
+            if (row >= m0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int col = cb + lk + 4 * q;
-            if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + li, cbw_cur + lk + 4 * q) = old[q] - acc[q];
+                for (int q = 0; q < 4; ++q) {
+                    const int col = cb + lk + 4 * q;
+                    A.atw(rbw + li, cbw_cur + lk + 4 * q) = (col >= m0 && col <= row) ? old[q] - acc[q] : old[q];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int col = cb + lk + 4 * q;
+                if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + li, cbw_cur + lk + 4 * q) = old[q] - acc[q];
+            }
         }
         cb = nc;
         b0 = nb0; b1 = nb1;
@@ -1757,10 +1774,22 @@ __device__ __forceinline__ void diag_tile(const S& A, const double* __restrict__
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, t[0], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, t[1], acc, 0, 0, 0);
     const int row = rb + li;
+    // as ldlt_tile_row: the entries outside the update are rewritten with their own value (above the
+    // diagonal this wave's factor writes L^T next; rows above m0 are the store unit's, left alone)
+    if constexpr (S::rewrite_masked) {
+        if (row >= m0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int col = rb + lk + 4 * q;
-        if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + li, rbw + lk + 4 * q) = old[q] - acc[q];
+            for (int q = 0; q < 4; ++q) {
+                const int col = rb + lk + 4 * q;
+                A.atw(rbw + li, rbw + lk + 4 * q) = (col >= m0 && col <= row) ? old[q] - acc[q] : old[q];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int col = rb + lk + 4 * q;
+            if (row >= m0 && col >= m0 && col <= row) A.atw(rbw + li, rbw + lk + 4 * q) = old[q] - acc[q];
+        }
     }
 }
 
