@@ -1618,9 +1618,16 @@ __device__ __forceinline__ void factor_block8_v(const S& A, const double (&v)[8]
         factor_column<7, true>(R, dl);
     }
     if (lane < 8) {
+        if constexpr (S::rewrite_masked) {
+            // no branch per store: the entries below the diagonal go to the row's padding column
+            // (LH_NPAD, never read)
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (q <= r) A.atw(kw + q, kw + r) = (q == r) ? dl[q] : R[q];
+            for (int q = 0; q < 8; ++q) A.atw(kw + q, q <= r ? kw + r : LH_NPAD) = (q == r) ? dl[q] : R[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q <= r) A.atw(kw + q, kw + r) = (q == r) ? dl[q] : R[q];
+        }
     } else if (lane < 16) {
         double2* n2 = reinterpret_cast<double2*>(No + 8 * r);
         double2* d2 = reinterpret_cast<double2*>(NDo + 8 * r);
