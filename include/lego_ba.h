@@ -59,10 +59,13 @@ typedef enum lh_strategy { LH_STRATEGY_DEFAULT = 0, LH_STRATEGY_1 = 1 } lh_strat
 typedef enum lh_linear_solver { LH_SOLVER_LDLT = 0, LH_SOLVER_PCG = 1 } lh_linear_solver;
 
 /* Arithmetic of the per-edge path.  FP64: double throughout, the residual a bitwise
-   mirror of the reference's (lego_types.h:200-216).  FP32_RESID: the camera point, residual, Huber
-   weight and Jacobians of each edge in float, every sum over edges (H blocks, b, chi2, the Schur
-   complement) in double: BASELINE config 2's "fp32 residuals + fp64 accumulate".  Parity to
-   tolerance, not to the bit. */
+   mirror of the reference's (lego_types.h:200-216).  FP32_RESID: BASELINE config 3's "fp32 residuals
+   + fp64 accumulate" as far as it can be taken without changing the LM decisions: each edge's
+   Jacobians (the projection derivative and its chain through the extrinsic and the pose rotation,
+   lego_types.h:218-254) in float, widened to double before any product that is summed; the camera
+   point, the residual, the Huber weight, rho0, chi2, b's residual factor and the gain ratio stay the
+   fp64 mirror, and every sum over edges (H blocks, b, chi2, the Schur complement) is double.  Parity
+   to tolerance, not to the bit. */
 typedef enum lh_precision { LH_PREC_FP64 = 0, LH_PREC_FP32_RESID = 1 } lh_precision;
 
 /* The per-trial exchange of a landmark-sharded solve (world_size > 1): RCCL on the handle's stream

@@ -242,6 +242,7 @@ struct lh_handle {
     ncclComm_t comm = nullptr;
     bool host_comm = false;       // LH_COMM_HOST with world_size > 1
     bool uploaded = false;
+    bool upload_joined = false;   // this upload has taken part in the sharded envelope all-reduce
     lh::Pool* pool = nullptr;
 
     // window
@@ -450,8 +451,19 @@ int rank_max(lh_handle* h, double* buf, int n);
 // Every exit after the first copy out of the pinned staging is queued must leave ev_staging recorded
 // behind it, or the next upload could rewrite (or reallocate) the staging while that DMA still reads
 // it: the error returns (LH_E_UNSUPPORTED envelope checks, a failed HIP call) record it here.
+//
+// A sharded upload holds one collective, the MAX all-reduce of the envelope of S (upload_body).  A rank that fails before it (a bad pixel, an unsupported window, an allocation)
+// still joins it, contributing its status in word 0 and nothing to the envelope, so the healthy ranks
+// are not left blocked in it: every rank then returns the largest status of any rank.
 int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
-    const int st = upload_body(h, w, sync);
+    h->upload_joined = false;
+    int st = upload_body(h, w, sync);
+    const bool sharded = h->host_comm || h->comm;
+    if (st != LH_OK && sharded && !h->upload_joined && w && w->n_poses > 0 && w->n_poses <= LH_PMAX_ANY) {
+        std::vector<double> buf(1 + (size_t)w->n_poses, -1e300);
+        buf[0] = (double)st;
+        rank_max(h, buf.data(), 1 + w->n_poses);
+    }
     if (st != LH_OK && !h->staging_pending && h->ev_staging) {
         if (hipEventRecord(h->ev_staging, h->stream) == hipSuccess) h->staging_pending = true;
     }
@@ -477,6 +489,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     lh::PlanCfg cfg;
     cfg.chunk_lm = h->opt.chunk_landmarks;
     lh::Plan& pl = h->plan;
+    const bool sharded = h->host_comm || h->comm;
     cfg.rank_invariant_pairs = h->opt.world_size > 1;
     int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
     if (st != LH_OK) {
@@ -484,39 +497,29 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         h->staging_pending = true;
         return st;
     }
-    // past LH_PMAX poses: LDL^T by k_ctrl_b when the reduced system is banded in natural pose order
-    // (any P up to LH_PMAX_ANY, one rank), else by k_ctrl_g (dense, up to LH_PMAX_WIN poses); PCG by
-    // k_ctrl_p (block-sparse, up to LH_PMAX_ANY)
-    static const int kBandSteps = 6 * LH_PMAX_ANY / 8;
-    std::vector<uint16_t> bunits;
-    h->band = false;
-    if (pl.P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && h->opt.world_size == 1 && !h->comm &&
-        !getenv("LH_NO_BAND")) {
-        const int n = 6 * pl.P, NE = (n + 15) & ~15, NT = NE / 16;
-        std::vector<int> pf(pl.P);
-        for (int p = 0; p < pl.P; ++p) pf[p] = p;
-        for (size_t c = 0; c < pl.chunk_mask.size(); ++c) {
-            const uint64_t m = pl.chunk_mask[c];
-            if (!m) continue;
-            const int lo = pl.chunk_base[c] + __builtin_ctzll(m);
-            for (uint64_t b = m; b; b &= b - 1) pf[pl.chunk_base[c] + __builtin_ctzll(b)] = std::min(pf[pl.chunk_base[c] + __builtin_ctzll(b)], lo);
+    // Pose p's first coupled pose: the lowest pose of any chunk window holding p (a chunk writes a block
+    // for every pair of its window).  It gives the envelope of S in natural pose order, from which k_ctrl's
+    // and k_ctrl_b's work units and the banded controller's eligibility follow; a sharded solve factors
+    // the sum of every rank's blocks, so it takes the union over the ranks (below, after every rank-local
+    // failure point).
+    std::vector<int> pf(pl.P);
+    for (int p = 0; p < pl.P; ++p) pf[p] = p;
+    for (size_t c = 0; c < pl.chunk_mask.size(); ++c) {
+        const uint64_t m = pl.chunk_mask[c];
+        if (!m) continue;
+        const int lo = pl.chunk_base[c] + __builtin_ctzll(m);
+        for (uint64_t b = m; b; b &= b - 1) {
+            const int p = pl.chunk_base[c] + __builtin_ctzll(b);
+            pf[p] = std::min(pf[p], lo);
         }
-        std::vector<int32_t> fcb(NT);
-        bool ok = true;
-        for (int I = 0; I < NT; ++I) {
-            int f = 1 << 20;
-            for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
-            fcb[I] = f >> 3;
-            if (I >= 8 && fcb[I] < 2 * I - 13) ok = false;   // a tile row must enter the window before it is used
-        }
-        if (ok) {
-            bunits.resize(16 * (size_t)kBandSteps);
-            const int order[11] = LH_ORDER_BAND;
-            ok = lh_ctrl_units(n, fcb.data(), order, 11, kBandSteps, bunits.data()) <= 11;
-        }
-        h->band = ok;
     }
-    if (pl.P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
+    // past LH_PMAX poses: LDL^T by k_ctrl_b when the reduced system is banded in natural pose order
+    // (any P up to LH_PMAX_ANY), else by k_ctrl_g (dense, up to LH_PMAX_WIN poses); PCG by k_ctrl_p
+    // (block-sparse, up to LH_PMAX_ANY).  Decided after the union below; the arena reserves the band's
+    // tables whenever it may run.
+    static const int kBandSteps = 6 * LH_PMAX_ANY / 8;
+    const bool band_possible = pl.P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && !getenv("LH_NO_BAND");
+    h->band = false;
     // a chunk window must fit one CU's LDS
     for (int T = 1; T <= LH_TMAX; ++T)
         if (pl.tgroup_begin[T + 1] > pl.tgroup_begin[T] && lh_lin_smem(T, pl.ncam) > (size_t)h->lds_limit)
@@ -544,8 +547,9 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         const size_t o_fix = part(pl.fixed_bits.size() * sizeof(uint64_t)), o_bptr = part(pl.brow_ptr.size() * sizeof(int32_t));
         const size_t o_bent = part(pl.brow_ent.size() * sizeof(uint32_t));
         const size_t o_units = part(16 * LH_NSTEP * sizeof(uint16_t));
-        const size_t o_bunits = part(h->band ? bunits.size() * sizeof(uint16_t) : 0);
-        const size_t o_bblk = part(h->band ? (size_t)P * 64 * sizeof(int32_t) : 0);
+        const size_t n_bunits = band_possible ? 16 * (size_t)kBandSteps : 0, n_bblk = band_possible ? (size_t)P * 64 : 0;
+        const size_t o_bunits = part(n_bunits * sizeof(uint16_t));
+        const size_t o_bblk = part(n_bblk * sizeof(int32_t));
         HIPCHK(h->d_arena.ensure(bytes));
         HIPCHK(h->s_arena.ensure(bytes));
         h->arena_bytes = bytes;
@@ -570,8 +574,8 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         bind(h->d_brow_ptr, h->s_brow_ptr, db, sb, o_bptr, pl.brow_ptr.size());
         bind(h->d_brow_ent, h->s_brow_ent, db, sb, o_bent, pl.brow_ent.size());
         bind(h->d_units, h->s_units, db, sb, o_units, 16 * LH_NSTEP);
-        bind(h->d_bunits, h->s_bunits, db, sb, o_bunits, h->band ? bunits.size() : 0);
-        bind(h->d_bblk, h->s_bblk, db, sb, o_bblk, h->band ? (size_t)P * 64 : 0);
+        bind(h->d_bunits, h->s_bunits, db, sb, o_bunits, n_bunits);
+        bind(h->d_bblk, h->s_bblk, db, sb, o_bblk, n_bblk);
     }
     HIPCHK(h->d_meta.ensure(pl.n_slots));
     HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
@@ -586,20 +590,6 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
-    if (h->band) {   // k_ctrl_b's L rows and ND blocks; L entries outside the envelope are never written: zero
-        const size_t NE = (size_t)((6 * P + 15) & ~15);
-        HIPCHK(h->d_band.ensure(NE * 128 + (size_t)(6 * LH_PMAX_ANY / 8) * 64));
-        HIPCHK(hipMemsetAsync(h->d_band.p, 0, NE * 128 * sizeof(double), h->stream));
-    } else if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
-        const size_t ng = (size_t)((6 * P + 31) & ~31);
-        const bool fresh = h->d_gA.n < ng * ng;
-        HIPCHK(h->d_gA.ensure(ng * ng));
-        if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
-        // k_dense's dense symmetric S, double-buffered with the committed state
-        const bool fresh_s = h->d_gS.n < 2 * ng * ng;
-        HIPCHK(h->d_gS.ensure(2 * ng * ng));
-        if (fresh_s) HIPCHK(hipMemsetAsync(h->d_gS.p, 0, h->d_gS.n * sizeof(double), h->stream));
-    }
     if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_PCG)   // k_ctrl_p's row-contiguous copy of S (36 per block-row entry)
         HIPCHK(h->d_gA.ensure(pl.brow_ent.size() * 36));
     HIPCHK(h->d_maxd.ensure(1));
@@ -657,44 +647,72 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         }
     }
 
-    // ---- k_ctrl's work units: the envelope of S in natural pose order.  Pose p's first coupled pose is
-    //      the lowest pose of any chunk window holding p (a chunk writes a block for every pair of its
-    //      window); a sharded solve takes the minimum over the ranks (one MAX all-reduce at upload). ----
+    // ---- the sharded upload's one collective: every rank-local failure point is behind us.  Word 0
+    //      carries the largest status of any rank (a rank that failed earlier joins from upload_impl with
+    //      its own), then -pf per pose: the union envelope.  Everything after it is decided on data
+    //      identical on every rank. ----
+    if (sharded) {
+        std::vector<double> neg(1 + (size_t)P);
+        neg[0] = 0.0;
+        for (int p = 0; p < P; ++p) neg[1 + p] = -(double)pf[p];
+        h->upload_joined = true;
+        const int st_r = rank_max(h, neg.data(), 1 + P);
+        if (st_r != LH_OK) return st_r;
+        if (neg[0] > 0.0) return (int)neg[0];
+        for (int p = 0; p < P; ++p) pf[p] = (int)(-neg[1 + p]);
+    }
+
+    // ---- the banded controller's eligibility (tile rows enter its window two steps before use) ----
+    std::vector<uint16_t> bunits;
+    if (band_possible) {
+        const int n = 6 * P, NE = (n + 15) & ~15, NT = NE / 16;
+        std::vector<int32_t> fcb(NT);
+        bool ok = true;
+        for (int I = 0; I < NT; ++I) {
+            int f = 1 << 20;
+            for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
+            fcb[I] = f >> 3;
+            if (I >= 8 && fcb[I] < 2 * I - 13) ok = false;   // a tile row must enter the window before it is used
+        }
+        if (ok) {
+            bunits.resize(16 * (size_t)kBandSteps);
+            const int order[11] = LH_ORDER_BAND;
+            ok = lh_ctrl_units(n, fcb.data(), order, 11, kBandSteps, bunits.data()) <= 11;
+        }
+        h->band = ok;
+    }
+    if (P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
+    if (h->band) {   // k_ctrl_b's L rows and ND blocks; L entries outside the envelope are never written: zero
+        const size_t NE = (size_t)((6 * P + 15) & ~15);
+        HIPCHK(h->d_band.ensure(NE * 128 + (size_t)(6 * LH_PMAX_ANY / 8) * 64));
+        HIPCHK(hipMemsetAsync(h->d_band.p, 0, NE * 128 * sizeof(double), h->stream));
+    } else if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
+        const size_t ng = (size_t)((6 * P + 31) & ~31);
+        const bool fresh = h->d_gA.n < ng * ng;
+        HIPCHK(h->d_gA.ensure(ng * ng));
+        if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
+        // k_dense's dense symmetric S, double-buffered with the committed state
+        const bool fresh_s = h->d_gS.n < 2 * ng * ng;
+        HIPCHK(h->d_gS.ensure(2 * ng * ng));
+        if (fresh_s) HIPCHK(hipMemsetAsync(h->d_gS.p, 0, h->d_gS.n * sizeof(double), h->stream));
+    }
+
+    // ---- k_ctrl's work units: the envelope of S in natural pose order ----
     if (P <= LH_PMAX) {
         int32_t fcb[8];
         for (int I = 0; I < 8; ++I) fcb[I] = 0;
-        {
-            std::vector<int> pf(P);
-            for (int p = 0; p < P; ++p) pf[p] = p;
-            for (size_t c = 0; c < pl.chunk_mask.size(); ++c) {
-                const uint64_t m = pl.chunk_mask[c];
-                if (!m) continue;
-                const int lo = pl.chunk_base[c] + __builtin_ctzll(m);
-                for (uint64_t b = m; b; b &= b - 1) {
-                    const int p = pl.chunk_base[c] + __builtin_ctzll(b);
-                    pf[p] = std::min(pf[p], lo);
-                }
-            }
-            if (h->host_comm || h->comm) {   // a sharded solve factors the sum of every rank's blocks: the union
-                std::vector<double> neg(P);
-                for (int p = 0; p < P; ++p) neg[p] = -(double)pf[p];
-                const int st_r = rank_max(h, neg.data(), P);
-                if (st_r != LH_OK) return st_r;
-                for (int p = 0; p < P; ++p) pf[p] = (int)(-neg[p]);
-            }
-            const int n = 6 * P, NE = (n + 15) & ~15;
-            for (int I = 0; I < NE / 16; ++I) {
-                int f = 1 << 20;
-                for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
-                fcb[I] = f >> 3;
-            }
-            // the two-chain schedule (opt-in, LH_ND=1): fewer steps where the window splits into decoupled
-            // parts, but the separator's fill makes the early steps heavier; on C3 it measured slower than
-            // the one-chain schedule
-            h->nd.nsteps = 0;
-            const char* nd_env = getenv("LH_ND");
-            if (h->opt.linear_solver == LH_SOLVER_LDLT && nd_env && nd_env[0] == '1') lh_ctrl_nd_plan(P, pf.data(), h->nd);
+        const int n = 6 * P, NE = (n + 15) & ~15;
+        for (int I = 0; I < NE / 16; ++I) {
+            int f = 1 << 20;
+            for (int r = 16 * I; r < 16 * I + 16; ++r) f = std::min(f, r < n ? 6 * pf[r / 6] : r);
+            fcb[I] = f >> 3;
         }
+        // the two-chain schedule (opt-in, LH_ND=1): fewer steps where the window splits into decoupled
+        // parts, but the separator's fill makes the early steps heavier; on C3 it measured slower than
+        // the one-chain schedule
+        h->nd.nsteps = 0;
+        const char* nd_env = getenv("LH_ND");
+        if (h->opt.linear_solver == LH_SOLVER_LDLT && nd_env && nd_env[0] == '1') lh_ctrl_nd_plan(P, pf.data(), h->nd);
         if (h->nd.nsteps > 0) {
             std::memcpy(h->s_units.p, h->nd.units, sizeof(h->nd.units));
         } else {

@@ -1211,6 +1211,24 @@ __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl)
     w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
     return w;
 }
+// The stop trial's summary and trace to the host words, then done, by ONE thread behind its own
+// system-scope fence.  A kernel boundary releases at agent scope only, and the trace entries were
+// decided by earlier kernels on other CUs, so every word the host reads after done is stored here,
+// from lh_ctrl (device memory, complete at this kernel's start or written by this thread).
+__device__ __noinline__ void publish_stop(const lh_ctrl* __restrict__ ctrl, volatile int* __restrict__ host_done) {
+    volatile lh_host_words* hw = reinterpret_cast<volatile lh_host_words*>(host_done);
+    const int tl = ctrl->trace_len, nt = tl < LH_TRACE ? tl : LH_TRACE;
+    hw->iter = ctrl->iter; hw->trials = ctrl->trials; hw->accepted = ctrl->accepted; hw->trace_len = tl;
+    hw->nonpd = ctrl->nonpd; hw->pcg_iters = ctrl->pcg_iters;
+    hw->chi2_initial = ctrl->chi2_initial; hw->chi = ctrl->chi; hw->lambda = ctrl->lambda;
+    for (int i = 0; i < nt; ++i) {
+        hw->trace_chi[i] = ctrl->trace_chi[i];
+        hw->trace_lambda[i] = ctrl->trace_lambda[i];
+    }
+    __threadfence_system();
+    host_done[0] = 1;
+}
+
 __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
                                              volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
@@ -1285,13 +1303,7 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
             }
         }
         if (trace) {
-            if (tl < LH_TRACE) {
-                ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam;
-                if (host_done) {   // the host's copy as it grows (posted stores: nothing waits here)
-                    volatile lh_host_words* hw = reinterpret_cast<volatile lh_host_words*>(host_done);
-                    hw->trace_chi[tl] = chi; hw->trace_lambda[tl] = lam;
-                }
-            }
+            if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
             tl += 1;
         }
         ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
@@ -1310,19 +1322,11 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         // advances past the stop trial, which bounds how many trials (and all-reduces) any rank
         // can have enqueued.  One 32-bit store: the host never sees a torn pair.
         if (host_done) {
-            if (done) {   // the summary (the trace is there already), then done, released to the host
-                const int nonpd = ctrl->nonpd, pcg = ctrl->pcg_iters;
-                volatile lh_host_words* hw = reinterpret_cast<volatile lh_host_words*>(host_done);
-                hw->iter = iter; hw->trials = trials; hw->accepted = nacc; hw->trace_len = tl;
-                hw->nonpd = nonpd; hw->pcg_iters = pcg;
-                hw->chi2_initial = chi0; hw->chi = chi; hw->lambda = lam;
+            if (done) {
                 ctrl->done_seq = seq;
-                if (raise_done) {
-                    __threadfence_system();
-                    host_done[0] = 1;
-                }
-                // else the same trial's controller raises it as it starts: its kernel begins after this
-                // one's stores are complete, so the summary needs no fence here (one that drained the L2)
+                if (raise_done) publish_stop(ctrl, host_done);   // reads back this thread's stores above
+                // else the same trial's controller publishes the summary from lh_ctrl and raises done
+                // (publish_stop): only stores of the thread that fences are ordered before done
             } else {
                 host_done[1] = 2 * seq + near;
             }
@@ -2440,8 +2444,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         accept = s_flags[1];
         lambda = s_lam;
     }
-    // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
-    if (decided && done && dseq == seq && tid == 0 && host_done) host_done[0] = 1;
+    // this trial's k_reduce stopped the loop: the summary goes to the host and done is raised here
+    if (decided && done && dseq == seq && tid == 0 && host_done) publish_stop(ctrl, host_done);
     if (done) return;
 #ifdef LH_STAMPS
     if (tid == 0) {
@@ -3016,7 +3020,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
         // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
-        if (done && tid == 0 && host_done && ctrl->done_seq == seq) host_done[0] = 1;
+        if (done && tid == 0 && host_done && ctrl->done_seq == seq) publish_stop(ctrl, host_done);
     } else {
         double tchi = 0.0, sl = 0.0, ndg = 0.0;
         CtrlWords cw{};

@@ -55,7 +55,8 @@ std::vector<int> llc_cpus() {
 // next free cores, and rank processes of one box (LOCAL_RANK) break ties from disjoint offsets.
 namespace {
 std::mutex g_pin_mu;
-std::vector<int> g_pin_use;   // per index into llc_cpus(): workers of live pools pinned there
+std::vector<int> g_pin_use;   // per CPU id: workers of live pools pinned there (pools made on threads of
+                              // different LLCs see different llc_cpus() lists, so counts key on the CPU)
 }
 
 Pool::Pool(int threads) {
@@ -71,9 +72,9 @@ Pool::Pool(int threads) {
         int pick = -1;
         {
             std::lock_guard<std::mutex> g(g_pin_mu);
-            if ((int)g_pin_use.size() < nc) g_pin_use.resize(nc, 0);
             for (int k = 0; k < nc; ++k) {
-                const int c = (offset + k) % nc;
+                const int c = cpus[(offset + k) % nc];
+                if (c >= (int)g_pin_use.size()) g_pin_use.resize(c + 1, 0);
                 if (pick < 0 || g_pin_use[c] < g_pin_use[pick]) pick = c;
             }
             ++g_pin_use[pick];
@@ -81,7 +82,7 @@ Pool::Pool(int threads) {
         pinned_.push_back(pick);
         cpu_set_t one;
         CPU_ZERO(&one);
-        CPU_SET(cpus[pick], &one);
+        CPU_SET(pick, &one);
         pthread_setaffinity_np(workers_.back().native_handle(), sizeof(one), &one);   // best effort
     }
 }

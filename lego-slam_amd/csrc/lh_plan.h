@@ -54,7 +54,7 @@ class Pool {
     std::atomic<int> active_{0};        // workers that may still touch job_'s job
     std::atomic<int> sleepers_{0};
     std::atomic<bool> stop_{false};
-    std::vector<int> pinned_;           // the LLC-list index each worker is pinned to (released on destruction)
+    std::vector<int> pinned_;           // the CPU id each worker is pinned to (its use count released on destruction)
 };
 
 struct PlanCfg {

@@ -39,15 +39,46 @@ def _rank_main(rank, world, rdzv, cfg, seed, family, opts, q):
             t = torch.from_numpy(buf)   # shares the library's host buffer
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
 
-        L = lego_ba.CONFIGS[cfg]["L"]
-        shard = window_shard(cfg, rank * L // world, (rank + 1) * L // world, seed=seed, family=family)
+        corrupt = opts.pop("corrupt_rank", None)
+        if isinstance(cfg, dict):   # a generated window (lego_ba.generate_window arguments), sharded by landmark
+            L = cfg["L"]
+            shard = sharded_generated(cfg, rank * L // world, (rank + 1) * L // world, seed)
+        else:
+            L = lego_ba.CONFIGS[cfg]["L"]
+            shard = window_shard(cfg, rank * L // world, (rank + 1) * L // world, seed=seed, family=family)
+        if corrupt == rank:   # a pixel no float holds: this rank's upload fails in the planner's fill
+            shard["obs_uv"] = np.array(shard["obs_uv"], np.float64)
+            shard["obs_uv"][len(shard["obs_uv"]) // 2, 0] = 100.1
         s = lego_ba.Solver(device=0, world_size=world, rank=rank, allreduce=allreduce, **opts)
-        r = s.solve(shard)
+        try:
+            r = s.solve(shard)
+        except lego_ba.LhError as e:
+            q.put((rank, {"status": e.status}))
+            s.close()
+            return
         r["exchanges"] = s.comm_count()
+        r["controller"] = s.controller()
+        r["status"] = 0
         s.close()
         q.put((rank, {k: v for k, v in r.items()}))
     finally:
         dist.destroy_process_group()
+
+
+def stable_generated(P, L, k=8, **kw):
+    """Generator arguments of a sliding window of P keyframes (landmarks seen by runs of k consecutive
+    keyframes), the stable family without outliers, first pose fixed: reproducible under reordering."""
+    from windows import STABLE
+    return dict(P=P, L=L, k=k, **dict(STABLE, outlier_frac=0.0), **kw)
+
+
+def sharded_generated(spec, l0, l1, seed):
+    import lego_ba
+    w = lego_ba.generate_window(seed=seed, lm_begin=l0, lm_end=l1, **spec)
+    f = np.zeros(spec["P"], np.uint8)
+    f[0] = 1
+    w["pose_fixed"] = f
+    return w
 
 
 def run_sharded(cfg, seed, family, world=2, timeout=100, **opts):
@@ -214,3 +245,74 @@ def test_ranks_must_agree_on_solver_options(opts):
             os.unlink(rdzv)
     want = lego_ba.LH_OK if opts[0] == opts[1] else lego_ba.LH_E_BADARG
     assert got == {0: want, 1: want}
+
+
+def test_a_failing_rank_does_not_strand_the_others():
+    """lh_upload of a sharded window holds one collective (the MAX all-reduce of the envelope of S).  A
+    rank whose upload fails before it (here a pixel no float holds, refused by the planner's fill) still
+    joins it with its status, and every rank returns that status: no rank is left blocked in the
+    collective, or in the first trial's exchange of a solve its peer never starts."""
+    import lego_ba
+    out = run_sharded("C2", 0, "stable_noout", corrupt_rank=1, timeout=60)
+    assert out[0]["status"] == out[1]["status"] == lego_ba.LH_E_BADARG
+
+
+def _generated_one_rank(spec, seed, **opts):
+    import lego_ba
+    w = sharded_generated(spec, 0, spec["L"], seed)
+    s = lego_ba.Solver(**opts)
+    r = s.solve(w)
+    r["controller"] = s.controller()
+    s.close()
+    return w, r
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("P,L,seed", [(64, 6000, 2), (128, 8000, 1)])
+def test_two_rank_sharded_banded_ldlt(P, L, seed):
+    """The banded LDL^T controller (k_ctrl_b, the reference's live solver problem.cpp:420) on a sharded
+    window: each rank factors the all-reduced system over the union envelope of the ranks' blocks and
+    takes the LM decision on the all-reduced chi2.  Gate mode 1 (the Huber gate's rounding residue
+    taken as 0): the oracle's LDLT at the north-star bar and the one-rank solve to summation order."""
+    import oracle_bind as ob
+    spec = stable_generated(P, L)
+    w, one = _generated_one_rank(spec, seed, gate_mode=1)
+    assert one["controller"] == "k_ctrl_b"
+    out = run_sharded(spec, seed, None, timeout=300, gate_mode=1)
+    a, b = out[0], out[1]
+    assert a["controller"] == b["controller"] == "k_ctrl_b"
+    assert (a["iterations"], a["trials"]) == (b["iterations"], b["trials"])
+    assert a["chi2_final"] == b["chi2_final"] and np.array_equal(a["pose_Tcw"], b["pose_Tcw"])
+    assert a["exchanges"] == b["exchanges"] == a["trials"] + 1
+    assert (a["iterations"], a["trials"]) == (one["iterations"], one["trials"])
+    assert rel(a["chi2_final"], one["chi2_final"]) < 1e-9
+    assert np.allclose(a["pose_Tcw"], one["pose_Tcw"], atol=1e-9)
+    o = ob.solve(w, gate_mode=1)
+    assert (a["iterations"], a["trials"]) == (o["iterations"], o["trials"])
+    assert rel(a["chi2_final"], o["chi2_final"]) < 1e-6
+    assert np.allclose(a["pose_Tcw"], o["pose_Tcw"], atol=1e-6)
+    lm = np.vstack([a["lm_xyz"], b["lm_xyz"]])
+    assert np.allclose(lm, o["lm_xyz"], atol=1e-6)
+
+
+@pytest.mark.timeout(400)
+def test_two_rank_sharded_pcg_past_64_keyframes():
+    """A sharded window past 64 keyframes on PCG (k_ctrl_p): the block list is rank-invariant (every pair
+    within 64 poses, lh_plan.cpp), so both ranks all-reduce the same compact buffer.  Against the
+    one-rank PCG solve and the oracle's PCG."""
+    import lego_ba
+    import oracle_bind as ob
+    spec = stable_generated(96, 6000)
+    w, one = _generated_one_rank(spec, 1, linear_solver=lego_ba.LH_SOLVER_PCG)
+    assert one["controller"] == "k_ctrl_p"
+    out = run_sharded(spec, 1, None, timeout=300, linear_solver=lego_ba.LH_SOLVER_PCG)
+    a, b = out[0], out[1]
+    assert a["controller"] == b["controller"] == "k_ctrl_p"
+    assert (a["iterations"], a["trials"]) == (b["iterations"], b["trials"])
+    assert a["chi2_final"] == b["chi2_final"] and np.array_equal(a["pose_Tcw"], b["pose_Tcw"])
+    assert (a["iterations"], a["trials"]) == (one["iterations"], one["trials"])
+    assert rel(a["chi2_final"], one["chi2_final"]) < 1e-6
+    o = ob.solve(w, linear_solver=1)
+    assert (a["iterations"], a["trials"]) == (o["iterations"], o["trials"])
+    assert rel(a["chi2_final"], o["chi2_final"]) < 1e-6
+    assert np.allclose(a["pose_Tcw"], o["pose_Tcw"], atol=1e-6)

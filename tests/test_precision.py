@@ -71,3 +71,42 @@ def test_fp32_mode_is_repeatable_and_a_valid_option():
     with pytest.raises(lego_ba.LhError) as e:
         lego_ba.Solver(device=0, precision=2)
     assert e.value.status == lego_ba.LH_E_BADARG
+
+
+def test_config3_as_written_fp32_and_pcg_against_the_oracle_pcg():
+    """BASELINE configs[2] as written: C3 (20 KF / 50 k landmarks / 400 k observations), fp32 residual
+    path + fp64 accumulation AND Schur + PCG, together, against the oracle's (fixed) PCG
+    (problem.cpp:584-614, oracle/lego_oracle.c pcg_solve) on the reproducible C3 window: the same
+    iterations and trials, the final chi2 and the poses within 1e-6 (north star), landmarks 1e-6."""
+    import oracle_bind as ob
+    w = window("C3", seed=0, family="stable_noout")
+    s = lego_ba.Solver(device=0, precision=lego_ba.LH_PREC_FP32_RESID, linear_solver=lego_ba.LH_SOLVER_PCG)
+    g = s.solve(w)
+    assert s.controller() == "k_ctrl"
+    assert g["pcg_iterations"] > 0
+    o = ob.solve(w, linear_solver=1)
+    assert (g["iterations"], g["trials"]) == (o["iterations"], o["trials"])
+    assert rel(g["chi2_initial"], o["chi2_initial"]) < 1e-12
+    assert rel(g["chi2_final"], o["chi2_final"]) <= 1e-6
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-6)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-6)
+    # and the reference's own solver (LDLT) on the same window lands at the same chi2
+    r = ob.solve(w)
+    assert rel(g["chi2_final"], r["chi2_final"]) <= 1e-6
+
+
+def test_fp32_mode_on_the_live_c3_configuration_lands_in_the_oracle_envelope():
+    """The reference's live configuration at the headline size (survey-default C3: free gauge, left
+    image only, 2 % outliers, reference Huber gate) in the fp32 mode.  No summation order of the
+    reference reproduces this window (tests/test_live_config.py: 16 oracle thread counts, 16 outcomes),
+    so the fp32 solve must end inside the envelope of those 16 outcomes, its iteration count in their
+    range, with the initial chi2 bitwise the fp64 evaluation's."""
+    import oracle_bind as ob
+    w = window("C3", seed=0)
+    g = lego_ba.Solver(device=0, precision=lego_ba.LH_PREC_FP32_RESID).solve(w)
+    runs = [ob.solve(w, n_threads=t) for t in range(1, 17)]
+    chis = [r["chi2_final"] for r in runs]
+    its = [r["iterations"] for r in runs]
+    assert rel(g["chi2_initial"], runs[0]["chi2_initial"]) < 1e-12
+    assert min(chis) * (1 - 1e-6) <= g["chi2_final"] <= max(chis) * (1 + 1e-6)
+    assert min(its) <= g["iterations"] <= max(its)
