@@ -520,6 +520,9 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     static const int kBandSteps = 6 * LH_PMAX_ANY / 8;
     const bool band_possible = pl.P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && !getenv("LH_NO_BAND");
     h->band = false;
+    // k_lin's write-through record stores address both record buffers through one buffer descriptor
+    // (32-bit byte offsets): up to ~8.3 M landmarks per rank
+    if ((size_t)2 * pl.n_rec * LH_REC * sizeof(double) > (size_t)INT32_MAX) return LH_E_UNSUPPORTED;
     // a chunk window must fit one CU's LDS
     for (int T = 1; T <= LH_TMAX; ++T)
         if (pl.tgroup_begin[T + 1] > pl.tgroup_begin[T] && lh_lin_smem(T, pl.ncam) > (size_t)h->lds_limit)

@@ -291,11 +291,9 @@ __device__ __forceinline__ void edge_pc(const double* __restrict__ pt, const dou
     }
 }
 
-// residual_ = z - pi(K (ext (T X))), pi(q) = q / (q_z + 1e-18)   (lego_types.h:200-216); Pc = ext (T X)
-__device__ __forceinline__ void edge_residual(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
-                                              bool ext_rot, const double X[3], double u, double v, const lh_params& prm,
-                                              double& r0, double& r1, double Pc[3]) {
-    edge_pc(pt, e, ext_id, ext_rot, X, Pc);
+// residual_ = z - pi(K Pc), pi(q) = q / (q_z + 1e-18)   (lego_types.h:200-216), from the camera point
+__device__ __forceinline__ void edge_res_pc(const double Pc[3], double u, double v, const lh_params& prm, double& r0,
+                                            double& r1) {
     const double fx = prm.K[0], fy = prm.K[1], cx = prm.K[2], cy = prm.K[3];
     double p0 = fx * Pc[0] + cx * Pc[2];                  // + 0 * Pc[1]: exact
     double p1 = fy * Pc[1] + cy * Pc[2];
@@ -304,6 +302,13 @@ __device__ __forceinline__ void edge_residual(const double* __restrict__ pt, con
     p1 /= den;
     r0 = u - p0;
     r1 = v - p1;
+}
+// the whole residual, Pc = ext (T X) returned
+__device__ __forceinline__ void edge_residual(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
+                                              bool ext_rot, const double X[3], double u, double v, const lh_params& prm,
+                                              double& r0, double& r1, double Pc[3]) {
+    edge_pc(pt, e, ext_id, ext_rot, X, Pc);
+    edge_res_pc(Pc, u, v, prm, r0, r1);
 }
 
 // HuberCost::compute (cost_function.cpp:5-17) + computeRobustInformation (base_edge.cpp:44-64)
@@ -653,6 +658,35 @@ __device__ __forceinline__ double wave_max(double v) {
     return fmax(__longlong_as_double(((long long)hi[0] << 32) | lo[0]), __longlong_as_double(((long long)hi[1] << 32) | lo[1]));
 }
 
+// k_lin's outputs (pair rows, per-edge rho0, landmark records) are read by later kernels only.  Stored
+// plain, they sit dirty in the XCD's L2 and the kernel's end-of-launch release writes them back
+// (~B / 6 TB/s at the boundary, MI355X_MICROARCH.md "boundary").  Write-through (sc1) stores leave no
+// dirty line behind: k_lin 37.4 -> 36.2 us per trial launch.  LH_WT / LH_WT_REC = 0
+// restore plain stores (A/B builds).
+#ifndef LH_WT
+#define LH_WT 1
+#endif
+#ifndef LH_WT_REC
+#define LH_WT_REC 1
+#endif
+
+__device__ __forceinline__ void st_out(double* p, double v) {
+    if constexpr (LH_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+// a landmark record's 16-byte pieces (rec_rsrc: a buffer descriptor over the record buffer)
+__device__ __forceinline__ void st_rec2(double2* p, double2 v, __amdgpu_buffer_rsrc_t rsrc, const double* base) {
+    if constexpr (LH_WT_REC) {
+        const int off = (int)((const char*)p - (const char*)base);
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        v4i x;
+        __builtin_memcpy(&x, &v, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, off, 0, 16);   // aux 16: sc1 (write-through)
+    } else {
+        *p = v;
+    }
+}
+
 static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
 
 template <int T, bool TRIAL, bool F32>
@@ -726,6 +760,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
     double* __restrict__ rn = rec + (size_t)cand * nrec * LH_REC;
+    // a descriptor over both record buffers (write-through record stores, LH_WT_REC)
+    const __amdgpu_buffer_rsrc_t rec_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(rec, 0, (int)((size_t)2 * nrec * LH_REC * sizeof(double)), 0x00020000);
 
     v4d acc[Cfg::NT];
 #pragma unroll
@@ -964,13 +1001,13 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
                 double Pc[3];
                 edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
                 edge_robust(E, prm);
-                edge_rho[o] = E.rho0;
+                st_out(edge_rho + o, E.rho0);
                 chi_acc += E.rho0;
             }
             if (lead) {
                 double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
-                reinterpret_cast<double2*>(rw)[0] = double2{X[0], X[1]};
-                rw[2] = X[2];
+                st_rec2(reinterpret_cast<double2*>(rw), double2{X[0], X[1]}, rec_rsrc, rec);
+                st_out(rw + 2, X[2]);
             }
             continue;
         }
@@ -991,7 +1028,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             edge_robust(E, prm);
             if constexpr (F32) edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
             else edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
-            edge_rho[o] = E.rho0;
+            st_out(edge_rho + o, E.rho0);
             chi_acc += E.rho0;
             const bool inl = prm.huber_delta <= 0.0 || E.e2 <= prm.huber_delta * prm.huber_delta;
             wf_n[o] = inl ? 1 : 0;
@@ -1026,14 +1063,15 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
             if (deg) ndeg += 1.0;
             double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
-            reinterpret_cast<double2*>(rw)[0] = double2{X[0], X[1]};
-            reinterpret_cast<double2*>(rw)[1] = double2{X[2], i00};
-            reinterpret_cast<double2*>(rw)[2] = double2{l10, i11};
-            reinterpret_cast<double2*>(rw)[3] = double2{l20, l21};
-            reinterpret_cast<double2*>(rw)[4] = double2{i22, h[6]};
-            reinterpret_cast<double2*>(rw)[5] = double2{h[7], h[8]};
-            reinterpret_cast<double2*>(rw)[6] = double2{h[0], h[3]};
-            reinterpret_cast<double2*>(rw)[7] = double2{h[5], 0.0};
+            double2* r2 = reinterpret_cast<double2*>(rw);
+            st_rec2(r2 + 0, double2{X[0], X[1]}, rec_rsrc, rec);
+            st_rec2(r2 + 1, double2{X[2], i00}, rec_rsrc, rec);
+            st_rec2(r2 + 2, double2{l10, i11}, rec_rsrc, rec);
+            st_rec2(r2 + 3, double2{l20, l21}, rec_rsrc, rec);
+            st_rec2(r2 + 4, double2{i22, h[6]}, rec_rsrc, rec);
+            st_rec2(r2 + 5, double2{h[7], h[8]}, rec_rsrc, rec);
+            st_rec2(r2 + 6, double2{h[0], h[3]}, rec_rsrc, rec);
+            st_rec2(r2 + 7, double2{h[5], 0.0}, rec_rsrc, rec);
         }
         STAMP(2);
 
@@ -1183,10 +1221,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
                     if ((ra >> 4) > (rc >> 4)) { const int x = ra; ra = rc; rc = x; }
                     const int R = ra >> 4, Cc = rc >> 4;
                     const int idx = (R * T - (R * (R - 1)) / 2 + (Cc - R)) * 256 + (ra & 15) * 16 + (rc & 15);
-                    row[lane] = s0[idx] + s1[idx];
+                    st_out(row + lane, s0[idx] + s1[idx]);
                 }
                 if (s == t && lane < LH_TASKS)
-                    row[36 + lane] = s0[Cfg::LS_TASK + s * LH_TASKS + lane] + s1[Cfg::LS_TASK + s * LH_TASKS + lane];
+                    st_out(row + 36 + lane, s0[Cfg::LS_TASK + s * LH_TASKS + lane] + s1[Cfg::LS_TASK + s * LH_TASKS + lane]);
             }
     }
     double* gs = csc + (size_t)chunk * 4;

@@ -43,7 +43,8 @@ for step in "$@"; do
     echo "== $step" >> "$OUT/steps.log"
     case $name in
     tests)
-        timeout -k 10 900 python -u -m pytest ${arg:-tests} -m gpu -x -v -rf --timeout 300 --timeout-method thread \
+        arg=${arg:-tests}
+        timeout -k 10 900 python -u -m pytest ${arg//,/ } -m gpu -x -v -rf --timeout 300 --timeout-method thread \
             -p no:cacheprovider > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
         tail -1 "$OUT/tests.log" ;;
     smoke)
