@@ -136,13 +136,15 @@ def native_oracle():
         return None, "-O3 -ffp-contract=off -fopenmp (parity build; native build failed)"
 
 
-def cxx_caller_ms(w, reps, exe=None, line=False, env=None):
+def cxx_caller_ms(w, reps, exe=None, line=False, env=None, both=False):
     """Median wall time of lh_solve on this window from the compiled C++ caller (tests/abi_caller.cpp,
     window file format there), or None when the binary is missing or fails.  line: return the caller's
-    whole timing line (prep / upload / solve / download of the last call) instead."""
+    whole timing line (prep / upload / solve / download of the last call) instead.  both: a pair, the
+    call that downloads the per-edge chi2 and the call with the outlier pass on the device (flags only;
+    None unless its flags equal the host pass's)."""
     exe = exe or os.path.join(ROOT, "lego-slam_amd", "lib", "abi_caller")
     if not os.path.exists(exe):
-        return None
+        return None if not both else (None, None)
     O = len(w["obs_pose"])
     ext = w.get("cam_ext")
     fixed = w.get("pose_fixed")
@@ -168,10 +170,14 @@ def cxx_caller_ms(w, reps, exe=None, line=False, env=None):
                                env=None if env is None else {**os.environ, **env})
         except subprocess.TimeoutExpired:
             return None
+        out = {}
         for ln in r.stdout.splitlines():
             if "lh_solve median" in ln:
-                return ln if line else round(float(ln.split("lh_solve median")[1].split()[0]), 3)
-    return None
+                key = "device" if "device outlier pass" in ln else "chi2"
+                ok = key == "chi2" or "flags equal" in ln
+                out[key] = ln if line else (round(float(ln.split("lh_solve median")[1].split()[0]), 3) if ok else None)
+        return out.get("chi2") if not both else (out.get("chi2"), out.get("device"))
+    return None if not both else (None, None)
 
 
 def make_window(name, family, seed, rank, world):
@@ -381,10 +387,24 @@ def main():
         runs.append(((time.perf_counter() - t0) * 1e3, r))
     runs.sort(key=lambda x: x[0])
     ms_h, rh = runs[2]
-    cxx = cxx_caller_ms(w, 15)
+    cxx, cxx_dev = cxx_caller_ms(w, 15, both=True)
+    # the outlier pass on the device (ABI 5): the flags come back instead of the per-edge chi2
+    runs_d = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        rd = sh.solve(w, outlier_chi2_th=5.991, want_edges=False)
+        runs_d.append(((time.perf_counter() - t0) * 1e3, rd))
+    runs_d.sort(key=lambda x: x[0])
+    ms_d, rd = runs_d[2]
     out["host_buffer_path"] = {"ms_per_solve": round(ms_h, 3), "iterations_per_s": round(rh["iterations"] / ms_h * 1e3, 3),
                                "cxx_caller_ms_per_solve": cxx,
                                "cxx_caller_iterations_per_s": round(rh["iterations"] / cxx * 1e3, 3) if cxx else None,
+                               "device_outlier_pass": {"ms_per_solve": round(ms_d, 3), "cxx_caller_ms_per_solve": cxx_dev,
+                                                       "download_ms": round(rd["time_download_ms"], 3),
+                                                       "note": "the same call with Backend::Optimize's outlier pass on "
+                                                               "the device (lh_result.is_outlier): flags instead of the "
+                                                               "per-edge chi2 cross the link; the C++ caller checks its "
+                                                               "flags against the host pass"},
                                "prep_ms": round(rh["time_prep_ms"], 3),
                                "copies_ms": round(rh["time_upload_ms"] - rh["time_prep_ms"], 3),
                                "solve_ms": round(rh["time_ms"], 3), "download_ms": round(rh["time_download_ms"], 3),

@@ -17,7 +17,8 @@
  *     solve(iterations)            problem.cpp:156 lh_solve
  *     edge->getRobustChi2()        base_edge.cpp:33 lh_result.edge_robust_chi2
  *     vertex->getEstimate()        base_vertex.h:34 lh_result.pose_Tcw / lm_xyz
- *     outlier threshold loop       backend_lego.cpp:163-194 lh_classify_outliers
+ *     outlier threshold loop       backend_lego.cpp:163-194 lh_result.is_outlier (on the device, ABI 5)
+ *                                                                  or lh_classify_outliers (host, on edge_robust_chi2)
  *     Frontend::EstimateCurrentPose frontend_lego.cpp:157-250 lh_estimate_pose (batched)
  *     LKOpticalFlow4Layer / 1Layer  algorithm.cpp:11-206      lh_lk_track
  *     ~Problem                     problem.cpp:32 lh_destroy
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define LH_ABI_VERSION 4
+#define LH_ABI_VERSION 5   /* lh_create accepts 4 and 5; the lh_result fields marked ABI 5 are read only at 5 */
 
 typedef enum lh_status {
     LH_OK = 0,
@@ -76,7 +77,7 @@ typedef enum lh_comm_mode { LH_COMM_RCCL = 0, LH_COMM_HOST = 1 } lh_comm_mode;
 typedef int (*lh_allreduce_fn)(void *user, double *buf, int64_t count, int32_t op);
 
 typedef struct lh_options {
-    int32_t abi_version;      /* must be LH_ABI_VERSION                                      */
+    int32_t abi_version;      /* LH_ABI_VERSION (4 is still accepted: no ABI-5 lh_result fields)   */
     int32_t max_iters;        /* outer LM iterations, solve(10)          backend_lego.cpp:161 */
     int32_t max_trials;       /* false_cnt_threshold = 10                problem.cpp:178      */
     int32_t strategy;         /* lh_strategy                             problem.h:45         */
@@ -167,6 +168,17 @@ typedef struct lh_result {
     double time_prep_ms;       /* lh_solve / lh_upload: host preprocessing of the window           */
     double time_upload_ms;     /* lh_solve / lh_upload: preprocessing + host-to-device copies      */
     double time_download_ms;   /* device-to-host copies of the requested outputs                   */
+    /* ---- ABI 5 (read only when lh_options.abi_version >= 5) ---- */
+    uint8_t *is_outlier;       /* [n_obs] window order, or NULL.  Backend::Optimize's outlier pass
+                                  (backend_lego.cpp:163-194) on the device over rho0 as last evaluated:
+                                  starting from outlier_chi2_th, the threshold doubles (at most 5 times)
+                                  while the inlier ratio is <= 0.5, then is_outlier = rho0 > threshold.
+                                  Only the flags cross the link (edge_robust_chi2 may stay NULL); the
+                                  same result as lh_classify_outliers on edge_robust_chi2          */
+    double outlier_chi2_th;    /* in: the pass's starting threshold (the reference's 5.991, :92)  */
+    double outlier_th;         /* out: the threshold after the doubling loop                       */
+    int64_t n_inlier;          /* out: the loop's last counts (the reference's LOG line, :196)     */
+    int64_t n_outlier;
 } lh_result;
 
 typedef struct lh_kernel_stats {

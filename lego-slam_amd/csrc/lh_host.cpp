@@ -30,6 +30,8 @@ extern "C" {
 hipError_t lh_prepare_lin(int lds_limit);
 size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
+hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
+                              double th0, unsigned long long* cnt, uint8_t* flags, double* res);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
@@ -271,6 +273,10 @@ struct lh_handle {
     HostBuf<float> s_uv;                                     // pixels, 2 floats per slot
     HostBuf<double> s_lm, s_rs;                              // s_rs: the host-exchange buffer
     HostBuf<double> s_out;                                   // pinned staging of the download
+    DevBuf<unsigned long long> d_ocnt;                       // the outlier pass's counts (ABI 5)
+    DevBuf<uint8_t> d_oflag;                                 // its flags, window order
+    DevBuf<double> d_ores;                                   // its threshold and counts
+    HostBuf<uint8_t> s_oflag;                                // pinned staging of the flags
     hipEvent_t ev_staging = nullptr;   // the upload's last copy out of the staging (reused by the next upload)
     bool staging_pending = false;
 
@@ -887,6 +893,11 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
 // Results into the caller's buffers: device -> pinned staging in one stream (poses, landmark
 // positions gathered into window order, per-edge rho0), then the staging is copied out on the
 // planner's threads (a pageable device-to-host copy runs at a fraction of the link).
+// the ABI-5 outlier flags were asked for (lh_result.is_outlier; read only at ABI 5)
+bool wants_outliers(const lh_handle* h, const lh_result* out) {
+    return out && h->opt.abi_version >= 5 && out->is_outlier != nullptr;
+}
+
 int download(lh_handle* h, lh_result* out, int cur) {
     hipStream_t s = h->stream;
     const int P = h->P;
@@ -894,8 +905,37 @@ int download(lh_handle* h, lh_result* out, int cur) {
     const size_t np = out->pose_Tcw ? 12 * (size_t)P : 0;
     const size_t nl = (out->lm_xyz && h->L) ? 3 * (size_t)h->L : 0;
     const size_t ne = (out->edge_robust_chi2 && h->O) ? (size_t)h->O : 0;
-    if (np + nl + ne == 0) {
+    const bool fl = wants_outliers(h, out);
+    // a sharded window's pass would need every rank's counts (the reference counts the whole window's
+    // edges); a sharded caller classifies from edge_robust_chi2 after its own all-reduce of the counts
+    if (fl && (h->comm || h->host_comm)) return LH_E_UNSUPPORTED;
+    if (fl) {   // Backend::Optimize's outlier pass on the device (backend_lego.cpp:163-194): flags + 3 scalars
+        const size_t O = (size_t)h->O;
+        HIPCHK(h->d_ocnt.ensure(5));
+        HIPCHK(h->d_oflag.ensure(std::max<size_t>(O, 1)));
+        HIPCHK(h->d_ores.ensure(3));
+        HIPCHK(h->s_oflag.ensure(O + 3 * sizeof(double)));
+        HIPCHK(lh_launch_outliers(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)O, out->outlier_chi2_th,
+                                  h->d_ocnt.p, h->d_oflag.p, h->d_ores.p));
+        uint8_t* sf = h->s_oflag.p;
+        HIPCHK(hipMemcpyAsync(sf, h->d_ores.p, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (O) HIPCHK(hipMemcpyAsync(sf + 3 * sizeof(double), h->d_oflag.p, O, hipMemcpyDeviceToHost, s));
+    }
+    if (np + nl + ne == 0 && !fl) {
         out->time_download_ms = 0.0;
+        return LH_OK;
+    }
+    if (np + nl + ne == 0) {
+        HIPCHK(hipStreamSynchronize(s));
+        const uint8_t* sf = h->s_oflag.p;
+        double r3[3];
+        std::memcpy(r3, sf, sizeof(r3));
+        out->outlier_th = r3[0];
+        out->n_inlier = (int64_t)r3[1];
+        out->n_outlier = (int64_t)r3[2];
+        const ByteSeg seg_f = {out->is_outlier, sf + 3 * sizeof(double), (size_t)h->O};
+        par_copy(h, &seg_f, 1);
+        out->time_download_ms = now_ms() - t0;
         return LH_OK;
     }
     HIPCHK(h->s_out.ensure(np + nl + ne));
@@ -918,8 +958,17 @@ int download(lh_handle* h, lh_result* out, int cur) {
     const ByteSeg seg[2] = {{out->pose_Tcw, st, np * sizeof(double)}, {out->lm_xyz, st + np, nl * sizeof(double)}};
     par_copy(h, seg, 2);
     HIPCHK(hipStreamSynchronize(s));
-    const ByteSeg seg_e = {out->edge_robust_chi2, st + np + nl, ne * sizeof(double)};
-    par_copy(h, &seg_e, 1);
+    const ByteSeg seg_e[2] = {{out->edge_robust_chi2, st + np + nl, ne * sizeof(double)},
+                              {fl ? out->is_outlier : nullptr, fl ? h->s_oflag.p + 3 * sizeof(double) : nullptr,
+                               fl ? (size_t)h->O : 0}};
+    par_copy(h, seg_e, 2);
+    if (fl) {
+        double r3[3];
+        std::memcpy(r3, h->s_oflag.p, sizeof(r3));
+        out->outlier_th = r3[0];
+        out->n_inlier = (int64_t)r3[1];
+        out->n_outlier = (int64_t)r3[2];
+    }
     out->time_download_ms = now_ms() - t0;
     return LH_OK;
 }
@@ -937,8 +986,8 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     // No arrays wanted (and no collectives, profiling or printout): the summary comes with done in the
     // mapped words, and the solve returns when the host sees it; later work on this handle is stream-
     // ordered behind the solve's kernels (lh_destroy synchronises)
-    const bool fast = out && !out->pose_Tcw && !out->lm_xyz && !out->edge_robust_chi2 && !h->comm && !h->host_comm &&
-                      !h->opt.profile && !h->opt.verbose;
+    const bool fast = out && !out->pose_Tcw && !out->lm_xyz && !out->edge_robust_chi2 && !wants_outliers(h, out) &&
+                      !h->comm && !h->host_comm && !h->opt.profile && !h->opt.verbose;
     const double t_start = now_ms();
     h->n_coll = 0;
     HIPCHK(hipEventRecord(e0, s));
@@ -1182,7 +1231,7 @@ int lh_comm_unique_id(uint8_t out[128]) {
 int lh_create(lh_handle** hp, const lh_options* opt) {
     if (!hp || !opt) return LH_E_BADARG;
     *hp = nullptr;
-    if (opt->abi_version != LH_ABI_VERSION) return LH_E_BADARG;
+    if (opt->abi_version != LH_ABI_VERSION && opt->abi_version != 4) return LH_E_BADARG;
     if (opt->max_iters < 0 || opt->max_trials < 0 || opt->world_size < 1 || opt->rank < 0 ||
         opt->rank >= opt->world_size || (opt->strategy != 0 && opt->strategy != 1))
         return LH_E_BADARG;
@@ -1273,6 +1322,7 @@ void lh_destroy(lh_handle* h) {
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
     h->s_out.release();
+    h->d_ocnt.release(); h->d_oflag.release(); h->d_ores.release(); h->s_oflag.release();
     if (h->ev_staging) (void)hipEventDestroy(h->ev_staging);
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);

@@ -4377,6 +4377,71 @@ hipError_t lh_launch_gather(hipStream_t st, const lh_ctrl* ctrl, const double* r
     return hipGetLastError();
 }
 
+// ---- Backend::Optimize's outlier pass (backend_lego.cpp:163-194) on the device, over rho0 as last
+//      evaluated (d_rho, slot order).  The loop counts edges with rho0 > th for th = th0 2^k, k < 5 (the
+//      thresholds it can visit: doubling is exact), so one pass counts all five (integer adds: the same
+//      counts in any order); the second pass replays the loop on the counts and writes one flag per edge
+//      in window order.  Only the flags (1 byte per edge instead of 8) cross the link. ----
+__global__ __launch_bounds__(256) void k_outlier_count(const double* __restrict__ rho, const int32_t* __restrict__ obs_perm,
+                                                       long nslots, double th0, unsigned long long* __restrict__ cnt) {
+    unsigned c[5] = {0u, 0u, 0u, 0u, 0u};
+    const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
+    for (long i = i0; i < nslots; i += st) {
+        if (obs_perm[i] < 0) continue;   // padding slot
+        const double r = rho[i];
+        double th = th0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            c[k] += (r > th) ? 1u : 0u;   // a NaN rho0 counts as an inlier, as in the reference
+            th *= 2;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        unsigned v = c[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(cnt + k, (unsigned long long)v);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_outlier_flags(const double* __restrict__ rho, const int32_t* __restrict__ obs_perm,
+                                                       long nslots, long n_obs, double th0,
+                                                       const unsigned long long* __restrict__ cnt,
+                                                       uint8_t* __restrict__ flags, double* __restrict__ res) {
+    // backend_lego.cpp:164-184, on the counts (every thread the same)
+    double th = th0;
+    long cin = 0, cout = 0;
+    for (int it = 0; it < 5; ++it) {
+        cout = (long)cnt[it];
+        cin = n_obs - cout;
+        const double ratio = cin / double(cin + cout);
+        if (ratio > 0.5) break;
+        th *= 2;
+    }
+    const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
+    for (long i = i0; i < nslots; i += st) {   // :186-194
+        const int o = obs_perm[i];
+        if (o >= 0) flags[o] = rho[i] > th ? 1 : 0;
+    }
+    if (i0 == 0) {
+        res[0] = th;
+        res[1] = (double)cin;
+        res[2] = (double)cout;
+    }
+}
+
+hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
+                              double th0, unsigned long long* cnt, uint8_t* flags, double* res) {
+    if (nslots <= 0) return hipSuccess;
+    const int blocks = (int)std::max(1L, std::min(2048L, (nslots + 255) / 256));
+    hipError_t e = hipMemsetAsync(cnt, 0, 5 * sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_outlier_count, dim3(blocks), dim3(256), 0, st, rho, obs_perm, nslots, th0, cnt);
+    hipLaunchKernelGGL(k_outlier_flags, dim3(blocks), dim3(256), 0, st, rho, obs_perm, nslots, n_obs, th0,
+                       (const unsigned long long*)cnt, flags, res);
+    return hipGetLastError();
+}
+
 // ---- LDL^T probe (tests): x = (S)^-1 b through k_ctrl's LDS layout and lds_ldlt_solve (natural
 //      order, a dense envelope) or lds_pcg_solve, for a dense symmetric S (row-major n x n, n <= LH_NPAD) ----
 __global__ __launch_bounds__(CT) void k_ldlt_probe(const double* __restrict__ S, const double* __restrict__ b, int n,

@@ -9,7 +9,7 @@
 //     (:126-133); one edge per observation whose feature is live, not an outlier, on a live frame,
 //     and on exactly one image (left -> camera 0, right -> camera 1, :101-124);
 //   * problem.solve(10) (:161) -> lh_solve;
-//   * the outlier threshold loop (:163-194) -> lh_classify_outliers, then the feature flags and
+//   * the outlier threshold loop (:163-194) -> lh_result.is_outlier (the loop on the device), then the feature flags and
 //     MapPoint::RemoveObservation for the outliers (:186-194);
 //   * the write-back of every pose and landmark vertex (:198-217).
 // The SLAM types enter through a traits class (pose / position / pixel conversions: Sophus and Eigen in
@@ -170,11 +170,14 @@ int optimize_window(lh_handle* h, KeyframesT& keyframes, LandmarksT& landmarks, 
     r.n_edges = win.n_obs;
 
     // ---- problem.solve(10) (:161) ----
-    std::vector<double> pose_out(pose12.size()), xyz_out(xyz.size()), rchi2(obs_pose.size());
+    // ---- and the outlier pass (:163-194) on the device: only the flags come back (ABI 5) ----
+    std::vector<double> pose_out(pose12.size()), xyz_out(xyz.size());
+    std::vector<uint8_t> is_outlier(obs_pose.size());
     lh_result res{};
     res.pose_Tcw = pose_out.data();
     res.lm_xyz = xyz_out.data();
-    res.edge_robust_chi2 = rchi2.data();
+    res.is_outlier = is_outlier.data();
+    res.outlier_chi2_th = chi2_th0;
     r.status = lh_solve(h, &win, &res);
     if (r.status != LH_OK) {
         if (rep) *rep = r;
@@ -185,10 +188,10 @@ int optimize_window(lh_handle* h, KeyframesT& keyframes, LandmarksT& landmarks, 
     r.chi2_initial = res.chi2_initial;
     r.chi2_final = res.chi2_final;
 
-    // ---- outliers (:163-194) ----
-    std::vector<uint8_t> is_outlier(obs_pose.size());
-    lh_classify_outliers(rchi2.data(), (int64_t)rchi2.size(), chi2_th0, is_outlier.data(), &r.chi2_th, &r.n_inlier,
-                         &r.n_outlier);
+    // ---- outliers (:163-194): the threshold loop ran on the device; the features' flags here ----
+    r.chi2_th = res.outlier_th;
+    r.n_inlier = res.n_inlier;
+    r.n_outlier = res.n_outlier;
     for (size_t e = 0; e < obs_feature.size(); ++e) {
         auto& feat = obs_feature[e];
         if (is_outlier[e]) {

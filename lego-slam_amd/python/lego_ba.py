@@ -121,7 +121,7 @@ def config_window(name, seed=0, **kw):
 # --------------------------------------------------------------------------
 
 LH_OK, LH_E_EMPTY, LH_E_BADARG, LH_E_HIP, LH_E_RCCL, LH_E_UNSUPPORTED, LH_E_STATE = range(7)
-LH_ABI_VERSION = 4
+LH_ABI_VERSION = 5
 LH_SOLVER_LDLT, LH_SOLVER_PCG = 0, 1
 LH_PREC_FP64, LH_PREC_FP32_RESID = 0, 1
 LH_COMM_RCCL, LH_COMM_HOST = 0, 1
@@ -164,6 +164,9 @@ class LhResult(C.Structure):
         ("lambda_final", C.c_double), ("time_ms", C.c_double), ("pcg_iterations", C.c_int32),
         ("degenerate", C.c_int32), ("time_prep_ms", C.c_double), ("time_upload_ms", C.c_double),
         ("time_download_ms", C.c_double),
+        # ABI 5: Backend::Optimize's outlier pass on the device (backend_lego.cpp:163-194)
+        ("is_outlier", C.c_void_p), ("outlier_chi2_th", C.c_double), ("outlier_th", C.c_double),
+        ("n_inlier", C.c_int64), ("n_outlier", C.c_int64),
     ]
 
 
@@ -333,7 +336,8 @@ class Solver:
         except Exception:
             pass
 
-    def _result(self, n_poses, n_lm, n_obs, trace_cap=64, want_states=True, want_edges=True, reuse=None):
+    def _result(self, n_poses, n_lm, n_obs, trace_cap=64, want_states=True, want_edges=True, reuse=None,
+                outlier_chi2_th=None):
         def buf(key, shape, want):
             if not want:
                 return None
@@ -351,6 +355,10 @@ class Solver:
         r.edge_robust_chi2 = _ptr(out["edge_robust_chi2"])
         r.trace_chi2, r.trace_lambda = _ptr(out["trace_chi2"]), _ptr(out["trace_lambda"])
         r.trace_cap = trace_cap
+        if outlier_chi2_th is not None:   # the device outlier pass (ABI 5): flags instead of per-edge chi2
+            out["is_outlier"] = np.zeros(n_obs, np.uint8)
+            r.is_outlier = _ptr(out["is_outlier"])
+            r.outlier_chi2_th = float(outlier_chi2_th)
         return r, out
 
     @staticmethod
@@ -361,13 +369,19 @@ class Solver:
         for f in ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "time_ms",
                   "pcg_iterations", "degenerate", "time_prep_ms", "time_upload_ms", "time_download_ms"):
             out[f] = getattr(r, f)
+        if "is_outlier" in out:
+            out["is_outlier"] = out["is_outlier"].astype(bool)
+            out["outlier_th"], out["n_inlier"], out["n_outlier"] = r.outlier_th, r.n_inlier, r.n_outlier
         return out
 
-    def solve(self, w, trace_cap=64, reuse=None):
+    def solve(self, w, trace_cap=64, reuse=None, outlier_chi2_th=None, want_edges=True):
         """lh_solve on host buffers.  reuse: a previous call's result dict whose output arrays are
-        written again (a caller's persistent buffers) instead of freshly allocated ones."""
+        written again (a caller's persistent buffers) instead of freshly allocated ones.
+        outlier_chi2_th: also run Backend::Optimize's outlier pass on the device from that threshold
+        (is_outlier, outlier_th, n_inlier, n_outlier); want_edges=False then skips the per-edge chi2."""
         ref = _WindowRef(w)
-        r, out = self._result(ref.s.n_poses, ref.s.n_landmarks, ref.s.n_obs, trace_cap, reuse=reuse)
+        r, out = self._result(ref.s.n_poses, ref.s.n_landmarks, ref.s.n_obs, trace_cap, want_edges=want_edges,
+                              reuse=reuse, outlier_chi2_th=outlier_chi2_th)
         _check(ba_lib().lh_solve(self.h, C.byref(ref.s), C.byref(r)), "lh_solve")
         return self._finish(r, out)
 
@@ -375,9 +389,10 @@ class Solver:
         self._win = _WindowRef(w)
         _check(ba_lib().lh_upload(self.h, C.byref(self._win.s)), "lh_upload")
 
-    def solve_resident(self, want_states=False, want_edges=False, trace_cap=64):
+    def solve_resident(self, want_states=False, want_edges=False, trace_cap=64, outlier_chi2_th=None):
         s = self._win.s
-        r, out = self._result(s.n_poses, s.n_landmarks, s.n_obs, trace_cap, want_states, want_edges)
+        r, out = self._result(s.n_poses, s.n_landmarks, s.n_obs, trace_cap, want_states, want_edges,
+                              outlier_chi2_th=outlier_chi2_th)
         _check(ba_lib().lh_solve_resident(self.h, C.byref(r)), "lh_solve_resident")
         return self._finish(r, out)
 

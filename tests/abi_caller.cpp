@@ -10,6 +10,9 @@
 // caller's own, as Backend::Optimize keeps them), and the median wall time of one lh_solve is printed:
 // the drop-in call's cost as a C++ caller pays it (bench.py's host_buffer_path reports it).
 //
+// With reps > 0 it also times the call with the outlier pass on the device (lh_result.is_outlier, ABI 5:
+// flags instead of the per-edge chi2) and checks those flags against the host pass.
+//
 // window.bin:  int32 P, int32 L, int64 O, int32 ncam, int32 has_fixed, double K[4],
 //              double pose[P][12], uint8 fixed[P] (if has_fixed), double lm[L][3],
 //              uint32 obs_pose[O], uint32 obs_lm[O], uint8 obs_cam[O], double obs_uv[O][2],
@@ -92,6 +95,33 @@ int main(int argc, char** argv) {
         printf("abi_caller: lh_solve median %.4f ms over %d (min %.4f): prep %.4f upload %.4f solve %.4f download %.4f\n",
                ms[ms.size() / 2], (int)ms.size(), ms[0], res.time_prep_ms, res.time_upload_ms, res.time_ms,
                res.time_download_ms);
+        // the same call with the outlier pass on the device (ABI 5): the flags come back instead of the
+        // per-edge chi2 (backend_lego.cpp:163-194 as Backend::Optimize runs it, integration/lh_backend.h)
+        std::vector<uint8_t> dflag(O);
+        lh_result rd5{};
+        rd5.pose_Tcw = pose_out.data();
+        rd5.lm_xyz = lm_out.data();
+        rd5.is_outlier = dflag.data();
+        rd5.outlier_chi2_th = 5.991;
+        ms.clear();
+        for (int i = 0; i < reps && st == LH_OK; ++i) {
+            const auto t0 = std::chrono::steady_clock::now();
+            st = lh_solve(h, &win, &rd5);
+            ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+        if (st == LH_OK) {
+            std::sort(ms.begin(), ms.end());
+            std::vector<uint8_t> hflag(O);
+            double th = 0.0;
+            int64_t ni = 0, no = 0;
+            lh_classify_outliers(rchi2.data(), O, 5.991, hflag.data(), &th, &ni, &no);
+            const bool same = hflag == dflag && th == rd5.outlier_th && ni == rd5.n_inlier && no == rd5.n_outlier;
+            printf("abi_caller (device outlier pass): lh_solve median %.4f ms over %d (min %.4f): prep %.4f upload %.4f "
+                   "solve %.4f download %.4f; flags %s the host pass\n",
+                   ms[ms.size() / 2], (int)ms.size(), ms[0], rd5.time_prep_ms, rd5.time_upload_ms, rd5.time_ms,
+                   rd5.time_download_ms, same ? "equal" : "DIFFER from");
+            if (!same) st = LH_E_STATE;
+        }
     }
 
     // outlier pass (backend_lego.cpp:163-194)

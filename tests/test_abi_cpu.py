@@ -62,6 +62,8 @@ int main(void) {
   P(lh_window, n_obs) P(lh_window, K) P(lh_window, cam_ext)
   P(lh_result, trace_cap) P(lh_result, chi2_initial) P(lh_result, time_ms) P(lh_result, pcg_iterations)
   P(lh_result, degenerate) P(lh_result, time_prep_ms) P(lh_result, time_upload_ms) P(lh_result, time_download_ms)
+  P(lh_result, is_outlier) P(lh_result, outlier_chi2_th) P(lh_result, outlier_th) P(lh_result, n_inlier)
+  P(lh_result, n_outlier)
   return 0;
 }
 """
@@ -90,7 +92,7 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
 
 def test_default_options_mirror_reference_constants():
     o = lego_ba.default_options()
-    assert o.abi_version == lego_ba.LH_ABI_VERSION == 4
+    assert o.abi_version == lego_ba.LH_ABI_VERSION == 5
     assert o.precision == lego_ba.LH_PREC_FP64          # double throughout: the residual mirrors the reference
     assert o.gate_mode == 0 and o.degenerate_guard == 0   # the reference's Huber gate and LU semantics
     assert o.comm_mode == lego_ba.LH_COMM_RCCL and o.chunk_landmarks == 0 and not o.allreduce
