@@ -40,8 +40,8 @@ import lego_ba  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFS = 78.6       # MI355X FP64 spec (vector = matrix); measured on the box:
                            # v_mfma_f64_16x16x4 72.0 TF, v_fma_f64 60.5 TF (lego-slam_amd/tools/ubench_fp64_peak.hip)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04r_pmc_k_lin.json")
-ROCPROF_K_LIN = os.path.join(ROOT, "profiles", "r04r_rocprof_k_lin.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05h_pmc_k_lin.json")
+ROCPROF_K_LIN = os.path.join(ROOT, "profiles", "r05f_rocprof_k_lin.json")
 WORKLOADS = {"C3": dict(P=20, L=50_000, k=8), "C4": dict(P=20, L=500_000, k=8)}
 
 

@@ -31,7 +31,7 @@ hipError_t lh_prepare_lin(int lds_limit);
 size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
-                              double th0, unsigned long long* cnt, uint8_t* flags, double* res);
+                              double th0, unsigned* part, uint8_t* flags);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
@@ -273,9 +273,8 @@ struct lh_handle {
     HostBuf<float> s_uv;                                     // pixels, 2 floats per slot
     HostBuf<double> s_lm, s_rs;                              // s_rs: the host-exchange buffer
     HostBuf<double> s_out;                                   // pinned staging of the download
-    DevBuf<unsigned long long> d_ocnt;                       // the outlier pass's counts (ABI 5)
-    DevBuf<uint8_t> d_oflag;                                 // its flags, window order
-    DevBuf<double> d_ores;                                   // its threshold and counts
+    DevBuf<unsigned> d_ocnt;                                 // the outlier pass's per-block counts (ABI 5)
+    DevBuf<uint8_t> d_oflag;                                 // its flags (window order), then threshold and counts
     HostBuf<uint8_t> s_oflag;                                // pinned staging of the flags
     hipEvent_t ev_staging = nullptr;   // the upload's last copy out of the staging (reused by the next upload)
     bool staging_pending = false;
@@ -909,17 +908,14 @@ int download(lh_handle* h, lh_result* out, int cur) {
     // a sharded window's pass would need every rank's counts (the reference counts the whole window's
     // edges); a sharded caller classifies from edge_robust_chi2 after its own all-reduce of the counts
     if (fl && (h->comm || h->host_comm)) return LH_E_UNSUPPORTED;
+    const size_t o_res = ((size_t)h->O + 15) & ~(size_t)15;   // the scalars behind the flags: one copy
     if (fl) {   // Backend::Optimize's outlier pass on the device (backend_lego.cpp:163-194): flags + 3 scalars
-        const size_t O = (size_t)h->O;
-        HIPCHK(h->d_ocnt.ensure(5));
-        HIPCHK(h->d_oflag.ensure(std::max<size_t>(O, 1)));
-        HIPCHK(h->d_ores.ensure(3));
-        HIPCHK(h->s_oflag.ensure(O + 3 * sizeof(double)));
-        HIPCHK(lh_launch_outliers(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)O, out->outlier_chi2_th,
-                                  h->d_ocnt.p, h->d_oflag.p, h->d_ores.p));
-        uint8_t* sf = h->s_oflag.p;
-        HIPCHK(hipMemcpyAsync(sf, h->d_ores.p, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
-        if (O) HIPCHK(hipMemcpyAsync(sf + 3 * sizeof(double), h->d_oflag.p, O, hipMemcpyDeviceToHost, s));
+        HIPCHK(h->d_ocnt.ensure(5 * 256));
+        HIPCHK(h->d_oflag.ensure(o_res + 3 * sizeof(double)));
+        HIPCHK(h->s_oflag.ensure(o_res + 3 * sizeof(double)));
+        HIPCHK(lh_launch_outliers(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O, out->outlier_chi2_th,
+                                  h->d_ocnt.p, h->d_oflag.p));
+        HIPCHK(hipMemcpyAsync(h->s_oflag.p, h->d_oflag.p, o_res + 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     if (np + nl + ne == 0 && !fl) {
         out->time_download_ms = 0.0;
@@ -929,11 +925,11 @@ int download(lh_handle* h, lh_result* out, int cur) {
         HIPCHK(hipStreamSynchronize(s));
         const uint8_t* sf = h->s_oflag.p;
         double r3[3];
-        std::memcpy(r3, sf, sizeof(r3));
+        std::memcpy(r3, sf + o_res, sizeof(r3));
         out->outlier_th = r3[0];
         out->n_inlier = (int64_t)r3[1];
         out->n_outlier = (int64_t)r3[2];
-        const ByteSeg seg_f = {out->is_outlier, sf + 3 * sizeof(double), (size_t)h->O};
+        const ByteSeg seg_f = {out->is_outlier, sf, (size_t)h->O};
         par_copy(h, &seg_f, 1);
         out->time_download_ms = now_ms() - t0;
         return LH_OK;
@@ -959,12 +955,11 @@ int download(lh_handle* h, lh_result* out, int cur) {
     par_copy(h, seg, 2);
     HIPCHK(hipStreamSynchronize(s));
     const ByteSeg seg_e[2] = {{out->edge_robust_chi2, st + np + nl, ne * sizeof(double)},
-                              {fl ? out->is_outlier : nullptr, fl ? h->s_oflag.p + 3 * sizeof(double) : nullptr,
-                               fl ? (size_t)h->O : 0}};
+                              {fl ? out->is_outlier : nullptr, fl ? h->s_oflag.p : nullptr, fl ? (size_t)h->O : 0}};
     par_copy(h, seg_e, 2);
     if (fl) {
         double r3[3];
-        std::memcpy(r3, h->s_oflag.p, sizeof(r3));
+        std::memcpy(r3, h->s_oflag.p + o_res, sizeof(r3));
         out->outlier_th = r3[0];
         out->n_inlier = (int64_t)r3[1];
         out->n_outlier = (int64_t)r3[2];
@@ -1322,7 +1317,7 @@ void lh_destroy(lh_handle* h) {
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
     h->s_out.release();
-    h->d_ocnt.release(); h->d_oflag.release(); h->d_ores.release(); h->s_oflag.release();
+    h->d_ocnt.release(); h->d_oflag.release(); h->s_oflag.release();
     if (h->ev_staging) (void)hipEventDestroy(h->ev_staging);
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);

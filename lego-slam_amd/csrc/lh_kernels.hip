@@ -1062,16 +1062,22 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         if (lead) {
             maxd = fmax(maxd, fmax(fabs(h[0]), fmax(fabs(h[3]), fabs(h[5]))));
             if (deg) ndeg += 1.0;
-            double* rw = rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC;
-            double2* r2 = reinterpret_cast<double2*>(rw);
-            st_rec2(r2 + 0, double2{X[0], X[1]}, rec_rsrc, rec);
-            st_rec2(r2 + 1, double2{X[2], i00}, rec_rsrc, rec);
-            st_rec2(r2 + 2, double2{l10, i11}, rec_rsrc, rec);
-            st_rec2(r2 + 3, double2{l20, l21}, rec_rsrc, rec);
-            st_rec2(r2 + 4, double2{i22, h[6]}, rec_rsrc, rec);
-            st_rec2(r2 + 5, double2{h[7], h[8]}, rec_rsrc, rec);
-            st_rec2(r2 + 6, double2{h[0], h[3]}, rec_rsrc, rec);
-            st_rec2(r2 + 7, double2{h[5], 0.0}, rec_rsrc, rec);
+        }
+        if (lmok) {
+            // the record's eight 16-byte pieces from the landmark's lanes (every lane of the group holds the
+            // same bits: butterfly totals, then the same arithmetic), piece q by lane q mod G: with G = 8 the
+            // wave writes its 8 records as one contiguous 1 KB store (one piece per lane), whole 128-B lines
+            // through the write-through path (8 pieces from the lead lane were 8 partial-line writes)
+            double2* r2 = reinterpret_cast<double2*>(rn + ((size_t)sb * LH_SB_LM + ls) * LH_REC);
+            for (int q = gj; q < 8; q += 1 << lg) {
+                // piece q by a select tree on its bits (no divergent branches): 0 {X0, X1}, 1 {X2, i00},
+                // 2 {l10, i11}, 3 {l20, l21}, 4 {i22, b0}, 5 {b1, b2}, 6 {H00, H11}, 7 {H22, 0}
+                const bool q0 = q & 1, q1 = q & 2, q2 = q & 4;
+                const double x01 = q0 ? X[2] : X[0], x23 = q0 ? l20 : l10, x45 = q0 ? h[7] : i22, x67 = q0 ? h[5] : h[0];
+                const double y01 = q0 ? i00 : X[1], y23 = q0 ? l21 : i11, y45 = q0 ? h[8] : h[6], y67 = q0 ? 0.0 : h[3];
+                const double x03 = q1 ? x23 : x01, x47 = q1 ? x67 : x45, y03 = q1 ? y23 : y01, y47 = q1 ? y67 : y45;
+                st_rec2(r2 + q, double2{q2 ? x47 : x03, q2 ? y47 : y03}, rec_rsrc, rec);
+            }
         }
         STAMP(2);
 
@@ -4379,14 +4385,16 @@ hipError_t lh_launch_gather(hipStream_t st, const lh_ctrl* ctrl, const double* r
 
 // ---- Backend::Optimize's outlier pass (backend_lego.cpp:163-194) on the device, over rho0 as last
 //      evaluated (d_rho, slot order).  The loop counts edges with rho0 > th for th = th0 2^k, k < 5 (the
-//      thresholds it can visit: doubling is exact), so one pass counts all five (integer adds: the same
-//      counts in any order); the second pass replays the loop on the counts and writes one flag per edge
-//      in window order.  Only the flags (1 byte per edge instead of 8) cross the link. ----
+//      thresholds it can visit: doubling is exact), so one pass counts all five, as per-block partials
+//      (integers: the same totals in any order, and no counter to zero first); the second pass sums the
+//      partials, replays the loop on the totals and writes one flag per edge in window order, with the
+//      threshold and the counts behind the flags, so one copy brings all of it back. ----
+#define LH_OCB 256   // blocks of the counting pass
 __global__ __launch_bounds__(256) void k_outlier_count(const double* __restrict__ rho, const int32_t* __restrict__ obs_perm,
-                                                       long nslots, double th0, unsigned long long* __restrict__ cnt) {
+                                                       long nslots, double th0, unsigned* __restrict__ part) {
+    __shared__ unsigned wsum[4][5];
     unsigned c[5] = {0u, 0u, 0u, 0u, 0u};
-    const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
-    for (long i = i0; i < nslots; i += st) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nslots; i += (long)gridDim.x * 256) {
         if (obs_perm[i] < 0) continue;   // padding slot
         const double r = rho[i];
         double th = th0;
@@ -4396,23 +4404,40 @@ __global__ __launch_bounds__(256) void k_outlier_count(const double* __restrict_
             th *= 2;
         }
     }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         unsigned v = c[k];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(cnt + k, (unsigned long long)v);
+        if (lane == 0) wsum[wave][k] = v;
     }
+    __syncthreads();
+    if (threadIdx.x < 5)
+        part[blockIdx.x * 5 + threadIdx.x] = wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
 }
 
 __global__ __launch_bounds__(256) void k_outlier_flags(const double* __restrict__ rho, const int32_t* __restrict__ obs_perm,
-                                                       long nslots, long n_obs, double th0,
-                                                       const unsigned long long* __restrict__ cnt,
-                                                       uint8_t* __restrict__ flags, double* __restrict__ res) {
-    // backend_lego.cpp:164-184, on the counts (every thread the same)
+                                                       long nslots, long n_obs, double th0, const unsigned* __restrict__ part,
+                                                       int nparts, uint8_t* __restrict__ flags, double* __restrict__ res) {
+    __shared__ long tot[5];
+    if (threadIdx.x < 64) {
+        long c[5] = {0, 0, 0, 0, 0};
+        for (int b = threadIdx.x; b < nparts; b += 64)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) c[k] += part[b * 5 + k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            long v = c[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (threadIdx.x == 0) tot[k] = v;
+        }
+    }
+    __syncthreads();
+    // backend_lego.cpp:164-184, on the totals (every thread the same)
     double th = th0;
     long cin = 0, cout = 0;
     for (int it = 0; it < 5; ++it) {
-        cout = (long)cnt[it];
+        cout = tot[it];
         cin = n_obs - cout;
         const double ratio = cin / double(cin + cout);
         if (ratio > 0.5) break;
@@ -4430,15 +4455,16 @@ __global__ __launch_bounds__(256) void k_outlier_flags(const double* __restrict_
     }
 }
 
+// part: LH_OCB * 5 counters; flags: n_obs bytes, then (16-byte aligned) the threshold and the two counts
 hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
-                              double th0, unsigned long long* cnt, uint8_t* flags, double* res) {
+                              double th0, unsigned* part, uint8_t* flags) {
     if (nslots <= 0) return hipSuccess;
-    const int blocks = (int)std::max(1L, std::min(2048L, (nslots + 255) / 256));
-    hipError_t e = hipMemsetAsync(cnt, 0, 5 * sizeof(unsigned long long), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_outlier_count, dim3(blocks), dim3(256), 0, st, rho, obs_perm, nslots, th0, cnt);
-    hipLaunchKernelGGL(k_outlier_flags, dim3(blocks), dim3(256), 0, st, rho, obs_perm, nslots, n_obs, th0,
-                       (const unsigned long long*)cnt, flags, res);
+    const int nb_c = (int)std::max(1L, std::min((long)LH_OCB, (nslots + 255) / 256));
+    const int nb_f = (int)std::max(1L, std::min(2048L, (nslots + 255) / 256));
+    double* res = reinterpret_cast<double*>(flags + ((n_obs + 15) & ~15L));
+    hipLaunchKernelGGL(k_outlier_count, dim3(nb_c), dim3(256), 0, st, rho, obs_perm, nslots, th0, part);
+    hipLaunchKernelGGL(k_outlier_flags, dim3(nb_f), dim3(256), 0, st, rho, obs_perm, nslots, n_obs, th0,
+                       (const unsigned*)part, nb_c, flags, res);
     return hipGetLastError();
 }
 
