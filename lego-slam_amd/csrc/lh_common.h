@@ -25,6 +25,8 @@
 #define LH_MAX_CAMS 4
 #define LH_TRACE 64
 #define LH_NPAD 128           // reduced system padded size (LDS LDLT)
+#define LH_IMG_AS (LH_NPAD + 2)                 // k_ctrl's LDS row stride (doubles)
+#define LH_IMG_SZ ((LH_NPAD + 1) * LH_IMG_AS)   // k_ctrl's LDS system image: NP rows of S + the rhs row (doubles)
 
 // pair row (k_lin -> k_reduce): S block landmark part (36) | the pose's 33 sums (diagonal pairs) | pad
 #define LH_ROW 72
@@ -147,6 +149,10 @@ struct lh_params {
     int32_t nd_a, nd_s, nd_long_first, nd_steps;   // k_ctrl's two-chain split (lh_ctrl_nd_plan; nd_steps 0: off)
     int32_t commit_in_reduce;   // 1: k_reduce copies an accepted trial's staged blocks to the committed system
                                 //    before it overwrites them (k_ctrl_b: no one-CU copy of a large system)
+    int32_t img;            // 1: k_reduce writes S's lower triangle and b_s straight into k_ctrl's LDS layout
+                            //    (img[0] staged, img[1] committed; one rank, P <= LH_PMAX, one-chain LDL^T)
+    int32_t band_narrow;    // 1: every row's envelope starts at most 56 rows above its 8-row block (k_ctrl_b's back
+                            //    substitution holds one row per lane: a 64-row window)
     double K[4];
 };
 

@@ -40,12 +40,14 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          int writer);
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
-                            lh_params prm, int n_chunks, int mode, int* host_done, int seq);
+                            lh_params prm, int n_chunks, int mode, int* host_done, int seq, double* img);
+hipError_t lh_launch_img_init(hipStream_t st, double* img, int n);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS,
-                          const int32_t* brow_ptr, const uint32_t* brow_ent, const uint16_t* units, lh_band_args band);
+                          const int32_t* brow_ptr, const uint32_t* brow_ent, const uint16_t* units, lh_band_args band,
+                          double* img);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
@@ -287,6 +289,7 @@ struct lh_handle {
     View<int32_t> d_bblk;
     DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64)
     bool band = false;            // this window's LDL^T runs in k_ctrl_b
+    bool band_narrow = false;     // ... and every row's envelope starts within 56 rows of its 8-row block
     lh_ctrl_nd nd{};              // k_ctrl's two-chain schedule (nd.nsteps 0: the one-chain one)
     View<int32_t> d_lm_perm;
     View<double> d_ptab_init, d_qt_init, d_ext;
@@ -301,6 +304,7 @@ struct lh_handle {
     View<int32_t> d_brow_ptr;    // the reduced system's block rows (Plan::brow_ptr / brow_ent, k_ctrl_p)
     View<uint32_t> d_brow_ent;
     DevBuf<uint8_t> d_wflag;     // [2][n_slots] inlier flags of each state buffer's linearisation (k_lin)
+    DevBuf<double> d_img;        // [2][LH_IMG_SZ] k_ctrl's LDS system image, staged / committed (prm.img)
     // frontend pose-only batch (lh_estimate_pose)
     // inputs and outputs each packed into one arena, so a call is one upload and one download
     // through pinned staging (a single frame is latency-bound: every extra copy costs ~10 us)
@@ -525,6 +529,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     static const int kBandSteps = 6 * LH_PMAX_ANY / 8;
     const bool band_possible = pl.P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && !getenv("LH_NO_BAND");
     h->band = false;
+    h->band_narrow = false;
     // k_lin's write-through record stores address both record buffers through one buffer descriptor
     // (32-bit byte offsets): up to ~8.3 M landmarks per rank
     if ((size_t)2 * pl.n_rec * LH_REC * sizeof(double) > (size_t)INT32_MAX) return LH_E_UNSUPPORTED;
@@ -688,6 +693,10 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
             ok = lh_ctrl_units(n, fcb.data(), order, 11, kBandSteps, bunits.data()) <= 11;
         }
         h->band = ok;
+        // k_ctrl_b's one-row-per-lane back substitution: block KB's L rows reach no column below KB - 56
+        bool narrow = ok && !getenv("LH_NO_NARROW");
+        for (int r = 0; r < n && narrow; ++r) narrow = 6 * pf[r / 6] >= (r & ~7) - 56;
+        h->band_narrow = narrow;
     }
     if (P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
     if (h->band) {   // k_ctrl_b's L rows and ND blocks; L entries outside the envelope are never written: zero
@@ -767,6 +776,15 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.no_evo = getenv("LH_NO_EVO") != nullptr;
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
+    prm.band_narrow = h->band_narrow ? 1 : 0;
+    // k_reduce hands k_ctrl the system in its LDS layout (one rank, P <= LH_PMAX, the one-chain LDL^T;
+    // LH_NO_IMG=1: the packed system and k_ctrl's scatter, an A/B switch)
+    prm.img = (prm.dec_in_reduce && P <= LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && h->nd.nsteps == 0 &&
+               !getenv("LH_NO_IMG")) ? 1 : 0;
+    if (prm.img) {
+        HIPCHK(h->d_img.ensure(2 * (size_t)LH_IMG_SZ));
+        HIPCHK(lh_launch_img_init(h->stream, h->d_img.p, 6 * P));
+    }
     prm.nd_steps = h->nd.nsteps;
     prm.nd_a = h->nd.a;
     prm.nd_s = h->nd.s;
@@ -860,7 +878,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
         Prof pr(h, KC_REDUCE);
         HIPCHK(lh_launch_reduce(s, h->d_rows.p, h->d_csc.p, h->d_pair_ptr.p, h->d_pair_pq.p, h->d_ctrl.p,
                                 h->d_rs_stage.p, h->d_rs_commit.p, h->d_maxd.p, h->prm, h->plan.n_chunks, mode, h->d_done,
-                                h->cur_trial));
+                                h->cur_trial, h->d_img.p));
         DBGSYNC("k_reduce");
     }
     if (h->comm) {
@@ -883,7 +901,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
             HIPCHK(lh_launch_dense(s, h->d_rs_stage.p, h->d_pair_pq.p, h->d_ctrl.p, h->d_gS.p, h->P));
         HIPCHK(lh_launch_ctrl(s, h->d_ctrl.p, h->d_rs_commit.p, h->d_rs_stage.p, h->d_maxd.p, h->d_rsmap.p, h->d_pair_pq.p,
                               h->d_dxp.p, h->prm, mode, h->d_done, h->cur_trial, h->d_gA.p, h->d_gS.p, h->d_brow_ptr.p,
-                              h->d_brow_ent.p, h->d_units.p, band_args(h)));
+                              h->d_brow_ent.p, h->d_units.p, band_args(h), h->d_img.p));
         DBGSYNC("k_ctrl");
     }
     return LH_OK;
@@ -1311,7 +1329,7 @@ void lh_destroy(lh_handle* h) {
     h->d_uv.release(); h->d_rec.release(); h->d_ptab.release(); h->d_out_xyz.release(); h->d_out_rho.release();
     h->d_ptab_init.release(); h->d_qt.release(); h->d_qt_init.release(); h->d_ext.release(); h->d_rho.release();
     h->d_rows.release(); h->d_csc.release(); h->d_gA.release(); h->d_gS.release(); h->d_rs_stage.release(); h->d_rs_commit.release(); h->d_rsmap.release(); h->d_maxd.release(); h->d_band.release();
-    h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release(); h->d_fixed.release();
+    h->d_dxp.release(); h->d_ctrl.release(); h->d_wflag.release(); h->d_img.release(); h->d_fixed.release();
     h->d_brow_ptr.release(); h->d_brow_ent.release(); h->d_arena.release(); h->s_arena.release();
     h->s_chunks.release(); h->s_sbs.release(); h->s_meta.release(); h->s_items.release(); h->s_pair_ptr.release();
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
@@ -1699,6 +1717,7 @@ int lh_debug_controller(lh_handle* h, int* which) {
     if (!h || !which) return LH_E_BADARG;
     if (!h->uploaded) return LH_E_STATE;
     *which = h->P <= LH_PMAX ? 0 : h->band ? 3 : h->prm.solver == LH_SOLVER_PCG ? 2 : 1;
+    if (h->band_narrow) *which |= 1 << 8;   // k_ctrl_b's one-row-per-lane back substitution
     return LH_OK;
 }
 

@@ -1404,7 +1404,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                                                lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
                                                double* __restrict__ rs_commit, double* __restrict__ maxd_out,
                                                lh_params prm, int n_chunks, int mode, volatile int* __restrict__ host_done,
-                                               int seq) {
+                                               int seq, double* __restrict__ img) {
     STAMP_DECL
     __shared__ double part[3][RW][64];
     const lh_rs_layout LY = lh_rs_make(prm.P, prm.npairs);
@@ -1415,9 +1415,20 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_lin wrote the chunk scalars only
-    if (prm.commit_in_reduce && mode != 0 && b < LY.npairs && done == 0 && wave == 0) {
+    if ((prm.commit_in_reduce | prm.img) && mode != 0 && b < LY.npairs && done == 0 && wave == 0) {
         if (__builtin_amdgcn_readfirstlane(ctrl->acc_hist[(seq - 1) & 1])) {
-            if (lane < 36) rs_commit[LY.off_S + b * 36 + lane] = rs[LY.off_S + b * 36 + lane];
+            if (prm.img) {   // this pair's entries of k_ctrl's image (their slots below), then the rhs row's
+                if (lane < 36) {
+                    const int ea_ = lane / 6, eb_ = lane - 6 * (lane / 6), gi = 6 * p + ea_, gj = 6 * q + eb_;
+                    const int idx = (p < q) ? gj * LH_IMG_AS + gi : ((ea_ >= eb_) ? gi * LH_IMG_AS + gj : -1);
+                    if (idx >= 0) img[LH_IMG_SZ + idx] = img[idx];
+                } else if (p == q && lane < 42) {
+                    const int idx = LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36);
+                    img[LH_IMG_SZ + idx] = img[idx];
+                }
+            } else if (lane < 36) {
+                rs_commit[LY.off_S + b * 36 + lane] = rs[LY.off_S + b * 36 + lane];
+            }
             if (p == q && lane >= 36 && lane < 54) {
                 const int k = lane - 36, part_off = (k < 6) ? LY.off_bs : (k < 12) ? LY.off_bp : LY.off_hd;
                 const int i = part_off + 6 * p + (k % 6);
@@ -1495,7 +1506,16 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
         double s = 0.0, h = 0.0;
         for (int w = 0; w < RW; ++w) { s += part[0][w][lane]; h += part[1][w][lane]; }
         if (lane < 36) {
-            rs[LY.off_S + b * 36 + lane] = (diag ? h : 0.0) - s;
+            const double v = (diag ? h : 0.0) - s;
+            if (prm.img) {
+                // k_ctrl's LDS layout (prm.img): entry (a, bb) of block (p, q) is S(6p + a, 6q + bb); its lower
+                // slot only (the upper triangle stays zero in the image, where the factor writes L^T)
+                const int gi = 6 * p + a, gj = 6 * q + bb;
+                if (p < q) img[gj * LH_IMG_AS + gi] = v;
+                else if (a >= bb) img[gi * LH_IMG_AS + gj] = v;
+            } else {
+                rs[LY.off_S + b * 36 + lane] = v;
+            }
             if (diag && a == bb) rs[LY.off_hd + 6 * p + a] = h;
         }
         // b_p (lanes 36..41) and bs = b_p - bsd (needs lane + 6)
@@ -1503,6 +1523,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
         if (diag && lane >= 36 && lane < 42) {
             rs[LY.off_bp + 6 * p + (lane - 36)] = h;
             rs[LY.off_bs + 6 * p + (lane - 36)] = h - bsd;
+            if (prm.img) img[LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36)] = h - bsd;   // the rhs row
         }
     }
     STAMP(20);
@@ -2375,13 +2396,14 @@ __device__ __forceinline__ void ctrl_step_tail(lh_ctrl* __restrict__ ctrl, const
     }
 }
 
-template <int SOLVER>
+template <int SOLVER, bool IMG>
 __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double* __restrict__ rs_commit,
                                              const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                              const uint16_t* __restrict__ pair_pq, const uint16_t* __restrict__ units,
                                              double* __restrict__ dxp, lh_params prm, int mode /* 0 init, 1 trial */,
-                                             volatile int* __restrict__ host_done, int seq) {
-    __shared__ double A[(NP + 1) * AS];   // S + lambda D (lower); L^T above, D in place; row NP = rhs -> z / D
+                                             volatile int* __restrict__ host_done, int seq, double* __restrict__ img) {
+    // S + lambda D (lower); L^T above, D in place; row NP = rhs -> z / D
+    __shared__ __attribute__((aligned(16))) double A[(NP + 1) * AS];
     __shared__ __attribute__((aligned(16))) double dg[NP];   // the PCG's vector (16-byte reads)
     __shared__ double bpv[NP], hdv[NP], xs[NP];
     __shared__ uint16_t s_units[16 * LH_NSTEP];
@@ -2394,6 +2416,11 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
     const bool decided = mode != 0 && prm.dec_in_reduce;   // k_reduce took this trial's LM decision
     const bool nd = SOLVER == 0 && prm.nd_steps > 0;        // the two-chain LDL^T schedule
+    // k_reduce wrote S and b_s in this kernel's LDS layout (img[0] staged, img[1] committed): the system
+    // arrives by a straight copy, no index math per entry (the scatter below was 2.2 us of wave 0's time)
+    constexpr bool imgp = IMG;   // (the host sets prm.img only for SOLVER 0 without the two-chain schedule)
+    static_assert(AS == LH_IMG_AS && (NP + 1) * AS == LH_IMG_SZ && LH_IMG_SZ % 2 == 0, "k_reduce's image layout");
+    constexpr int IMG2 = LH_IMG_SZ / 2, NIMG = (IMG2 + CT - 1) / CT;
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
     // [160 + wave]: the wave's HW_ID word (SIMD in bits 5:4): which waves share wave 0's SIMD
@@ -2429,11 +2456,32 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int ibase = (tid < ER) ? tid : (1 << 30);   // threads past ER hold no element
     double vs[NLD];
     uint32_t mp[NLD];
+    double2 iv[NIMG];                   // imgp: this thread's double pairs tid + CT u of the image
+    double bpx = 0.0, hdx = 0.0;        // imgp: b_p and diag H_pp of row tid (the packed buffer)
+    const double2* __restrict__ img2 = reinterpret_cast<const double2*>(img);
+    // only the pairs that carry data are read (the lower triangle of the real rows and the rhs row: ~45 % of the
+    // image at C3); the rest are zeros or the identity padding, written without a load (img_need, img_fill)
+    auto img_need = [&](int k) {
+        const int e = 2 * k, row = e / AS, col = e - AS * row;
+        return k < IMG2 && ((row < n && col <= row) || (row == NP && col < n));
+    };
+    auto img_fill = [&](int k) {
+        const int e = 2 * k, row = e / AS, col = e - AS * row;
+        const bool pad = row >= n && row < NE;   // as k_img_init: identity on rows [n, NE)
+        return double2{(pad && col == row) ? 1.0 : 0.0, (pad && col + 1 == row) ? 1.0 : 0.0};
+    };
+    if constexpr (imgp) {
 #pragma unroll
-    for (int u = 0; u < NLD; ++u) {
-        const int i = u * ER + ibase;
-        vs[u] = (i < LY.total) ? rs_stage[i] : 0.0;
-        mp[u] = pqw[min(blk0 + (ER / 36) * u, max(LY.npairs - 1, 0))];
+        for (int u = 0; u < NIMG; ++u) iv[u] = img2[img_need(tid + CT * u) ? tid + CT * u : 0];
+        bpx = rs_stage[LY.off_bp + min(tid, n - 1)];
+        hdx = rs_stage[LY.off_hd + min(tid, n - 1)];
+    } else {
+#pragma unroll
+        for (int u = 0; u < NLD; ++u) {
+            const int i = u * ER + ibase;
+            vs[u] = (i < LY.total) ? rs_stage[i] : 0.0;
+            mp[u] = pqw[min(blk0 + (ER / 36) * u, max(LY.npairs - 1, 0))];
+        }
     }
     uint32_t unit2 = 0;   // two unit words per thread (SOLVER 0)
     if (SOLVER == 0 && tid < 8 * LH_NSTEP) unit2 = reinterpret_cast<const uint32_t*>(units)[tid];
@@ -2443,7 +2491,11 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // and committed, selected once the decision is known; the scatter leaves block 0 alone.
     const bool early0 = SOLVER == 0 && !(prm.nd_steps > 0) && n >= 8;
     double b0s[8], b0c[8];
-    if (early0 && wave == 0) {
+    if (imgp && early0 && wave == 0) {   // rows 0-7 of the staged image (the upper entries are zeros, unused)
+        const int r = lane & 7;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b0s[q] = img[r * AS + q];
+    } else if (!imgp && early0 && wave == 0) {
         const int r = lane & 7;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -2457,13 +2509,30 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         }
     }
 
+    // imgp: the staged image goes into LDS as it arrives, before the decision is known (a trial is accepted
+    // far more often than not; a rejected one overwrites it with the committed image); block 0 is wave 0's
+    // (a macro, not a lambda: a captured array would live in scratch memory)
+#define LH_IMG_TO_LDS()                                                                                        \
+    do {                                                                                                       \
+        double2* A2_ = reinterpret_cast<double2*>(A);                                                          \
+        _Pragma("unroll") for (int u = 0; u < NIMG; ++u) {                                                     \
+            const int k = tid + CT * u, e = 2 * k, row = e / AS, col = e - AS * row; /* AS even: no straddle */ \
+            if (k < IMG2 && !(early0 && row < 8 && col < 8)) A2_[k] = img_need(k) ? iv[u] : img_fill(k);      \
+        }                                                                                                      \
+    } while (0)
+    if constexpr (imgp) LH_IMG_TO_LDS();
+
     if (!decided) {
         if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
             double mx = 0.0;
+            if constexpr (imgp) {
+                if (tid < n) mx = fabs(hdx);
+            } else {
 #pragma unroll
-            for (int u = 0; u < NLD; ++u) {
-                const int i = u * ER + ibase;
-                if (i >= LY.off_hd && i < LY.off_hd + n) mx = fmax(mx, fabs(vs[u]));
+                for (int u = 0; u < NLD; ++u) {
+                    const int i = u * ER + ibase;
+                    if (i >= LY.off_hd && i < LY.off_hd + n) mx = fmax(mx, fabs(vs[u]));
+                }
             }
             for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
             if (lane == 0) s_red[wave] = mx;
@@ -2499,8 +2568,44 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
 #endif
     CSTAMP(1);
+#ifdef LH_STAMPS
+    if (tid == 0) __builtin_amdgcn_s_waitcnt(0);   // (diagnostic) thread 0's staged-system loads have arrived
+#endif
+    CSTAMP(2);
 
     // ---------------- 2. commit, diag + lambda, scatter into LDS (natural order) ----------------
+    if constexpr (imgp) {
+        // The image: a straight copy (16-byte LDS stores at consecutive addresses, issued above), lambda
+        // added on the diagonal of the real rows by the thread that stored it (the identity padding and the
+        // zero upper triangle come with the image).  k_reduce commits an accepted system to img[1] before
+        // the next trial overwrites img[0] (commit_in_reduce's role), so nothing here copies S.
+        if (!accept) {
+            const double2* __restrict__ imgc2 = reinterpret_cast<const double2*>(img + LH_IMG_SZ);
+#pragma unroll
+            for (int u = 0; u < NIMG; ++u) iv[u] = imgc2[img_need(tid + CT * u) ? tid + CT * u : 0];
+            bpx = rs_commit[LY.off_bp + min(tid, n - 1)];
+            hdx = rs_commit[LY.off_hd + min(tid, n - 1)];
+            if (early0 && wave == 0) {
+                const int r = lane & 7;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) b0s[q] = img[LH_IMG_SZ + r * AS + q];
+            }
+            LH_IMG_TO_LDS();
+        }
+#undef LH_IMG_TO_LDS
+#pragma unroll
+        for (int u = 0; u < NIMG; ++u) {
+            const int k = tid + CT * u, e = 2 * k, row = e / AS, col = e - AS * row;
+            if (k < IMG2 && row < n && (col == row || col + 1 == row) && !(early0 && row < 8)) {
+                double& d = A[row * AS + row];
+                d = (prm.strategy == 0) ? d + lambda : d + lambda * d;
+            }
+        }
+        if (tid < n) {
+            bpv[tid] = bpx;
+            hdv[tid] = hdx;
+        }
+    } else {
     if (!accept) {   // rollback: the committed system, with the new lambda
 #pragma unroll
         for (int u = 0; u < NLD; ++u) {
@@ -2553,13 +2658,15 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             A[c * AS + r] = 0.0;
         }
     }
+    }   // packed path
     if (SOLVER == 0 && tid < 8 * LH_NSTEP) reinterpret_cast<uint32_t*>(s_units)[tid] = unit2;
+    CSTAMP(3);
     if (early0 && wave == 0) {
         const int r = lane & 7;
         double v[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            double x = accept ? b0s[q] : b0c[q];
+            double x = (imgp || accept) ? b0s[q] : b0c[q];
             if (q == r) x = (prm.strategy == 0) ? x + lambda : x + lambda * x;
             v[q] = x;
         }
@@ -3012,6 +3119,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 // workgroup; the LM bookkeeping is k_reduce's (dec_in_reduce: one rank) or thread 0's (the initial
 // linearisation); k_reduce also commits accepted systems (commit_in_reduce), so nothing here copies S.
 // ============================================================================
+template <bool B> struct BoolTag { static constexpr bool value = B; };
 #define BNMAX (6 * LH_PMAX_ANY)         // largest reduced system (1536 rows)
 #define BSTEP_MAX (BNMAX / 8)           // LDL^T steps
 // the stream loaders: waves 12-15 (moving them off wave 0's SIMD, to 11 and 13-15, measured slower: the
@@ -3210,6 +3318,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                     unsigned long long lt1_ = __builtin_amdgcn_s_memtime();
                     if (wv == BZW && lane == 0) atomicAdd(&lh_stamps[56], lt1_ - lt0_);
 #endif
+#ifdef LH_BAND_WSLEEP
+                    __builtin_amdgcn_s_sleep(LH_BAND_WSLEEP);   // (A/B) the writes after the units' read burst
+#endif
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int r = 16 * Iw + 2 * k + lrow, c = 16 * (Iw - 7) + lcol;
@@ -3315,7 +3426,15 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             __hip_atomic_store(&bring_ready[j % BRING], j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     } else {
-        auto row_of = [&](int KB, int sl) { const int lo = KB - 120; return lo + ((lane + 64 * sl - lo) & 127); };
+      // NW (band_narrow: every row's envelope within 56 rows of its block): one held row per lane, the
+      // window [KB - 56, KB + 8); else two, the window [KB - 120, KB + 8)
+      auto consumer = [&](auto nw_tag) {
+        constexpr bool NW = decltype(nw_tag)::value;
+        constexpr int WROWS = NW ? 64 : 128;
+        auto row_of = [&](int KB, int sl) {
+            const int lo = KB + 8 - WROWS;
+            return lo + ((lane + 64 * sl - lo) & (WROWS - 1));
+        };
         // every block in [j0, j1] published (one round trip for the batch; producers run far ahead)
         auto wait_ready = [&](int j0, int j1) {
             for (;;) {
@@ -3341,20 +3460,20 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 l0[v] = p0[v * (LH_LBW - 1)];
-                l1[v] = p1[v * (LH_LBW - 1)];
+                l1[v] = NW ? 0.0 : p1[v * (LH_LBW - 1)];
             }
         };
         double y0, y1;
         {
             const int r0 = row_of(nb - 8, 0), r1 = row_of(nb - 8, 1);
             y0 = (r0 >= 0) ? z[r0] : 0.0;
-            y1 = (r1 >= 0) ? z[r1] : 0.0;
+            y1 = (!NW && r1 >= 0) ? z[r1] : 0.0;
         }
         // block j with its L entries ca / cb: x_b = ND_b y_b, then the held rows' updates
 #ifdef LH_STAMPS
         unsigned long long bs_[3] = {0, 0, 0}, ba_ = 0, bb_ = 0;
 #define BSUB_STAMP(i) do { __builtin_amdgcn_sched_barrier(0); bb_ = __builtin_amdgcn_s_memtime(); \
-        if ((i) >= 0) bs_[i] += bb_ - ba_; ba_ = bb_; __builtin_amdgcn_sched_barrier(0); } while (0)
+        if ((i) >= 0) bs_[(i) < 0 ? 0 : (i)] += bb_ - ba_; ba_ = bb_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define BSUB_STAMP(i)
 #endif
@@ -3368,9 +3487,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         auto solve_blk = [&](int j, const double (&ca)[8], const double (&cb)[8]) {
             BSUB_STAMP(-1);
             const int KB = nb - 8 - 8 * j;
-            const int sb_ = (KB >> 6) & 1, kl = KB & 63;
+            const int sb_ = NW ? 0 : (KB >> 6) & 1, kl = KB & 63;
             const bool mine = lane >= kl && lane < kl + 8;
-            const int re = KB - 128 + (lane - kl);                       // the row entering this lane's slot
+            const int re = KB - WROWS + (lane - kl);                     // the row entering this lane's slot
             const double zin = z[max(re, 0)];
             const double ys = sb_ ? y1 : y0;
             double yb[8];
@@ -3394,11 +3513,13 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             for (int v = 0; v < 8; ++v) xb[v] = readlane_d(xv, kl + v);
             const double sa = ((ca[0] * xb[0] + ca[1] * xb[1]) + (ca[2] * xb[2] + ca[3] * xb[3])) +
                               ((ca[4] * xb[4] + ca[5] * xb[5]) + (ca[6] * xb[6] + ca[7] * xb[7]));
-            const double sbb = ((cb[0] * xb[0] + cb[1] * xb[1]) + (cb[2] * xb[2] + cb[3] * xb[3])) +
-                               ((cb[4] * xb[4] + cb[5] * xb[5]) + (cb[6] * xb[6] + cb[7] * xb[7]));
             // rows past the band have zero L; the block's own rows (r >= KB) take no update
             if (row_of(KB, 0) < KB) y0 -= sa;
-            if (row_of(KB, 1) < KB) y1 -= sbb;
+            if constexpr (!NW) {
+                const double sbb = ((cb[0] * xb[0] + cb[1] * xb[1]) + (cb[2] * xb[2] + cb[3] * xb[3])) +
+                                   ((cb[4] * xb[4] + cb[5] * xb[5]) + (cb[6] * xb[6] + cb[7] * xb[7]));
+                if (row_of(KB, 1) < KB) y1 -= sbb;
+            }
             if (mine) {
                 y[KB + (lane - kl)] = xv;                                // the solution, natural order
                 const double zi = re >= 0 ? zin : 0.0;
@@ -3447,6 +3568,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         }
 #endif
 #undef BSUB_STAMP
+      };
+      if (prm.band_narrow) consumer(BoolTag<true>{});
+      else consumer(BoolTag<false>{});
     }
     __syncthreads();
     CSTAMP(8);
@@ -4273,10 +4397,24 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
 
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
                             const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
-                            lh_params prm, int n_chunks, int mode, int* host_done, int seq) {
+                            lh_params prm, int n_chunks, int mode, int* host_done, int seq, double* img) {
     const int npairs = prm.npairs;
     hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, rows, csc, pair_ptr, pair_pq, ctrl,
-                       rs_stage, rs_commit, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq);
+                       rs_stage, rs_commit, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq, img);
+    return hipGetLastError();
+}
+
+// k_ctrl's two LDS images (prm.img): zero (the upper triangle where the factor writes L^T, padding
+// columns) with the identity on the padding rows [n, ne); k_reduce fills the lower triangle and the rhs
+__global__ __launch_bounds__(256) void k_img_init(double* __restrict__ img, int n, int ne) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * LH_IMG_SZ; i += gridDim.x * 256) {
+        const int e = i % LH_IMG_SZ, r = e / LH_IMG_AS, c = e - LH_IMG_AS * r;
+        img[i] = (r == c && r >= n && r < ne) ? 1.0 : 0.0;
+    }
+}
+
+hipError_t lh_launch_img_init(hipStream_t st, double* img, int n) {
+    hipLaunchKernelGGL(k_img_init, dim3(64), dim3(256), 0, st, img, n, (n + 15) & ~15);
     return hipGetLastError();
 }
 
@@ -4291,7 +4429,7 @@ hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_
 hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, const double* rs_stage, const double* maxd,
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
-                          const uint32_t* brow_ent, const uint16_t* units, lh_band_args band) {
+                          const uint32_t* brow_ent, const uint16_t* units, lh_band_args band, double* img) {
     if (prm.P > LH_PMAX && prm.solver == 0 && band.bblk)
         hipLaunchKernelGGL(k_ctrl_b, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk, band.units,
                            band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq);
@@ -4302,11 +4440,14 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
-        hipLaunchKernelGGL(k_ctrl<1>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units, dxp,
-                           prm, mode, (volatile int*)host_done, seq);
+        hipLaunchKernelGGL((k_ctrl<1, false>), dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
+                           dxp, prm, mode, (volatile int*)host_done, seq, img);
+    else if (prm.img)
+        hipLaunchKernelGGL((k_ctrl<0, true>), dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
+                           dxp, prm, mode, (volatile int*)host_done, seq, img);
     else
-        hipLaunchKernelGGL(k_ctrl<0>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units, dxp,
-                           prm, mode, (volatile int*)host_done, seq);
+        hipLaunchKernelGGL((k_ctrl<0, false>), dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq,
+                           units, dxp, prm, mode, (volatile int*)host_done, seq, img);
     return hipGetLastError();
 }
 
@@ -4318,20 +4459,20 @@ __global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const 
                                                double* __restrict__ qt, const double* __restrict__ qt_init, int nqt,
                                                double* __restrict__ ptab, const double* __restrict__ ptab_init, int nptab,
                                                double* __restrict__ dxp, int ndxp, lh_ctrl* __restrict__ ctrl) {
-    // one thread per 16-B piece of a record (8 per record)
-    const long n2 = (long)nrec * (LH_REC / 2);
+    // one thread per 16-B piece of X in a record of buffer 0 (the first two of its eight): the initial
+    // linearisation reads only X (no back substitution) and writes every piece of buffer 1, and each later
+    // linearisation rewrites its candidate buffer whole, so the rest of buffer 0 is never read first
+    const long n2 = (long)nrec * 2;
     const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
     for (long i = i0; i < n2; i += st) {
-        const int r = (int)(i >> 3), q = (int)(i & 7);
+        const int r = (int)(i >> 1), q = (int)(i & 1);
         double2 v = {0.0, 0.0};
-        if (q < 2) {
-            const int l = lm_perm[r];
-            if (l >= 0) {
-                const double* X = lm_in + 3 * (size_t)l;
-                v = (q == 0) ? double2{X[0], X[1]} : double2{X[2], 0.0};
-            }
+        const int l = lm_perm[r];
+        if (l >= 0) {
+            const double* X = lm_in + 3 * (size_t)l;
+            v = (q == 0) ? double2{X[0], X[1]} : double2{X[2], 0.0};
         }
-        rec[i] = v;
+        rec[(size_t)r * (LH_REC / 2) + q] = v;
     }
     if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < nqt; i += 256) qt[i] = qt_init[i];
@@ -4345,7 +4486,7 @@ __global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const 
 hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
                            double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
                            double* dxp, int ndxp, lh_ctrl* ctrl) {
-    const long n2 = (long)nrec * (LH_REC / 2);
+    const long n2 = (long)nrec * 2;
     const int blocks = (int)std::max(1L, std::min(2048L, (n2 + 255) / 256));
     hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, st, reinterpret_cast<double2*>(rec), lm_perm, lm_in, nrec,
                        qt, qt_init, nqt, ptab, ptab_init, nptab, dxp, ndxp, ctrl);

@@ -473,7 +473,14 @@ class Solver:
         or 'k_ctrl_b'."""
         v = C.c_int(0)
         _check(ba_lib().lh_debug_controller(self.h, C.byref(v)), "lh_debug_controller")
-        return ("k_ctrl", "k_ctrl_g", "k_ctrl_p", "k_ctrl_b")[v.value]
+        return ("k_ctrl", "k_ctrl_g", "k_ctrl_p", "k_ctrl_b")[v.value & 0xff]
+
+    def band_narrow(self):
+        """k_ctrl_b runs its one-row-per-lane back substitution (every row's envelope within 56 rows of its
+        8-row block; lh_debug_controller bit 8)."""
+        v = C.c_int(0)
+        _check(ba_lib().lh_debug_controller(self.h, C.byref(v)), "lh_debug_controller")
+        return bool(v.value >> 8 & 1)
 
     def comm_count(self):
         """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""

@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import lego_ba  # noqa: E402
 from windows import window  # noqa: E402
 
-NAMES = ["start", "prefetch + LM decision", "commit + diag", "pivot rank", "scatter into LDS", "block 0 factor",
+NAMES = ["start", "prefetch + LM decision", "staged system arrived", "wave 0's scatter share", "block 0 factor + barrier", "unit words",
          "LDLT steps", "back substitution", "dx scatter", "trig / q_T", "pose compose", "pose / table stores", "tail"]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 if cfg.startswith("P"):   # P<n>: an n-keyframe window of C3's size (n > 21: k_ctrl_g; its phase 5 is unused)

@@ -97,8 +97,8 @@ for step in "$@"; do
         scr=${arg%%,*}
         rest=""
         [ "$scr" != "$arg" ] && rest=${arg#*,}
-        timeout -k 10 600 python3 $scr ${rest//,/ } > "$OUT/$(basename $scr .py).log" 2>&1 || { tail -30 "$OUT/$(basename $scr .py).log"; exit 1; }
-        tail -30 "$OUT/$(basename $scr .py).log" ;;
+        timeout -k 10 600 python3 $scr ${rest//,/ } > "$OUT/$(basename $scr .py)$SFX.log" 2>&1 || { tail -30 "$OUT/$(basename $scr .py)$SFX.log"; exit 1; }
+        tail -30 "$OUT/$(basename $scr .py)$SFX.log" ;;
     env)
         export "$arg"
         SFX="_${arg//[^A-Za-z0-9]/_}" ;;

@@ -389,6 +389,51 @@ def test_banded_ldlt_past_64_keyframes(P, L, seed):
     assert np.allclose(gf["lm_xyz"], of["lm_xyz"], atol=1e-6)
 
 
+def test_banded_back_substitution_row_windows(monkeypatch):
+    """k_ctrl_b's back substitution holds one row per lane when every row's envelope starts within 56 rows of
+    its 8-row block (8-keyframe runs: 47 rows), two rows per lane otherwise.  A row takes the same products
+    in the same order either way, so on a narrow window the two forms agree bitwise (LH_NO_NARROW=1 forces
+    the two-row form)."""
+    w = _stable_window(128, 8000, 3)
+    s = lego_ba.Solver()
+    a = s.solve(w)
+    assert s.controller() == "k_ctrl_b" and s.band_narrow()
+    monkeypatch.setenv("LH_NO_NARROW", "1")
+    t = lego_ba.Solver()
+    b = t.solve(w)
+    assert t.controller() == "k_ctrl_b" and not t.band_narrow()
+    assert a["iterations"] == b["iterations"] and a["trials"] == b["trials"]
+    assert a["chi2_final"] == b["chi2_final"]
+    assert np.array_equal(a["pose_Tcw"], b["pose_Tcw"]) and np.array_equal(a["lm_xyz"], b["lm_xyz"])
+    s.close()
+    t.close()
+
+
+def test_banded_ldlt_wide_band():
+    """A banded window whose landmarks span 11 keyframes: rows reach 60-70 columns back, past the
+    one-row-per-lane back substitution's 56, so k_ctrl_b holds two rows per lane.  (Runs of 15, the reference's
+    window length, make chunk windows of 16 poses: 13 units in a step, past k_ctrl_b's 11, so LDL^T refuses
+    them past 64 keyframes and PCG takes them.)  One trial at the single-trial bar, the full solve against the
+    oracle's LDLT."""
+    w = lego_ba.generate_window(P=96, L=6000, k=11, seed=2, **dict(__import__("windows").STABLE, outlier_frac=0.0))
+    f = np.zeros(96, np.uint8)
+    f[0] = 1
+    w["pose_fixed"] = f
+    s1 = lego_ba.Solver(max_iters=1, max_trials=1)
+    g = s1.solve(w)
+    assert s1.controller() == "k_ctrl_b" and not s1.band_narrow()
+    o = ob.solve(w, max_iters=1, max_trials=1)
+    assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
+    assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
+    assert np.allclose(g["lm_xyz"], o["lm_xyz"], atol=1e-7)
+    gf = lego_ba.Solver().solve(w)
+    of, spread, its = oracle_envelope(w, threads=(1, 8))
+    assert gf["iterations"] in its
+    assert rel(gf["chi2_final"], of["chi2_final"]) < max(1e-6, 10 * spread)
+    assert np.allclose(gf["pose_Tcw"], of["pose_Tcw"], atol=1e-6)
+    assert np.allclose(gf["lm_xyz"], of["lm_xyz"], atol=1e-6)
+
+
 def test_large_window_strategy1():
     """STRATEGY1 (lambda scaled by the diagonal, problem.cpp:420) on a 32-keyframe window: one trial
     at the single-trial bar, the full solve inside the oracle's envelope."""
