@@ -153,6 +153,8 @@ struct lh_params {
                             //    (img[0] staged, img[1] committed; one rank, P <= LH_PMAX, one-chain LDL^T)
     int32_t band_narrow;    // 1: every row's envelope starts at most 56 rows above its 8-row block (k_ctrl_b's back
                             //    substitution holds one row per lane: a 64-row window)
+    int32_t bimg;           // 1: k_reduce writes S's lower band straight into k_ctrl_b's band image (one rank, banded
+                            //    LDL^T): the stream loaders read it without the block-index round trip
     double K[4];
 };
 
@@ -229,6 +231,19 @@ LH_HD static inline int lh_ctrl_units(int n, const int32_t* tile_fcb, const int*
 #define LH_ORDER_CTRL {1, 2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12}
 // k_ctrl_b: waves 12-15 stream tile rows into the window instead
 #define LH_ORDER_BAND {1, 2, 3, 5, 6, 7, 9, 10, 11, 4, 8}
+
+// k_ctrl_b's band image (prm.bimg): tile row I (rows 16 I .. 16 I + 15) holds columns 16 (I - 7) .. 16 I + 15,
+// 128 per row, the order k_ctrl_b's stream loaders read (a banded window's rows start at or after column
+// 16 I - 104, lh_host.cpp); two copies (staged, committed) of ceil16(6P) / 16 tile rows each
+#define LH_BIMG_TR (16 * 128)
+LH_HD static inline int lh_bimg_idx(int r, int c) {
+    const int I = r >> 4;
+    return I * LH_BIMG_TR + (r & 15) * 128 + (c - 16 * (I - 7));
+}
+LH_HD static inline bool lh_bimg_in(int r, int c) {
+    const int o = c - 16 * ((r >> 4) - 7);
+    return c <= r && o >= 0 && o < 128;
+}
 
 // k_ctrl_b's per-window tables (bblk null: no banded controller for this window)
 struct lh_band_args {

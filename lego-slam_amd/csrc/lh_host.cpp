@@ -777,6 +777,14 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
     prm.band_narrow = h->band_narrow ? 1 : 0;
+    // k_reduce writes the band straight into k_ctrl_b's loader order (one rank; LH_NO_BIMG=1: the packed
+    // blocks and the loaders' block-index round trip, an A/B switch)
+    prm.bimg = (h->band && prm.dec_in_reduce && !getenv("LH_NO_BIMG")) ? 1 : 0;
+    if (prm.bimg) {   // entries no pair block writes stay zero: cleared per window
+        const size_t nbi = 2 * (size_t)((6 * P + 15) >> 4) * LH_BIMG_TR;
+        HIPCHK(h->d_img.ensure(nbi));
+        HIPCHK(hipMemsetAsync(h->d_img.p, 0, nbi * sizeof(double), h->stream));
+    }
     // k_reduce hands k_ctrl the system in its LDS layout (one rank, P <= LH_PMAX, the one-chain LDL^T;
     // LH_NO_IMG=1: the packed system and k_ctrl's scatter, an A/B switch)
     prm.img = (prm.dec_in_reduce && P <= LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && h->nd.nsteps == 0 &&

@@ -1426,6 +1426,13 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                     const int idx = LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36);
                     img[LH_IMG_SZ + idx] = img[idx];
                 }
+            } else if (prm.bimg) {   // this pair's entries of k_ctrl_b's band image
+                const int bsz = ((6 * prm.P + 15) >> 4) * LH_BIMG_TR;
+                if (lane < 36) {
+                    const int ea_ = lane / 6, eb_ = lane - 6 * (lane / 6), gi = 6 * p + ea_, gj = 6 * q + eb_;
+                    const int r_ = (p < q) ? gj : gi, c_ = (p < q) ? gi : gj;
+                    if ((p < q || ea_ >= eb_) && lh_bimg_in(r_, c_)) img[bsz + lh_bimg_idx(r_, c_)] = img[lh_bimg_idx(r_, c_)];
+                }
             } else if (lane < 36) {
                 rs_commit[LY.off_S + b * 36 + lane] = rs[LY.off_S + b * 36 + lane];
             }
@@ -1513,6 +1520,10 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                 const int gi = 6 * p + a, gj = 6 * q + bb;
                 if (p < q) img[gj * LH_IMG_AS + gi] = v;
                 else if (a >= bb) img[gi * LH_IMG_AS + gj] = v;
+            } else if (prm.bimg) {
+                // k_ctrl_b's band image (prm.bimg): the lower slot, (row, column) = (6q + bb, 6p + a) for p < q
+                const int gi = 6 * p + a, gj = 6 * q + bb, r_ = (p < q) ? gj : gi, c_ = (p < q) ? gi : gj;
+                if ((p < q || a >= bb) && lh_bimg_in(r_, c_)) img[lh_bimg_idx(r_, c_)] = v;
             } else {
                 rs[LY.off_S + b * 36 + lane] = v;
             }
@@ -3126,7 +3137,11 @@ template <bool B> struct BoolTag { static constexpr bool value = B; };
 // wave forming z then set the step); wave 12 also forms z and copies ND out
 __device__ __forceinline__ bool band_loader(int w) { return w >= 12; }
 __device__ __forceinline__ int band_loader_slot(int w) { return w - 12; }
-#define BZW 12
+#ifndef LH_BZW
+#define LH_BZW 8   // the wave that forms z and copies ND out: a unit wave idle in most steps (wave 12, a loader:
+                    // P = 128 0.2113 against 0.2104 ms per trial, profiles/r05l_band_ab_bzw8.txt)
+#endif
+#define BZW LH_BZW
 
 // S(r, c), c <= r < n, of the packed system: block (pose(c), pose(r)) through the per-window table
 // bblk[p * 64 + d] (the block of pose pair (p, p + d), -1 where no chunk couples them)
@@ -3148,7 +3163,8 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                                                const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                                const int32_t* __restrict__ bblk, const uint16_t* __restrict__ bunits,
                                                double* __restrict__ Lg, double* __restrict__ NDg, double* __restrict__ dxp,
-                                               lh_params prm, int mode, volatile int* __restrict__ host_done, int seq) {
+                                               lh_params prm, int mode, volatile int* __restrict__ host_done, int seq,
+                                               const double* __restrict__ bimg) {
     __shared__ __attribute__((aligned(16))) double A[128 * AS];   // the circular window of the lower band
     __shared__ __attribute__((aligned(16))) double y[BNMAX];   // rhs (forward substitution), then x
     __shared__ double z[BNMAX];                             // D^-1 L^-1 b
@@ -3216,6 +3232,10 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
 #endif
     CSTAMP(1);
     const double* __restrict__ src = accept ? rs_stage : rs_commit;
+    // prm.bimg: k_reduce wrote the band in the loaders' order (lh_bimg_idx; staged, then committed): one load per
+    // element, no block-index round trip before it
+    const bool bim = prm.bimg != 0;
+    const double* __restrict__ bsrc = bimg + (accept ? 0 : (size_t)NT * LH_BIMG_TR);
 
     // ---------------- the rhs, the first 8 tile rows, this wave's unit words ----------------
     for (int i = tid; i < NE; i += CT) {
@@ -3229,12 +3249,28 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         constexpr int PER = 128 * 128 / CT;
         const int c0 = tid & 127, rr = tid >> 7;
         int bk[PER];
+        if (bim) {
+            double bv[PER];
 #pragma unroll
-        for (int k = 0; k < PER; ++k) bk[k] = band_block(bblk, 8 * k + rr, c0, n);
+            for (int k = 0; k < PER; ++k) {
+                const int r = 8 * k + rr;
+                bv[k] = (r < NE && c0 <= r) ? bsrc[lh_bimg_idx(r, c0)] : 0.0;
+            }
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int r = 8 * k + rr;
-            A[r * AS + c0] = (r < NE && c0 <= r) ? band_value(src, bk[k], r, c0, lambda, prm.strategy, n) : 0.0;
+            for (int k = 0; k < PER; ++k) {
+                const int r = 8 * k + rr;
+                double v = bv[k];
+                if (r == c0) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
+                A[r * AS + c0] = v;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) bk[k] = band_block(bblk, 8 * k + rr, c0, n);
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const int r = 8 * k + rr;
+                A[r * AS + c0] = (r < NE && c0 <= r) ? band_value(src, bk[k], r, c0, lambda, prm.strategy, n) : 0.0;
+            }
         }
     }
     uint32_t uwa = 0, uwb = 0;   // this wave's unit words: steps 2j, 2j + 1 in u32 j (lane j, lane j + 64)
@@ -3316,29 +3352,50 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                     __builtin_amdgcn_s_waitcnt(0);
                     __builtin_amdgcn_sched_barrier(0);
                     unsigned long long lt1_ = __builtin_amdgcn_s_memtime();
-                    if (wv == BZW && lane == 0) atomicAdd(&lh_stamps[56], lt1_ - lt0_);
+                    if (wv == 12 && lane == 0) atomicAdd(&lh_stamps[56], lt1_ - lt0_);
 #endif
-#ifdef LH_BAND_WSLEEP
-                    __builtin_amdgcn_s_sleep(LH_BAND_WSLEEP);   // (A/B) the writes after the units' read burst
-#endif
+                    if (bim) {
+                        // pairs: lane lq holds columns 2 (lq mod 64) + {0, 1} of rows 16 Iw + 4 k + lq / 64 (lval[2k],
+                        // lval[2k + 1]): one 16-byte store each, consecutive lanes on consecutive pairs
+                        const int c = 16 * (Iw - 7) + 2 * (lq & 63);
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int r = 16 * Iw + 2 * k + lrow, c = 16 * (Iw - 7) + lcol;
-                        double v = ((lok >> k) & 1) ? lval[k] : 0.0;
-                        if (r == c) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
-                        SY.at(r, c) = (c <= r) ? v : 0.0;
+                        for (int k = 0; k < 4; ++k) {
+                            const int r = 16 * Iw + 4 * k + (lq >> 6);
+                            double v0 = lval[2 * k], v1 = lval[2 * k + 1];
+                            if (r == c) v0 = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v0 + lambda : v0 + lambda * v0);
+                            if (r == c + 1) v1 = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v1 + lambda : v1 + lambda * v1);
+                            *reinterpret_cast<double2*>(&SY.at(r, c)) = double2{(c <= r) ? v0 : 0.0, (c + 1 <= r) ? v1 : 0.0};
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            const int r = 16 * Iw + 2 * k + lrow, c = 16 * (Iw - 7) + lcol;
+                            double v = ((lok >> k) & 1) ? lval[k] : 0.0;
+                            if (r == c) v = (r >= n) ? 1.0 : ((prm.strategy == 0) ? v + lambda : v + lambda * v);
+                            SY.at(r, c) = (c <= r) ? v : 0.0;
+                        }
                     }
 #ifdef LH_STAMPS
                     __builtin_amdgcn_s_waitcnt(0);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (wv == BZW && lane == 0) {
+                    if (wv == 12 && lane == 0) {
                         atomicAdd(&lh_stamps[57], __builtin_amdgcn_s_memtime() - lt1_);
                         atomicAdd(&lh_stamps[58], 1ull);
                     }
 #endif
                 }
                 const int Ia = t / 2 + 8;
-                if (Ia < NT) {
+                if (bim && Ia < NT) {
+                    // tile row Ia's values from the band image, two steps before they are written: the pair at
+                    // row 16 Ia + 4 k + lq / 64, columns 16 (Ia - 7) + 2 (lq mod 64) + {0, 1} is double2 256 k + lq
+                    const double2* __restrict__ bt = reinterpret_cast<const double2*>(bsrc + (size_t)Ia * LH_BIMG_TR) + lq;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const double2 v = bt[256 * k];
+                        lval[2 * k] = v.x;
+                        lval[2 * k + 1] = v.y;
+                    }
+                } else if (Ia < NT) {
                     const int c = 16 * (Ia - 7) + lcol, pc = c / 6;
                     lok = 0;
 #pragma unroll
@@ -3348,7 +3405,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                         lok |= (c <= r && r < n && d < 64) ? (1u << k) : 0u;
                     }
                 }
-            } else {
+            } else if (!bim) {
                 const int Ib = (t - 1) / 2 + 8;
                 if (Ib < NT) {
                     const int c = 16 * (Ib - 7) + lcol;
@@ -4432,7 +4489,7 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           const uint32_t* brow_ent, const uint16_t* units, lh_band_args band, double* img) {
     if (prm.P > LH_PMAX && prm.solver == 0 && band.bblk)
         hipLaunchKernelGGL(k_ctrl_b, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk, band.units,
-                           band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq);
+                           band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
     else if (prm.P > LH_PMAX && prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch

@@ -409,6 +409,28 @@ def test_banded_back_substitution_row_windows(monkeypatch):
     t.close()
 
 
+@pytest.mark.parametrize("P,L,k,seed", [(96, 6000, 11, 1), (128, 50000, 8, 3)])
+def test_band_image_equals_packed_blocks(P, L, k, seed, monkeypatch):
+    """k_reduce writes a one-rank banded window's S straight into k_ctrl_b's loader order (the band image); the
+    loaders then read each element with one load instead of a block-index round trip and a value load.  The
+    values and their arithmetic are the same, so the solve is bitwise the one over the packed blocks
+    (LH_NO_BIMG=1), rejected trials (the committed image) included."""
+    w = lego_ba.generate_window(P=P, L=L, k=k, seed=seed, **dict(__import__("windows").STABLE, outlier_frac=0.0))
+    w["pose_fixed"] = np.eye(1, P, dtype=np.uint8)[0]
+    s = lego_ba.Solver()
+    a = s.solve(w)
+    assert s.controller() == "k_ctrl_b"
+    monkeypatch.setenv("LH_NO_BIMG", "1")
+    t = lego_ba.Solver()
+    b = t.solve(w)
+    assert a["trials"] > a["iterations"] or P == 96   # the P = 128 window rejects trials: the committed image is read
+    assert a["iterations"] == b["iterations"] and a["trials"] == b["trials"]
+    assert a["chi2_final"] == b["chi2_final"]
+    assert np.array_equal(a["pose_Tcw"], b["pose_Tcw"]) and np.array_equal(a["lm_xyz"], b["lm_xyz"])
+    s.close()
+    t.close()
+
+
 def test_banded_ldlt_wide_band():
     """A banded window whose landmarks span 11 keyframes: rows reach 60-70 columns back, past the
     one-row-per-lane back substitution's 56, so k_ctrl_b holds two rows per lane.  (Runs of 15, the reference's
