@@ -356,7 +356,9 @@ class Solver:
         r.trace_chi2, r.trace_lambda = _ptr(out["trace_chi2"]), _ptr(out["trace_lambda"])
         r.trace_cap = trace_cap
         if outlier_chi2_th is not None:   # the device outlier pass (ABI 5): flags instead of per-edge chi2
-            out["is_outlier"] = np.zeros(n_obs, np.uint8)
+            prev = reuse.get("is_outlier") if reuse is not None else None   # a bool view of uint8 0 / 1
+            ok = prev is not None and prev.shape == (n_obs,) and prev.dtype in (np.bool_, np.uint8)
+            out["is_outlier"] = prev.view(np.uint8) if ok else np.zeros(n_obs, np.uint8)
             r.is_outlier = _ptr(out["is_outlier"])
             r.outlier_chi2_th = float(outlier_chi2_th)
         return r, out
@@ -370,7 +372,7 @@ class Solver:
                   "pcg_iterations", "degenerate", "time_prep_ms", "time_upload_ms", "time_download_ms"):
             out[f] = getattr(r, f)
         if "is_outlier" in out:
-            out["is_outlier"] = out["is_outlier"].astype(bool)
+            out["is_outlier"] = out["is_outlier"].view(bool)   # the device writes 0 / 1: no copy
             out["outlier_th"], out["n_inlier"], out["n_outlier"] = r.outlier_th, r.n_inlier, r.n_outlier
         return out
 
