@@ -6,18 +6,23 @@ reference stop rule.  value = LM iterations (of the whole window) completed per 
 
 Workloads (BASELINE.json configs); fp64 throughout (>= the reference's double):
   C3  20 KF / 50 000 landmarks / 400 000 obs on one GPU: the metric window (the N = 1 default).
-  C4  20 KF / 500 000 landmarks / 4 000 000 obs, landmark-sharded over N GPUs (500 000 / N landmarks
-      and their observations per rank, poses replicated, one RCCL all-reduce of the reduced pose
-      system per LM trial): the multi-GPU window (the N > 1 default), "scaling": "strong".  value
-      counts iterations of the whole window (no factor N).  The N = 1 line carries the same window on
-      one GPU ("c4_1gpu") as the base of the scaling ratio.  C4 runs in gate_mode 1 (the Huber gate's
-      analytically-zero rounding residue taken as 0): with the reference gate its trajectory depends
-      on the summation order, hence on the rank count (the oracle alone ends after 4 or 7 iterations
-      depending on its thread count, profiles/r03_c4_oracle_gate_envelope.json); in gate_mode 1 every
-      rank count runs the same trajectory (tests/test_multirank_gpu.py), so the N lines time the same
-      iterations and trials.
+  C3w C3 per GPU, the N > 1 default ("scaling": "weak"): a 20 KF window of 50 000 N landmarks /
+      400 000 N observations, landmark-sharded so every rank holds one C3-sized shard (poses
+      replicated, one RCCL all-reduce of the reduced pose system per LM trial).  The unit is one LM
+      iteration over one C3-sized shard, so value = N x (LM iterations of the whole window) / s: the
+      units all ranks processed over the max-over-ranks time (at N = 1 exactly C3's value), and
+      value(N) / (N value(1)) is the weak-scaling efficiency (the per-GPU work is C3's at every N).
+      BASELINE config 4 (500 000 landmarks on 8 GPUs, 62 500 per GPU) is this shape at N = 8.
+  C4  20 KF / 500 000 landmarks / 4 000 000 obs, landmark-sharded over N GPUs (--workload C4,
+      "scaling": "strong": value counts iterations of the whole window, no factor N).  The N = 1 line
+      carries it on one GPU ("c4_1gpu") and each rank's share of it ("c4_shards_1gpu").  C4 runs in
+      gate_mode 1 (the Huber gate's analytically-zero rounding residue taken as 0): with the reference
+      gate its trajectory depends on the summation order, hence on the rank count (the oracle alone
+      ends after 4 or 7 iterations depending on its thread count,
+      profiles/r03_c4_oracle_gate_envelope.json); in gate_mode 1 every rank count runs the same
+      trajectory (tests/test_multirank_gpu.py).
 
-Usage: python bench.py [--gpus N --steps K --warmup W] [--workload C3|C4]
+Usage: python bench.py [--gpus N --steps K --warmup W] [--workload C3|C3w|C4]
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -44,7 +49,9 @@ FP64_PEAK_TFS = 78.6       # MI355X FP64 spec (vector = matrix);
 # earlier in the same GPU call, before they are committed)
 PMC_TRAFFIC = os.environ.get("LH_PMC_JSON", os.path.join(ROOT, "profiles", "r05p_pmc_k_lin.json"))
 ROCPROF_K_LIN = os.environ.get("LH_ROCPROF_JSON", os.path.join(ROOT, "profiles", "r05p_rocprof_k_lin.json"))
-WORKLOADS = {"C3": dict(P=20, L=50_000, k=8), "C4": dict(P=20, L=500_000, k=8)}
+# L: landmarks of the window; per_rank: L per rank (the window has L N landmarks; weak scaling)
+WORKLOADS = {"C3": dict(P=20, L=50_000, k=8), "C3w": dict(P=20, L=50_000, k=8, per_rank=True),
+             "C4": dict(P=20, L=500_000, k=8)}
 
 
 def survey_bytes_per_iteration(n_obs, n_lm):
@@ -191,7 +198,7 @@ def make_window(name, family, seed, rank, world):
         params.update(STABLE)
     if family == "stable_noout":
         params["outlier_frac"] = 0.0
-    L = c["L"]
+    L = c["L"] * world if c.get("per_rank") else c["L"]
     w = lego_ba.generate_window(P=c["P"], L=L, k=c["k"], seed=seed, lm_begin=rank * L // world,
                                 lm_end=(rank + 1) * L // world, **params)
     if family.startswith("stable"):
@@ -262,8 +269,8 @@ def main():
     # 1000 C3 solves is ~1.1 s of GPU work: long enough for the driver's utilisation sampling to see it
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="auto", choices=["auto", "C3", "C4"],
-                    help="auto: C3 on one GPU, C4 sharded over N > 1")
+    ap.add_argument("--workload", default="auto", choices=["auto", "C3", "C3w", "C4"],
+                    help="auto: C3 on one GPU, C3w (one C3-sized shard per GPU, weak scaling) over N > 1")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--family", default="stable_noout", choices=["stable_noout", "stable", "default"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -280,7 +287,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world != 1:
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
-    name = args.workload if args.workload != "auto" else ("C3" if world == 1 else "C4")
+    name = args.workload if args.workload != "auto" else ("C3" if world == 1 else "C3w")
 
     import torch
     dist = None
@@ -330,7 +337,7 @@ def main():
     solver.set_profiling(False)
     n_obs, n_lm = len(w["obs_pose"]), len(w["lm_xyz"])
     c = WORKLOADS[name]
-    cfg_key = f"{name}-{args.family}-s{args.seed}"
+    cfg_key = f"{name}-{args.family}-s{args.seed}" + (f"-x{world}" if WORKLOADS[name].get("per_rank") else "")
     rl, rl_hbm = roofline(solver, n_obs, n_lm, c["k"], cfg_key)
 
     if rank != 0:
@@ -339,7 +346,10 @@ def main():
             dist.destroy_process_group()
         return
 
-    value = iters / dt
+    weak = bool(WORKLOADS[name].get("per_rank"))
+    L_win = c["L"] * world if weak else c["L"]
+    # C3w: one unit = one LM iteration over one C3-sized shard; every rank processes its shard's
+    value = iters * (world if weak else 1) / dt
     nprof = max(2, min(20, args.steps // 4))
     out = {
         "metric": "LM iterations/sec + ms/solve, 20KF/50k-pts/400k-obs window; final chi2 vs ref",
@@ -350,17 +360,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic (tools/window_gen.c, family={args.family}, seed={args.seed})",
-        "config": {"workload": f"{name}: sliding-window BA solve(10), {c['P']} KF / {c['L']} landmarks / "
-                               f"{c['L'] * c['k']} obs" + (f", landmark-sharded over {world} GPUs" if world > 1 else ""),
-                   "keyframes": c["P"], "landmarks": c["L"], "landmarks_per_gpu": c["L"] // world,
+        "config": {"workload": f"{name}: sliding-window BA solve(10), {c['P']} KF / {L_win} landmarks / "
+                               f"{L_win * c['k']} obs" + (f", landmark-sharded over {world} GPUs" if world > 1 else "")
+                               + (" (one C3-sized shard per GPU)" if weak else ""),
+                   "keyframes": c["P"], "landmarks": L_win, "landmarks_per_gpu": L_win // world,
                    "obs_this_rank": n_obs, "parallelism": f"landmark-shard x{world}",
                    "exchange": ("none" if world == 1 else ("RCCL all-reduce" if args.comm == "rccl"
                                                           else "host transport over gloo (rehearsal)"))},
         "gate_mode": gate,
+        "value_definition": ("N x LM iterations of the whole window per second: the C3-sized shard-iterations all "
+                             "ranks processed over the max-over-ranks time (weak scaling; N = 1 is C3's value)"
+                             if weak and world > 1 else "LM iterations of the whole window per second"),
         "iterations_per_solve": iters / args.steps,
         "trials_per_solve": trials / args.steps,
         "trials_per_s": round(trials / dt, 3),
