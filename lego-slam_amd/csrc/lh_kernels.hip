@@ -2431,7 +2431,11 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // arrives by a straight copy, no index math per entry (the scatter below was 2.2 us of wave 0's time)
     constexpr bool imgp = IMG;   // (the host sets prm.img only for SOLVER 0 without the two-chain schedule)
     static_assert(AS == LH_IMG_AS && (NP + 1) * AS == LH_IMG_SZ && LH_IMG_SZ % 2 == 0, "k_reduce's image layout");
-    constexpr int IMG2 = LH_IMG_SZ / 2, NIMG = (IMG2 + CT - 1) / CT;
+    // the image is copied by waves 1-15 (wave 0 factors block 0 meanwhile): copy thread ctid = tid - 64 takes the
+    // double pairs ctid + CW u
+    constexpr int CW = CT - 64, IMG2 = LH_IMG_SZ / 2, NIMG = (IMG2 + CW - 1) / CW;
+    const int ctid = tid - 64;
+    const bool cpw = tid >= 64;
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
     // [160 + wave]: the wave's HW_ID word (SIMD in bits 5:4): which waves share wave 0's SIMD
@@ -2467,7 +2471,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int ibase = (tid < ER) ? tid : (1 << 30);   // threads past ER hold no element
     double vs[NLD];
     uint32_t mp[NLD];
-    double2 iv[NIMG];                   // imgp: this thread's double pairs tid + CT u of the image
+    double2 iv[NIMG];                   // imgp: this copy thread's double pairs ctid + CW u of the image
     double bpx = 0.0, hdx = 0.0;        // imgp: b_p and diag H_pp of row tid (the packed buffer)
     const double2* __restrict__ img2 = reinterpret_cast<const double2*>(img);
     // only the pairs that carry data are read (the lower triangle of the real rows and the rhs row: ~45 % of the
@@ -2482,8 +2486,6 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         return double2{(pad && col == row) ? 1.0 : 0.0, (pad && col + 1 == row) ? 1.0 : 0.0};
     };
     if constexpr (imgp) {
-#pragma unroll
-        for (int u = 0; u < NIMG; ++u) iv[u] = img2[img_need(tid + CT * u) ? tid + CT * u : 0];
         bpx = rs_stage[LY.off_bp + min(tid, n - 1)];
         hdx = rs_stage[LY.off_hd + min(tid, n - 1)];
     } else {
@@ -2526,12 +2528,41 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #define LH_IMG_TO_LDS()                                                                                        \
     do {                                                                                                       \
         double2* A2_ = reinterpret_cast<double2*>(A);                                                          \
-        _Pragma("unroll") for (int u = 0; u < NIMG; ++u) {                                                     \
-            const int k = tid + CT * u, e = 2 * k, row = e / AS, col = e - AS * row; /* AS even: no straddle */ \
+        if (cpw) _Pragma("unroll") for (int u = 0; u < NIMG; ++u) {                                            \
+            const int k = ctid + CW * u, e = 2 * k, row = e / AS, col = e - AS * row; /* AS even: no straddle */\
             if (k < IMG2 && !(early0 && row < 8 && col < 8)) A2_[k] = img_need(k) ? iv[u] : img_fill(k);      \
         }                                                                                                      \
     } while (0)
-    if constexpr (imgp) LH_IMG_TO_LDS();
+    // imgp with k_reduce's decision known: wave 0 factors block 0 first, while the image is still in flight (its
+    // rows come in their own loads, b0s; the image copy leaves block 0 alone), then copies its share
+    bool f0_done = false;
+    if constexpr (imgp) {
+    if (cpw) {   // wave-uniform: the copy waves' image loads and copy, apart from wave 0's factor (registers)
+#pragma unroll
+        for (int u = 0; u < NIMG; ++u) iv[u] = img2[img_need(ctid + CW * u) ? ctid + CW * u : 0];
+        LH_IMG_TO_LDS();
+    }
+#ifndef LH_NO_F0_FIRST
+    else if (early0 && decided && !done) {
+        if (!accept) {   // a rejected trial factors the committed block 0
+            const int r = lane & 7;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) b0s[q] = img[LH_IMG_SZ + r * AS + q];
+        }
+        const int r = lane & 7;
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            double x = b0s[q];
+            if (q == r) x = (prm.strategy == 0) ? x + lambda : x + lambda * x;
+            v[q] = x;
+        }
+        LdltBlockLds& F0 = ldlt_lds();
+        factor_block8_v(LdsSys{A}, v, F0.N[0], F0.ND[0], 0, lane);
+        f0_done = true;
+    }
+#endif
+    }
 
     if (!decided) {
         if (mode == 0) {   // max |diag H_pp| for computeLambdaInitLM (problem.cpp:486-496)
@@ -2593,10 +2624,10 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         if (!accept) {
             const double2* __restrict__ imgc2 = reinterpret_cast<const double2*>(img + LH_IMG_SZ);
 #pragma unroll
-            for (int u = 0; u < NIMG; ++u) iv[u] = imgc2[img_need(tid + CT * u) ? tid + CT * u : 0];
+            for (int u = 0; u < NIMG; ++u) iv[u] = imgc2[(cpw && img_need(ctid + CW * u)) ? ctid + CW * u : 0];
             bpx = rs_commit[LY.off_bp + min(tid, n - 1)];
             hdx = rs_commit[LY.off_hd + min(tid, n - 1)];
-            if (early0 && wave == 0) {
+            if (early0 && wave == 0 && !f0_done) {
                 const int r = lane & 7;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) b0s[q] = img[LH_IMG_SZ + r * AS + q];
@@ -2606,8 +2637,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
 #undef LH_IMG_TO_LDS
 #pragma unroll
         for (int u = 0; u < NIMG; ++u) {
-            const int k = tid + CT * u, e = 2 * k, row = e / AS, col = e - AS * row;
-            if (k < IMG2 && row < n && (col == row || col + 1 == row) && !(early0 && row < 8)) {
+            const int k = ctid + CW * u, e = 2 * k, row = e / AS, col = e - AS * row;
+            if (cpw && k < IMG2 && row < n && (col == row || col + 1 == row) && !(early0 && row < 8)) {
                 double& d = A[row * AS + row];
                 d = (prm.strategy == 0) ? d + lambda : d + lambda * d;
             }
@@ -2672,7 +2703,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }   // packed path
     if (SOLVER == 0 && tid < 8 * LH_NSTEP) reinterpret_cast<uint32_t*>(s_units)[tid] = unit2;
     CSTAMP(3);
-    if (early0 && wave == 0) {
+    if (early0 && wave == 0 && !f0_done) {
         const int r = lane & 7;
         double v[8];
 #pragma unroll
