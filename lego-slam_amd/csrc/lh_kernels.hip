@@ -674,6 +674,14 @@ __device__ __forceinline__ void st_out(double* p, double v) {
     if constexpr (LH_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
 }
+// k_reduce's outputs (the reduced system, its LDS images) likewise, read by the controller that follows
+#ifndef LH_WT_RED
+#define LH_WT_RED 1   // k_reduce 6.86 / 6.86 -> 6.71 / 6.66 us, k_ctrl +0.06 (same-box A/B, profiles/r05s_ab_wt_reduce.txt)
+#endif
+__device__ __forceinline__ void st_red(double* p, double v) {
+    if constexpr (LH_WT_RED) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
 // a landmark record's 16-byte pieces (rec_rsrc: a buffer descriptor over the record buffer)
 __device__ __forceinline__ void st_rec2(double2* p, double2 v, __amdgpu_buffer_rsrc_t rsrc, const double* base) {
     if constexpr (LH_WT_REC) {
@@ -1421,25 +1429,25 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                 if (lane < 36) {
                     const int ea_ = lane / 6, eb_ = lane - 6 * (lane / 6), gi = 6 * p + ea_, gj = 6 * q + eb_;
                     const int idx = (p < q) ? gj * LH_IMG_AS + gi : ((ea_ >= eb_) ? gi * LH_IMG_AS + gj : -1);
-                    if (idx >= 0) img[LH_IMG_SZ + idx] = img[idx];
+                    if (idx >= 0) st_red(img + LH_IMG_SZ + idx, img[idx]);
                 } else if (p == q && lane < 42) {
                     const int idx = LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36);
-                    img[LH_IMG_SZ + idx] = img[idx];
+                    st_red(img + LH_IMG_SZ + idx, img[idx]);
                 }
             } else if (prm.bimg) {   // this pair's entries of k_ctrl_b's band image
                 const int bsz = ((6 * prm.P + 15) >> 4) * LH_BIMG_TR;
                 if (lane < 36) {
                     const int ea_ = lane / 6, eb_ = lane - 6 * (lane / 6), gi = 6 * p + ea_, gj = 6 * q + eb_;
                     const int r_ = (p < q) ? gj : gi, c_ = (p < q) ? gi : gj;
-                    if ((p < q || ea_ >= eb_) && lh_bimg_in(r_, c_)) img[bsz + lh_bimg_idx(r_, c_)] = img[lh_bimg_idx(r_, c_)];
+                    if ((p < q || ea_ >= eb_) && lh_bimg_in(r_, c_)) st_red(img + bsz + lh_bimg_idx(r_, c_), img[lh_bimg_idx(r_, c_)]);
                 }
             } else if (lane < 36) {
-                rs_commit[LY.off_S + b * 36 + lane] = rs[LY.off_S + b * 36 + lane];
+                st_red(rs_commit + LY.off_S + b * 36 + lane, rs[LY.off_S + b * 36 + lane]);
             }
             if (p == q && lane >= 36 && lane < 54) {
                 const int k = lane - 36, part_off = (k < 6) ? LY.off_bs : (k < 12) ? LY.off_bp : LY.off_hd;
                 const int i = part_off + 6 * p + (k % 6);
-                rs_commit[i] = rs[i];
+                st_red(rs_commit + i, rs[i]);
             }
         }
     }
@@ -1518,23 +1526,23 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                 // k_ctrl's LDS layout (prm.img): entry (a, bb) of block (p, q) is S(6p + a, 6q + bb); its lower
                 // slot only (the upper triangle stays zero in the image, where the factor writes L^T)
                 const int gi = 6 * p + a, gj = 6 * q + bb;
-                if (p < q) img[gj * LH_IMG_AS + gi] = v;
-                else if (a >= bb) img[gi * LH_IMG_AS + gj] = v;
+                if (p < q) st_red(img + gj * LH_IMG_AS + gi, v);
+                else if (a >= bb) st_red(img + gi * LH_IMG_AS + gj, v);
             } else if (prm.bimg) {
                 // k_ctrl_b's band image (prm.bimg): the lower slot, (row, column) = (6q + bb, 6p + a) for p < q
                 const int gi = 6 * p + a, gj = 6 * q + bb, r_ = (p < q) ? gj : gi, c_ = (p < q) ? gi : gj;
-                if ((p < q || a >= bb) && lh_bimg_in(r_, c_)) img[lh_bimg_idx(r_, c_)] = v;
+                if ((p < q || a >= bb) && lh_bimg_in(r_, c_)) st_red(img + lh_bimg_idx(r_, c_), v);
             } else {
-                rs[LY.off_S + b * 36 + lane] = v;
+                st_red(rs + LY.off_S + b * 36 + lane, v);
             }
-            if (diag && a == bb) rs[LY.off_hd + 6 * p + a] = h;
+            if (diag && a == bb) st_red(rs + LY.off_hd + 6 * p + a, h);
         }
         // b_p (lanes 36..41) and bs = b_p - bsd (needs lane + 6)
         const double bsd = __shfl_down(h, 6);
         if (diag && lane >= 36 && lane < 42) {
-            rs[LY.off_bp + 6 * p + (lane - 36)] = h;
-            rs[LY.off_bs + 6 * p + (lane - 36)] = h - bsd;
-            if (prm.img) img[LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36)] = h - bsd;   // the rhs row
+            st_red(rs + LY.off_bp + 6 * p + (lane - 36), h);
+            st_red(rs + LY.off_bs + 6 * p + (lane - 36), h - bsd);
+            if (prm.img) st_red(img + LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36), h - bsd);   // the rhs row
         }
     }
     STAMP(20);
