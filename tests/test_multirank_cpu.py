@@ -87,3 +87,32 @@ def test_sharded_window_generation_matches_global_window():
         order_r = np.lexsort((ref["obs_pose"], ref["obs_lm"]))
         for key in ("obs_pose", "obs_lm", "obs_uv"):
             assert np.array_equal(np.asarray(part[key])[order_p], np.asarray(ref[key])[order_r]), key
+
+
+def test_bench_weak_scaling_shards():
+    """bench.py's N > 1 default (C3w): rank r of N holds landmarks [50 000 r, 50 000 (r + 1)) of a window of
+    50 000 N landmarks, i.e. one C3-sized shard per rank; N = 1 is exactly C3.  (Checked at a reduced size
+    through the same make_window path.)"""
+    import importlib
+    import sys
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    bench = importlib.import_module("bench")
+    saved = dict(bench.WORKLOADS)
+    try:
+        bench.WORKLOADS["C3w"] = dict(P=8, L=600, k=6, per_rank=True)
+        bench.WORKLOADS["C3"] = dict(P=8, L=600, k=6)
+        one = bench.make_window("C3", "stable_noout", 0, 0, 1)
+        wc = bench.make_window("C3w", "stable_noout", 0, 0, 1)
+        for key in ("pose_Tcw", "lm_xyz", "obs_pose", "obs_lm", "obs_uv"):
+            assert np.array_equal(np.asarray(one[key]), np.asarray(wc[key])), key
+        full = lego_ba.generate_window(P=8, L=1800, k=6, seed=0,
+                                       **dict(__import__("windows").STABLE, outlier_frac=0.0))
+        for r in range(3):
+            part = bench.make_window("C3w", "stable_noout", 0, r, 3)
+            assert len(part["lm_xyz"]) == 600
+            ref = ob.landmark_shard(full, 600 * r, 600 * (r + 1))
+            assert np.array_equal(part["lm_xyz"], ref["lm_xyz"])
+            assert np.array_equal(part["pose_Tcw"], full["pose_Tcw"])
+    finally:
+        bench.WORKLOADS.clear()
+        bench.WORKLOADS.update(saved)
