@@ -3162,8 +3162,10 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 // of keyframes, so row r's nonzeros start at its envelope fc(r) >= r - 104 (the host checks this per
 // window, lh_host.cpp; other windows go to k_ctrl_g or PCG).  The blocked LDL^T of k_ctrl then needs
 // only 8 tile rows (128 rows) of S at a time: the window holds them in one CU's LDS as a circular
-// buffer (BandSys), and waves 12-15 stream the next tile row in (its block-index loads two steps
-// ahead, its values one step ahead, written into the slots of the tile row that just retired).  L goes
+// buffer (BandSys), and waves 12-15 stream the next tile row in, written into the slots of the tile row
+// that just retired: one rank reads it from the band image k_reduce wrote in the loaders' order (prm.bimg,
+// two steps ahead); a sharded solve from the all-reduced packed blocks (block indices two steps ahead,
+// values one step ahead).  L goes
 // to global memory row by row, ND per block; the back substitution (one wave) reads them back.  The
 // per-step work units come from the same envelope (lh_ctrl_units over 11 unit waves).  One 1024-thread
 // workgroup; the LM bookkeeping is k_reduce's (dec_in_reduce: one rank) or thread 0's (the initial
@@ -3379,7 +3381,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         }
         if (band_loader(wv)) {
             // tile row I enters the window at step 2 I - 14, into the slots of tile row I - 8 (retired
-            // after step 2 I - 15); its block indices are loaded at step 2 I - 16, its values at 2 I - 15
+            // after step 2 I - 15).  From the band image (prm.bimg, one rank) its values are loaded at step
+            // 2 I - 16, in pairs; from the packed blocks (sharded solves) its block indices at 2 I - 16 and its
+            // values at 2 I - 15
             // Every load is unconditional (clamped index): a conditional load becomes a branch whose join
             // waits for it.  Selections and the diagonal's lambda wait until the values are written.
             if ((t & 1) == 0) {
