@@ -3175,7 +3175,7 @@ template <bool B> struct BoolTag { static constexpr bool value = B; };
 #define BNMAX (6 * LH_PMAX_ANY)         // largest reduced system (1536 rows)
 #define BSTEP_MAX (BNMAX / 8)           // LDL^T steps
 // the stream loaders: waves 12-15 (moving them off wave 0's SIMD, to 11 and 13-15, measured slower: the
-// wave forming z then set the step); wave 12 also forms z and copies ND out
+// wave forming z then set the step); z and the ND copy are wave LH_BZW's (below)
 __device__ __forceinline__ bool band_loader(int w) { return w >= 12; }
 __device__ __forceinline__ int band_loader_slot(int w) { return w - 12; }
 #ifndef LH_BZW
