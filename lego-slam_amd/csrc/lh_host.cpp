@@ -38,8 +38,8 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag,
                          long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat,
                          int writer);
-hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
-                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
+hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* red_tab, int nred,
+                            lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
                             lh_params prm, int n_chunks, int mode, int* host_done, int seq, double* img);
 hipError_t lh_launch_img_init(hipStream_t st, double* img, int n);
 hipError_t lh_launch_ldlt_g_probe(const double* S, const double* b, int n, double* x, double* gA);
@@ -260,7 +260,7 @@ struct lh_handle {
     // pinned staging of the upload
     View<lh_chunk> s_chunks;                                  // the per-window tables: views into s_arena
     View<lh_subbatch> s_sbs;
-    View<uint32_t> s_items, s_pair_ptr, s_rsmap, s_brow_ent;
+    View<uint32_t> s_items, s_pair_ptr, s_rsmap, s_brow_ent, s_red;
     View<uint16_t> s_pair_pq;
     View<uint16_t> s_units;                                   // k_ctrl's work units (lh_ctrl_units)
     View<uint16_t> s_bunits;                                  // k_ctrl_b's work units
@@ -284,7 +284,8 @@ struct lh_handle {
     // device buffers
     View<lh_chunk> d_chunks;                                  // the per-window tables: views into d_arena
     View<lh_subbatch> d_sbs;
-    View<uint32_t> d_pair_ptr, d_items, d_rsmap;
+    View<uint32_t> d_pair_ptr, d_items, d_rsmap, d_red;
+    int n_red = 0;   // k_reduce's pair blocks (d_red: 4 words each, then the scalar block's sentinel)
     View<uint16_t> d_pair_pq, d_units, d_bunits;
     View<int32_t> d_bblk;
     DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64)
@@ -563,6 +564,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         const size_t n_bunits = band_possible ? 16 * (size_t)kBandSteps : 0, n_bblk = band_possible ? (size_t)P * 64 : 0;
         const size_t o_bunits = part(n_bunits * sizeof(uint16_t));
         const size_t o_bblk = part(n_bblk * sizeof(int32_t));
+        const size_t o_red = part(4 * ((size_t)pl.npairs + 1) * sizeof(uint32_t));
         HIPCHK(h->d_arena.ensure(bytes));
         HIPCHK(h->s_arena.ensure(bytes));
         h->arena_bytes = bytes;
@@ -589,6 +591,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         bind(h->d_units, h->s_units, db, sb, o_units, 16 * LH_NSTEP);
         bind(h->d_bunits, h->s_bunits, db, sb, o_bunits, n_bunits);
         bind(h->d_bblk, h->s_bblk, db, sb, o_bblk, n_bblk);
+        bind(h->d_red, h->s_red, db, sb, o_red, 4 * ((size_t)pl.npairs + 1));
     }
     HIPCHK(h->d_meta.ensure(pl.n_slots));
     HIPCHK(h->d_uv.ensure(2 * pl.n_slots));
@@ -628,6 +631,28 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         return fs;
     }
     std::memcpy(h->s_pair_ptr.p, pl.pair_ptr.data(), pl.pair_ptr.size() * sizeof(uint32_t));
+    // k_reduce's blocks: one per pose pair that some chunk's rows reach ({block, first row, end row, p | q << 16}),
+    // then the scalar block's sentinel.  One rank skips the pairs no chunk couples: their blocks of S are zero
+    // for the whole window (the reduced-system buffers are cleared per window, below).  A sharded solve keeps
+    // every pair: a rank's empty pair still has to write its zero contribution over last trial's all-reduced sum.
+    {
+        const bool skip = h->opt.world_size == 1 && !getenv("LH_NO_RED_SKIP");
+        uint32_t* rt = h->s_red.p;
+        int k = 0;
+        for (int b = 0; b < pl.npairs; ++b) {
+            const uint32_t ib = pl.pair_ptr[b], ie = pl.pair_ptr[b + 1];
+            if (skip && ib == ie) continue;
+            rt[4 * k] = (uint32_t)b; rt[4 * k + 1] = ib; rt[4 * k + 2] = ie;
+            rt[4 * k + 3] = (uint32_t)pl.pair_list[2 * b] | ((uint32_t)pl.pair_list[2 * b + 1] << 16);
+            ++k;
+        }
+        rt[4 * k] = (uint32_t)pl.npairs; rt[4 * k + 1] = 0; rt[4 * k + 2] = 0; rt[4 * k + 3] = 0;
+        h->n_red = k;
+        if (skip) {   // the skipped pairs' blocks (and every buffer slot k_reduce never writes) read as zero
+            HIPCHK(hipMemsetAsync(h->d_rs_stage.p, 0, h->LY.total * sizeof(double), h->stream));
+            HIPCHK(hipMemsetAsync(h->d_rs_commit.p, 0, h->LY.total * sizeof(double), h->stream));
+        }
+    }
     std::memcpy(h->s_fixed.p, pl.fixed_bits.data(), pl.fixed_bits.size() * sizeof(uint64_t));
     std::memcpy(h->s_brow_ptr.p, pl.brow_ptr.data(), pl.brow_ptr.size() * sizeof(int32_t));
     std::memcpy(h->s_brow_ent.p, pl.brow_ent.data(), pl.brow_ent.size() * sizeof(uint32_t));
@@ -884,7 +909,7 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
     }
     {
         Prof pr(h, KC_REDUCE);
-        HIPCHK(lh_launch_reduce(s, h->d_rows.p, h->d_csc.p, h->d_pair_ptr.p, h->d_pair_pq.p, h->d_ctrl.p,
+        HIPCHK(lh_launch_reduce(s, h->d_rows.p, h->d_csc.p, h->d_red.p, h->n_red, h->d_ctrl.p,
                                 h->d_rs_stage.p, h->d_rs_commit.p, h->d_maxd.p, h->prm, h->plan.n_chunks, mode, h->d_done,
                                 h->cur_trial, h->d_img.p));
         DBGSYNC("k_reduce");

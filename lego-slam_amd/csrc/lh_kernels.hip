@@ -1408,7 +1408,7 @@ __device__ __forceinline__ int hpp_index(int a, int b) {   // packed upper 6x6, 
 // when the previous trial was accepted (before this trial overwrites them; an evaluate-only trial
 // copies and writes nothing): a controller that factors a large system then never copies it.
 __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, const double* __restrict__ csc,
-                                               const uint32_t* __restrict__ pair_ptr, const uint16_t* __restrict__ pair_pq,
+                                               const uint4* __restrict__ red_tab, int nred,
                                                lh_ctrl* __restrict__ ctrl, double* __restrict__ rs,
                                                double* __restrict__ rs_commit, double* __restrict__ maxd_out,
                                                lh_params prm, int n_chunks, int mode, volatile int* __restrict__ host_done,
@@ -1416,11 +1416,13 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     STAMP_DECL
     __shared__ double part[3][RW][64];
     const lh_rs_layout LY = lh_rs_make(prm.P, prm.npairs);
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // the stop flag and this block's pair words are independent loads: one round trip for all
-    const int bq = b < LY.npairs ? b : 0;
-    const int ib = pair_ptr[bq], ie = pair_ptr[bq + 1];
-    const int p = pair_pq[2 * bq], q = pair_pq[2 * bq + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the stop flag and this block's pair words (one 16-byte entry of the host's table: the pairs some chunk
+    // reaches, then the scalar block's sentinel {npairs, 0, 0, 0}) are independent loads: one round trip
+    const uint4 rt = red_tab[min((int)blockIdx.x, nred)];
+    const int b = (int)blockIdx.x < nred ? (int)rt.x : LY.npairs;
+    const int ib = (int)rt.y, ie = (int)rt.z;
+    const int p = (int)(rt.w & 0xffffu), q = (int)(rt.w >> 16);
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_lin wrote the chunk scalars only
     if ((prm.commit_in_reduce | prm.img) && mode != 0 && b < LY.npairs && done == 0 && wave == 0) {
@@ -4495,12 +4497,11 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     return hipGetLastError();
 }
 
-hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* pair_ptr,
-                            const uint16_t* pair_pq, lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
+hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* red_tab, int nred,
+                            lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
                             lh_params prm, int n_chunks, int mode, int* host_done, int seq, double* img) {
-    const int npairs = prm.npairs;
-    hipLaunchKernelGGL(k_reduce, dim3(npairs + 1), dim3(RT), 0, st, rows, csc, pair_ptr, pair_pq, ctrl,
-                       rs_stage, rs_commit, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq, img);
+    hipLaunchKernelGGL(k_reduce, dim3(nred + 1), dim3(RT), 0, st, rows, csc, reinterpret_cast<const uint4*>(red_tab),
+                       nred, ctrl, rs_stage, rs_commit, maxd, prm, n_chunks, mode, (volatile int*)host_done, seq, img);
     return hipGetLastError();
 }
 

@@ -57,10 +57,10 @@ for step in "$@"; do
         timeout -k 10 300 python3 $QUICK > "$OUT/quick$SFX.json" 2> "$OUT/quick$SFX.err" || { tail -20 "$OUT/quick$SFX.err"; exit 1; }
         cat "$OUT/quick$SFX.json" ;;
     trace)
-        rm -rf "$OUT/trace"
-        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $QUICK \
-            > "$OUT/trace.log" 2>&1 || { tail -20 "$OUT/trace.log"; exit 1; }
-        kstats trace "$OUT/trace" | tee "$OUT/trace_summary.txt" ;;
+        rm -rf "$OUT/trace$SFX"
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace$SFX" -o run --output-format csv -- python3 $QUICK \
+            > "$OUT/trace$SFX.log" 2>&1 || { tail -20 "$OUT/trace$SFX.log"; exit 1; }
+        kstats "trace$SFX" "$OUT/trace$SFX" | tee "$OUT/trace_summary$SFX.txt" ;;
     pmc)
         mkdir -p "$OUT/pmc"
         pass() {   # name, counters...
