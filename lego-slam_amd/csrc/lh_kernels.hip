@@ -4093,6 +4093,40 @@ __device__ __forceinline__ void po_ldlt6_lds(const double* H, const double* bv, 
 }
 
 #pragma clang fp contract(off)
+// sin and cos of |x| <= 0.8 by their Taylor series to x^17 / x^18 in Horner form on x^2 (the next terms are
+// below 1e-19): within 1 ulp of the host libm's sin / cos (2e7 samples, 1-2 % of them 1 ulp apart; the
+// device library's sincos is not bitwise the host's either).  A frame's pose step is small, so its angle
+// takes this path; larger ones take the library's sincos.
+__device__ __forceinline__ void po_sincos_small(double x, double& s, double& c) {
+    const double x2 = x * x;
+    double p = -8.22063524662433e-18;
+    p = __builtin_fma(p, x2, 2.8114572543455206e-15);
+    p = __builtin_fma(p, x2, -7.647163731819816e-13);
+    p = __builtin_fma(p, x2, 1.6059043836821613e-10);
+    p = __builtin_fma(p, x2, -2.505210838544172e-08);
+    p = __builtin_fma(p, x2, 2.7557319223985893e-06);
+    p = __builtin_fma(p, x2, -0.0001984126984126984);
+    p = __builtin_fma(p, x2, 0.008333333333333333);
+    p = __builtin_fma(p, x2, -0.16666666666666666);
+    s = __builtin_fma(x * x2, p, x);
+    double q = 4.110317623312165e-19;
+    q = __builtin_fma(q, x2, -1.5619206968586225e-16);
+    q = __builtin_fma(q, x2, 4.779477332387385e-14);
+    q = __builtin_fma(q, x2, -1.1470745597729725e-11);
+    q = __builtin_fma(q, x2, 2.08767569878681e-09);
+    q = __builtin_fma(q, x2, -2.755731922398589e-07);
+    q = __builtin_fma(q, x2, 2.48015873015873e-05);
+    q = __builtin_fma(q, x2, -0.001388888888888889);
+    q = __builtin_fma(q, x2, 0.041666666666666664);
+    q = __builtin_fma(q, x2, -0.5);
+    c = __builtin_fma(x2, q, 1.0);
+}
+// the library's sincos out of line (its registers are not live across the frame's pose update)
+__device__ __attribute__((noinline)) double2 po_sincos_libm(double x) {
+    double s, c;
+    sincos(x, &s, &c);
+    return double2{s, c};
+}
 // VertexPose::add: T12 <- (SE3::exp(d) * SE3(T12)).matrix(), NaN/Inf step -> zero (lego_types.h:61-91),
 // on one wave: every lane computes the same result, except that lane 0 takes sin/cos(theta/2) and
 // lane 1 sin/cos(theta) in one sincos pass.  qT = the quaternion of SE3(T12) (d_q_from_R of its
@@ -4109,7 +4143,19 @@ __device__ __forceinline__ void po_pose_add_wave(const double (&d_in)[6], const 
     }
     const double th = d_twist_theta(d);
     double sn, cs;
-    sincos(lane == 1 ? th : 0.5 * th, &sn, &cs);
+    const double ang = lane == 1 ? th : 0.5 * th;
+#ifndef LH_PO_LIBM_SINCOS
+    if (__builtin_amdgcn_readfirstlane((int)(th <= 0.8)))   // th: the same in every lane
+        po_sincos_small(ang, sn, cs);
+    else
+    {
+        const double2 r = po_sincos_libm(ang);
+        sn = r.x;
+        cs = r.y;
+    }
+#else
+    sincos(ang, &sn, &cs);
+#endif
     const double sh = readlane_d(sn, 0), ch = readlane_d(cs, 0), st = readlane_d(sn, 1), ct = readlane_d(cs, 1);
     double qe[4], te[3], qn[4], tr[3], Rn[9];
     d_se3_exp_trig(d, sh, ch, st, ct, qe, te);
