@@ -313,7 +313,8 @@ int lh_debug_time_lin(lh_handle *h, int reps, double *ms);
 int lh_debug_comm_count(lh_handle *h, int64_t *n);
 /* the controller the uploaded window's trials run: 0 k_ctrl (LDS, <= 21 poses), 1 k_ctrl_g (dense
    LDL^T in global memory), 2 k_ctrl_p (PCG on the block-sparse system), 3 k_ctrl_b (banded LDL^T);
-   bit 8: k_ctrl_b's back substitution holds one row per lane (every row's envelope within 56 rows) */
+   bit 8: k_ctrl_b's back substitution holds one row per lane (every row's envelope within 56 rows);
+   bit 9: some k_ctrl_b step needs more than 11 unit waves, so its stream loaders take units too */
 int lh_debug_controller(lh_handle *h, int *which);
 
 #ifdef __cplusplus

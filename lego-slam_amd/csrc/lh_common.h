@@ -155,6 +155,7 @@ struct lh_params {
                             //    substitution holds one row per lane: a 64-row window)
     int32_t bimg;           // 1: k_reduce writes S's lower band straight into k_ctrl_b's band image (one rank, banded
                             //    LDL^T): the stream loaders read it without the block-index round trip
+    int32_t band_lu;        // 1: some banded LDL^T step needs more than 11 unit waves: the stream loaders take units
     double K[4];
 };
 
@@ -229,8 +230,11 @@ LH_HD static inline int lh_ctrl_units(int n, const int32_t* tile_fcb, const int*
 }
 // k_ctrl: all 15 waves take units, wave 0's SIMD-mates (4, 8, 12) last
 #define LH_ORDER_CTRL {1, 2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12}
-// k_ctrl_b: waves 12-15 stream tile rows into the window instead
-#define LH_ORDER_BAND {1, 2, 3, 5, 6, 7, 9, 10, 11, 4, 8}
+// k_ctrl_b: waves 12-15 stream tile rows into the window; a step needing more than 11 units gives the rest
+// to them (their loads and window writes are a few instructions per step from the band image), wave 0's
+// SIMD-mate 12 last
+#define LH_ORDER_BAND {1, 2, 3, 5, 6, 7, 9, 10, 11, 4, 8, 13, 14, 15, 12}
+#define LH_BAND_UNIT_WAVES 15   // 11 unit waves, then the 4 stream loaders (k_ctrl_b<true>)
 
 // k_ctrl_b's band image (prm.bimg): tile row I (rows 16 I .. 16 I + 15) holds columns 16 (I - 7) .. 16 I + 15,
 // 128 per row, the order k_ctrl_b's stream loaders read (a banded window's rows start at or after column

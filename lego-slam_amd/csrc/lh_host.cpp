@@ -291,6 +291,7 @@ struct lh_handle {
     DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64)
     bool band = false;            // this window's LDL^T runs in k_ctrl_b
     bool band_narrow = false;     // ... and every row's envelope starts within 56 rows of its 8-row block
+    bool band_lu = false;         // ... and some step needs the stream loaders as unit waves too
     lh_ctrl_nd nd{};              // k_ctrl's two-chain schedule (nd.nsteps 0: the one-chain one)
     View<int32_t> d_lm_perm;
     View<double> d_ptab_init, d_qt_init, d_ext;
@@ -531,6 +532,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     const bool band_possible = pl.P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT && !getenv("LH_NO_BAND");
     h->band = false;
     h->band_narrow = false;
+    h->band_lu = false;
     // k_lin's write-through record stores address both record buffers through one buffer descriptor
     // (32-bit byte offsets): up to ~8.3 M landmarks per rank
     if ((size_t)2 * pl.n_rec * LH_REC * sizeof(double) > (size_t)INT32_MAX) return LH_E_UNSUPPORTED;
@@ -714,8 +716,12 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         }
         if (ok) {
             bunits.resize(16 * (size_t)kBandSteps);
-            const int order[11] = LH_ORDER_BAND;
-            ok = lh_ctrl_units(n, fcb.data(), order, 11, kBandSteps, bunits.data()) <= 11;
+            const int order[LH_BAND_UNIT_WAVES] = LH_ORDER_BAND;
+            // the 11 unit waves when every step fits them (k_ctrl_b<false>), else with the loaders too
+            const int w11 = lh_ctrl_units(n, fcb.data(), order, 11, kBandSteps, bunits.data());
+            h->band_lu = w11 > 11;
+            if (h->band_lu)
+                ok = lh_ctrl_units(n, fcb.data(), order, LH_BAND_UNIT_WAVES, kBandSteps, bunits.data()) <= LH_BAND_UNIT_WAVES;
         }
         h->band = ok;
         // k_ctrl_b's one-row-per-lane back substitution: block KB's L rows reach no column below KB - 56
@@ -802,6 +808,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
     prm.band_narrow = h->band_narrow ? 1 : 0;
+    prm.band_lu = h->band_lu ? 1 : 0;
     // k_reduce writes the band straight into k_ctrl_b's loader order (one rank; LH_NO_BIMG=1: the packed
     // blocks and the loaders' block-index round trip, an A/B switch)
     prm.bimg = (h->band && prm.dec_in_reduce && !getenv("LH_NO_BIMG")) ? 1 : 0;
@@ -1751,6 +1758,7 @@ int lh_debug_controller(lh_handle* h, int* which) {
     if (!h->uploaded) return LH_E_STATE;
     *which = h->P <= LH_PMAX ? 0 : h->band ? 3 : h->prm.solver == LH_SOLVER_PCG ? 2 : 1;
     if (h->band_narrow) *which |= 1 << 8;   // k_ctrl_b's one-row-per-lane back substitution
+    if (h->band_lu) *which |= 1 << 9;       // k_ctrl_b's stream loaders take units (k_ctrl_b<true>)
     return LH_OK;
 }
 

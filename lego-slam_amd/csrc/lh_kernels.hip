@@ -3202,6 +3202,9 @@ __device__ __forceinline__ double band_value(const double* __restrict__ src, int
     return v;
 }
 
+// LU: some step needs more than the 11 unit waves (chunk windows of ~16 poses), so the stream loaders take units
+// too (a separate instantiation: the loaders' unit path costs ~1 % where no step needs it)
+template <bool LU>
 __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const double* __restrict__ rs_commit,
                                                const double* __restrict__ rs_stage, const double* __restrict__ maxd_in,
                                                const int32_t* __restrict__ bblk, const uint16_t* __restrict__ bunits,
@@ -3375,7 +3378,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
                 LDLT_SSTAMP(0);
                 factor_block8(SY, Nl[par ^ 1], NDl[par ^ 1], m0, lane);
                 LDLT_SSTAMP(1);
-            } else if (!band_loader(wv) && (uw & LH_UNIT_VALID)) {
+            } else if ((LU || !band_loader(wv)) && (uw & LH_UNIT_VALID)) {   // LU: the loaders too (steps of 12-15 units)
                 const int I = g0 + (uw & 7), jb0 = g0 + ((uw >> 3) & 7), jb1 = g0 + ((uw >> 6) & 15);
                 ldlt_tile_row(SY, N, ND, k0, 16 * I, 16 * jb0, 16 * jb1, -1, (uw & LH_UNIT_STORE) != 0, lane);
             }
@@ -4578,8 +4581,14 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
                           const uint32_t* brow_ent, const uint16_t* units, lh_band_args band, double* img) {
     if (prm.P > LH_PMAX && prm.solver == 0 && band.bblk)
-        hipLaunchKernelGGL(k_ctrl_b, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk, band.units,
-                           band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
+    {
+        if (prm.band_lu)
+            hipLaunchKernelGGL(k_ctrl_b<true>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk,
+                               band.units, band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
+        else
+            hipLaunchKernelGGL(k_ctrl_b<false>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk,
+                               band.units, band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
+    }
     else if (prm.P > LH_PMAX && prm.solver == 1)
         hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch

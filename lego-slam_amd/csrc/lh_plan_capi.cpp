@@ -105,11 +105,12 @@ extern "C" {
 // workers must never touch a retired job).  Returns the sum of all indices visited.
 // the controllers' per-step work units (lh_common.h lh_ctrl_units) for an n-row system whose tile row I
 // first reaches 8-column block fcb[I]: band 0 -> k_ctrl's table (15 unit waves, LH_NSTEP steps), band 1
-// -> k_ctrl_b's (11 unit waves, 6 LH_PMAX_ANY / 8 steps).  Returns the most units a step needed.
+// -> k_ctrl_b's (15 unit waves, the stream loaders last, 6 LH_PMAX_ANY / 8 steps).  Returns the most units a step needed.
 int lhp_ctrl_units(int n, const int32_t* fcb, int band, uint16_t* units) {
     if (band) {
-        const int order[11] = LH_ORDER_BAND;
-        return lh_ctrl_units(n, fcb, order, 11, 6 * LH_PMAX_ANY / 8, units);
+        const int order[LH_BAND_UNIT_WAVES] = LH_ORDER_BAND;   // as lh_host.cpp: the 11 unit waves, else the loaders too
+        const int w = lh_ctrl_units(n, fcb, order, 11, 6 * LH_PMAX_ANY / 8, units);
+        return w <= 11 ? w : lh_ctrl_units(n, fcb, order, LH_BAND_UNIT_WAVES, 6 * LH_PMAX_ANY / 8, units);
     }
     const int order[15] = LH_ORDER_CTRL;
     return lh_ctrl_units(n, fcb, order, 15, LH_NSTEP, units);

@@ -477,6 +477,12 @@ class Solver:
         _check(ba_lib().lh_debug_controller(self.h, C.byref(v)), "lh_debug_controller")
         return ("k_ctrl", "k_ctrl_g", "k_ctrl_p", "k_ctrl_b")[v.value & 0xff]
 
+    def band_loader_units(self):
+        """k_ctrl_b's stream loaders take work units (some step needs more than 11; lh_debug_controller bit 9)."""
+        v = C.c_int(0)
+        _check(ba_lib().lh_debug_controller(self.h, C.byref(v)), "lh_debug_controller")
+        return bool(v.value >> 9 & 1)
+
     def band_narrow(self):
         """k_ctrl_b runs its one-row-per-lane back substitution (every row's envelope within 56 rows of its
         8-row block; lh_debug_controller bit 8)."""

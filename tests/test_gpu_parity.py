@@ -431,19 +431,19 @@ def test_band_image_equals_packed_blocks(P, L, k, seed, monkeypatch):
     t.close()
 
 
-def test_banded_ldlt_wide_band():
-    """A banded window whose landmarks span 11 keyframes: rows reach 60-70 columns back, past the
-    one-row-per-lane back substitution's 56, so k_ctrl_b holds two rows per lane.  (Runs of 15, the reference's
-    window length, make chunk windows of 16 poses: 13 units in a step, past k_ctrl_b's 11, so LDL^T refuses
-    them past 64 keyframes and PCG takes them.)  One trial at the single-trial bar, the full solve against the
-    oracle's LDLT."""
-    w = lego_ba.generate_window(P=96, L=6000, k=11, seed=2, **dict(__import__("windows").STABLE, outlier_frac=0.0))
+@pytest.mark.parametrize("k", [11, 15])
+def test_banded_ldlt_wide_band(k):
+    """Banded windows whose landmarks span 11 and 15 keyframes (15: the reference's window length, map.h:82):
+    rows reach 60-95 columns back, past the one-row-per-lane back substitution's 56, so k_ctrl_b holds two rows
+    per lane; 15-keyframe runs make 16-pose chunk windows and steps of 13 units, which the stream loaders
+    share.  One trial at the single-trial bar, the full solve against the oracle's LDLT."""
+    w = lego_ba.generate_window(P=96, L=6000, k=k, seed=2, **dict(__import__("windows").STABLE, outlier_frac=0.0))
     f = np.zeros(96, np.uint8)
     f[0] = 1
     w["pose_fixed"] = f
     s1 = lego_ba.Solver(max_iters=1, max_trials=1)
     g = s1.solve(w)
-    assert s1.controller() == "k_ctrl_b" and not s1.band_narrow()
+    assert s1.controller() == "k_ctrl_b" and not s1.band_narrow() and s1.band_loader_units() == (k == 15)
     o = ob.solve(w, max_iters=1, max_trials=1)
     assert rel(g["chi2_final"], o["chi2_final"]) < 1e-9
     assert np.allclose(g["pose_Tcw"], o["pose_Tcw"], atol=1e-9)
