@@ -316,6 +316,10 @@ int lh_debug_comm_count(lh_handle *h, int64_t *n);
    bit 8: k_ctrl_b's back substitution holds one row per lane (every row's envelope within 56 rows);
    bit 9: some k_ctrl_b step needs more than 11 unit waves, so its stream loaders take units too */
 int lh_debug_controller(lh_handle *h, int *which);
+/* the LM chains (k_lin, k_reduce, exchange, controller) the last solve decided past the initial
+   linearisation: its trials, plus one re-linearisation per evaluate-only trial accepted outside the
+   final iteration (a trial after a rejection only evaluates).  Solves that return arrays only. */
+int lh_debug_chains(lh_handle *h, int *chains);
 
 #ifdef __cplusplus
 }

@@ -120,6 +120,9 @@ struct lh_ctrl {
     int32_t acc_hist[2];       // trial seq's LM decision (accepted) at [seq & 1]: read by its controller, and by
                                // the next trial's k_reduce when it commits the staged system (commit_in_reduce)
     int32_t done_seq;          // the trial whose decision stopped the loop (its controller raises the host's done)
+    int32_t relin;             // an evaluate-only trial was accepted outside the final iteration: the next chain
+                               // (k_lin, k_reduce, k_ctrl) linearises the committed state instead of a trial
+    int32_t seq_last;          // the last chain (trial or re-linearisation) a live decision was taken on
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
 };
 
@@ -141,6 +144,8 @@ struct lh_params {
     int32_t solver;         // 0 LDL^T (Eigen LDLT, problem.cpp:420), 1 PCG (problem.cpp:422, :584-614)
     int32_t gate_mode;      // 0 reference Huber gate (base_edge.cpp:55); 1 diagnostic (residue taken as 0)
     int32_t no_evo;         // 1: every trial linearises in full (diagnostic A/B of ctrl.evo; env LH_NO_EVO)
+    int32_t eval_first;     // 1: a trial after a rejection in its iteration only evaluates (ctrl.evo); an accepted
+                            //    one is linearised by the next chain (ctrl.relin).  Env LH_NO_EVAL_FIRST: 0
     double huber_delta, stop_dchi2, tau, lambda_cap, lambda_init;
     double pcg_tol;         // PCG stop: ||r|| <= pcg_tol ||b|| (reference 1e-6, problem.cpp:597)
     int32_t pcg_max_it;     // PCG cap (<= 0: 2 * rows, problem.cpp:422)

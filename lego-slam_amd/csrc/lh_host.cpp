@@ -317,6 +317,7 @@ struct lh_handle {
     DevBuf<uint8_t> k_img[2], k_succ;
     DevBuf<float> k_kp1, k_kp2;
     lh_ctrl* h_ctrl = nullptr;   // pinned
+    int last_chains = -1;        // lh_debug_chains: the last synchronous solve's stop chain
     int* h_done = nullptr;       // pinned, mapped lh_host_words: [0] k_ctrl raises it when the LM loop stops, [1] progress
                                  // word 2 * (last live trial) + (one iteration from max_iters)
     int* d_done = nullptr;       // device alias of h_done
@@ -805,6 +806,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.pcg_tol = h->opt.pcg_tol;
     prm.pcg_max_it = h->opt.pcg_max_iters;
     prm.no_evo = getenv("LH_NO_EVO") != nullptr;
+    prm.eval_first = getenv("LH_NO_EVAL_FIRST") == nullptr;
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
     prm.band_narrow = h->band_narrow ? 1 : 0;
@@ -1050,7 +1052,8 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     bool stopped = false;
     int st = enqueue_trial(h, 0, &stopped);
     if (st != LH_OK) return st;
-    const int max_total = (h->opt.max_iters > 0) ? h->opt.max_iters * std::max(1, h->opt.max_trials) : 0;
+    // every trial, plus one re-linearisation chain per iteration at most (an evaluate-only acceptance, ctrl.relin)
+    const int max_total = (h->opt.max_iters > 0) ? h->opt.max_iters * (std::max(1, h->opt.max_trials) + (h->prm.eval_first ? 1 : 0)) : 0;
     const int depth = h->host_comm ? 1 : (h->opt.trials_per_sync > 0 ? std::min(h->opt.trials_per_sync, 32) : 2);
     int enq = 0;
     if (h->host_comm) {
@@ -1118,6 +1121,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         out->time_upload_ms = h->last_upload_ms;
         out->time_download_ms = 0.0;
         h->event_next = 0;
+        h->last_chains = -1;   // (not in the host words)
         return LH_OK;
     }
     HIPCHK(hipEventRecord(e1, s));
@@ -1125,11 +1129,11 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     HIPCHK(hipStreamSynchronize(s));
     const lh_ctrl& c = *h->h_ctrl;
     if (h->comm) {
-        // Equal collective counts on every rank.  The progress word only advances on live trials,
-        // so no rank enqueued more than (stop trial) + depth trials; the stop trial is decided by
+        // Equal collective counts on every rank.  The progress word only advances on live chains,
+        // so no rank enqueued more than (stop chain) + depth chains; the stop chain is decided by
         // identical all-reduced data, so every rank tops up to the same target.  The extra
         // all-reduces carry no data anyone reads (the device has stopped).
-        const int target = std::min(c.trials + depth, max_total);
+        const int target = std::min(c.seq_last + depth, max_total);
         if (enq > target) return LH_E_STATE;   // cannot happen: the bound above
         for (; enq < target; ++enq) {
             NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
@@ -1140,6 +1144,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     const int cur = c.cur;
+    h->last_chains = c.seq_last;
 
     if (out) {
         out->iterations = c.iter;
@@ -1168,7 +1173,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
             printf("Iteration = %d,\tChi = %g,\tLambda = %g\n", i, c.trace_chi[i], c.trace_lambda[i]);
         printf("\nInfo: \nTimeCost(SolveProblem) = %g ms\n", (double)ms);
     }
-    if (h->opt.profile) collect_profile(h, c.trials);
+    if (h->opt.profile) collect_profile(h, c.seq_last);
     else h->event_next = 0;
     return LH_OK;
 }
@@ -1750,6 +1755,12 @@ int lh_debug_time_lin(lh_handle* h, int reps, double* ms) {
 int lh_debug_comm_count(lh_handle* h, int64_t* n) {
     if (!h || !n) return LH_E_BADARG;
     *n = h->n_coll;
+    return LH_OK;
+}
+
+int lh_debug_chains(lh_handle* h, int* chains) {
+    if (!h || !chains) return LH_E_BADARG;
+    *chains = h->last_chains;
     return LH_OK;
 }
 

@@ -716,6 +716,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // round trips before the first sub-batch).
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
+    // the re-linearisation of an evaluate-only acceptance (ctrl->relin, ctrl_lm_step): no back substitution and
+    // no candidate; the committed landmarks and pose tables are linearised into the candidate side, which the
+    // chain's decision commits (the writer copies the committed poses and tables across first)
+    const bool relin = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->relin) != 0;
     // The candidate poses of a trial (VertexPose::add of the step k_ctrl solved) are built here, not in
     // the serial controller: every chunk builds its own window's candidate pose tables (wave 3, below),
     // and block 0 of one launch per trial (writer) stores every candidate pose and its tables, which a
@@ -723,6 +727,12 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     if (TRIAL && writer && blockIdx.x == 0) {
         if (done) return;
         const int P = prm.P, nc = prm.ncam, cnd = 1 - cur;
+        if (relin) {
+            for (int i = threadIdx.x; i < P * 12; i += 256) pose_mat[(size_t)cnd * P * 12 + i] = pose_mat[(size_t)cur * P * 12 + i];
+            for (int i = threadIdx.x; i < P * nc * LH_PT; i += 256)
+                pose_tab[(size_t)cnd * P * nc * LH_PT + i] = pose_tab[(size_t)cur * P * nc * LH_PT + i];
+            return;
+        }
         for (int p = threadIdx.x; p < P; p += 256) {
             double Tc[12], To[12];
 #pragma unroll
@@ -867,7 +877,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // and their tables (lane = (slot, camera)) while the other waves start their first back
     // substitution, which needs only the committed tables; they wait on cflag before their first
     // evaluation at the candidate.  Waves 2 and 3 run one sub-batch fewer than wave 0 in most chunks.
-    if (TRIAL && wave == cwave) {
+    if (TRIAL && !relin && wave == cwave) {
         if (lane < U) {
             double To[12];
             d_pose_candidate(pmc, wdx + 6 * lane, To);
@@ -884,7 +894,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         }
         __hip_atomic_store(cflag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    bool tabs_ready = !TRIAL;
+    bool tabs_ready = !TRIAL || relin;
+    const double* wt_l = relin ? wt_c : wt_n;   // the tables the edges are evaluated and linearised at
 
     for (; sb < (int)sb_end; sb += LH_WAVES) {
         const lh_subbatch S = S_n;       // scalar words, prefetched one sub-batch ahead (sb is wave-uniform)
@@ -939,7 +950,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         const bool ext_rot = (prm.ext_rot_identity >> cam) & 1;
 
         // ---- back-substitution of the pending pose step (problem.cpp:426-429) ----
-        if (TRIAL) {
+        if (TRIAL && !relin) {
             double v3[3] = {0.0, 0.0, 0.0};
             if (live) {
                 const double* pt = wt_c + (slot * ncam + cam) * LH_PT_LDS;
@@ -1004,7 +1015,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 
         if (evo) {   // the same evaluation as below, without the linearisation
             if (has) {
-                const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
+                const double* pt = wt_l + (slot * ncam + cam) * LH_PT_LDS;
                 EdgeEval E;
                 double Pc[3];
                 edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
@@ -1029,7 +1040,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         // [landmark][slot][33]: unique writer; a wave's 16-lane store group covers distinct cells
         double* trow = scr + ((ls & 7) * Cfg::UMAX + slot) * LH_TASKS;
         if (has) {
-            const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
+            const double* pt = wt_l + (slot * ncam + cam) * LH_PT_LDS;
             EdgeEval E;
             double Pc[3];
             edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
@@ -1254,6 +1265,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
 struct CtrlWords {
     double chi, lam, ni, last, spose, chi0;
     int iter, fc, trials, nacc, done, cur, tl;
+    int evo, relin;   // this trial only evaluated; this chain re-linearises (the previous trial was such an acceptance)
 };
 __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl) {
     CtrlWords w;
@@ -1261,6 +1273,7 @@ __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl)
     w.chi0 = ctrl->chi2_initial;
     w.iter = ctrl->iter; w.fc = ctrl->false_cnt; w.trials = ctrl->trials; w.nacc = ctrl->accepted;
     w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
+    w.evo = ctrl->evo; w.relin = ctrl->relin;
     return w;
 }
 // The stop trial's summary and trace to the host words, then done, by ONE thread behind its own
@@ -1281,16 +1294,25 @@ __device__ __noinline__ void publish_stop(const lh_ctrl* __restrict__ ctrl, vola
     host_done[0] = 1;
 }
 
-__device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
+// Returns 1 when this trial was an evaluate-only one accepted outside the final iteration: there is no new
+// system to factor (its controller stops here) and the next chain re-linearises the accepted state (relin).
+// That chain's decision commits the new linearisation (like the initial one) and leaves the LM state alone.
+__device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
                                              volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
                                              int& cur_o, double& lam_o, bool raise_done = true) {
     double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
     int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
     int done = w.done, cur = w.cur;
-    int accept = 0, trace = 0;
+    int accept = 0, trace = 0, relin = 0;
     if (!done) {
-        if (mode == 0) {
+        if (mode != 0 && w.relin) {
+            // the re-linearisation of an evaluate-only acceptance: its records and pose tables were written
+            // to the candidate side (k_lin), which becomes the committed one; lambda, chi2 and the counts
+            // were updated by the acceptance
+            cur = 1 - cur;
+            accept = 1;
+        } else if (mode == 0) {
             // computeLambdaInitLM (problem.cpp:470-504)
             ni = 2.0;
             chi = tchi;
@@ -1346,6 +1368,7 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
                 fc += 1;             // rollbackStates: the committed buffers are untouched
                 inner_end = fc >= prm.max_trials;
             }
+            relin = (ok && w.evo) ? 1 : 0;   // (cleared below when the loop stops)
             if (inner_end) {
                 iter += 1;
                 if (last - chi < prm.stop_dchi2) done = 1;
@@ -1362,11 +1385,17 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
         ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
         ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
         ctrl->acc_hist[seq & 1] = accept;
+        ctrl->seq_last = seq;
+        if (done) relin = 0;
+        ctrl->relin = relin;
         // The next trial is in the final iteration when one more completed iteration reaches max_iters.
         // Its decision then either stops the loop (accept, or the last rejection) or leads to another
-        // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).
+        // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).  With
+        // prm.eval_first a trial after a rejection in its iteration also only evaluates: a run of
+        // rejections (every solve that stops on a stalled chi2 ends with max_trials of them) then pays
+        // evaluations only, and an acceptance among them one re-linearisation chain (relin).
         const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
-        ctrl->evo = (done || prm.no_evo) ? 0 : near;
+        ctrl->evo = (done || relin || prm.no_evo) ? 0 : (near | ((prm.eval_first && fc > 0) ? 1 : 0));
         // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
         // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
         // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
@@ -1388,6 +1417,7 @@ __device__ __forceinline__ void ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const C
     accept_o = accept;
     cur_o = cur;
     lam_o = lam;
+    return relin;
 }
 
 // ============================================================================
@@ -2462,7 +2492,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
     // the decision's words: uniform loads in the same round trip as the system
-    int done = 0, accept = 0;
+    int done = 0, accept = 0, skip = 0;
     double lambda = 0.0;
     int dseq = -1;
     if (decided) {
@@ -2470,6 +2500,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
         dseq = __builtin_amdgcn_readfirstlane(ctrl->done_seq);
+        skip = __builtin_amdgcn_readfirstlane(ctrl->relin);   // an evaluate-only acceptance: nothing to factor
     }
     // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
@@ -2553,7 +2584,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         LH_IMG_TO_LDS();
     }
 #ifndef LH_NO_F0_FIRST
-    else if (early0 && decided && !done) {
+    else if (early0 && decided && !done && !skip) {
         if (!accept) {   // a rejected trial factors the committed block 0
             const int r = lane & 7;
 #pragma unroll
@@ -2599,7 +2630,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             }
             int d_o, a_o, c_o;
             double lam_n;
-            ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            s_flags[2] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
             s_flags[0] = d_o;
             s_flags[1] = a_o;
             s_lam = lam_n;
@@ -2607,11 +2638,12 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         lds_barrier();
         done = s_flags[0];
         accept = s_flags[1];
+        skip = s_flags[2];
         lambda = s_lam;
     }
     // this trial's k_reduce stopped the loop: the summary goes to the host and done is raised here
     if (decided && done && dseq == seq && tid == 0 && host_done) publish_stop(ctrl, host_done);
-    if (done) return;
+    if (done || skip) return;
 #ifdef LH_STAMPS
     if (tid == 0) {
         atomicAdd(&lh_stamps[32], ct_start);
@@ -3050,7 +3082,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         }
         int done, accept, cur;
         double lam_n;
-        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        s_flags[3] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
@@ -3058,7 +3090,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     }
     lds_barrier();
     const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
-    if (done) return;
+    if (done || s_flags[3]) return;   // stopped, or an evaluate-only acceptance (nothing to factor)
     const double lambda = s_lam;
 
 #ifdef LH_STAMPS
@@ -3227,11 +3259,12 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
     // ---------------- the decision ----------------
-    int done = 0, accept = 0;
+    int done = 0, accept = 0, skip = 0;
     double lambda = 0.0;
     if (decided) {
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
+        skip = __builtin_amdgcn_readfirstlane(ctrl->relin);   // an evaluate-only acceptance: nothing to factor
         lambda = ctrl->lambda;
         // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
         if (done && tid == 0 && host_done && ctrl->done_seq == seq) publish_stop(ctrl, host_done);
@@ -3258,7 +3291,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             }
             int d_o, a_o, c_o;
             double lam_n;
-            ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            s_flags[2] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
             s_flags[0] = d_o;
             s_flags[1] = a_o;
             s_lam = lam_n;
@@ -3266,9 +3299,10 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         lds_barrier();
         done = s_flags[0];
         accept = s_flags[1];
+        skip = s_flags[2];
         lambda = s_lam;
     }
-    if (done) return;
+    if (done || skip) return;
 #ifdef LH_STAMPS
     if (tid == 0) {
         atomicAdd(&lh_stamps[32], ct_start);
@@ -3756,7 +3790,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         }
         int done, accept, cur;
         double lam_n;
-        ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        s_flags[3] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
@@ -3764,7 +3798,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
     }
     lds_barrier();
     const int done = s_flags[0], accept = s_flags[1];
-    if (done) return;
+    if (done || s_flags[3]) return;   // stopped, or an evaluate-only acceptance (nothing to factor)
     const double lambda = s_lam;
 
     // ---------------- the chosen system (the candidate's on accept, committed on it; else the committed one) ----------------

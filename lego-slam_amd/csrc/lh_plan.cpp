@@ -396,22 +396,40 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
         if (sb_n > 0) { t_first.push_back(sb_start); t_lg.push_back((uint8_t)sb_lg); }
         sb_n = 0;
     };
+    // The current chunk lives in locals (mask, base, first landmark, tile count) and is pushed when the
+    // next one starts; a landmark whose poses the chunk already holds skips the union tests.
+    uint64_t cmask = 0;
+    int cbase = 0, clm0 = 0, ctiles = 0;
+    bool have = false;
+    auto push_chunk = [&]() {
+        if (!have) return;
+        pl.chunk_lm0.push_back(clm0);
+        pl.chunk_mask.push_back(cmask);
+        pl.chunk_base.push_back(cbase);
+    };
     for (int i = 0; i < Lact; ++i) {
         // the landmark's mask relative to the current chunk's base (landmarks come in ascending first
         // pose, so the base is the chunk's first pose); past 64 poses from the base it starts a chunk
-        const int sh = pl.chunk_lm0.empty() ? 64 : ob[i] - pl.chunk_base.back();
-        const uint64_t m = (sh < 64 && (om[i] >> (63 - sh)) <= 1) ? om[i] << sh : 0ull;
-        const bool fresh = pl.chunk_lm0.empty() || m == 0 || (i - pl.chunk_lm0.back()) >= chunk_lm ||
-                           popc(pl.chunk_mask.back() | m) > LH_UMAX ||
-                           chunk_tiles(pl.chunk_mask.back() | m) > std::max(chunk_tiles(pl.chunk_mask.back()), chunk_tiles(m));
+        const uint64_t oi = om[i];
+        const int sh = have ? ob[i] - cbase : 64;
+        const uint64_t m = (sh < 64 && (oi >> (63 - sh)) <= 1) ? oi << sh : 0ull;
+        bool fresh = m == 0 || (i - clm0) >= chunk_lm;
+        if (!fresh && (cmask | m) != cmask) {
+            const uint64_t u = cmask | m;
+            fresh = popc(u) > LH_UMAX || chunk_tiles(u) > std::max(ctiles, chunk_tiles(m));
+        }
         if (fresh) {
             close_sb();
-            pl.chunk_lm0.push_back(i);
-            pl.chunk_mask.push_back(0ull);
-            pl.chunk_base.push_back(ob[i]);
+            push_chunk();
+            have = true;
+            clm0 = i;
+            cmask = oi;
+            cbase = ob[i];
             c_sb0.push_back((int32_t)t_first.size());
+        } else {
+            cmask |= m;
         }
-        pl.chunk_mask.back() |= fresh ? om[i] : m;
+        ctiles = chunk_tiles(cmask);
         const int lgn = std::max(sb_lg, (int)olg[i]);
         if (sb_n > 0 && sb_n < LH_SB_LM && ((sb_n + 1) << lgn) <= LH_SB_OBS) {
             ++sb_n;
@@ -423,6 +441,7 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
             sb_lg = olg[i];
         }
     }
+    push_chunk();
     close_sb();
     const int NC = (int)pl.chunk_mask.size();
     pl.chunk_lm0.push_back(Lact);

@@ -207,7 +207,7 @@ ABI_SYMBOLS = [
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
     "lh_estimate_pose", "lh_lk_track",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
-    "lh_debug_time_lin", "lh_debug_comm_count", "lh_debug_controller",
+    "lh_debug_time_lin", "lh_debug_comm_count", "lh_debug_controller", "lh_debug_chains",
 ]
 
 _balib = None
@@ -242,6 +242,7 @@ def ba_lib():
         lib.lh_debug_time_lin.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
         lib.lh_debug_comm_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
         lib.lh_debug_controller.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        lib.lh_debug_chains.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         _balib = lib
     return _balib
 
@@ -489,6 +490,13 @@ class Solver:
         v = C.c_int(0)
         _check(ba_lib().lh_debug_controller(self.h, C.byref(v)), "lh_debug_controller")
         return bool(v.value >> 8 & 1)
+
+    def chains(self):
+        """LM chains the last solve decided past the initial linearisation: its trials plus the
+        re-linearisations of evaluate-only acceptances (lh_debug_chains)."""
+        v = C.c_int(0)
+        _check(ba_lib().lh_debug_chains(self.h, C.byref(v)), "lh_debug_chains")
+        return v.value
 
     def comm_count(self):
         """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""

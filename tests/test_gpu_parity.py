@@ -671,7 +671,8 @@ def test_collective_count_is_a_function_of_the_stop_trial(monkeypatch, depth):
     for _ in range(3):
         r = s.solve(w)
         counts.add(s.comm_count())
-    assert counts == {1 + min(r["trials"] + depth, 100)}
+    # chains: the trials, plus a re-linearisation per evaluate-only acceptance (at most one per iteration)
+    assert counts == {1 + min(s.chains() + depth, 10 * (10 + 1))} and s.chains() >= r["trials"]
     s.close()
 
 
@@ -700,6 +701,53 @@ def test_final_iteration_trials_evaluate_only(cfg, family, kw, monkeypatch):
         assert full[k] == evo[k], k
     for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
         assert np.array_equal(full[k], evo[k]), k
+
+
+# After a rejection a trial only evaluates (prm.eval_first): a run of rejections (every solve that stops on a
+# stalled chi2 ends with max_trials of them, problem.cpp:189-218) pays evaluations only, and an acceptance
+# among them costs one re-linearisation chain (ctrl.relin).  LH_NO_EVAL_FIRST=1 linearises every trial
+# outside the final iteration; both must agree bit for bit on every controller, and the windows below
+# (rejections followed by acceptances) must run re-linearisation chains past their trials.
+EVAL_FIRST_CASES = [
+    ("C1 k_ctrl", dict(cfg="C1", seed=0), {}, "k_ctrl"),
+    ("mini k_ctrl", dict(cfg="mini", seed=0), {}, "k_ctrl"),
+    ("C2 strategy 1", dict(cfg="C2", seed=0), dict(strategy=1), "k_ctrl"),
+    ("C2 PCG", dict(cfg="C2", seed=0), dict(linear_solver=lego_ba.LH_SOLVER_PCG), "k_ctrl"),
+    ("C2 max_trials 3", dict(cfg="C2", seed=3), dict(max_trials=3), "k_ctrl"),
+    ("P32 dense", dict(P=32, L=3000, seed=1, pose_mode=1, k_min=2, k_max=8), {}, "k_ctrl_g"),
+    ("P96 banded", dict(P=96, L=6000, seed=2), {}, "k_ctrl_b"),
+    ("P96 PCG", dict(P=96, L=6000, seed=2), dict(linear_solver=lego_ba.LH_SOLVER_PCG), "k_ctrl_p"),
+]
+
+
+def _eval_first_run(wargs, kw, env_off, monkeypatch):
+    wargs = dict(wargs)
+    w = window(wargs.pop("cfg"), seed=wargs.pop("seed")) if "cfg" in wargs else \
+        lego_ba.generate_window(k=8, **wargs)
+    if env_off:
+        monkeypatch.setenv("LH_NO_EVAL_FIRST", "1")
+    s = lego_ba.Solver(**kw)
+    r = s.solve(w)
+    r["controller"] = s.controller()
+    r["chains"] = s.chains()
+    s.close()
+    monkeypatch.delenv("LH_NO_EVAL_FIRST", raising=False)
+    return r
+
+
+def test_trials_after_a_rejection_evaluate_first(monkeypatch):
+    relin_cases = 0
+    for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
+        full = _eval_first_run(wargs, kw, True, monkeypatch)
+        ef = _eval_first_run(wargs, kw, False, monkeypatch)
+        assert ef["controller"] == ctrl, name
+        for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "chi2_initial"):
+            assert full[k] == ef[k], (name, k)
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
+            assert np.array_equal(full[k], ef[k]), (name, k)
+        assert full["chains"] == full["trials"] and ef["chains"] >= ef["trials"], name
+        relin_cases += ef["chains"] > ef["trials"]
+    assert relin_cases >= 6
 
 
 # ---------------------------------------------------------------------------------------------
