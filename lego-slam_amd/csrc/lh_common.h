@@ -116,7 +116,9 @@ struct lh_ctrl {
     int32_t iter, false_cnt, trials, accepted, done, cur, trace_len;
     int32_t nonpd;             // rank-deficient H_ll landmarks at the initial linearisation
     int32_t pcg_iters;         // PCG iterations summed over the solve's trials
-    int32_t evo;               // the next trial is in the final LM iteration: k_lin evaluates only
+    int32_t evo;               // the next trial only evaluates (the final LM iteration, or after a rejection)
+    int32_t evo_seq[2];        // trial seq's evo at [seq & 1]: written by the previous chain's decision, so the
+                               // kernels after this trial's decision (k_reduce's blocks, k_ctrl) still read it
     int32_t acc_hist[2];       // trial seq's LM decision (accepted) at [seq & 1]: read by its controller, and by
                                // the next trial's k_reduce when it commits the staged system (commit_in_reduce)
     int32_t done_seq;          // the trial whose decision stopped the loop (its controller raises the host's done)

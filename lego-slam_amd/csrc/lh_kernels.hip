@@ -1395,7 +1395,9 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
         // rejections (every solve that stops on a stalled chi2 ends with max_trials of them) then pays
         // evaluations only, and an acceptance among them one re-linearisation chain (relin).
         const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
-        ctrl->evo = (done || relin || prm.no_evo) ? 0 : (near | ((prm.eval_first && fc > 0) ? 1 : 0));
+        const int evo_n = (done || relin || prm.no_evo) ? 0 : (near | ((prm.eval_first && fc > 0) ? 1 : 0));
+        ctrl->evo = evo_n;
+        ctrl->evo_seq[(seq + 1) & 1] = evo_n;
         // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
         // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
         // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
@@ -1409,7 +1411,10 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
                 // else the same trial's controller publishes the summary from lh_ctrl and raises done
                 // (publish_stop): only stores of the thread that fences are ordered before done
             } else {
-                host_done[1] = 2 * seq + near;
+                // near also when the next trial's rejection would end its iteration at an unchanged chi2 (a
+                // stalled solve's last trial: the stop rule then ends the loop), so no chain is left past it
+                const int last_try = (fc + 1 >= prm.max_trials && last - chi < prm.stop_dchi2) ? 1 : 0;
+                host_done[1] = 2 * seq + (near | last_try);
             }
         }
     }
@@ -1454,9 +1459,12 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     const int ib = (int)rt.y, ie = (int)rt.z;
     const int p = (int)(rt.w & 0xffffu), q = (int)(rt.w >> 16);
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
-    const int evo = __builtin_amdgcn_readfirstlane(ctrl->evo);   // k_lin wrote the chunk scalars only
-    if ((prm.commit_in_reduce | prm.img) && mode != 0 && b < LY.npairs && done == 0 && wave == 0) {
-        if (__builtin_amdgcn_readfirstlane(ctrl->acc_hist[(seq - 1) & 1])) {
+    // k_lin wrote the chunk scalars only (this trial's word: the scalar block's decision writes the next one's)
+    const int evo = mode != 0 ? __builtin_amdgcn_readfirstlane(ctrl->evo_seq[seq & 1]) : 0;
+    const bool copy_prev = (prm.commit_in_reduce | prm.img) && mode != 0 && b < LY.npairs && done == 0 && wave == 0;
+    const int prev_acc = copy_prev ? __builtin_amdgcn_readfirstlane(ctrl->acc_hist[(seq - 1) & 1]) : 0;
+    if (copy_prev) {
+        if (prev_acc) {
             if (prm.img) {   // this pair's entries of k_ctrl's image (their slots below), then the rhs row's
                 if (lane < 36) {
                     const int ea_ = lane / 6, eb_ = lane - 6 * (lane / 6), gi = 6 * p + ea_, gj = 6 * q + eb_;
@@ -1481,6 +1489,26 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                 const int i = part_off + 6 * p + (k % 6);
                 st_red(rs_commit + i, rs[i]);
             }
+        }
+    }
+    // An evaluate-only trial writes no system, and if it is rejected its controller factors the committed one:
+    // k_ctrl's image path loads the staged image before the decision is known, so this pair's committed
+    // entries (image slots, rhs row, b_s, b_p, diag H_pp) are copied to the staged side here, and that
+    // controller then needs no second load after a rejection.  After an accepted trial the copy above has
+    // just made the two sides equal, and this one is skipped.
+    if (prm.img && evo && !prev_acc && b < LY.npairs && done == 0 && wave == 0) {
+        if (lane < 36) {
+            const int ea_ = lane / 6, eb_ = lane - 6 * (lane / 6), gi = 6 * p + ea_, gj = 6 * q + eb_;
+            const int idx = (p < q) ? gj * LH_IMG_AS + gi : ((ea_ >= eb_) ? gi * LH_IMG_AS + gj : -1);
+            if (idx >= 0) st_red(img + idx, img[LH_IMG_SZ + idx]);
+        } else if (p == q && lane < 42) {
+            const int idx = LH_NPAD * LH_IMG_AS + 6 * p + (lane - 36);
+            st_red(img + idx, img[LH_IMG_SZ + idx]);
+        }
+        if (p == q && lane >= 36 && lane < 54) {
+            const int k = lane - 36, part_off = (k < 6) ? LY.off_bs : (k < 12) ? LY.off_bp : LY.off_hd;
+            const int i = part_off + 6 * p + (k % 6);
+            st_red(rs + i, rs_commit[i]);
         }
     }
     // (p > q and ib > ie never hold: they make the exit test need the pair words, so the compiler issues
@@ -2495,12 +2523,14 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     int done = 0, accept = 0, skip = 0;
     double lambda = 0.0;
     int dseq = -1;
+    bool staged_is_commit = false;   // an evaluate-only trial: k_reduce copied the committed system to the staged side
     if (decided) {
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
         dseq = __builtin_amdgcn_readfirstlane(ctrl->done_seq);
         skip = __builtin_amdgcn_readfirstlane(ctrl->relin);   // an evaluate-only acceptance: nothing to factor
+        staged_is_commit = imgp && __builtin_amdgcn_readfirstlane(ctrl->evo_seq[seq & 1]) != 0;
     }
     // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
@@ -2585,7 +2615,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
 #ifndef LH_NO_F0_FIRST
     else if (early0 && decided && !done && !skip) {
-        if (!accept) {   // a rejected trial factors the committed block 0
+        if (!accept && !staged_is_commit) {   // a rejected trial factors the committed block 0
             const int r = lane & 7;
 #pragma unroll
             for (int q = 0; q < 8; ++q) b0s[q] = img[LH_IMG_SZ + r * AS + q];
@@ -2662,8 +2692,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         // The image: a straight copy (16-byte LDS stores at consecutive addresses, issued above), lambda
         // added on the diagonal of the real rows by the thread that stored it (the identity padding and the
         // zero upper triangle come with the image).  k_reduce commits an accepted system to img[1] before
-        // the next trial overwrites img[0] (commit_in_reduce's role), so nothing here copies S.
-        if (!accept) {
+        // the next trial overwrites img[0] (commit_in_reduce's role), so nothing here copies S.  After an
+        // evaluate-only trial the staged side already holds the committed system (k_reduce), so no reload.
+        if (!accept && !staged_is_commit) {
             const double2* __restrict__ imgc2 = reinterpret_cast<const double2*>(img + LH_IMG_SZ);
 #pragma unroll
             for (int u = 0; u < NIMG; ++u) iv[u] = imgc2[(cpw && img_need(ctid + CW * u)) ? ctid + CW * u : 0];

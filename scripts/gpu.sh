@@ -14,6 +14,7 @@
 #   ab=LIB             rocprofv3 A/B of the current library against LIB, alternated twice (k_lin, k_reduce,
 #                      k_ctrl* averages and the bench line of each)
 #   py=SCRIPT[,ARGS]   python3 SCRIPT ARGS (a measurement script under scripts/)
+#   pytrace=SCRIPT[,ARGS]  rocprofv3 --kernel-trace --stats of that script (per-kernel averages; the raw trace kept)
 #   bin=PATH           a diagnostic binary built in-tree (lego-slam_amd/lib/ubench_*)
 #   env=VAR=VALUE      export VAR for the steps after it (their outputs get a _VAR_VALUE suffix); unenv=VAR
 set -u
@@ -99,6 +100,16 @@ for step in "$@"; do
         [ "$scr" != "$arg" ] && rest=${arg#*,}
         timeout -k 10 600 python3 $scr ${rest//,/ } > "$OUT/$(basename $scr .py)$SFX.log" 2>&1 || { tail -30 "$OUT/$(basename $scr .py)$SFX.log"; exit 1; }
         tail -30 "$OUT/$(basename $scr .py)$SFX.log" ;;
+    pytrace)
+        scr=${arg%%,*}
+        rest=""
+        [ "$scr" != "$arg" ] && rest=${arg#*,}
+        nm=pytrace_$(basename $scr .py)$SFX
+        rm -rf "$OUT/$nm"
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/$nm" -o run --output-format csv -- python3 $scr ${rest//,/ } \
+            > "$OUT/$nm.log" 2>&1 || { tail -20 "$OUT/$nm.log"; exit 1; }
+        tail -8 "$OUT/$nm.log"
+        kstats "$nm" "$OUT/$nm" | tee "$OUT/${nm}_summary.txt" ;;
     env)
         export "$arg"
         SFX="_${arg//[^A-Za-z0-9]/_}" ;;
