@@ -707,7 +707,9 @@ def test_final_iteration_trials_evaluate_only(cfg, family, kw, monkeypatch):
 # stalled chi2 ends with max_trials of them, problem.cpp:189-218) pays evaluations only, and an acceptance
 # among them costs one re-linearisation chain (ctrl.relin).  LH_NO_EVAL_FIRST=1 linearises every trial
 # outside the final iteration; both must agree bit for bit on every controller, and the windows below
-# (rejections followed by acceptances) must run re-linearisation chains past their trials.
+# (rejections followed by acceptances) must run re-linearisation chains past their trials.  Most are chaotic
+# windows, picked on the current kernels' trajectories (`scripts/eval_first_cases.py` lists the chains per
+# window): a change of rounding in k_lin moves where their rejections fall, and the list with it.
 EVAL_FIRST_CASES = [
     ("C1 k_ctrl", dict(cfg="C1", seed=0), {}, "k_ctrl"),
     ("mini k_ctrl", dict(cfg="mini", seed=0), {}, "k_ctrl"),
