@@ -392,7 +392,26 @@ class Solver:
         self._win = _WindowRef(w)
         _check(ba_lib().lh_upload(self.h, C.byref(self._win.s)), "lh_upload")
 
+    _SCALARS = ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "time_ms",
+                "pcg_iterations", "degenerate", "time_prep_ms", "time_upload_ms", "time_download_ms")
+
     def solve_resident(self, want_states=False, want_edges=False, trace_cap=64, outlier_chi2_th=None):
+        if not want_states and not want_edges and outlier_chi2_th is None:
+            # the array-free solve (the library's fast path): one lh_result and trace buffers per solver,
+            # reused; the returned trace is a copy of the entries written
+            fr = getattr(self, "_fast", None)
+            if fr is None or fr[0] != trace_cap:
+                tc, tl = np.zeros(trace_cap), np.zeros(trace_cap)
+                r = LhResult()
+                r.trace_chi2, r.trace_lambda, r.trace_cap = _ptr(tc), _ptr(tl), trace_cap
+                fr = self._fast = (trace_cap, r, C.byref(r), tc, tl)
+            _, r, rref, tc, tl = fr
+            _check(ba_lib().lh_solve_resident(self.h, rref), "lh_solve_resident")
+            n = r.trace_len
+            out = {f: getattr(r, f) for f in self._SCALARS}
+            out.update(pose_Tcw=None, lm_xyz=None, edge_robust_chi2=None, trace_chi2=tc[:n].copy(),
+                       trace_lambda=tl[:n].copy())
+            return out
         s = self._win.s
         r, out = self._result(s.n_poses, s.n_landmarks, s.n_obs, trace_cap, want_states, want_edges,
                               outlier_chi2_th=outlier_chi2_th)
