@@ -1045,7 +1045,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
                       !h->comm && !h->host_comm && !h->opt.profile && !h->opt.verbose;
     const double t_start = now_ms();
     h->n_coll = 0;
-    HIPCHK(hipEventRecord(e0, s));
+    if (!fast) HIPCHK(hipEventRecord(e0, s));   // (the array-free solve times itself on the host clock)
     HIPCHK(lh_launch_reset(s, h->d_rec.p, h->d_lm_perm.p, h->d_lm_in.p, h->n_rec, h->d_qt.p, h->d_qt_init.p, 24 * P,
                            h->d_ptab.p, h->d_ptab_init.p, (int)(2 * PT), h->d_dxp.p, 6 * std::max(P, 1), h->d_ctrl.p));
     DBGSYNC("k_reset");
