@@ -257,6 +257,17 @@ LH_HD static inline bool lh_bimg_in(int r, int c) {
 }
 
 // k_ctrl_b's per-window tables (bblk null: no banded controller for this window)
+// The restart of a resident solve, done by the initial linearisation's block 0 (k_lin<T, false>): controller
+// zeroed, both pose and pose-table buffers from their initial copies, the step zeroed; its chunks read the
+// landmarks straight from the window (lm_perm, lm_in) and the initial tables from ptab_init.
+struct lh_reset_args {
+    const int32_t* lm_perm;    // record -> window landmark (-1: padding)
+    const double* lm_in;       // [L][3] the uploaded landmark positions
+    const double* qt_init;     // [2][P][12] initial poses (both slots)
+    const double* ptab_init;   // [2][P * ncam * LH_PT] initial pose tables (both slots)
+    int nqt, nptab, ndxp;
+};
+
 struct lh_band_args {
     const int32_t* bblk;     // [P * 64] block of pose pair (p, p + d), -1 if absent
     const uint16_t* units;   // [16 waves][6 LH_PMAX_ANY / 8 steps] unit words

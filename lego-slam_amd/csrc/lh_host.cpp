@@ -37,7 +37,7 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag,
                          long nslots, lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat,
-                         int writer);
+                         int writer, lh_reset_args rst);
 hipError_t lh_launch_reduce(hipStream_t st, const double* rows, const double* csc, const uint32_t* red_tab, int nred,
                             lh_ctrl* ctrl, double* rs_stage, double* rs_commit, double* maxd,
                             lh_params prm, int n_chunks, int mode, int* host_done, int seq, double* img);
@@ -869,7 +869,12 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
 // with no chunks when the window has none) stores the trial's candidate poses and pose tables.
 int launch_lin(lh_handle* h, int trial) {
     hipStream_t s = h->stream;
-    int writer = trial ? 1 : 0;
+    // block 0 of the first launch: a trial's candidate poses and tables, or (the initial linearisation) the
+    // restart of the solve from the uploaded window
+    int writer = 1;
+    const int P = h->P;
+    const lh_reset_args rst{h->d_lm_perm.p, h->d_lm_in.p, h->d_qt_init.p, h->d_ptab_init.p, 24 * P,
+                            (int)(2 * (size_t)P * h->ncam * LH_PT), 6 * std::max(P, 1)};
     for (int T = 1; T <= LH_TMAX; ++T) {
         const int c0 = h->plan.tgroup_begin[T], c1 = h->plan.tgroup_begin[T + 1];
         const bool last = T == LH_TMAX;
@@ -877,7 +882,7 @@ int launch_lin(lh_handle* h, int trial) {
         HIPCHK(lh_launch_lin(T, trial, c1 - c0, c0, s, h->d_chunks.p, h->d_sbs.p, h->d_uv.p, h->d_meta.p, h->d_rec.p,
                              h->d_ptab.p, h->d_ext.p, h->d_ctrl.p, h->d_dxp.p, h->d_rho.p, h->d_rows.p,
                              h->d_csc.p, h->d_items.p, h->d_wflag.p, (long)h->n_slots, h->prm, h->n_rec,
-                             h->d_fixed.p, h->d_qt.p, writer));
+                             h->d_fixed.p, h->d_qt.p, writer, rst));
         writer = 0;
         DBGSYNC("k_lin");
     }
@@ -1031,8 +1036,6 @@ int download(lh_handle* h, lh_result* out, int cur) {
 int solve_resident_impl(lh_handle* h, lh_result* out) {
     if (!h->uploaded) return LH_E_STATE;
     hipStream_t s = h->stream;
-    const int P = h->P;
-    const size_t PT = (size_t)P * h->ncam * LH_PT;
     hipEvent_t e0 = next_event(h), e1 = next_event(h);
     if (!e0 || !e1) return LH_E_HIP;
     volatile int* hd = h->h_done;   // [0] done, [1] progress word (ctrl_lm_step)
@@ -1046,9 +1049,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     const double t_start = now_ms();
     h->n_coll = 0;
     if (!fast) HIPCHK(hipEventRecord(e0, s));   // (the array-free solve times itself on the host clock)
-    HIPCHK(lh_launch_reset(s, h->d_rec.p, h->d_lm_perm.p, h->d_lm_in.p, h->n_rec, h->d_qt.p, h->d_qt_init.p, 24 * P,
-                           h->d_ptab.p, h->d_ptab_init.p, (int)(2 * PT), h->d_dxp.p, 6 * std::max(P, 1), h->d_ctrl.p));
-    DBGSYNC("k_reset");
+    // (the restart -- controller, poses, tables, step -- is the initial linearisation's block 0, launch_lin)
     bool stopped = false;
     int st = enqueue_trial(h, 0, &stopped);
     if (st != LH_OK) return st;

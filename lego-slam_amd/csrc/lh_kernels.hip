@@ -705,7 +705,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     double* __restrict__ edge_rho, double* __restrict__ rows, double* __restrict__ csc,
     const uint32_t* __restrict__ crow, uint8_t* __restrict__ wflag, long nslots,
     lh_params prm, int nrec, const uint64_t* __restrict__ fixed_bits, int chunk_base,
-    double* __restrict__ pose_mat, int writer) {
+    double* __restrict__ pose_mat, int writer, lh_reset_args rst) {
     using Cfg = LinCfg<T>;
     extern __shared__ __attribute__((aligned(16))) double dsm[];
 
@@ -714,8 +714,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // included; (2) the pose-table and pose-step values, whose addresses need the chunk's pose slots.
     // Written as per-element loops, each loop iteration waited for its own loads (ten serialised
     // round trips before the first sub-batch).
-    const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
-    const int cur = __builtin_amdgcn_readfirstlane(ctrl->cur);
+    // the initial linearisation restarts the solve (rst, its writer block below): the controller is not read
+    const int done = TRIAL ? __builtin_amdgcn_readfirstlane(ctrl->done) : 0;
+    const int cur = TRIAL ? __builtin_amdgcn_readfirstlane(ctrl->cur) : 0;
     // the re-linearisation of an evaluate-only acceptance (ctrl->relin, ctrl_lm_step): no back substitution and
     // no candidate; the committed landmarks and pose tables are linearised into the candidate side, which the
     // chain's decision commits (the writer copies the committed poses and tables across first)
@@ -724,6 +725,14 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // the serial controller: every chunk builds its own window's candidate pose tables (wave 3, below),
     // and block 0 of one launch per trial (writer) stores every candidate pose and its tables, which a
     // later trial reads as committed and the caller as the result.
+    if (!TRIAL && writer && blockIdx.x == 0) {   // the restart (what a separate reset kernel did)
+        int* c = reinterpret_cast<int*>(const_cast<lh_ctrl*>(ctrl));
+        for (int i = threadIdx.x; i < (int)(sizeof(lh_ctrl) / sizeof(int)); i += 256) c[i] = 0;   // cur = 0
+        for (int i = threadIdx.x; i < rst.nqt; i += 256) pose_mat[i] = rst.qt_init[i];
+        for (int i = threadIdx.x; i < rst.nptab; i += 256) pose_tab[i] = rst.ptab_init[i];
+        for (int i = threadIdx.x; i < rst.ndxp; i += 256) const_cast<double*>(dxp)[i] = 0.0;
+        return;
+    }
     if (TRIAL && writer && blockIdx.x == 0) {
         if (done) return;
         const int P = prm.P, nc = prm.ncam, cnd = 1 - cur;
@@ -745,11 +754,11 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         }
         return;
     }
-    const int chunk = chunk_base + blockIdx.x - ((TRIAL && writer) ? 1 : 0);
+    const int chunk = chunk_base + blockIdx.x - (writer ? 1 : 0);
     // a trial of the final LM iteration (ctrl->evo, ctrl_lm_step): back substitution and the
     // candidate's evaluation only (landmark positions, rho0 per edge, chi2 and the gain scale)
     const bool evo = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->evo) != 0;
-    const double lambda = ctrl->lambda;
+    const double lambda = TRIAL ? ctrl->lambda : 0.0;
     const uint32_t* __restrict__ chw = reinterpret_cast<const uint32_t*>(chunks + chunk);
     const uint32_t sb_begin = __builtin_amdgcn_readfirstlane(chw[0]), sb_end = __builtin_amdgcn_readfirstlane(chw[1]);
     const int U = (int)(__builtin_amdgcn_readfirstlane(chw[2]) & 0xffu);   // lh_chunk: {sb_begin, sb_end, U, T, ...}
@@ -777,6 +786,17 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     const int cwave = LH_WAVES - 1 - (blockIdx.x & 1);
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
+    // piece lane & 7 of sub-batch sbx's record (lane >> 3); the initial linearisation reads only X, from the window
+    auto rec_piece = [&](int sbx) -> double2 {
+        if constexpr (TRIAL) {
+            return rc2[(size_t)sbx * 64 + lane];
+        } else {
+            const int q = lane & 7, l = rst.lm_perm[sbx * LH_SB_LM + (lane >> 3)];
+            if (q > 1 || l < 0) return double2{0.0, 0.0};
+            const double* X = rst.lm_in + 3 * (size_t)l;
+            return q == 0 ? double2{X[0], X[1]} : double2{X[2], 0.0};
+        }
+    };
     double* __restrict__ rn = rec + (size_t)cand * nrec * LH_REC;
     // a descriptor over both record buffers (write-through record stores, LH_WT_REC)
     const __amdgpu_buffer_rsrc_t rec_rsrc =
@@ -816,7 +836,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
         const float2 z = reinterpret_cast<const float2*>(obs_uv)[o];   // the float pixel, widened exactly
         u_n = (double)z.x;
         v_n = (double)z.y;
-        r_n = rc2[(size_t)sbc * 64 + lane];
+        r_n = rec_piece(sbc);
     }
     {
         // round 1: the pose slot of each table element this thread copies, the extrinsics, the
@@ -848,7 +868,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             const int i = tid + 256 * k;
             const size_t g = (size_t)tp[k] * per + min(max(i - tsl[k] * per, 0), per - 1);
             tc[k] = pose_tab[(size_t)cur * PT + g];
-            tn[k] = TRIAL ? 0.0 : pose_tab[(size_t)cand * PT + g];   // a trial builds its candidate tables
+            tn[k] = TRIAL ? 0.0 : rst.ptab_init[(size_t)cand * PT + g];   // a trial builds its candidate tables
         }
         if (TRIAL && wave == cwave) {   // the committed pose of slot lane (lane < U)
             const uint32_t pp = min((uint32_t)cpose[min(lane, umax1)], pmax1);
@@ -917,7 +937,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
             const float2 z = reinterpret_cast<const float2*>(obs_uv)[on];
             u_n = (double)z.x;
             v_n = (double)z.y;
-            r_n = rc2[(size_t)sbn * 64 + lane];
+            r_n = rec_piece(sbn);
         }
         // landmark records through LDS: lane -> its landmark's record (records LH_REC_LDS apart)
         reinterpret_cast<double2*>(scr)[(lane >> 3) * (LH_REC_LDS / 2) + (lane & 7)] = rr;
@@ -4576,8 +4596,9 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
                          double* edge_rho, double* rows, double* csc, const uint32_t* crow, uint8_t* wflag, long nslots,
-                         lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat, int writer) {
-    writer = (trial && writer) ? 1 : 0;   // block 0 stores the trial's candidate poses and tables
+                         lh_params prm, int nrec, const uint64_t* fixed_bits, double* pose_mat, int writer,
+                         lh_reset_args rst) {
+    writer = writer ? 1 : 0;   // block 0 stores the trial's candidate poses and tables (the restart, initially)
     if (nchunks + writer <= 0) return hipSuccess;
     dim3 g(nchunks + writer), b(256);
 #define LH_LIN(TT, TR)                                                                                             \
@@ -4586,11 +4607,11 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
         if (prm.precision == 1)                                                                                    \
             hipLaunchKernelGGL((k_lin<TT, TR, true>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
                                dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base,     \
-                               pose_mat, writer);                                                                  \
+                               pose_mat, writer, rst);                                                             \
         else                                                                                                       \
             hipLaunchKernelGGL((k_lin<TT, TR, false>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
                                dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base,     \
-                               pose_mat, writer);                                                                  \
+                               pose_mat, writer, rst);                                                             \
     } while (0)
     switch (T * 2 + (trial ? 1 : 0)) {
         case 2: LH_LIN(1, false); break;
