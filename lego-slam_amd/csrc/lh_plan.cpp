@@ -383,66 +383,114 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
     // rather than let the union grow past the larger of the two tile counts.  A sub-batch takes
     // landmarks while it holds < 8 and (n + 1) << lg <= 64 (landmark l owns the aligned lane group
     // [l*G, l*G + k_l) of its 64 slots, G = 2^lg the largest pow2ceil(k) in the sub-batch).
-    pl.chunk_lm0.clear();
-    pl.chunk_mask.clear();
-    pl.chunk_base.clear();
+    // The pass runs over segments of the span order in parallel, each cut where the first pose changes
+    // and started as a fresh chunk; the segments are then joined only if the serial pass would have started
+    // a fresh chunk at every cut too (a sliding window's chunks end where the first pose moves: the union
+    // with the next run of poses raises the tile count), else the serial pass runs: the same plan either way.
+    struct Cut {
+        std::vector<int32_t> lm0, base, sb0, tfirst;   // sb0: relative to this segment's sub-batches
+        std::vector<uint64_t> mask;
+        std::vector<uint8_t> tlg;
+        uint64_t cmask = 0;
+        int cbase = 0, clm0 = 0, ctiles = 0;
+        bool have = false;
+    };
+    auto fresh_at = [&](const Cut& c, int i, uint64_t& m) {
+        const uint64_t oi = om[i];
+        const int sh = c.have ? ob[i] - c.cbase : 64;
+        m = (sh < 64 && (oi >> (63 - sh)) <= 1) ? oi << sh : 0ull;
+        bool fresh = m == 0 || (i - c.clm0) >= chunk_lm;
+        if (!fresh && (c.cmask | m) != c.cmask) {
+            const uint64_t u = c.cmask | m;
+            fresh = popc(u) > LH_UMAX || chunk_tiles(u) > std::max(c.ctiles, chunk_tiles(m));
+        }
+        return fresh;
+    };
+    auto cut_range = [&](int i0, int i1, Cut& c) {
+        c.tfirst.reserve((size_t)(i1 - i0) / 4 + 8);
+        c.tlg.reserve((size_t)(i1 - i0) / 4 + 8);
+        int sb_start = 0, sb_n = 0, sb_lg = 0;
+        auto close_sb = [&]() {
+            if (sb_n > 0) { c.tfirst.push_back(sb_start); c.tlg.push_back((uint8_t)sb_lg); }
+            sb_n = 0;
+        };
+        // the current chunk lives in c's locals and is pushed when the next one starts
+        auto push_chunk = [&]() {
+            if (!c.have) return;
+            c.lm0.push_back(c.clm0);
+            c.mask.push_back(c.cmask);
+            c.base.push_back(c.cbase);
+        };
+        for (int i = i0; i < i1; ++i) {
+            // the landmark's mask relative to the current chunk's base (landmarks come in ascending first
+            // pose, so the base is the chunk's first pose); past 64 poses from the base it starts a chunk
+            uint64_t m;
+            if (fresh_at(c, i, m)) {
+                close_sb();
+                push_chunk();
+                c.have = true;
+                c.clm0 = i;
+                c.cmask = om[i];
+                c.cbase = ob[i];
+                c.sb0.push_back((int32_t)c.tfirst.size());
+            } else {
+                c.cmask |= m;
+            }
+            c.ctiles = chunk_tiles(c.cmask);
+            const int lgn = std::max(sb_lg, (int)olg[i]);
+            if (sb_n > 0 && sb_n < LH_SB_LM && ((sb_n + 1) << lgn) <= LH_SB_OBS) {
+                ++sb_n;
+                sb_lg = lgn;
+            } else {
+                close_sb();
+                sb_start = i;
+                sb_n = 1;
+                sb_lg = olg[i];
+            }
+        }
+        push_chunk();
+        close_sb();
+    };
+    // segment starts: about two per pool thread, each moved forward to the next change of first pose
+    std::vector<int> seg{0};
+    {
+        const int want = pool ? 2 * pool->size() : 1;
+        for (int k = 1; k < want; ++k) {
+            int i = (int)((int64_t)Lact * k / want);
+            i = std::max(i, seg.back() + 1);
+            while (i < Lact && ob[i] == ob[i - 1]) ++i;
+            if (i < Lact && i > seg.back()) seg.push_back(i);
+        }
+        seg.push_back(Lact);
+    }
+    const int nseg = (int)seg.size() - 1;
+    std::vector<Cut> cuts((size_t)std::max(nseg, 1));
+    if (pool && nseg > 1) pool->run(nseg, [&](int k) { cut_range(seg[k], seg[k + 1], cuts[k]); });
+    else for (int k = 0; k < nseg; ++k) cut_range(seg[k], seg[k + 1], cuts[k]);
+    bool joined = true;
+    for (int k = 1; k < nseg && joined; ++k) {
+        uint64_t m;
+        joined = fresh_at(cuts[k - 1], seg[k], m);
+    }
+    if (!joined) {   // a chunk would run across a cut: the serial pass
+        cuts.assign(1, Cut{});
+        cut_range(0, Lact, cuts[0]);
+    }
     std::vector<int32_t> c_sb0;              // per chunk (creation order): its first sub-batch
     std::vector<int32_t> t_first;            // sub-batches in creation order: first position
     std::vector<uint8_t> t_lg;
-    t_first.reserve((size_t)Lact / 4 + 16);
-    t_lg.reserve((size_t)Lact / 4 + 16);
-    int sb_start = 0, sb_n = 0, sb_lg = 0;
-    auto close_sb = [&]() {
-        if (sb_n > 0) { t_first.push_back(sb_start); t_lg.push_back((uint8_t)sb_lg); }
-        sb_n = 0;
-    };
-    // The current chunk lives in locals (mask, base, first landmark, tile count) and is pushed when the
-    // next one starts; a landmark whose poses the chunk already holds skips the union tests.
-    uint64_t cmask = 0;
-    int cbase = 0, clm0 = 0, ctiles = 0;
-    bool have = false;
-    auto push_chunk = [&]() {
-        if (!have) return;
-        pl.chunk_lm0.push_back(clm0);
-        pl.chunk_mask.push_back(cmask);
-        pl.chunk_base.push_back(cbase);
-    };
-    for (int i = 0; i < Lact; ++i) {
-        // the landmark's mask relative to the current chunk's base (landmarks come in ascending first
-        // pose, so the base is the chunk's first pose); past 64 poses from the base it starts a chunk
-        const uint64_t oi = om[i];
-        const int sh = have ? ob[i] - cbase : 64;
-        const uint64_t m = (sh < 64 && (oi >> (63 - sh)) <= 1) ? oi << sh : 0ull;
-        bool fresh = m == 0 || (i - clm0) >= chunk_lm;
-        if (!fresh && (cmask | m) != cmask) {
-            const uint64_t u = cmask | m;
-            fresh = popc(u) > LH_UMAX || chunk_tiles(u) > std::max(ctiles, chunk_tiles(m));
-        }
-        if (fresh) {
-            close_sb();
-            push_chunk();
-            have = true;
-            clm0 = i;
-            cmask = oi;
-            cbase = ob[i];
-            c_sb0.push_back((int32_t)t_first.size());
-        } else {
-            cmask |= m;
-        }
-        ctiles = chunk_tiles(cmask);
-        const int lgn = std::max(sb_lg, (int)olg[i]);
-        if (sb_n > 0 && sb_n < LH_SB_LM && ((sb_n + 1) << lgn) <= LH_SB_OBS) {
-            ++sb_n;
-            sb_lg = lgn;
-        } else {
-            close_sb();
-            sb_start = i;
-            sb_n = 1;
-            sb_lg = olg[i];
-        }
+    pl.chunk_lm0.clear();
+    pl.chunk_mask.clear();
+    pl.chunk_base.clear();
+    for (const Cut& c : cuts) {
+        const int32_t off = (int32_t)t_first.size();
+        for (int32_t v : c.sb0) c_sb0.push_back(v + off);
+        pl.chunk_lm0.insert(pl.chunk_lm0.end(), c.lm0.begin(), c.lm0.end());
+        pl.chunk_mask.insert(pl.chunk_mask.end(), c.mask.begin(), c.mask.end());
+        pl.chunk_base.insert(pl.chunk_base.end(), c.base.begin(), c.base.end());
+        t_first.insert(t_first.end(), c.tfirst.begin(), c.tfirst.end());
+        t_lg.insert(t_lg.end(), c.tlg.begin(), c.tlg.end());
     }
-    push_chunk();
-    close_sb();
     const int NC = (int)pl.chunk_mask.size();
     pl.chunk_lm0.push_back(Lact);
     c_sb0.push_back((int32_t)t_first.size());
