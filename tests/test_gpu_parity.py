@@ -738,7 +738,7 @@ def _eval_first_run(wargs, kw, env_off, monkeypatch):
 
 
 def test_trials_after_a_rejection_evaluate_first(monkeypatch):
-    relin_cases = 0
+    relin = []
     for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
         full = _eval_first_run(wargs, kw, True, monkeypatch)
         ef = _eval_first_run(wargs, kw, False, monkeypatch)
@@ -748,8 +748,11 @@ def test_trials_after_a_rejection_evaluate_first(monkeypatch):
         for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
             assert np.array_equal(full[k], ef[k]), (name, k)
         assert full["chains"] == full["trials"] and ef["chains"] >= ef["trials"], name
-        relin_cases += ef["chains"] > ef["trials"]
-    assert relin_cases >= 6
+        if ef["chains"] > ef["trials"]:
+            relin.append(name)
+    # six of the eight re-linearise on the current kernels; a change of rounding may move a chaotic window's
+    # rejections, so the bar is four
+    assert len(relin) >= 4, relin
 
 
 # ---------------------------------------------------------------------------------------------
