@@ -11,8 +11,11 @@ from test_gpu_parity import EVAL_FIRST_CASES  # noqa: E402
 
 
 def mk(wargs):
+    from windows import multi_camera
     wargs = dict(wargs)
-    return window(wargs.pop("cfg"), seed=wargs.pop("seed")) if "cfg" in wargs else lego_ba.generate_window(k=8, **wargs)
+    cams = wargs.pop("cams", 0)
+    w = window(wargs.pop("cfg"), seed=wargs.pop("seed")) if "cfg" in wargs else lego_ba.generate_window(k=8, **wargs)
+    return multi_camera(w, cams, seed=1) if cams else w
 
 
 for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
