@@ -726,6 +726,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // and block 0 of one launch per trial (writer) stores every candidate pose and its tables, which a
     // later trial reads as committed and the caller as the result.
     if (!TRIAL && writer && blockIdx.x == 0) {   // the restart (what a separate reset kernel did)
+        // (ctrl and dxp are read-only to every trial launch; in this launch no other block reads them, and
+        // the controller words written here are read by the later kernels of the chain)
         int* c = reinterpret_cast<int*>(const_cast<lh_ctrl*>(ctrl));
         for (int i = threadIdx.x; i < (int)(sizeof(lh_ctrl) / sizeof(int)); i += 256) c[i] = 0;   // cur = 0
         for (int i = threadIdx.x; i < rst.nqt; i += 256) pose_mat[i] = rst.qt_init[i];
