@@ -662,10 +662,13 @@ def test_c4_window_one_gpu_parity():
 # The per-trial exchange must issue the same number of collectives on every rank: the stop trial is
 # decided by identical all-reduced data, and each rank tops up to min(stop trial + depth, cap).
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("depth", [1, 2, 5])
-def test_collective_count_is_a_function_of_the_stop_trial(monkeypatch, depth):
+@pytest.mark.parametrize("depth,cfg,family", [(1, "C2", "stable_noout"), (2, "C2", "stable_noout"),
+                                               (5, "C2", "stable_noout"), (2, "mini", "default")])
+def test_collective_count_is_a_function_of_the_stop_trial(monkeypatch, depth, cfg, family):
+    """(mini, default: rejections followed by acceptances, so re-linearisation chains run through the
+    exchange and the controller's own decision, the path every sharded solve takes)"""
     monkeypatch.setenv("LH_FORCE_RCCL", "1")
-    w = window("C2", seed=0, family="stable_noout")
+    w = window(cfg, seed=0, family=family)
     s = lego_ba.Solver(trials_per_sync=depth)
     counts = set()
     for _ in range(3):
@@ -673,6 +676,16 @@ def test_collective_count_is_a_function_of_the_stop_trial(monkeypatch, depth):
         counts.add(s.comm_count())
     # chains: the trials, plus a re-linearisation per evaluate-only acceptance (at most one per iteration)
     assert counts == {1 + min(s.chains() + depth, 10 * (10 + 1))} and s.chains() >= r["trials"]
+    if family == "default":
+        assert s.chains() > r["trials"]
+        monkeypatch.setenv("LH_NO_EVAL_FIRST", "1")
+        t = lego_ba.Solver(trials_per_sync=depth)
+        f = t.solve(w)
+        t.close()
+        for k in ("iterations", "trials", "chi2_final", "lambda_final"):
+            assert f[k] == r[k], k
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2"):
+            assert np.array_equal(f[k], r[k]), k
     s.close()
 
 
