@@ -189,7 +189,13 @@ typedef struct lh_kernel_stats {
 typedef struct lh_handle lh_handle;
 
 const char *lh_strerror(int status);
+/* The defaults for a caller built against ABI `abi` (its LH_ABI_VERSION at compile time): abi_version = abi, so the
+   library reads exactly the lh_result fields that caller's struct has.  Callers write lh_default_options(&opt),
+   which this header maps to lh_default_options_v(&opt, LH_ABI_VERSION).  The plain symbol lh_default_options,
+   which binaries built against the ABI-4 header call, fills abi_version = 4 (no ABI-5 fields read). */
+void lh_default_options_v(lh_options *opt, int abi);
 void lh_default_options(lh_options *opt);
+#define lh_default_options(opt) lh_default_options_v((opt), LH_ABI_VERSION)
 const char *lh_kernel_name(int kernel_class);
 
 /* RCCL: rank 0 creates the id and ships it to the other ranks (any transport). */
@@ -320,6 +326,10 @@ int lh_debug_controller(lh_handle *h, int *which);
    linearisation: its trials, plus one re-linearisation per evaluate-only trial accepted outside the
    final iteration (a trial after a rejection only evaluates).  Solves that return arrays only. */
 int lh_debug_chains(lh_handle *h, int *chains);
+/* the lambda ladder: the rungs a factoring controller of the uploaded window builds (1: off),
+   and the rejections of the last solve whose step a rung had already solved, so that no controller factored
+   for them.  Solves that return arrays only (else skipped = -1). */
+int lh_debug_ladder(lh_handle *h, int *rungs, int *skipped);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,7 @@
 #define LH_TASKS 33           // per-pose values a sub-batch emits: Hpp(21) bp(6) bsd(6)
 #define LH_MAX_CAMS 4
 #define LH_TRACE 64
+#define LH_LAD 16             // lambda-ladder rungs at most (one controller workgroup each, lh_ctrl.lad)
 #define LH_NPAD 128           // reduced system padded size (LDS LDLT)
 #define LH_IMG_AS (LH_NPAD + 2)                 // k_ctrl's LDS row stride (doubles)
 #define LH_IMG_SZ ((LH_NPAD + 1) * LH_IMG_AS)   // k_ctrl's LDS system image: NP rows of S + the rhs row (doubles)
@@ -112,7 +113,7 @@ LH_HD static inline lh_rs_layout lh_rs_make(int P, int npairs) {
 
 // LM controller state (device resident, mirrors Problem's members problem.h:157-165)
 struct lh_ctrl {
-    double chi, lambda, ni, last_chi, spose, chi2_initial;
+    double chi, lambda, ni, last_chi, chi2_initial;
     int32_t iter, false_cnt, trials, accepted, done, cur, trace_len;
     int32_t nonpd;             // rank-deficient H_ll landmarks at the initial linearisation
     int32_t pcg_iters;         // PCG iterations summed over the solve's trials
@@ -125,6 +126,15 @@ struct lh_ctrl {
     int32_t relin;             // an evaluate-only trial was accepted outside the final iteration: the next chain
                                // (k_lin, k_reduce, k_ctrl) linearises the committed state instead of a trial
     int32_t seq_last;          // the last chain (trial or re-linearisation) a live decision was taken on
+    // The lambda ladder: a controller that factors a system may also factor it at the lambdas
+    // the next rejections would try (lambda *= ni, ni *= 2; STRATEGY1 min(11 lambda, 1e7): problem.cpp:550-551,
+    // :576), one workgroup per rung, so a rejection whose rung exists needs no factor (lskip).
+    int32_t lad;               // the rung the pending step (dxp + lad * n, spose_l[lad]) belongs to
+    int32_t lad_n;             // rungs the last factoring controller built (1: the step alone)
+    int32_t lskip;             // this chain's decision was a rejection onto a built rung: its controller exits
+    int32_t lskips;            // such decisions in this solve (lh_debug_ladder)
+    int32_t lad_its[LH_LAD];   // PCG iterations of each rung's solve (counted when the rung is used)
+    double spose_l[LH_LAD];    // pose part of each rung's gain denominator (isGoodStepInLM's scale)
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
 };
 
@@ -163,6 +173,9 @@ struct lh_params {
     int32_t bimg;           // 1: k_reduce writes S's lower band straight into k_ctrl_b's band image (one rank, banded
                             //    LDL^T): the stream loaders read it without the block-index round trip
     int32_t band_lu;        // 1: some banded LDL^T step needs more than 11 unit waves: the stream loaders take units
+    int32_t ladder;         // lambda-ladder rungs a factoring controller builds (1: off; k_ctrl, k_ctrl_b with
+                            //    dec_in_reduce; env LH_NO_LADDER=1: 1)
+    int32_t ladder_eager;   // 1: every factor builds the ladder; 0: only a factor after a rejection (env LH_LADDER_LAZY)
     double K[4];
 };
 

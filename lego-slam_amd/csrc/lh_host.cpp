@@ -32,6 +32,10 @@ size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
                               double th0, unsigned* part, uint8_t* flags);
+hipError_t lh_launch_outlier_counts(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
+                                    double th0, unsigned* part, double* tot);
+hipError_t lh_launch_outlier_flags(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
+                                   double th0, const double* gtot, uint8_t* flags);
 hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStream_t st, const lh_chunk* chunks,
                          const lh_subbatch* sbs, const float* obs_uv, const uint32_t* obs_meta, double* rec,
                          double* ptab, const double* ext, const lh_ctrl* ctrl, const double* dxp,
@@ -50,9 +54,6 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           double* img);
 hipError_t lh_launch_dense(hipStream_t st, const double* rs_stage, const uint16_t* pair_pq, const lh_ctrl* ctrl,
                            double* gS, int P);
-hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
-                           double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
-                           double* dxp, int ndxp, lh_ctrl* ctrl);
 hipError_t lh_launch_gather(hipStream_t st, const lh_ctrl* ctrl, const double* rec, const int32_t* lm_perm, int nrec,
                             const double* rho, const int32_t* obs_perm, long nslots, double* out_xyz, double* out_rho);
 hipError_t lh_launch_ldlt_probe(const double* S, const double* b, int n, double* x, int solver, double tol, int max_it,
@@ -247,6 +248,7 @@ struct lh_handle {
     bool host_comm = false;       // LH_COMM_HOST with world_size > 1
     bool uploaded = false;
     bool upload_joined = false;   // this upload has taken part in the sharded envelope all-reduce
+    bool upload_tail = false;     // ... and every rank passed it: the upload's closing status all-reduce follows
     lh::Pool* pool = nullptr;
 
     // window
@@ -277,6 +279,7 @@ struct lh_handle {
     HostBuf<double> s_out;                                   // pinned staging of the download
     DevBuf<unsigned> d_ocnt;                                 // the outlier pass's per-block counts (ABI 5)
     DevBuf<uint8_t> d_oflag;                                 // its flags (window order), then threshold and counts
+    DevBuf<double> d_otot;                                   // a sharded pass: this rank's counts, then all ranks' sums
     HostBuf<uint8_t> s_oflag;                                // pinned staging of the flags
     hipEvent_t ev_staging = nullptr;   // the upload's last copy out of the staging (reused by the next upload)
     bool staging_pending = false;
@@ -318,6 +321,7 @@ struct lh_handle {
     DevBuf<float> k_kp1, k_kp2;
     lh_ctrl* h_ctrl = nullptr;   // pinned
     int last_chains = -1;        // lh_debug_chains: the last synchronous solve's stop chain
+    int last_lskips = -1;        // lh_debug_ladder: its rejections onto a built ladder rung
     int* h_done = nullptr;       // pinned, mapped lh_host_words: [0] k_ctrl raises it when the LM loop stops, [1] progress
                                  // word 2 * (last live trial) + (one iteration from max_iters)
     int* d_done = nullptr;       // device alias of h_done
@@ -467,14 +471,26 @@ int rank_max(lh_handle* h, double* buf, int n);
 // A sharded upload holds one collective, the MAX all-reduce of the envelope of S (upload_body).  A rank that fails before it (a bad pixel, an unsupported window, an allocation)
 // still joins it, contributing its status in word 0 and nothing to the envelope, so the healthy ranks
 // are not left blocked in it: every rank then returns the largest status of any rank.
+//
+// A rank can also fail after that collective (the controllers' buffers, the image initialisation, the arena
+// copy), when its peers have already passed it: so every rank that passed it (all of them, or none: the
+// collective's status word is shared) closes the upload with a second MAX all-reduce of its final status, and
+// a rank whose tail failed takes the others down with it instead of leaving them in the first trial's exchange.
 int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     h->upload_joined = false;
+    h->upload_tail = false;
     int st = upload_body(h, w, sync);
     const bool sharded = h->host_comm || h->comm;
     if (st != LH_OK && sharded && !h->upload_joined && w && w->n_poses > 0 && w->n_poses <= LH_PMAX_ANY) {
         std::vector<double> buf(1 + (size_t)w->n_poses, -1e300);
         buf[0] = (double)st;
         rank_max(h, buf.data(), 1 + w->n_poses);
+    }
+    if (sharded && h->upload_tail) {
+        double fs = (double)st;
+        const int st_r = rank_max(h, &fs, 1);
+        if (st == LH_OK) st = (st_r != LH_OK) ? st_r : (int)fs;
+        if (st != LH_OK) h->uploaded = false;
     }
     if (st != LH_OK && !h->staging_pending && h->ev_staging) {
         if (hipEventRecord(h->ev_staging, h->stream) == hipSuccess) h->staging_pending = true;
@@ -612,7 +628,11 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_PCG)   // k_ctrl_p's row-contiguous copy of S (36 per block-row entry)
         HIPCHK(h->d_gA.ensure(pl.brow_ent.size() * 36));
     HIPCHK(h->d_maxd.ensure(1));
-    HIPCHK(h->d_dxp.ensure(6 * (size_t)std::max(P, 1)));
+    // the lambda ladder's rungs (one rank: k_reduce decides, so every controller workgroup reads the decision;
+    // LH_NO_LADDER=1: one rung, the A/B switch); one pending step per rung
+    const int ladder = (h->opt.world_size == 1 && !h->comm && !getenv("LH_NO_LADDER"))
+                           ? std::max(1, std::min(h->opt.max_trials, LH_LAD)) : 1;
+    HIPCHK(h->d_dxp.ensure((size_t)ladder * 6 * (size_t)std::max(P, 1)));
     HIPCHK(h->d_ctrl.ensure(1));
     HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
     HIPCHK(h->d_out_rho.ensure(pl.O));
@@ -688,10 +708,11 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         }
     }
 
-    // ---- the sharded upload's one collective: every rank-local failure point is behind us.  Word 0
-    //      carries the largest status of any rank (a rank that failed earlier joins from upload_impl with
-    //      its own), then -pf per pose: the union envelope.  Everything after it is decided on data
-    //      identical on every rank. ----
+    // ---- the sharded upload's envelope collective.  Word 0 carries the largest status of any rank (a rank
+    //      that failed earlier joins from upload_impl with its own), then -pf per pose: the union envelope.
+    //      Everything after it is decided on data identical on every rank; a rank-local failure after it
+    //      (allocations, the image initialisation, the copies) is shared by upload_impl's closing status
+    //      all-reduce. ----
     if (sharded) {
         std::vector<double> neg(1 + (size_t)P);
         neg[0] = 0.0;
@@ -701,6 +722,10 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         if (st_r != LH_OK) return st_r;
         if (neg[0] > 0.0) return (int)neg[0];
         for (int p = 0; p < P; ++p) pf[p] = (int)(-neg[1 + p]);
+        h->upload_tail = true;
+        // (test hook) this rank fails after the collective, as a failed allocation in the tail would
+        const char* fail_env = getenv("LH_TEST_FAIL_AFTER_ENVELOPE");
+        if (fail_env && atoi(fail_env) == h->opt.rank) return LH_E_HIP;
     }
 
     // ---- the banded controller's eligibility (tile rows enter its window two steps before use) ----
@@ -733,8 +758,9 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     if (P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
     if (h->band) {   // k_ctrl_b's L rows and ND blocks; L entries outside the envelope are never written: zero
         const size_t NE = (size_t)((6 * P + 15) & ~15);
-        HIPCHK(h->d_band.ensure(NE * 128 + (size_t)(6 * LH_PMAX_ANY / 8) * 64));
-        HIPCHK(hipMemsetAsync(h->d_band.p, 0, NE * 128 * sizeof(double), h->stream));
+        const size_t per = NE * 128 + (size_t)(6 * LH_PMAX_ANY / 8) * 64;   // one rung's (k_ctrl_b's layout)
+        HIPCHK(h->d_band.ensure((size_t)ladder * per));
+        HIPCHK(hipMemsetAsync(h->d_band.p, 0, (size_t)ladder * per * sizeof(double), h->stream));
     } else if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
         const size_t ng = (size_t)((6 * P + 31) & ~31);
         const bool fresh = h->d_gA.n < ng * ng;
@@ -809,6 +835,12 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.eval_first = getenv("LH_NO_EVAL_FIRST") == nullptr;
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
+    // k_ctrl and k_ctrl_b with k_reduce's decision build the ladder (k_ctrl_g, k_ctrl_p and sharded solves decide in
+    // their controller: one rung)
+    prm.ladder = (prm.dec_in_reduce && (P <= LH_PMAX || h->band)) ? ladder : 1;
+    // every factor builds the ladder (LH_LADDER_LAZY=1: only a factor after a rejection; the live configuration
+    // measured 7 582 against 7 251 it/s, the headline window unchanged, profiles/r06c_*)
+    prm.ladder_eager = getenv("LH_LADDER_LAZY") ? 0 : 1;
     prm.band_narrow = h->band_narrow ? 1 : 0;
     prm.band_lu = h->band_lu ? 1 : 0;
     // k_reduce writes the band straight into k_ctrl_b's loader order (one rank; LH_NO_BIMG=1: the packed
@@ -970,16 +1002,35 @@ int download(lh_handle* h, lh_result* out, int cur) {
     const size_t nl = (out->lm_xyz && h->L) ? 3 * (size_t)h->L : 0;
     const size_t ne = (out->edge_robust_chi2 && h->O) ? (size_t)h->O : 0;
     const bool fl = wants_outliers(h, out);
-    // a sharded window's pass would need every rank's counts (the reference counts the whole window's
-    // edges); a sharded caller classifies from edge_robust_chi2 after its own all-reduce of the counts
-    if (fl && (h->comm || h->host_comm)) return LH_E_UNSUPPORTED;
     const size_t o_res = ((size_t)h->O + 15) & ~(size_t)15;   // the scalars behind the flags: one copy
     if (fl) {   // Backend::Optimize's outlier pass on the device (backend_lego.cpp:163-194): flags + 3 scalars
         HIPCHK(h->d_ocnt.ensure(5 * 256));
         HIPCHK(h->d_oflag.ensure(o_res + 3 * sizeof(double)));
         HIPCHK(h->s_oflag.ensure(o_res + 3 * sizeof(double)));
-        HIPCHK(lh_launch_outliers(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O, out->outlier_chi2_th,
-                                  h->d_ocnt.p, h->d_oflag.p));
+        if (h->comm || h->host_comm) {
+            // a sharded window: the reference counts the whole window's edges, so each rank counts its own, the
+            // five counts and the edge counts are summed over the ranks (one 6-double exchange: every rank of the
+            // handle asks for the flags alike, as it solves alike), and each rank flags its edges at the
+            // threshold the totals give
+            HIPCHK(h->d_otot.ensure(6));
+            HIPCHK(lh_launch_outlier_counts(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O,
+                                            out->outlier_chi2_th, h->d_ocnt.p, h->d_otot.p));
+            if (h->comm) {
+                NCCLCHK(ncclAllReduce(h->d_otot.p, h->d_otot.p, 6, ncclFloat64, ncclSum, h->comm, s));
+            } else {
+                double t6[6];
+                HIPCHK(hipMemcpyAsync(t6, h->d_otot.p, sizeof(t6), hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                if (h->opt.allreduce(h->opt.allreduce_user, t6, 6, 0) != 0) return LH_E_RCCL;
+                HIPCHK(hipMemcpyAsync(h->d_otot.p, t6, sizeof(t6), hipMemcpyHostToDevice, s));
+                HIPCHK(hipStreamSynchronize(s));   // (t6 is on this stack frame)
+            }
+            HIPCHK(lh_launch_outlier_flags(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O,
+                                           out->outlier_chi2_th, h->d_otot.p, h->d_oflag.p));
+        } else {
+            HIPCHK(lh_launch_outliers(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O, out->outlier_chi2_th,
+                                      h->d_ocnt.p, h->d_oflag.p));
+        }
         HIPCHK(hipMemcpyAsync(h->s_oflag.p, h->d_oflag.p, o_res + 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     if (np + nl + ne == 0 && !fl) {
@@ -1123,6 +1174,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         out->time_download_ms = 0.0;
         h->event_next = 0;
         h->last_chains = -1;   // (not in the host words)
+        h->last_lskips = -1;
         return LH_OK;
     }
     HIPCHK(hipEventRecord(e1, s));
@@ -1146,6 +1198,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     const int cur = c.cur;
     h->last_chains = c.seq_last;
+    h->last_lskips = c.lskips;
 
     if (out) {
         out->iterations = c.iter;
@@ -1247,10 +1300,14 @@ const char* lh_strerror(int status) {
 
 const char* lh_kernel_name(int kc) { return (kc >= 0 && kc < KC_N) ? kKernelNames[kc] : ""; }
 
-void lh_default_options(lh_options* o) {
+// (the exported symbol, not the header's macro: binaries built against the ABI-4 header call it by this name)
+#undef lh_default_options
+void lh_default_options(lh_options* o) { lh_default_options_v(o, 4); }
+
+void lh_default_options_v(lh_options* o, int abi) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
-    o->abi_version = LH_ABI_VERSION;
+    o->abi_version = abi;
     o->max_iters = 10;
     o->max_trials = 10;
     o->strategy = LH_STRATEGY_DEFAULT;
@@ -1381,7 +1438,7 @@ void lh_destroy(lh_handle* h) {
     h->s_rsmap.release(); h->s_pair_pq.release(); h->s_obs_perm.release(); h->s_lm_perm.release(); h->s_uv.release();
     h->s_lm.release(); h->s_qt.release(); h->s_ptab.release(); h->s_ext.release(); h->s_rs.release();
     h->s_out.release();
-    h->d_ocnt.release(); h->d_oflag.release(); h->s_oflag.release();
+    h->d_ocnt.release(); h->d_oflag.release(); h->s_oflag.release(); h->d_otot.release();
     if (h->ev_staging) (void)hipEventDestroy(h->ev_staging);
     if (h->h_ctrl) (void)hipHostFree(h->h_ctrl);
     if (h->h_done) (void)hipHostFree(h->h_done);
@@ -1762,6 +1819,14 @@ int lh_debug_comm_count(lh_handle* h, int64_t* n) {
 int lh_debug_chains(lh_handle* h, int* chains) {
     if (!h || !chains) return LH_E_BADARG;
     *chains = h->last_chains;
+    return LH_OK;
+}
+
+int lh_debug_ladder(lh_handle* h, int* rungs, int* skipped) {
+    if (!h || !rungs || !skipped) return LH_E_BADARG;
+    if (!h->uploaded) return LH_E_STATE;
+    *rungs = h->prm.ladder;
+    *skipped = h->last_lskips;
     return LH_OK;
 }
 

@@ -721,6 +721,8 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // no candidate; the committed landmarks and pose tables are linearised into the candidate side, which the
     // chain's decision commits (the writer copies the committed poses and tables across first)
     const bool relin = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->relin) != 0;
+    // the pending step: lambda-ladder rung ctrl->lad's (the rung the last decision moved to; 0 after a factor)
+    if (TRIAL) dxp += (size_t)__builtin_amdgcn_readfirstlane(ctrl->lad) * prm.n;
     // The candidate poses of a trial (VertexPose::add of the step k_ctrl solved) are built here, not in
     // the serial controller: every chunk builds its own window's candidate pose tables (wave 3, below),
     // and block 0 of one launch per trial (writer) stores every candidate pose and its tables, which a
@@ -1288,14 +1290,23 @@ struct CtrlWords {
     double chi, lam, ni, last, spose, chi0;
     int iter, fc, trials, nacc, done, cur, tl;
     int evo, relin;   // this trial only evaluated; this chain re-linearises (the previous trial was such an acceptance)
+    int lad, lad_n;   // the rung this trial's step came from; the rungs built (lh_ctrl.lad)
 };
 __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl) {
     CtrlWords w;
-    w.chi = ctrl->chi; w.lam = ctrl->lambda; w.ni = ctrl->ni; w.last = ctrl->last_chi; w.spose = ctrl->spose;
+    w.chi = ctrl->chi; w.lam = ctrl->lambda; w.ni = ctrl->ni; w.last = ctrl->last_chi;
     w.chi0 = ctrl->chi2_initial;
     w.iter = ctrl->iter; w.fc = ctrl->false_cnt; w.trials = ctrl->trials; w.nacc = ctrl->accepted;
     w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
     w.evo = ctrl->evo; w.relin = ctrl->relin;
+    w.lad = ctrl->lad; w.lad_n = ctrl->lad_n;
+    // every rung's gain part is loaded and the trial's selected (no load that waits on lad)
+    double sp[LH_LAD];
+#pragma unroll
+    for (int i = 0; i < LH_LAD; ++i) sp[i] = ctrl->spose_l[i];
+    w.spose = sp[0];
+#pragma unroll
+    for (int i = 1; i < LH_LAD; ++i) w.spose = (w.lad == i) ? sp[i] : w.spose;
     return w;
 }
 // The stop trial's summary and trace to the host words, then done, by ONE thread behind its own
@@ -1327,6 +1338,7 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
     int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
     int done = w.done, cur = w.cur;
     int accept = 0, trace = 0, relin = 0;
+    int lad = 0, lskip = 0;   // the next step's rung: 0 after any factor; a rejection moves up the ladder
     if (!done) {
         if (mode != 0 && w.relin) {
             // the re-linearisation of an evaluate-only acceptance: its records and pose tables were written
@@ -1389,6 +1401,12 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
             } else {
                 fc += 1;             // rollbackStates: the committed buffers are untouched
                 inner_end = fc >= prm.max_trials;
+                // the lambda just set is the next rung's (the ladder applied the same updates in the same order):
+                // its step is already solved, so this chain's controller has nothing to factor
+                if (w.lad + 1 < w.lad_n) {
+                    lad = w.lad + 1;
+                    lskip = 1;
+                }
             }
             relin = (ok && w.evo) ? 1 : 0;   // (cleared below when the loop stops)
             if (inner_end) {
@@ -1406,6 +1424,11 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
         ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
         ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
         ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+        if (done) lskip = 0;
+        ctrl->lad = lad;
+        ctrl->lskip = lskip;
+        if (lskip) ctrl->lskips += 1;
+        if (lskip && prm.solver == 1) ctrl->pcg_iters += ctrl->lad_its[lad];   // the rung's solve counts now
         ctrl->acc_hist[seq & 1] = accept;
         ctrl->seq_last = seq;
         if (done) relin = 0;
@@ -2161,6 +2184,7 @@ struct LdltTail {
     const double* hdv;
     double lambda;
     int strategy;
+    int rung;   // the lambda-ladder rung this controller workgroup solves (lh_ctrl.spose_l)
 };
 __device__ __forceinline__ void ldlt_tail(const LdltTail& tl, int n, int lane, double y0, double y1) {
     auto term = [&](int r, double d) {
@@ -2171,7 +2195,7 @@ __device__ __forceinline__ void ldlt_tail(const LdltTail& tl, int n, int lane, d
     };
     double sp[1] = {term(lane, y0) + term(lane + 64, y1)};
     group_sum(sp, 6);
-    if (lane == 0) tl.ctrl->spose = sp[0];
+    if (lane == 0) tl.ctrl->spose_l[tl.rung] = sp[0];
 }
 
 // Phases 3-4 of k_ctrl on a padded system already in LDS (A lower + rhs row NP, zeros in the upper
@@ -2473,12 +2497,12 @@ __device__ __forceinline__ int lds_pcg_solve(double* __restrict__ A, double* __r
 
 // The controllers' tail (xs: the pose step in pose order, in LDS): the pose part of the gain
 // denominator (isGoodStepInLM's scale, problem.cpp:528-533), the wave partials summed in wave order
-// into ctrl->spose, and (dxp non-null) the step stored for k_lin.  The candidate poses
+// into ctrl->spose_l[rung], and (dxp non-null) the step stored for k_lin.  The candidate poses
 // (VertexPose::add) are built by the next k_lin (d_pose_candidate).  All NT threads.
 template <int NT>
 __device__ __forceinline__ void ctrl_step_tail(lh_ctrl* __restrict__ ctrl, const lh_params& prm, int n, double lambda,
                                                const double* xs, const double* bpv, const double* hdv, double* s_red,
-                                               double* __restrict__ dxp) {
+                                               double* __restrict__ dxp, int rung = 0) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double sp = 0.0;
     for (int i = tid; i < n; i += NT) {
@@ -2493,7 +2517,7 @@ __device__ __forceinline__ void ctrl_step_tail(lh_ctrl* __restrict__ ctrl, const
     if (tid == 0) {
         double s2 = 0.0;
         for (int w = 0; w < NT / 64; ++w) s2 += s_red[w];
-        ctrl->spose = s2;
+        ctrl->spose_l[rung] = s2;
     }
 }
 
@@ -2543,16 +2567,29 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     // the decision's words: uniform loads in the same round trip as the system
     int done = 0, accept = 0, skip = 0;
-    double lambda = 0.0;
+    double lambda = 0.0, ni = 0.0;
     int dseq = -1;
     bool staged_is_commit = false;   // an evaluate-only trial: k_reduce copied the committed system to the staged side
+    // workgroup `rung` > 0 of a ladder launch: the same system at the lambda of the rung-th rejection (only a decided
+    // trial: its workgroups all read the decision k_reduce took; otherwise thread 0 below decides, for workgroup 0)
+    const int rung = (int)blockIdx.x;
+#ifdef LH_STAMPS
+    if (rung) return;   // (the diagnostic build times one controller)
+#endif
+    if (!decided && rung) return;
     if (decided) {
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
         lambda = ctrl->lambda;
+        ni = ctrl->ni;
         dseq = __builtin_amdgcn_readfirstlane(ctrl->done_seq);
-        skip = __builtin_amdgcn_readfirstlane(ctrl->relin);   // an evaluate-only acceptance: nothing to factor
+        // an evaluate-only acceptance (nothing to factor), or a rejection onto a built rung (its step is solved)
+        skip = __builtin_amdgcn_readfirstlane(ctrl->relin) | __builtin_amdgcn_readfirstlane(ctrl->lskip);
         staged_is_commit = imgp && __builtin_amdgcn_readfirstlane(ctrl->evo_seq[seq & 1]) != 0;
+        for (int i = 0; i < rung; ++i) {   // the rung's lambda (block 0's early factor below uses it)
+            if (prm.strategy == 0) { lambda *= ni; ni *= 2; }
+            else lambda = fmin(lambda * 11.0, 1e7);
+        }
     }
     // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
@@ -2694,8 +2731,14 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         lambda = s_lam;
     }
     // this trial's k_reduce stopped the loop: the summary goes to the host and done is raised here
-    if (decided && done && dseq == seq && tid == 0 && host_done) publish_stop(ctrl, host_done);
+    if (decided && done && dseq == seq && tid == 0 && host_done && rung == 0) publish_stop(ctrl, host_done);
     if (done || skip) return;
+    // the ladder: a decided factor builds prm.ladder rungs (every factor, or with ladder_eager off only one after a
+    // rejection); rung r factors at the lambda r more rejections set, by ctrl_lm_step's own updates in its order
+    const bool build = decided && prm.ladder > 1 && (prm.ladder_eager || !accept);
+    if (rung != 0 && (!build || rung >= prm.ladder)) return;
+    if (rung == 0 && tid == 0) ctrl->lad_n = build ? prm.ladder : 1;
+    dxp += (size_t)rung * n;
 #ifdef LH_STAMPS
     if (tid == 0) {
         atomicAdd(&lh_stamps[32], ct_start);
@@ -2754,7 +2797,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     for (int u = 0; u < NLD; ++u) {
         const int i = u * ER + ibase;
         const double v = vs[u];
-        if (accept && i < LY.total) rs_commit[i] = v;
+        if (accept && rung == 0 && i < LY.total) rs_commit[i] = v;
         if (i < LY.off_bs) {
             // S element i: pose pair (p, q), p <= q, entry (ea, eb) -> rows 6 p + ea, 6 q + eb.  The
             // upper slot of every off-diagonal entry is zeroed: the factor stores L^T there where the
@@ -2816,15 +2859,19 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // ---------------- 3-4. blocked LDL^T with the forward substitution in row NP; back substitution ----------------
     if constexpr (SOLVER == 1) {
         const int its = lds_pcg_solve(A, xs, dg, s_pcg, n, tid, prm.pcg_tol, (prm.pcg_max_it > 0 ? prm.pcg_max_it : 2 * n) + 1);
-        if (tid == 0) ctrl->pcg_iters += its;
+        if (tid == 0) {
+            ctrl->lad_its[rung] = its;
+            if (rung == 0) ctrl->pcg_iters += its;   // a higher rung's count is added when a rejection uses it
+        }
     } else {
         if (nd) lds_ldlt_solve_nd(A, xs, n, tid, s_units, prm);
-        else lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units, LdltTail{ctrl, dxp, bpv, hdv, lambda, prm.strategy}, early0);
+        else lds_ldlt_solve(A, xs, n, NE, tid, nullptr, s_units, LdltTail{ctrl, dxp, bpv, hdv, lambda, prm.strategy, rung},
+                            early0);
     }
     CSTAMP(8);
 
     // the one-chain LDL^T took the tail in its back-substitution wave
-    if (SOLVER == 1 || nd) ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, dxp);
+    if (SOLVER == 1 || nd) ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, dxp, rung);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -3314,13 +3361,25 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     // ---------------- the decision ----------------
     int done = 0, accept = 0, skip = 0;
     double lambda = 0.0;
+    // workgroup `rung` > 0: a lambda-ladder rung (k_ctrl's scheme: a decided trial only), with its own L rows and ND
+    const int rung = (int)blockIdx.x;
+#ifdef LH_STAMPS
+    if (rung) return;
+#endif
+    if (!decided && rung) return;
     if (decided) {
         done = __builtin_amdgcn_readfirstlane(ctrl->done);
         accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
-        skip = __builtin_amdgcn_readfirstlane(ctrl->relin);   // an evaluate-only acceptance: nothing to factor
+        // an evaluate-only acceptance (nothing to factor), or a rejection onto a built rung (its step is solved)
+        skip = __builtin_amdgcn_readfirstlane(ctrl->relin) | __builtin_amdgcn_readfirstlane(ctrl->lskip);
         lambda = ctrl->lambda;
+        double ni = ctrl->ni;
+        for (int i = 0; i < rung; ++i) {
+            if (prm.strategy == 0) { lambda *= ni; ni *= 2; }
+            else lambda = fmin(lambda * 11.0, 1e7);
+        }
         // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
-        if (done && tid == 0 && host_done && ctrl->done_seq == seq) publish_stop(ctrl, host_done);
+        if (done && tid == 0 && host_done && ctrl->done_seq == seq && rung == 0) publish_stop(ctrl, host_done);
     } else {
         double tchi = 0.0, sl = 0.0, ndg = 0.0;
         CtrlWords cw{};
@@ -3356,6 +3415,15 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
         lambda = s_lam;
     }
     if (done || skip) return;
+    {
+        const bool build = decided && prm.ladder > 1 && (prm.ladder_eager || !accept);
+        if (rung != 0 && (!build || rung >= prm.ladder)) return;
+        if (rung == 0 && tid == 0) ctrl->lad_n = build ? prm.ladder : 1;
+        const size_t NEs = (size_t)NE;
+        Lg += (size_t)rung * (NEs * LH_LBW + (size_t)BSTEP_MAX * 64);   // lh_band_args: per rung, L rows | ND
+        NDg += (size_t)rung * (NEs * LH_LBW + (size_t)BSTEP_MAX * 64);
+        dxp += (size_t)rung * n;
+    }
 #ifdef LH_STAMPS
     if (tid == 0) {
         atomicAdd(&lh_stamps[32], ct_start);
@@ -3766,7 +3834,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     }
     __syncthreads();
     CSTAMP(8);
-    ctrl_step_tail<CT>(ctrl, prm, n, lambda, y, src + LY.off_bp, src + LY.off_hd, s_red, dxp);
+    ctrl_step_tail<CT>(ctrl, prm, n, lambda, y, src + LY.off_bp, src + LY.off_hd, s_red, dxp, rung);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -4668,13 +4736,14 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
                           const uint32_t* brow_ent, const uint16_t* units, lh_band_args band, double* img) {
+    const dim3 gl(prm.ladder > 1 ? prm.ladder : 1);   // one workgroup per lambda-ladder rung (k_ctrl, k_ctrl_b)
     if (prm.P > LH_PMAX && prm.solver == 0 && band.bblk)
     {
         if (prm.band_lu)
-            hipLaunchKernelGGL(k_ctrl_b<true>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk,
+            hipLaunchKernelGGL(k_ctrl_b<true>, gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk,
                                band.units, band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
         else
-            hipLaunchKernelGGL(k_ctrl_b<false>, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk,
+            hipLaunchKernelGGL(k_ctrl_b<false>, gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, band.bblk,
                                band.units, band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
     }
     else if (prm.P > LH_PMAX && prm.solver == 1)
@@ -4684,56 +4753,14 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
         hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
-        hipLaunchKernelGGL((k_ctrl<1, false>), dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
+        hipLaunchKernelGGL((k_ctrl<1, false>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
                            dxp, prm, mode, (volatile int*)host_done, seq, img);
     else if (prm.img)
-        hipLaunchKernelGGL((k_ctrl<0, true>), dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
+        hipLaunchKernelGGL((k_ctrl<0, true>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
                            dxp, prm, mode, (volatile int*)host_done, seq, img);
     else
-        hipLaunchKernelGGL((k_ctrl<0, false>), dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq,
+        hipLaunchKernelGGL((k_ctrl<0, false>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq,
                            units, dxp, prm, mode, (volatile int*)host_done, seq, img);
-    return hipGetLastError();
-}
-
-// ---- k_reset: restart a resident solve from the uploaded window (one launch instead of five copies):
-//      committed landmark records = {X of the window landmark, zeros} (records are read as X only by the
-//      initial linearisation), poses and pose tables from their initial copies, controller zeroed ----
-__global__ __launch_bounds__(256) void k_reset(double2* __restrict__ rec, const int32_t* __restrict__ lm_perm,
-                                               const double* __restrict__ lm_in, int nrec,
-                                               double* __restrict__ qt, const double* __restrict__ qt_init, int nqt,
-                                               double* __restrict__ ptab, const double* __restrict__ ptab_init, int nptab,
-                                               double* __restrict__ dxp, int ndxp, lh_ctrl* __restrict__ ctrl) {
-    // one thread per 16-B piece of X in a record of buffer 0 (the first two of its eight): the initial
-    // linearisation reads only X (no back substitution) and writes every piece of buffer 1, and each later
-    // linearisation rewrites its candidate buffer whole, so the rest of buffer 0 is never read first
-    const long n2 = (long)nrec * 2;
-    const long i0 = (long)blockIdx.x * 256 + threadIdx.x, st = (long)gridDim.x * 256;
-    for (long i = i0; i < n2; i += st) {
-        const int r = (int)(i >> 1), q = (int)(i & 1);
-        double2 v = {0.0, 0.0};
-        const int l = lm_perm[r];
-        if (l >= 0) {
-            const double* X = lm_in + 3 * (size_t)l;
-            v = (q == 0) ? double2{X[0], X[1]} : double2{X[2], 0.0};
-        }
-        rec[(size_t)r * (LH_REC / 2) + q] = v;
-    }
-    if (blockIdx.x == 0) {
-        for (int i = threadIdx.x; i < nqt; i += 256) qt[i] = qt_init[i];
-        for (int i = threadIdx.x; i < nptab; i += 256) ptab[i] = ptab_init[i];
-        for (int i = threadIdx.x; i < ndxp; i += 256) dxp[i] = 0.0;
-        int* c = reinterpret_cast<int*>(ctrl);
-        for (int i = threadIdx.x; i < (int)(sizeof(lh_ctrl) / sizeof(int)); i += 256) c[i] = 0;   // cur = 0
-    }
-}
-
-hipError_t lh_launch_reset(hipStream_t st, double* rec, const int32_t* lm_perm, const double* lm_in, int nrec,
-                           double* qt, const double* qt_init, int nqt, double* ptab, const double* ptab_init, int nptab,
-                           double* dxp, int ndxp, lh_ctrl* ctrl) {
-    const long n2 = (long)nrec * 2;
-    const int blocks = (int)std::max(1L, std::min(2048L, (n2 + 255) / 256));
-    hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, st, reinterpret_cast<double2*>(rec), lm_perm, lm_in, nrec,
-                       qt, qt_init, nqt, ptab, ptab_init, nptab, dxp, ndxp, ctrl);
     return hipGetLastError();
 }
 
@@ -4801,11 +4828,33 @@ __global__ __launch_bounds__(256) void k_outlier_count(const double* __restrict_
         part[blockIdx.x * 5 + threadIdx.x] = wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
 }
 
+// A sharded window's pass (the reference counts the whole window's edges): the counting blocks' partials summed
+// into this rank's {5 counts, its edge count} as doubles (exact below 2^53), which the handle's exchange sums
+// over the ranks before k_outlier_flags reads them (gtot)
+__global__ __launch_bounds__(64) void k_outlier_total(const unsigned* __restrict__ part, int nparts, long n_obs,
+                                                      double* __restrict__ tot) {
+    long c[5] = {0, 0, 0, 0, 0};
+    for (int b = threadIdx.x; b < nparts; b += 64)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) c[k] += part[b * 5 + k];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        long v = c[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (threadIdx.x == 0) tot[k] = (double)v;
+    }
+    if (threadIdx.x == 0) tot[5] = (double)n_obs;
+}
+
 __global__ __launch_bounds__(256) void k_outlier_flags(const double* __restrict__ rho, const int32_t* __restrict__ obs_perm,
                                                        long nslots, long n_obs, double th0, const unsigned* __restrict__ part,
-                                                       int nparts, uint8_t* __restrict__ flags, double* __restrict__ res) {
+                                                       int nparts, uint8_t* __restrict__ flags, double* __restrict__ res,
+                                                       const double* __restrict__ gtot) {
     __shared__ long tot[5];
-    if (threadIdx.x < 64) {
+    if (gtot) {   // the all-ranks totals (k_outlier_total + the exchange)
+        if (threadIdx.x < 5) tot[threadIdx.x] = (long)gtot[threadIdx.x];
+        n_obs = (long)gtot[5];
+    } else if (threadIdx.x < 64) {
         long c[5] = {0, 0, 0, 0, 0};
         for (int b = threadIdx.x; b < nparts; b += 64)
 #pragma unroll
@@ -4849,7 +4898,25 @@ hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* 
     double* res = reinterpret_cast<double*>(flags + ((n_obs + 15) & ~15L));
     hipLaunchKernelGGL(k_outlier_count, dim3(nb_c), dim3(256), 0, st, rho, obs_perm, nslots, th0, part);
     hipLaunchKernelGGL(k_outlier_flags, dim3(nb_f), dim3(256), 0, st, rho, obs_perm, nslots, n_obs, th0,
-                       (const unsigned*)part, nb_c, flags, res);
+                       (const unsigned*)part, nb_c, flags, res, (const double*)nullptr);
+    return hipGetLastError();
+}
+
+// the sharded pass in two halves around the exchange of tot[6] (this rank's counts and edge count)
+hipError_t lh_launch_outlier_counts(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
+                                    double th0, unsigned* part, double* tot) {
+    const int nb_c = (int)std::max(1L, std::min((long)LH_OCB, (nslots + 255) / 256));
+    if (nslots > 0) hipLaunchKernelGGL(k_outlier_count, dim3(nb_c), dim3(256), 0, st, rho, obs_perm, nslots, th0, part);
+    hipLaunchKernelGGL(k_outlier_total, dim3(1), dim3(64), 0, st, (const unsigned*)part, nslots > 0 ? nb_c : 0, n_obs, tot);
+    return hipGetLastError();
+}
+
+hipError_t lh_launch_outlier_flags(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
+                                   double th0, const double* gtot, uint8_t* flags) {
+    const int nb_f = (int)std::max(1L, std::min(2048L, (nslots + 255) / 256));
+    double* res = reinterpret_cast<double*>(flags + ((n_obs + 15) & ~15L));
+    hipLaunchKernelGGL(k_outlier_flags, dim3(nb_f), dim3(256), 0, st, rho, obs_perm, nslots, n_obs, th0,
+                       (const unsigned*)nullptr, 0, flags, res, gtot);
     return hipGetLastError();
 }
 

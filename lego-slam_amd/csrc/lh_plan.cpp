@@ -220,8 +220,13 @@ int plan_structure(const lh_window* w, const PlanCfg& cfg, bool allow_empty, Pla
             bd |= !ok;
             us |= l < prev;
             pl.csr[o] = o;
-            if (ok && !us)   // the landmarks from the previous observation's (exclusive) to this one start here
-                for (int64_t q = o > 0 ? (int64_t)prev + 1 : 0; q <= (int64_t)l; ++q) pl.lm_ptr[q] = o;
+            // the landmarks from the previous observation's (exclusive) to this one start here.  Blocks write
+            // disjoint ranges when the input is grouped by landmark; when it is not, two locally sorted blocks
+            // can write one entry (ThreadSanitizer found it, scripts/sanitize.sh) before the counting sort below
+            // rebuilds lm_ptr, so the stores are relaxed atomics (plain stores on x86): no data race, same code
+            if (ok && !us)
+                for (int64_t q = o > 0 ? (int64_t)prev + 1 : 0; q <= (int64_t)l; ++q)
+                    __atomic_store_n(&pl.lm_ptr[q], (int64_t)o, __ATOMIC_RELAXED);
             prev = l;
         }
         // the measurement is a cv::KeyPoint's float pixel widened (toVec2, algorithm.h:37): the device

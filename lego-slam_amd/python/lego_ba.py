@@ -14,7 +14,7 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # lego-slam_amd/
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 BA_LIB = os.environ.get("LH_LIB") or os.path.join(LIB_DIR, "liblego_ba.so")
-WIN_LIB = os.path.join(LIB_DIR, "liblego_window.so")
+WIN_LIB = os.environ.get("LH_WIN_LIB") or os.path.join(LIB_DIR, "liblego_window.so")   # (env: sanitizer builds)
 
 # --------------------------------------------------------------------------
 # window generator
@@ -202,12 +202,12 @@ class LhKernelStats(C.Structure):
 
 # every symbol include/lego_ba.h declares (tests check the .so exports them all)
 ABI_SYMBOLS = [
-    "lh_strerror", "lh_default_options", "lh_kernel_name", "lh_comm_unique_id",
+    "lh_strerror", "lh_default_options", "lh_default_options_v", "lh_kernel_name", "lh_comm_unique_id",
     "lh_create", "lh_destroy", "lh_solve", "lh_upload", "lh_solve_resident",
     "lh_kernel_stats_get", "lh_kernel_stats_reset", "lh_classify_outliers", "lh_set_profiling",
     "lh_estimate_pose", "lh_lk_track",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
-    "lh_debug_time_lin", "lh_debug_comm_count", "lh_debug_controller", "lh_debug_chains",
+    "lh_debug_time_lin", "lh_debug_comm_count", "lh_debug_controller", "lh_debug_chains", "lh_debug_ladder",
 ]
 
 _balib = None
@@ -223,6 +223,7 @@ def ba_lib():
         lib.lh_strerror.restype = C.c_char_p
         lib.lh_strerror.argtypes = [C.c_int]
         lib.lh_default_options.argtypes = [C.POINTER(LhOptions)]
+        lib.lh_default_options_v.argtypes = [C.POINTER(LhOptions), C.c_int]
         lib.lh_kernel_name.restype = C.c_char_p
         lib.lh_kernel_name.argtypes = [C.c_int]
         lib.lh_comm_unique_id.argtypes = [C.c_void_p]
@@ -243,13 +244,14 @@ def ba_lib():
         lib.lh_debug_comm_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
         lib.lh_debug_controller.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         lib.lh_debug_chains.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        lib.lh_debug_ladder.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _balib = lib
     return _balib
 
 
 def default_options(**kw):
     o = LhOptions()
-    ba_lib().lh_default_options(C.byref(o))
+    ba_lib().lh_default_options_v(C.byref(o), LH_ABI_VERSION)   # what the header's lh_default_options(&o) expands to
     for k, v in kw.items():
         if k == "comm_id":
             for i in range(128):
@@ -517,6 +519,13 @@ class Solver:
         _check(ba_lib().lh_debug_chains(self.h, C.byref(v)), "lh_debug_chains")
         return v.value
 
+    def ladder(self):
+        """(rungs the uploaded window's factoring controller builds, rejections of the last solve that used a
+        built rung instead of a factor) (lh_debug_ladder)."""
+        r, k = C.c_int(0), C.c_int(0)
+        _check(ba_lib().lh_debug_ladder(self.h, C.byref(r), C.byref(k)), "lh_debug_ladder")
+        return r.value, k.value
+
     def comm_count(self):
         """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""
         n = C.c_int64(0)
@@ -551,7 +560,7 @@ def classify_outliers(edge_rchi2, chi2_th=5.991):
 # --------------------------------------------------------------------------
 # window planner (liblego_plan.so: lh_plan.cpp alone, host C++; CPU tests and timings)
 # --------------------------------------------------------------------------
-PLAN_LIB = os.path.join(LIB_DIR, "liblego_plan.so")
+PLAN_LIB = os.environ.get("LH_PLAN_LIB") or os.path.join(LIB_DIR, "liblego_plan.so")   # (env: sanitizer builds)
 LH_TMAX = 6
 
 # lh_chunk / lh_subbatch (lego-slam_amd/csrc/lh_common.h)

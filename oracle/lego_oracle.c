@@ -887,6 +887,7 @@ static int good_step(prob_t *pb) {
         scale = 0.5 * scale;
         scale += 1e-10;
         double rho = (pb->chi - temp_chi) / scale;
+        if (pb->opt.verbose >= 2) printf("trial rho %.17g chi %.17g tchi %.17g lambda %.17g\n", rho, pb->chi, temp_chi, pb->lambda);
         if (rho > 0 && isfinite(temp_chi)) {
             double alpha = 1.0 - pow((2 * rho - 1), 3);
             alpha = fmin(alpha, 2.0 / 3.0);
@@ -905,6 +906,7 @@ static int good_step(prob_t *pb) {
         scale = 0.5 * scale;
         scale += 1e-10;
         double rho = (pb->chi - temp_chi) / scale;
+        if (pb->opt.verbose >= 2) printf("trial rho %.17g chi %.17g tchi %.17g lambda %.17g\n", rho, pb->chi, temp_chi, pb->lambda);
         if (rho > 0 && isfinite(temp_chi)) {
             pb->lambda = fmax(pb->lambda / 9.0, 1e-7);
             pb->chi = temp_chi;

@@ -4,15 +4,16 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-resets = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_reset")]
-i0, i1 = resets[-3], resets[-2]          # one whole timed solve (k_reset .. next k_reset)
+# a solve starts with its initial linearisation (k_lin<T, false, ...>, whose block 0 restarts the solve)
+resets = [i for i, r in enumerate(rows) if "k_lin<" in r["Kernel_Name"] and ", false," in r["Kernel_Name"]]
+i0, i1 = resets[-3], resets[-2]          # one whole timed solve (initial k_lin .. the next one)
 prev = None
 print("one solve(10) of the C3 bench window under rocprofv3 --kernel-trace")
 print(f"{'kernel':24s} {'dur us':>8s} {'gap us':>8s}")
 last = i0
 for i in range(i0, i1):
     r = rows[i]
-    if not r["Kernel_Name"].startswith(("k_reset", "void k_lin", "k_reduce", "k_ctrl", "void k_ctrl")):
+    if not r["Kernel_Name"].startswith(("void k_lin", "k_reduce", "k_ctrl", "void k_ctrl")):
         break                              # the solve ends at its last controller launch
     last = i
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_LIB = os.path.join(ROOT, "oracle", "liblego_oracle.so")
+ORACLE_LIB = os.environ.get("LH_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liblego_oracle.so")   # (env: sanitizer builds)
 
 
 class OrcOptions(C.Structure):

@@ -90,6 +90,21 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
             assert getattr(cls, f).offset == v, key
 
 
+def test_default_options_are_keyed_on_the_callers_abi():
+    """A binary built against the ABI-4 header calls the plain symbol lh_default_options: it gets abi_version 4, so
+    the library never reads the ABI-5 lh_result fields its smaller struct lacks.  The header maps
+    lh_default_options(&o) to lh_default_options_v(&o, LH_ABI_VERSION), the caller's compile-time version."""
+    lib = lego_ba.ba_lib()
+    o = lego_ba.LhOptions()
+    o.abi_version = 99
+    lib.lh_default_options(C.byref(o))
+    assert o.abi_version == 4 and o.max_iters == 10 and o.huber_delta == 5.991
+    lib.lh_default_options_v(C.byref(o), 5)
+    assert o.abi_version == 5 and o.max_iters == 10
+    hdr = open(os.path.join(ROOT, "include", "lego_ba.h")).read()
+    assert "#define lh_default_options(opt) lh_default_options_v((opt), LH_ABI_VERSION)" in hdr
+
+
 def test_default_options_mirror_reference_constants():
     o = lego_ba.default_options()
     assert o.abi_version == lego_ba.LH_ABI_VERSION == 5

@@ -751,13 +751,13 @@ def _eval_first_run(wargs, kw, env_off, monkeypatch):
     r = s.solve(w)
     r["controller"] = s.controller()
     r["chains"] = s.chains()
+    r["ladder"] = s.ladder()
     s.close()
     monkeypatch.delenv("LH_NO_EVAL_FIRST", raising=False)
     return r
 
 
 def test_trials_after_a_rejection_evaluate_first(monkeypatch):
-    relin = []
     for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
         full = _eval_first_run(wargs, kw, True, monkeypatch)
         ef = _eval_first_run(wargs, kw, False, monkeypatch)
@@ -767,11 +767,112 @@ def test_trials_after_a_rejection_evaluate_first(monkeypatch):
         for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
             assert np.array_equal(full[k], ef[k]), (name, k)
         assert full["chains"] == full["trials"] and ef["chains"] >= ef["trials"], name
-        if ef["chains"] > ef["trials"]:
-            relin.append(name)
-    # six of the first eight re-linearise on the current kernels; a change of rounding may move a chaotic
-    # window's rejections, so the bar is four
-    assert len(relin) >= 4, relin
+
+
+# The re-linearisation chain on windows that must take it (tests/windows.py RELIN_WINDOWS: a rejection and then
+# an acceptance inside an iteration before the last, by a margin no summation order moves; the oracle's
+# accept/reject string is pinned by scripts/relin_windows.py).  The GPU must take the oracle's decisions (same
+# iterations, trials, acceptances), run more chains than trials, and equal the eval-first-off solve bit for bit.
+def _relin_run(gen, opt, env, monkeypatch):
+    from windows import relin_window
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = lego_ba.Solver(max_iters=3, **opt)
+    r = s.solve(relin_window(gen))
+    r["controller"], r["chains"], r["ladder"] = s.controller(), s.chains(), s.ladder()
+    s.close()
+    for k in env:
+        monkeypatch.delenv(k)
+    return r
+
+
+@pytest.mark.parametrize("case", range(9))
+def test_rejection_then_acceptance_relinearises(case, monkeypatch):
+    from windows import RELIN_WINDOWS, relin_window
+    kind, gen, opt, dec, ctrl = RELIN_WINDOWS[case]
+    o = ob.solve(relin_window(gen), max_iters=3, **opt)
+    assert (o["iterations"], o["trials"], o["accepted"]) == (3, len(dec), dec.count("A")), kind
+    ef = _relin_run(gen, opt, {}, monkeypatch)
+    full = _relin_run(gen, opt, {"LH_NO_EVAL_FIRST": "1"}, monkeypatch)
+    assert ef["controller"] == ctrl, kind
+    assert (ef["iterations"], ef["trials"], ef["accepted"]) == (o["iterations"], o["trials"], o["accepted"]), kind
+    assert ef["chains"] > ef["trials"] and full["chains"] == full["trials"], (kind, ef["chains"], ef["trials"])
+    for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "chi2_initial", "pcg_iterations"):
+        assert full[k] == ef[k], (kind, k)
+    for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
+        assert np.array_equal(full[k], ef[k]), (kind, k)
+    assert ef["chi2_final"] < ef["chi2_initial"]
+    # the lambda ladder on the same window: bitwise the one-rung run; on k_ctrl / k_ctrl_b the rejections after
+    # the first of a run use built rungs (with the ladder off none does)
+    one = _relin_run(gen, opt, {"LH_NO_LADDER": "1"}, monkeypatch)
+    for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "pcg_iterations"):
+        assert one[k] == ef[k], (kind, k)
+    for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
+        assert np.array_equal(one[k], ef[k]), (kind, k)
+    assert one["ladder"] == (1, 0), kind
+    if ctrl in ("k_ctrl", "k_ctrl_b"):
+        assert ef["ladder"] == (10, _ladder_skips(dec, 10, eager=True)), (kind, ef["ladder"])
+        lazy = _relin_run(gen, opt, {"LH_LADDER_LAZY": "1"}, monkeypatch)
+        assert lazy["ladder"] == (10, _ladder_skips(dec, 10, eager=False)), (kind, lazy["ladder"])
+        assert lazy["chi2_final"] == ef["chi2_final"] and np.array_equal(lazy["pose_Tcw"], ef["pose_Tcw"]), kind
+    else:
+        assert ef["ladder"] == (1, 0), kind
+
+
+def _ladder_skips(dec, rungs, eager):
+    """The rejections of a decision string that land on a built rung.  The initial linearisation's controller
+    decides itself and builds one rung; a decided factor builds `rungs` (eager: every factor; lazy: a factor after
+    a rejection): after an acceptance (eager), or at the first rejection of a run that found no rung.  The last
+    decision stops the loop and needs no step."""
+    lad, lad_n, n = 0, 1, 0
+    for i, d in enumerate(dec):
+        last = i == len(dec) - 1
+        if d == "A":
+            lad, lad_n = 0, (rungs if eager else 1)
+        elif lad + 1 < lad_n and not last:
+            lad, n = lad + 1, n + 1
+        else:
+            lad, lad_n = 0, rungs
+    return n
+
+
+# The lambda ladder (DESIGN.md 2.2a): a controller that factors (LH_LADDER_LAZY=1: only one that factors after a
+# rejection) also factors the same system at the lambdas the next rejections would set
+# (problem.cpp:550-551, STRATEGY1 :576), one workgroup per rung, and a rejection onto a built rung skips its
+# factor.  Every rung runs the serial controller's code at bit-identical lambdas, so the solve must equal the
+# one-rung run (LH_NO_LADDER=1) bit for bit on every controller that builds a ladder (k_ctrl LDL^T and PCG,
+# k_ctrl_b), and the windows with rejection runs must have used rungs.
+def _ladder_run(wargs, kw, env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = _eval_first_run(wargs, kw, False, monkeypatch)
+    for k in env:
+        monkeypatch.delenv(k)
+    return r
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_lambda_ladder_is_bitwise_the_serial_chain(monkeypatch, eager):
+    used = []
+    for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
+        env = {} if eager else {"LH_LADDER_LAZY": "1"}
+        serial = _ladder_run(wargs, kw, {"LH_NO_LADDER": "1"}, monkeypatch)
+        lad = _ladder_run(wargs, kw, env, monkeypatch)
+        assert serial["ladder"] == (1, 0), name
+        for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "chi2_initial", "pcg_iterations"):
+            assert serial[k] == lad[k], (name, k)
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
+            assert np.array_equal(serial[k], lad[k]), (name, k)
+        rungs, skipped = lad["ladder"]
+        if ctrl in ("k_ctrl", "k_ctrl_b"):
+            assert rungs == min(kw.get("max_trials", 10), 16), name
+            if skipped > 0:
+                used.append(name)
+            # every rejection past the one that built a ladder used a rung, unless a run outgrew the ladder
+            assert skipped <= lad["trials"] - lad["accepted"], name
+        else:
+            assert (rungs, skipped) == (1, 0), name
+    assert len(used) >= 4, used
 
 
 # ---------------------------------------------------------------------------------------------

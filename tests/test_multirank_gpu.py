@@ -40,6 +40,9 @@ def _rank_main(rank, world, rdzv, cfg, seed, family, opts, q):
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
 
         corrupt = opts.pop("corrupt_rank", None)
+        fail_after = opts.pop("fail_after_rank", None)
+        if fail_after is not None:   # lh_host.cpp's test hook: that rank fails after the envelope collective
+            os.environ["LH_TEST_FAIL_AFTER_ENVELOPE"] = str(fail_after)
         if isinstance(cfg, dict):   # a generated window (lego_ba.generate_window arguments), sharded by landmark
             L = cfg["L"]
             shard = sharded_generated(cfg, rank * L // world, (rank + 1) * L // world, seed)
@@ -49,9 +52,10 @@ def _rank_main(rank, world, rdzv, cfg, seed, family, opts, q):
         if corrupt == rank:   # a pixel no float holds: this rank's upload fails in the planner's fill
             shard["obs_uv"] = np.array(shard["obs_uv"], np.float64)
             shard["obs_uv"][len(shard["obs_uv"]) // 2, 0] = 100.1
+        oth = opts.pop("outlier_th", None)
         s = lego_ba.Solver(device=0, world_size=world, rank=rank, allreduce=allreduce, **opts)
         try:
-            r = s.solve(shard)
+            r = s.solve(shard) if oth is None else s.solve(shard, outlier_chi2_th=oth)
         except lego_ba.LhError as e:
             q.put((rank, {"status": e.status}))
             s.close()
@@ -256,6 +260,35 @@ def test_a_failing_rank_does_not_strand_the_others():
     import lego_ba
     out = run_sharded("C2", 0, "stable_noout", corrupt_rank=1, timeout=60)
     assert out[0]["status"] == out[1]["status"] == lego_ba.LH_E_BADARG
+
+
+@pytest.mark.parametrize("cfg,seed,family,th", [("C2", 1, "default", 5.991), ("mini", 2, "default", 5.991),
+                                                 ("C2", 0, "stable_noout", 1e-6)])
+def test_sharded_outlier_pass_equals_the_whole_window(cfg, seed, family, th):
+    """Backend::Optimize's outlier pass (backend_lego.cpp:163-194) counts the whole window's edges: on a sharded
+    handle each rank counts its own, the counts are summed over the ranks (one exchange of 6 doubles), and each
+    rank flags its edges at the threshold the totals give.  The flags (rank 0's shard then rank 1's: the window
+    order), the threshold and the counts must equal lh_classify_outliers on the two ranks' rho0 taken together,
+    and every rank must report the same threshold and counts.  (th 1e-6: the doubling loop runs out.)"""
+    import lego_ba
+    out = run_sharded(cfg, seed, family, outlier_th=th)
+    a, b = out[0], out[1]
+    assert a["status"] == b["status"] == 0
+    rho = np.concatenate([a["edge_robust_chi2"], b["edge_robust_chi2"]])
+    flags, th_ref, n_in, n_out = lego_ba.classify_outliers(rho, th)
+    assert np.array_equal(np.concatenate([a["is_outlier"], b["is_outlier"]]).astype(bool), flags)
+    for r in (a, b):
+        assert (r["outlier_th"], r["n_inlier"], r["n_outlier"]) == (th_ref, n_in, n_out)
+    assert a["exchanges"] == b["exchanges"] == a["chains"] + 1   # the pass's exchange is not a solve collective
+
+
+def test_a_rank_failing_after_the_upload_collective_takes_the_others_down():
+    """A rank can fail after the envelope collective too (its controller buffers, the image initialisation, the
+    copies: here lh_host.cpp's test hook), when its peers have passed it.  The upload's closing status
+    all-reduce hands every rank that status, so no rank starts a solve whose exchange its peer never joins."""
+    import lego_ba
+    out = run_sharded("C2", 0, "stable_noout", fail_after_rank=1, timeout=60)
+    assert out[0]["status"] == out[1]["status"] == lego_ba.LH_E_HIP
 
 
 def _generated_one_rank(spec, seed, **opts):
