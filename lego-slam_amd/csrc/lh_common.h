@@ -133,6 +133,8 @@ struct lh_ctrl {
     int32_t lad_n;             // rungs the last factoring controller built (1: the step alone)
     int32_t lskip;             // this chain's decision was a rejection onto a built rung: its controller exits
     int32_t lskips;            // such decisions in this solve (lh_debug_ladder)
+    int32_t dec_tag;           // seq + 1 once workgroup 0 of a controller that decides itself has decided chain seq
+                               // (its rung workgroups wait for it; zeroed with the controller at every restart)
     int32_t lad_its[LH_LAD];   // PCG iterations of each rung's solve (counted when the rung is used)
     double spose_l[LH_LAD];    // pose part of each rung's gain denominator (isGoodStepInLM's scale)
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
@@ -176,6 +178,7 @@ struct lh_params {
     int32_t ladder;         // lambda-ladder rungs a factoring controller builds (1: off; k_ctrl, k_ctrl_b with
                             //    dec_in_reduce; env LH_NO_LADDER=1: 1)
     int32_t ladder_eager;   // 1: every factor builds the ladder; 0: only a factor after a rejection (env LH_LADDER_LAZY)
+    int32_t lad_stride;     // doubles of a rung's global scratch (k_ctrl_g: its gA; k_ctrl_p: its row copy of S)
     double K[4];
 };
 

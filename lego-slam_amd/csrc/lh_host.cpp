@@ -291,7 +291,8 @@ struct lh_handle {
     int n_red = 0;   // k_reduce's pair blocks (d_red: 4 words each, then the scalar block's sentinel)
     View<uint16_t> d_pair_pq, d_units, d_bunits;
     View<int32_t> d_bblk;
-    DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64)
+    DevBuf<double> d_band;        // k_ctrl_b: L rows (ceil16(6P) x 128) | ND per block (steps x 64), per ladder rung
+    size_t lad_stride = 0;        // doubles of d_gA per ladder rung (k_ctrl_g, k_ctrl_p)
     bool band = false;            // this window's LDL^T runs in k_ctrl_b
     bool band_narrow = false;     // ... and every row's envelope starts within 56 rows of its 8-row block
     bool band_lu = false;         // ... and some step needs the stream loaders as unit waves too
@@ -625,13 +626,15 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
-    if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_PCG)   // k_ctrl_p's row-contiguous copy of S (36 per block-row entry)
-        HIPCHK(h->d_gA.ensure(pl.brow_ent.size() * 36));
+    // the lambda ladder's rungs, one controller workgroup each (LH_NO_LADDER=1: one rung, the A/B
+    // switch): one pending step per rung, and per rung the controller's global scratch
+    const int ladder = !getenv("LH_NO_LADDER") ? std::max(1, std::min(h->opt.max_trials, LH_LAD)) : 1;
+    h->lad_stride = 0;
+    if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_PCG) {   // k_ctrl_p's row-contiguous copy of S (36 per block-row entry)
+        h->lad_stride = pl.brow_ent.size() * 36;
+        HIPCHK(h->d_gA.ensure((size_t)ladder * h->lad_stride));
+    }
     HIPCHK(h->d_maxd.ensure(1));
-    // the lambda ladder's rungs (one rank: k_reduce decides, so every controller workgroup reads the decision;
-    // LH_NO_LADDER=1: one rung, the A/B switch); one pending step per rung
-    const int ladder = (h->opt.world_size == 1 && !h->comm && !getenv("LH_NO_LADDER"))
-                           ? std::max(1, std::min(h->opt.max_trials, LH_LAD)) : 1;
     HIPCHK(h->d_dxp.ensure((size_t)ladder * 6 * (size_t)std::max(P, 1)));
     HIPCHK(h->d_ctrl.ensure(1));
     HIPCHK(h->d_out_xyz.ensure(3 * (size_t)pl.L));
@@ -763,8 +766,9 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         HIPCHK(hipMemsetAsync(h->d_band.p, 0, (size_t)ladder * per * sizeof(double), h->stream));
     } else if (P > LH_PMAX && h->opt.linear_solver == LH_SOLVER_LDLT) {   // k_ctrl_g's system, stride ceil32(6P); zeroed once
         const size_t ng = (size_t)((6 * P + 31) & ~31);
-        const bool fresh = h->d_gA.n < ng * ng;
-        HIPCHK(h->d_gA.ensure(ng * ng));
+        h->lad_stride = ng * ng;   // one gA per ladder rung
+        const bool fresh = h->d_gA.n < (size_t)ladder * ng * ng;
+        HIPCHK(h->d_gA.ensure((size_t)ladder * ng * ng));
         if (fresh) HIPCHK(hipMemsetAsync(h->d_gA.p, 0, h->d_gA.n * sizeof(double), h->stream));
         // k_dense's dense symmetric S, double-buffered with the committed state
         const bool fresh_s = h->d_gS.n < 2 * ng * ng;
@@ -835,9 +839,11 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.eval_first = getenv("LH_NO_EVAL_FIRST") == nullptr;
     prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
     prm.commit_in_reduce = h->band ? 1 : 0;
-    // k_ctrl and k_ctrl_b with k_reduce's decision build the ladder (k_ctrl_g, k_ctrl_p and sharded solves decide in
-    // their controller: one rung)
-    prm.ladder = (prm.dec_in_reduce && (P <= LH_PMAX || h->band)) ? ladder : 1;
+    // every controller builds the ladder: with k_reduce's decision (one rank, k_ctrl and k_ctrl_b) its rungs read it
+    // from lh_ctrl; a controller that decides itself (the initial linearisation, sharded solves, k_ctrl_g, k_ctrl_p)
+    // publishes its workgroup 0's decision to its rungs (ladder_publish / ladder_wait)
+    prm.ladder = ladder;
+    prm.lad_stride = (int32_t)h->lad_stride;
     // every factor builds the ladder (LH_LADDER_LAZY=1: only a factor after a rejection; the live configuration
     // measured 7 582 against 7 251 it/s, the headline window unchanged, profiles/r06c_*)
     prm.ladder_eager = getenv("LH_LADDER_LAZY") ? 0 : 1;

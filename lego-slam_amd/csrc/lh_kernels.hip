@@ -697,8 +697,11 @@ __device__ __forceinline__ void st_rec2(double2* p, double2 v, __amdgpu_buffer_r
 
 static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
 
+#ifndef LH_LIN_OCC
+#define LH_LIN_OCC 2   // k_lin<T <= 3> workgroups per CU the registers are budgeted for
+#endif
 template <int T, bool TRIAL, bool F32>
-__global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
+__global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
     const lh_chunk* __restrict__ chunks, const lh_subbatch* __restrict__ sbs, const float* __restrict__ obs_uv,
     const uint32_t* __restrict__ obs_meta, double* __restrict__ rec, double* __restrict__ pose_tab,
     const double* __restrict__ ext, const lh_ctrl* __restrict__ ctrl, const double* __restrict__ dxp,
@@ -787,7 +790,15 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     double pmc[12];
     // the wave that builds the candidate pose tables: 3 or 2 by block parity, so the two chunks sharing a
     // CU build them on different SIMDs (measured 37.7 -> 37.5 us per k_lin against wave 3 in both)
-    const int cwave = LH_WAVES - 1 - (blockIdx.x & 1);
+#ifndef LH_SB_ROT
+#define LH_SB_ROT 0
+#endif
+    // The chunk's sub-batches go round-robin over its waves from wave `rot`: a chunk of 13 gives that wave a
+    // fourth.  Two chunks share a CU (and each SIMD holds one wave of each): rotating one of them by two moves its
+    // heavy wave off the SIMD the other's heavy wave is on (A/B: LH_SB_ROT 1 by block parity, 2 by dispatch
+    // round, blockIdx / 256).  The candidate-table wave is a light one.
+    const int rot = (LH_SB_ROT == 1) ? 2 * (blockIdx.x & 1) : (LH_SB_ROT == 2) ? 2 * ((blockIdx.x >> 8) & 1) : 0;
+    const int cwave = (LH_SB_ROT == 0) ? LH_WAVES - 1 - (blockIdx.x & 1) : (rot + 3 - (blockIdx.x & 1)) & 3;
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
     // piece lane & 7 of sub-batch sbx's record (lane >> 3); the initial linearisation reads only X, from the window
@@ -821,7 +832,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? 2 : 1) void k_lin(
     // prefetch is unconditional (index clamped to the chunk) so the compiler can keep it in
     // flight with counted vmcnt waits across the iteration.
     const int sb_last = (int)sb_end - 1;
-    int sb = (int)sb_begin + wave;
+    int sb = (int)sb_begin + ((wave - rot) & (LH_WAVES - 1));
     // wflag[buffer][slot]: 1 where the linearisation that produced that buffer's state found the edge
     // an inlier (e2 <= delta^2, or no robust kernel), i.e. its robust weight W is exactly I
     const uint8_t* __restrict__ wf_c = wflag + (size_t)cur * nslots;
@@ -1327,9 +1338,10 @@ __device__ __noinline__ void publish_stop(const lh_ctrl* __restrict__ ctrl, vola
     host_done[0] = 1;
 }
 
-// Returns 1 when this trial was an evaluate-only one accepted outside the final iteration: there is no new
-// system to factor (its controller stops here) and the next chain re-linearises the accepted state (relin).
-// That chain's decision commits the new linearisation (like the initial one) and leaves the LM state alone.
+// Returns 1 when the controller has nothing to factor: this trial was an evaluate-only one accepted outside the
+// final iteration (the next chain re-linearises the accepted state, relin; that chain's decision commits the new
+// linearisation like the initial one and leaves the LM state alone), or a rejection whose step a lambda-ladder
+// rung already holds (lskip).
 __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
                                              volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
@@ -1467,7 +1479,47 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
     accept_o = accept;
     cur_o = cur;
     lam_o = lam;
-    return relin;
+    return relin | lskip;   // nothing to factor: an evaluate-only acceptance, or a rejection onto a built rung
+}
+
+// ---- the lambda ladder's rung workgroups (lh_ctrl.lad) ----
+// Workgroup 0 of a controller that takes the LM decision itself (the initial linearisation, sharded solves,
+// k_ctrl_g, k_ctrl_p) publishes it: ctrl_lm_step's words, then dec_tag = seq + 1 (release).  Its rung workgroups
+// wait for that tag (acquire) and read the decision from lh_ctrl like a controller after k_reduce's decision.
+// Workgroups are dispatched in order, so workgroup 0 is resident whatever the rungs do: the wait ends.
+__device__ __forceinline__ void ladder_publish(lh_ctrl* __restrict__ ctrl, int seq) {
+    __hip_atomic_store(&ctrl->dec_tag, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ladder_wait(const lh_ctrl* __restrict__ ctrl, int seq) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(&ctrl->dec_tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq + 1)
+            __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every wave's loads below see workgroup 0's words
+}
+// the decision as a rung reads it, and the rung's lambda: the updates `rung` more rejections apply to lambda and
+// ni, in ctrl_lm_step's order (DEFAULT problem.cpp:550-551, STRATEGY1 :576), so each is bit-identical
+struct LadderDec {
+    int done, accept, skip;
+    double lambda;
+};
+__device__ __forceinline__ LadderDec ladder_read(const lh_ctrl* __restrict__ ctrl, const lh_params& prm, int seq, int rung) {
+    LadderDec d;
+    d.done = __builtin_amdgcn_readfirstlane(ctrl->done);
+    d.accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
+    // an evaluate-only acceptance (nothing to factor), or a rejection onto a built rung (its step is solved)
+    d.skip = __builtin_amdgcn_readfirstlane(ctrl->relin) | __builtin_amdgcn_readfirstlane(ctrl->lskip);
+    double lambda = ctrl->lambda, ni = ctrl->ni;
+    for (int i = 0; i < rung; ++i) {
+        if (prm.strategy == 0) { lambda *= ni; ni *= 2; }
+        else lambda = fmin(lambda * 11.0, 1e7);
+    }
+    d.lambda = lambda;
+    return d;
+}
+// a factoring controller's rung count: prm.ladder rungs at every factor (ladder_eager) or a factor after a rejection
+__device__ __forceinline__ bool ladder_build(const lh_params& prm, int accept) {
+    return prm.ladder > 1 && (prm.ladder_eager || !accept);
 }
 
 // ============================================================================
@@ -2539,7 +2591,10 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15;
     const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
-    const bool decided = mode != 0 && prm.dec_in_reduce;   // k_reduce took this trial's LM decision
+    // k_reduce took this trial's LM decision; a rung workgroup > 0 reads it (or workgroup 0's) from lh_ctrl
+    const int rung = (int)blockIdx.x;
+    const bool dec_src = mode != 0 && prm.dec_in_reduce;
+    const bool decided = dec_src || rung > 0;
     const bool nd = SOLVER == 0 && prm.nd_steps > 0;        // the two-chain LDL^T schedule
     // k_reduce wrote S and b_s in this kernel's LDS layout (img[0] staged, img[1] committed): the system
     // arrives by a straight copy, no index math per entry (the scatter below was 2.2 us of wave 0's time)
@@ -2567,29 +2622,25 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     }
     // the decision's words: uniform loads in the same round trip as the system
     int done = 0, accept = 0, skip = 0;
-    double lambda = 0.0, ni = 0.0;
+    double lambda = 0.0;
     int dseq = -1;
     bool staged_is_commit = false;   // an evaluate-only trial: k_reduce copied the committed system to the staged side
-    // workgroup `rung` > 0 of a ladder launch: the same system at the lambda of the rung-th rejection (only a decided
-    // trial: its workgroups all read the decision k_reduce took; otherwise thread 0 below decides, for workgroup 0)
-    const int rung = (int)blockIdx.x;
+    // workgroup `rung` > 0 of a ladder launch: the same system at the lambda of the rung-th rejection
 #ifdef LH_STAMPS
     if (rung) return;   // (the diagnostic build times one controller)
 #endif
-    if (!decided && rung) return;
+    // (the initial linearisation's controller builds no ladder: its release on workgroup 0's path cost ~5 us per
+    // solve, and a rejection right after it refactors and builds one)
+    if (rung && mode == 0) return;
+    if (rung && !dec_src) ladder_wait(ctrl, seq);   // workgroup 0 decides (thread 0 below) and publishes
     if (decided) {
-        done = __builtin_amdgcn_readfirstlane(ctrl->done);
-        accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
-        lambda = ctrl->lambda;
-        ni = ctrl->ni;
+        const LadderDec d = ladder_read(ctrl, prm, seq, rung);   // (the rung's lambda: block 0's early factor uses it)
+        done = d.done;
+        accept = d.accept;
+        skip = d.skip;
+        lambda = d.lambda;
         dseq = __builtin_amdgcn_readfirstlane(ctrl->done_seq);
-        // an evaluate-only acceptance (nothing to factor), or a rejection onto a built rung (its step is solved)
-        skip = __builtin_amdgcn_readfirstlane(ctrl->relin) | __builtin_amdgcn_readfirstlane(ctrl->lskip);
         staged_is_commit = imgp && __builtin_amdgcn_readfirstlane(ctrl->evo_seq[seq & 1]) != 0;
-        for (int i = 0; i < rung; ++i) {   // the rung's lambda (block 0's early factor below uses it)
-            if (prm.strategy == 0) { lambda *= ni; ni *= 2; }
-            else lambda = fmin(lambda * 11.0, 1e7);
-        }
     }
     // Round u covers elements [ER u, ER u + ER), thread t < ER element ER u + t (coalesced): its entry
     // (ea, eb) of a 6x6 S block is the same in every round and its block advances by 28, so the
@@ -2720,6 +2771,7 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             int d_o, a_o, c_o;
             double lam_n;
             s_flags[2] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
             s_flags[0] = d_o;
             s_flags[1] = a_o;
             s_lam = lam_n;
@@ -2731,11 +2783,11 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
         lambda = s_lam;
     }
     // this trial's k_reduce stopped the loop: the summary goes to the host and done is raised here
-    if (decided && done && dseq == seq && tid == 0 && host_done && rung == 0) publish_stop(ctrl, host_done);
+    if (dec_src && done && dseq == seq && tid == 0 && host_done && rung == 0) publish_stop(ctrl, host_done);
     if (done || skip) return;
-    // the ladder: a decided factor builds prm.ladder rungs (every factor, or with ladder_eager off only one after a
+    // the ladder: a factor builds prm.ladder rungs (every factor, or with ladder_eager off only one after a
     // rejection); rung r factors at the lambda r more rejections set, by ctrl_lm_step's own updates in its order
-    const bool build = decided && prm.ladder > 1 && (prm.ladder_eager || !accept);
+    const bool build = mode != 0 && ladder_build(prm, accept);
     if (rung != 0 && (!build || rung >= prm.ladder)) return;
     if (rung == 0 && tid == 0) ctrl->lad_n = build ? prm.ladder : 1;
     dxp += (size_t)rung * n;
@@ -3158,15 +3210,33 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 #endif
 
     // ---------------- controller words, pose matrices, max |diag| (mode 0) ----------------
+    // workgroup `rung` > 0: a lambda-ladder rung with its own gA; it waits for workgroup 0's decision
+    const int rung = (int)blockIdx.x;
+#ifdef LH_STAMPS
+    if (rung) return;
+#endif
+    if (rung && mode == 0) return;   // (the initial linearisation builds no ladder, as k_ctrl)
+    if (rung) {
+        ladder_wait(ctrl, seq);
+        const LadderDec d = ladder_read(ctrl, prm, seq, rung);
+        if (tid == 0) {
+            s_flags[0] = d.done;
+            s_flags[1] = d.accept;
+            s_flags[2] = ctrl->cur;
+            s_flags[3] = d.skip;
+            s_lam = d.lambda;
+        }
+        lds_barrier();
+    }
     double tchi = 0.0, sl = 0.0, ndg = 0.0;
     CtrlWords cw{};
-    if (tid == 0) {
+    if (tid == 0 && !rung) {
         cw = ctrl_load(ctrl);
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
-    {
+    if (!rung) {
         double mx = 0.0;
         if (mode == 0)
             for (int i = tid; i < n; i += GT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
@@ -3174,7 +3244,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         if (lane == 0) s_red[wave] = mx;
     }
     lds_barrier();
-    if (tid == 0) {
+    if (tid == 0 && !rung) {
         double mdiag = 0.0;
         if (mode == 0) {
             for (int w = 0; w < GT / 64; ++w) mdiag = fmax(mdiag, s_red[w]);
@@ -3183,6 +3253,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         int done, accept, cur;
         double lam_n;
         s_flags[3] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
@@ -3190,8 +3261,15 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     }
     lds_barrier();
     const int done = s_flags[0], accept = s_flags[1], cur = s_flags[2];
-    if (done || s_flags[3]) return;   // stopped, or an evaluate-only acceptance (nothing to factor)
+    if (done || s_flags[3]) return;   // stopped, an evaluate-only acceptance, or a rejection onto a built rung
     const double lambda = s_lam;
+    {
+        const bool build = mode != 0 && ladder_build(prm, accept);
+        if (rung != 0 && (!build || rung >= prm.ladder)) return;
+        if (rung == 0 && tid == 0) ctrl->lad_n = build ? prm.ladder : 1;
+        gA += (size_t)rung * prm.lad_stride;
+        dxp += (size_t)rung * n;
+    }
 
 #ifdef LH_STAMPS
     if (tid == 0) {
@@ -3245,7 +3323,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
 
     // ---------------- commit (the packed right-hand sides), gather gA (permuted lower triangle) ----------------
     // S itself is double-buffered as gS (the decision picked the buffer): only the part after it commits
-    if (accept)
+    if (accept && rung == 0)
         for (int i = LY.off_bs + tid; i < LY.total; i += GT) rs_commit[i] = src[i];
     // gA(r, c) = S(perm r, perm c), r > c: a wave per row (lanes over columns), so its stores are
     // contiguous and its loads fall in one row of gS; eight rows per wave at a time, 48 loads in flight
@@ -3282,7 +3360,7 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
     for (int i = tid; i < n; i += GT) { xs[perm[i]] = yv[i]; dxp[perm[i]] = yv[i]; }
     lds_barrier();
     CSTAMP(8);
-    ctrl_step_tail<GT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, nullptr);
+    ctrl_step_tail<GT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red, nullptr, rung);
     CSTAMP(12);
 #ifdef LH_STAMPS
     if (tid == 0) atomicAdd(&lh_stamps[63], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -3354,32 +3432,29 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const int P = prm.P, n = 6 * P, NE = (n + 15) & ~15, nb = (n + 7) & ~7, NT = NE / 16, nstep = nb / 8;
     const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
-    const bool decided = mode != 0 && prm.dec_in_reduce;
+    // workgroup `rung` > 0: a lambda-ladder rung (k_ctrl's scheme), with its own L rows and ND
+    const int rung = (int)blockIdx.x;
+    const bool dec_src = mode != 0 && prm.dec_in_reduce;
+    const bool decided = dec_src || rung > 0;
 #ifdef LH_STAMPS
     const unsigned long long ct_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
     // ---------------- the decision ----------------
     int done = 0, accept = 0, skip = 0;
     double lambda = 0.0;
-    // workgroup `rung` > 0: a lambda-ladder rung (k_ctrl's scheme: a decided trial only), with its own L rows and ND
-    const int rung = (int)blockIdx.x;
 #ifdef LH_STAMPS
     if (rung) return;
 #endif
-    if (!decided && rung) return;
+    if (rung && mode == 0) return;   // (the initial linearisation builds no ladder, as k_ctrl)
+    if (rung && !dec_src) ladder_wait(ctrl, seq);   // workgroup 0 decides and publishes
     if (decided) {
-        done = __builtin_amdgcn_readfirstlane(ctrl->done);
-        accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
-        // an evaluate-only acceptance (nothing to factor), or a rejection onto a built rung (its step is solved)
-        skip = __builtin_amdgcn_readfirstlane(ctrl->relin) | __builtin_amdgcn_readfirstlane(ctrl->lskip);
-        lambda = ctrl->lambda;
-        double ni = ctrl->ni;
-        for (int i = 0; i < rung; ++i) {
-            if (prm.strategy == 0) { lambda *= ni; ni *= 2; }
-            else lambda = fmin(lambda * 11.0, 1e7);
-        }
+        const LadderDec d = ladder_read(ctrl, prm, seq, rung);
+        done = d.done;
+        accept = d.accept;
+        skip = d.skip;
+        lambda = d.lambda;
         // this trial's k_reduce stopped the loop: the host's done is raised here (ctrl_lm_step)
-        if (done && tid == 0 && host_done && ctrl->done_seq == seq && rung == 0) publish_stop(ctrl, host_done);
+        if (dec_src && done && tid == 0 && host_done && ctrl->done_seq == seq && rung == 0) publish_stop(ctrl, host_done);
     } else {
         double tchi = 0.0, sl = 0.0, ndg = 0.0;
         CtrlWords cw{};
@@ -3404,6 +3479,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             int d_o, a_o, c_o;
             double lam_n;
             s_flags[2] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
             s_flags[0] = d_o;
             s_flags[1] = a_o;
             s_lam = lam_n;
@@ -3416,7 +3492,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
     }
     if (done || skip) return;
     {
-        const bool build = decided && prm.ladder > 1 && (prm.ladder_eager || !accept);
+        const bool build = mode != 0 && ladder_build(prm, accept);
         if (rung != 0 && (!build || rung >= prm.ladder)) return;
         if (rung == 0 && tid == 0) ctrl->lad_n = build ? prm.ladder : 1;
         const size_t NEs = (size_t)NE;
@@ -3887,15 +3963,33 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
     const lh_rs_layout LY = lh_rs_make(P, prm.npairs);
 
     // ---------------- controller words, pose matrices, max |diag| (mode 0), the LM decision ----------------
+    // workgroup `rung` > 0: a lambda-ladder rung with its own row copy of S; it waits for workgroup
+    // 0's decision
+    const int rung = (int)blockIdx.x;
+#ifdef LH_STAMPS
+    if (rung) return;
+#endif
+    if (rung && mode == 0) return;   // (the initial linearisation builds no ladder, as k_ctrl)
+    if (rung) {
+        ladder_wait(ctrl, seq);
+        const LadderDec d = ladder_read(ctrl, prm, seq, rung);
+        if (tid == 0) {
+            s_flags[0] = d.done;
+            s_flags[1] = d.accept;
+            s_flags[3] = d.skip;
+            s_lam = d.lambda;
+        }
+        lds_barrier();
+    }
     double tchi = 0.0, sl = 0.0, ndg = 0.0;
     CtrlWords cw{};
-    if (tid == 0) {
+    if (tid == 0 && !rung) {
         cw = ctrl_load(ctrl);
         tchi = 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2];
         sl = rs_stage[LY.off_sc + LH_SC_SCALE];
         ndg = rs_stage[LY.off_sc + LH_SC_NDEG];
     }
-    {
+    if (!rung) {
         double mx = 0.0;
         if (mode == 0)
             for (int i = tid; i < n; i += CT) mx = fmax(mx, fabs(rs_stage[LY.off_hd + i]));
@@ -3903,7 +3997,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         if (lane == 0) s_red[0][wave] = mx;
     }
     lds_barrier();
-    if (tid == 0) {
+    if (tid == 0 && !rung) {
         double mdiag = 0.0;
         if (mode == 0) {
             for (int w = 0; w < CT / 64; ++w) mdiag = fmax(mdiag, s_red[0][w]);
@@ -3912,6 +4006,7 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         int done, accept, cur;
         double lam_n;
         s_flags[3] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
         s_flags[0] = done;
         s_flags[1] = accept;
         s_flags[2] = cur;
@@ -3919,12 +4014,19 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
     }
     lds_barrier();
     const int done = s_flags[0], accept = s_flags[1];
-    if (done || s_flags[3]) return;   // stopped, or an evaluate-only acceptance (nothing to factor)
+    if (done || s_flags[3]) return;   // stopped, an evaluate-only acceptance, or a rejection onto a built rung
     const double lambda = s_lam;
+    {
+        const bool build = mode != 0 && ladder_build(prm, accept);
+        if (rung != 0 && (!build || rung >= prm.ladder)) return;
+        if (rung == 0 && tid == 0) ctrl->lad_n = build ? prm.ladder : 1;
+        ell += (size_t)rung * prm.lad_stride;
+        dxp += (size_t)rung * n;
+    }
 
     // ---------------- the chosen system (the candidate's on accept, committed on it; else the committed one) ----------------
     const double* __restrict__ src = accept ? rs_stage : rs_commit;
-    if (accept)
+    if (accept && rung == 0)
         for (int i = tid; i < LY.total; i += CT) rs_commit[i] = rs_stage[i];
     const double* __restrict__ Sb = src + LY.off_S;
     // per thread rows r = tid + CT u: damped diagonal, Jacobi preconditioner, right-hand side
@@ -4068,9 +4170,12 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         const int r = tid + CT * u;
         if (r < n) { xs[r] = x[u]; dxp[r] = x[u]; }
     }
-    if (tid == 0) ctrl->pcg_iters += steps;
+    if (tid == 0) {
+        ctrl->lad_its[rung] = steps;
+        if (rung == 0) ctrl->pcg_iters += steps;   // a higher rung's count is added when a rejection uses it
+    }
     lds_barrier();
-    ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red[0], nullptr);
+    ctrl_step_tail<CT>(ctrl, prm, n, lambda, xs, bpv, hdv, s_red[0], nullptr, rung);
 }
 
 // ============================================================================
@@ -4671,9 +4776,12 @@ hipError_t lh_launch_lin(int T, int trial, int nchunks, int chunk_base, hipStrea
     writer = writer ? 1 : 0;   // block 0 stores the trial's candidate poses and tables (the restart, initially)
     if (nchunks + writer <= 0) return hipSuccess;
     dim3 g(nchunks + writer), b(256);
+    // (diagnostic) LH_TEST_LIN_LDS_PAD bytes of extra LDS per workgroup: fewer k_lin workgroups per CU, for the
+    // latency-hiding probe of scripts/occupancy_probe.py
+    static const size_t lds_pad = getenv("LH_TEST_LIN_LDS_PAD") ? (size_t)atol(getenv("LH_TEST_LIN_LDS_PAD")) : 0;
 #define LH_LIN(TT, TR)                                                                                             \
     do {                                                                                                           \
-        const size_t smem = lin_smem_bytes<TT>(prm.ncam);                                                \
+        const size_t smem = lin_smem_bytes<TT>(prm.ncam) + lds_pad;                                      \
         if (prm.precision == 1)                                                                                    \
             hipLaunchKernelGGL((k_lin<TT, TR, true>), g, b, smem, st, chunks, sbs, obs_uv, obs_meta, rec, ptab, ext, ctrl, \
                                dxp, edge_rho, rows, csc, crow, wflag, nslots, prm, nrec, fixed_bits, chunk_base,     \
@@ -4736,7 +4844,7 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                           const uint32_t* rsmap, const uint16_t* pair_pq, double* dxp, lh_params prm, int mode,
                           int* host_done, int seq, double* gA, const double* gS, const int32_t* brow_ptr,
                           const uint32_t* brow_ent, const uint16_t* units, lh_band_args band, double* img) {
-    const dim3 gl(prm.ladder > 1 ? prm.ladder : 1);   // one workgroup per lambda-ladder rung (k_ctrl, k_ctrl_b)
+    const dim3 gl(prm.ladder > 1 ? prm.ladder : 1);   // one workgroup per lambda-ladder rung
     if (prm.P > LH_PMAX && prm.solver == 0 && band.bblk)
     {
         if (prm.band_lu)
@@ -4747,10 +4855,10 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
                                band.units, band.Lg, band.NDg, dxp, prm, mode, (volatile int*)host_done, seq, img);
     }
     else if (prm.P > LH_PMAX && prm.solver == 1)
-        hipLaunchKernelGGL(k_ctrl_p, dim3(1), dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
+        hipLaunchKernelGGL(k_ctrl_p, gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, brow_ptr, brow_ent,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA);   // gA: the PCG's row scratch
     else if (prm.P > LH_PMAX)
-        hipLaunchKernelGGL(k_ctrl_g, dim3(1), dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
+        hipLaunchKernelGGL(k_ctrl_g, gl, dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
     else if (prm.solver == 1)
         hipLaunchKernelGGL((k_ctrl<1, false>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,

@@ -802,28 +802,24 @@ def test_rejection_then_acceptance_relinearises(case, monkeypatch):
     for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
         assert np.array_equal(full[k], ef[k]), (kind, k)
     assert ef["chi2_final"] < ef["chi2_initial"]
-    # the lambda ladder on the same window: bitwise the one-rung run; on k_ctrl / k_ctrl_b the rejections after
-    # the first of a run use built rungs (with the ladder off none does)
+    # the lambda ladder on the same window: bitwise the one-rung run, and every rejection with a built rung used it
+    # (with the ladder off none does)
     one = _relin_run(gen, opt, {"LH_NO_LADDER": "1"}, monkeypatch)
     for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "pcg_iterations"):
         assert one[k] == ef[k], (kind, k)
     for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
         assert np.array_equal(one[k], ef[k]), (kind, k)
     assert one["ladder"] == (1, 0), kind
-    if ctrl in ("k_ctrl", "k_ctrl_b"):
-        assert ef["ladder"] == (10, _ladder_skips(dec, 10, eager=True)), (kind, ef["ladder"])
-        lazy = _relin_run(gen, opt, {"LH_LADDER_LAZY": "1"}, monkeypatch)
-        assert lazy["ladder"] == (10, _ladder_skips(dec, 10, eager=False)), (kind, lazy["ladder"])
-        assert lazy["chi2_final"] == ef["chi2_final"] and np.array_equal(lazy["pose_Tcw"], ef["pose_Tcw"]), kind
-    else:
-        assert ef["ladder"] == (1, 0), kind
+    assert ef["ladder"] == (10, _ladder_skips(dec, 10, eager=True)), (kind, ef["ladder"])
+    lazy = _relin_run(gen, opt, {"LH_LADDER_LAZY": "1"}, monkeypatch)
+    assert lazy["ladder"] == (10, _ladder_skips(dec, 10, eager=False)), (kind, lazy["ladder"])
+    assert lazy["chi2_final"] == ef["chi2_final"] and np.array_equal(lazy["pose_Tcw"], ef["pose_Tcw"]), kind
 
 
 def _ladder_skips(dec, rungs, eager):
-    """The rejections of a decision string that land on a built rung.  The initial linearisation's controller
-    decides itself and builds one rung; a decided factor builds `rungs` (eager: every factor; lazy: a factor after
-    a rejection): after an acceptance (eager), or at the first rejection of a run that found no rung.  The last
-    decision stops the loop and needs no step."""
+    """The rejections of a decision string that land on a built rung.  The initial linearisation's controller builds
+    no ladder; a later factor builds `rungs` (eager: every one, each acceptance's; lazy: only the first rejection of
+    a run that found no rung).  The last decision stops the loop and needs no step."""
     lad, lad_n, n = 0, 1, 0
     for i, d in enumerate(dec):
         last = i == len(dec) - 1
@@ -840,8 +836,9 @@ def _ladder_skips(dec, rungs, eager):
 # rejection) also factors the same system at the lambdas the next rejections would set
 # (problem.cpp:550-551, STRATEGY1 :576), one workgroup per rung, and a rejection onto a built rung skips its
 # factor.  Every rung runs the serial controller's code at bit-identical lambdas, so the solve must equal the
-# one-rung run (LH_NO_LADDER=1) bit for bit on every controller that builds a ladder (k_ctrl LDL^T and PCG,
-# k_ctrl_b), and the windows with rejection runs must have used rungs.
+# one-rung run (LH_NO_LADDER=1) bit for bit on every controller (k_ctrl LDL^T and PCG, k_ctrl_b, k_ctrl_g,
+# k_ctrl_p: the last two, and the initial linearisation's controller, take the decision themselves and publish it
+# to their rung workgroups), and the windows with rejection runs must have used rungs.
 def _ladder_run(wargs, kw, env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -864,14 +861,10 @@ def test_lambda_ladder_is_bitwise_the_serial_chain(monkeypatch, eager):
         for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
             assert np.array_equal(serial[k], lad[k]), (name, k)
         rungs, skipped = lad["ladder"]
-        if ctrl in ("k_ctrl", "k_ctrl_b"):
-            assert rungs == min(kw.get("max_trials", 10), 16), name
-            if skipped > 0:
-                used.append(name)
-            # every rejection past the one that built a ladder used a rung, unless a run outgrew the ladder
-            assert skipped <= lad["trials"] - lad["accepted"], name
-        else:
-            assert (rungs, skipped) == (1, 0), name
+        assert rungs == min(kw.get("max_trials", 10), 16), name
+        if skipped > 0:
+            used.append((name, ctrl))
+        assert skipped <= lad["trials"] - lad["accepted"], name
     assert len(used) >= 4, used
 
 

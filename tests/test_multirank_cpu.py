@@ -89,30 +89,33 @@ def test_sharded_window_generation_matches_global_window():
             assert np.array_equal(np.asarray(part[key])[order_p], np.asarray(ref[key])[order_r]), key
 
 
-def test_bench_weak_scaling_shards():
-    """bench.py's N > 1 default (C3w): rank r of N holds landmarks [50 000 r, 50 000 (r + 1)) of a window of
-    50 000 N landmarks, i.e. one C3-sized shard per rank; N = 1 is exactly C3.  (Checked at a reduced size
-    through the same make_window path.)"""
+def test_bench_c4_strong_scaling_shards():
+    """bench.py's N > 1 default is BASELINE config 4's C4 window at every N (strong scaling): rank r of N holds
+    landmarks [L r / N, L (r + 1) / N) of the one window, the ranks' shards together are the window, and value
+    counts C3-equivalent work (C4 = 10 C3 windows; C3w, the weak-scaling side workload, N).  (The shards are
+    checked at a reduced size through the same make_window path.)"""
     import importlib
     import sys
     sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
     bench = importlib.import_module("bench")
+    assert bench.default_workload(1) == "C3" and all(bench.default_workload(n) == "C4" for n in (2, 4, 8))
+    assert bench.c3_units("C3", 1) == 1.0 and all(bench.c3_units("C4", n) == 10.0 for n in (1, 2, 8))
+    assert bench.c3_units("C3w", 4) == 4.0
+    c4 = bench.WORKLOADS["C4"]
+    assert (c4["P"], c4["L"], c4["k"]) == (20, 500_000, 8)   # 4 000 000 observations
     saved = dict(bench.WORKLOADS)
     try:
-        bench.WORKLOADS["C3w"] = dict(P=8, L=600, k=6, per_rank=True)
-        bench.WORKLOADS["C3"] = dict(P=8, L=600, k=6)
-        one = bench.make_window("C3", "stable_noout", 0, 0, 1)
-        wc = bench.make_window("C3w", "stable_noout", 0, 0, 1)
-        for key in ("pose_Tcw", "lm_xyz", "obs_pose", "obs_lm", "obs_uv"):
-            assert np.array_equal(np.asarray(one[key]), np.asarray(wc[key])), key
-        full = lego_ba.generate_window(P=8, L=1800, k=6, seed=0,
-                                       **dict(__import__("windows").STABLE, outlier_frac=0.0))
-        for r in range(3):
-            part = bench.make_window("C3w", "stable_noout", 0, r, 3)
-            assert len(part["lm_xyz"]) == 600
-            ref = ob.landmark_shard(full, 600 * r, 600 * (r + 1))
-            assert np.array_equal(part["lm_xyz"], ref["lm_xyz"])
-            assert np.array_equal(part["pose_Tcw"], full["pose_Tcw"])
+        bench.WORKLOADS["C4"] = dict(P=8, L=1800, k=6)
+        full = bench.make_window("C4", "stable_noout", 0, 0, 1)
+        for n in (2, 3):
+            parts = [bench.make_window("C4", "stable_noout", 0, r, n) for r in range(n)]
+            assert sum(len(p["lm_xyz"]) for p in parts) == 1800
+            assert np.array_equal(np.vstack([p["lm_xyz"] for p in parts]), full["lm_xyz"])
+            assert np.array_equal(np.concatenate([p["obs_uv"] for p in parts]), full["obs_uv"])
+            for r, p in enumerate(parts):
+                ref = ob.landmark_shard(full, 1800 * r // n, 1800 * (r + 1) // n)
+                assert np.array_equal(p["lm_xyz"], ref["lm_xyz"])
+                assert np.array_equal(p["pose_Tcw"], full["pose_Tcw"]) and p["pose_fixed"][0] == 1
     finally:
         bench.WORKLOADS.clear()
         bench.WORKLOADS.update(saved)

@@ -39,6 +39,7 @@ def _rank_main(rank, world, rdzv, cfg, seed, family, opts, q):
             t = torch.from_numpy(buf)   # shares the library's host buffer
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
 
+        os.environ.update(opts.pop("env", {}))
         corrupt = opts.pop("corrupt_rank", None)
         fail_after = opts.pop("fail_after_rank", None)
         if fail_after is not None:   # lh_host.cpp's test hook: that rank fails after the envelope collective
@@ -280,6 +281,27 @@ def test_sharded_outlier_pass_equals_the_whole_window(cfg, seed, family, th):
     for r in (a, b):
         assert (r["outlier_th"], r["n_inlier"], r["n_outlier"]) == (th_ref, n_in, n_out)
     assert a["exchanges"] == b["exchanges"] == a["chains"] + 1   # the pass's exchange is not a solve collective
+
+
+@pytest.mark.parametrize("case", [0, 4, 8])
+def test_sharded_lambda_ladder_is_bitwise_the_serial_chain(case):
+    """A sharded solve's controller takes the LM decision itself (after the exchange): its workgroup 0 publishes the
+    decision to the lambda ladder's rung workgroups (ladder_publish / ladder_wait).  Every rank's solve must equal
+    the one-rung run (LH_NO_LADDER=1) bit for bit, the exchanges included, on windows that reject (tests/windows.py
+    RELIN_WINDOWS: k_ctrl, k_ctrl_b and k_ctrl_p sharded two ways)."""
+    from windows import RELIN_WINDOWS
+    _, gen, opt, _, _ = RELIN_WINDOWS[case]
+    gen = dict(gen)
+    seed = gen.pop("seed")
+    lad = run_sharded(gen, seed, None, max_iters=3, **opt)
+    one = run_sharded(gen, seed, None, max_iters=3, env={"LH_NO_LADDER": "1"}, **opt)
+    for r in (0, 1):
+        a, b = lad[r], one[r]
+        for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "exchanges", "chains"):
+            assert a[k] == b[k], (r, k)
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2"):
+            assert np.array_equal(a[k], b[k]), (r, k)
+    assert lad[0]["trials"] > lad[0]["accepted"]   # the windows reject (so rungs are used)
 
 
 def test_a_rank_failing_after_the_upload_collective_takes_the_others_down():
