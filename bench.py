@@ -291,9 +291,10 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="only the timed line (no side measurements)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="length of the cpu_baseline sample")
     ap.add_argument("--trials-per-sync", type=int, default=0)
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
-                    help="per-trial exchange with N > 1: RCCL over xGMI (the product path), or the ABI's "
-                         "host transport over gloo (a rehearsal of the N-rank flow on fewer GPUs)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host", "p2p"],
+                    help="per-trial exchange with N > 1: RCCL over xGMI (the default), the one-shot peer-write "
+                         "exchange on the device (LH_COMM_P2P: IPC-mapped buffers, bootstrap over gloo), or the "
+                         "ABI's host transport over gloo (a rehearsal of the N-rank flow on fewer GPUs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,7 +311,7 @@ def main():
         dist.init_process_group("gloo")
     ndev = max(1, torch.cuda.device_count())
     if world > 1 and args.comm == "rccl" and ndev < world:
-        raise SystemExit(f"{world} ranks need {world} GPUs for RCCL (found {ndev}); --comm host rehearses on fewer")
+        raise SystemExit(f"{world} ranks need {world} GPUs for RCCL (found {ndev}); --comm host or p2p rehearse on fewer")
     local = local % ndev
     torch.cuda.set_device(local)
 
@@ -327,6 +328,8 @@ def main():
             t = torch.from_numpy(buf)   # the library's pinned exchange buffer
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
         extra = dict(allreduce=allreduce)
+        if args.comm == "p2p":
+            extra["comm_mode"] = lego_ba.LH_COMM_P2P
     solver = lego_ba.Solver(device=local, world_size=world, rank=rank, comm_id=comm_id, gate_mode=gate,
                             trials_per_sync=args.trials_per_sync, **extra)
     solver.upload(w)
@@ -402,8 +405,9 @@ def main():
                                + (" (one C3-sized shard per GPU)" if weak else ""),
                    "keyframes": c["P"], "landmarks": L_win, "landmarks_per_gpu": L_win // world,
                    "obs_this_rank": n_obs, "parallelism": f"landmark-shard x{world}",
-                   "exchange": ("none" if world == 1 else ("RCCL all-reduce" if args.comm == "rccl"
-                                                          else "host transport over gloo (rehearsal)"))},
+                   "exchange": ("none" if world == 1 else {"rccl": "RCCL all-reduce",
+                                                           "p2p": "one-shot peer-write exchange (LH_COMM_P2P)",
+                                                           "host": "host transport over gloo (rehearsal)"}[args.comm])},
         "gate_mode": gate,
         "value_definition": ("LM iterations of the whole window per second" if units == 1.0 else
                              f"C3-equivalent LM iterations per second: {units:g} x the LM iterations of the whole "

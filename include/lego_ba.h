@@ -71,8 +71,12 @@ typedef enum lh_precision { LH_PREC_FP64 = 0, LH_PREC_FP32_RESID = 1 } lh_precis
 
 /* The per-trial exchange of a landmark-sharded solve (world_size > 1): RCCL on the handle's stream
    (one process per GPU), or a caller-supplied all-reduce over host buffers (any transport: MPI, gloo,
-   sockets), called once per LM trial from inside lh_solve on the calling thread. */
-typedef enum lh_comm_mode { LH_COMM_RCCL = 0, LH_COMM_HOST = 1 } lh_comm_mode;
+   sockets), called once per LM trial from inside lh_solve on the calling thread, or (LH_COMM_P2P) a one-shot
+   exchange on the device: every rank writes its partial reduced system into every rank's IPC-mapped buffer
+   (xGMI between GPUs) and sums the ranks' slots in rank order; the caller's all-reduce (as LH_COMM_HOST) then
+   only carries the upload-time agreement and the IPC handles.  At most 16 ranks; every rank's device must be
+   able to map the others' memory. */
+typedef enum lh_comm_mode { LH_COMM_RCCL = 0, LH_COMM_HOST = 1, LH_COMM_P2P = 2 } lh_comm_mode;
 /* in-place all-reduce of count doubles over the ranks; op 0 = sum, 1 = max; returns 0 on success */
 typedef int (*lh_allreduce_fn)(void *user, double *buf, int64_t count, int32_t op);
 

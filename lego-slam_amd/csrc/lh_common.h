@@ -272,6 +272,17 @@ LH_HD static inline bool lh_bimg_in(int r, int c) {
     return c <= r && o >= 0 && o < 128;
 }
 
+// ---- the one-shot peer-write exchange (LH_COMM_P2P) ---------------------------
+// Every rank owns one exchange buffer, IPC-mapped into every peer: [2 parities][world slots][slot doubles], then
+// [2 parities][world] 64-bit arrival tags.  Per LM trial each rank writes its partial reduced system into slot
+// `rank` of every rank's buffer (its own included) and then, behind a system-scope release, its tag; each rank
+// waits for all tags of the trial in its own buffer and sums the slots in rank order.  Tags are (solve << 32) |
+// (chain + 1): a tag of an earlier chain or solve never matches.
+#define LH_P2P_MAX 16
+struct lh_peers {
+    double* p[LH_P2P_MAX];   // every rank's exchange buffer, mapped into this process (p[rank]: its own)
+};
+
 // k_ctrl_b's per-window tables (bblk null: no banded controller for this window)
 // The restart of a resident solve, done by the initial linearisation's block 0 (k_lin<T, false>): controller
 // zeroed, both pose and pose-table buffers from their initial copies, the step zeroed; its chunks read the

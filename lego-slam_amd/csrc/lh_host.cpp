@@ -32,6 +32,8 @@ size_t lh_lin_smem(int T, int ncam);
 hipError_t lh_launch_nop(hipStream_t st);
 hipError_t lh_launch_outliers(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
                               double th0, unsigned* part, uint8_t* flags);
+hipError_t lh_launch_p2p(hipStream_t st, double* rs, double* maxd, int n, lh_peers peers, int rank, int world,
+                         int parity, unsigned long long tag, long slot, int mode, int* err);
 hipError_t lh_launch_outlier_counts(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
                                     double th0, unsigned* part, double* tot);
 hipError_t lh_launch_outlier_flags(hipStream_t st, const double* rho, const int32_t* obs_perm, long nslots, long n_obs,
@@ -246,6 +248,13 @@ struct lh_handle {
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
     bool host_comm = false;       // LH_COMM_HOST with world_size > 1
+    bool p2p = false;             // LH_COMM_P2P with world_size > 1 (the caller's all-reduce carries the rest)
+    DevBuf<double> d_xchg;        // P2P: this rank's exchange buffer (lh_common.h), IPC-exported
+    lh_peers peers{};             // every rank's exchange buffer as mapped here (opened IPC handles)
+    long xchg_slot = 0;           // doubles per slot
+    uint32_t solve_gen = 0;       // P2P tags: solves so far (the same count on every rank)
+    int* h_xerr = nullptr;        // P2P: host-mapped failure word (a peer's tag did not arrive)
+    int* d_xerr = nullptr;
     bool uploaded = false;
     bool upload_joined = false;   // this upload has taken part in the sharded envelope all-reduce
     bool upload_tail = false;     // ... and every rank passed it: the upload's closing status all-reduce follows
@@ -464,6 +473,7 @@ hipError_t spin_wait(hipEvent_t ev) {
 // kernels on the same stream.  Either way the next upload waits for them before it rewrites the staging.
 int upload_body(lh_handle* h, const lh_window* w, bool sync);
 int rank_max(lh_handle* h, double* buf, int n);
+int p2p_setup(lh_handle* h);
 
 // Every exit after the first copy out of the pinned staging is queued must leave ev_staging recorded
 // behind it, or the next upload could rewrite (or reallocate) the staging while that DMA still reads
@@ -481,7 +491,7 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
     h->upload_joined = false;
     h->upload_tail = false;
     int st = upload_body(h, w, sync);
-    const bool sharded = h->host_comm || h->comm;
+    const bool sharded = h->host_comm || h->comm || h->p2p;
     if (st != LH_OK && sharded && !h->upload_joined && w && w->n_poses > 0 && w->n_poses <= LH_PMAX_ANY) {
         std::vector<double> buf(1 + (size_t)w->n_poses, -1e300);
         buf[0] = (double)st;
@@ -491,6 +501,11 @@ int upload_impl(lh_handle* h, const lh_window* w, bool sync) {
         double fs = (double)st;
         const int st_r = rank_max(h, &fs, 1);
         if (st == LH_OK) st = (st_r != LH_OK) ? st_r : (int)fs;
+        if (st != LH_OK) h->uploaded = false;
+    }
+    // the peer-write exchange's buffers once every rank's upload is through (its collectives run on all ranks)
+    if (st == LH_OK && h->p2p) {
+        st = p2p_setup(h);
         if (st != LH_OK) h->uploaded = false;
     }
     if (st != LH_OK && !h->staging_pending && h->ev_staging) {
@@ -518,7 +533,7 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     lh::PlanCfg cfg;
     cfg.chunk_lm = h->opt.chunk_landmarks;
     lh::Plan& pl = h->plan;
-    const bool sharded = h->host_comm || h->comm;
+    const bool sharded = h->host_comm || h->comm || h->p2p;
     cfg.rank_invariant_pairs = h->opt.world_size > 1;
     int st = lh::plan_structure(w, cfg, h->opt.world_size > 1, pl, h->pool);
     if (st != LH_OK) {
@@ -949,6 +964,14 @@ lh_band_args band_args(lh_handle* h) {
     return lh_band_args{h->d_bblk.p, h->d_bunits.p, h->d_band.p, h->d_band.p + NE * 128};
 }
 
+// P2P: the exchange of chain `seq` (lh_launch_p2p; tags carry the solve count, so no stale tag ever matches)
+hipError_t p2p_exchange(lh_handle* h, int mode, int seq) {
+    const unsigned long long tag = ((unsigned long long)h->solve_gen << 32) | (unsigned long long)(seq + 1);
+    ++h->n_coll;
+    return lh_launch_p2p(h->stream, h->d_rs_stage.p, h->d_maxd.p, h->LY.total, h->peers, h->opt.rank, h->opt.world_size,
+                         seq & 1, tag, h->xchg_slot, mode, h->d_xerr);
+}
+
 // One LM trial (mode 1) or the initial linearisation (mode 0).  *stopped is set (host transport
 // only) when the device had already stopped: no exchange and no k_ctrl were issued.
 int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
@@ -971,6 +994,9 @@ int enqueue_trial(lh_handle* h, int mode, bool* stopped) {
         if (mode == 0) NCCLCHK(ncclAllReduce(h->d_maxd.p, h->d_maxd.p, 1, ncclFloat64, ncclMax, h->comm, s));
         NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
         ++h->n_coll;
+    } else if (h->p2p) {
+        Prof pr(h, KC_ALLREDUCE);
+        HIPCHK(p2p_exchange(h, mode, h->cur_trial));
     } else if (h->host_comm) {
         HIPCHK(hipStreamSynchronize(s));
         if (mode != 0 && h->h_done[0]) {   // device-determined, identical on every rank
@@ -1102,9 +1128,13 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     // mapped words, and the solve returns when the host sees it; later work on this handle is stream-
     // ordered behind the solve's kernels (lh_destroy synchronises)
     const bool fast = out && !out->pose_Tcw && !out->lm_xyz && !out->edge_robust_chi2 && !wants_outliers(h, out) &&
-                      !h->comm && !h->host_comm && !h->opt.profile && !h->opt.verbose;
+                      !h->comm && !h->host_comm && !h->p2p && !h->opt.profile && !h->opt.verbose;
     const double t_start = now_ms();
     h->n_coll = 0;
+    if (h->p2p) {
+        ++h->solve_gen;   // every rank solves the same number of times
+        if (*h->h_xerr) return LH_E_RCCL;   // an earlier exchange failed: the peers are not in step
+    }
     if (!fast) HIPCHK(hipEventRecord(e0, s));   // (the array-free solve times itself on the host clock)
     // (the restart -- controller, poses, tables, step -- is the initial linearisation's block 0, launch_lin)
     bool stopped = false;
@@ -1140,6 +1170,10 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
             if ((++spin & 4095) == 0 && (query_often || now_ms() - t_query > 50.0)) {
                 const hipError_t q = hipStreamQuery(s);
                 if (q != hipSuccess && q != hipErrorNotReady) return LH_E_HIP;
+                if (h->p2p && *h->h_xerr) {   // a peer's tag did not arrive (k_p2p_sum gave up)
+                    (void)hipStreamSynchronize(s);
+                    return LH_E_RCCL;
+                }
                 t_query = now_ms();
             }
             __builtin_ia32_pause();
@@ -1187,7 +1221,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     HIPCHK(hipMemcpyAsync(h->h_ctrl, h->d_ctrl.p, sizeof(lh_ctrl), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const lh_ctrl& c = *h->h_ctrl;
-    if (h->comm) {
+    if (h->comm || h->p2p) {
         // Equal collective counts on every rank.  The progress word only advances on live chains,
         // so no rank enqueued more than (stop chain) + depth chains; the stop chain is decided by
         // identical all-reduced data, so every rank tops up to the same target.  The extra
@@ -1195,10 +1229,15 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
         const int target = std::min(c.seq_last + depth, max_total);
         if (enq > target) return LH_E_STATE;   // cannot happen: the bound above
         for (; enq < target; ++enq) {
-            NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
-            ++h->n_coll;
+            if (h->p2p) {
+                HIPCHK(p2p_exchange(h, 1, ++h->cur_trial));   // the chain numbers continue as the trials' did
+            } else {
+                NCCLCHK(ncclAllReduce(h->d_rs_stage.p, h->d_rs_stage.p, (size_t)h->LY.total, ncclFloat64, ncclSum, h->comm, s));
+                ++h->n_coll;
+            }
         }
         HIPCHK(hipStreamSynchronize(s));
+        if (h->p2p && *h->h_xerr) return LH_E_RCCL;
     }
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
@@ -1246,7 +1285,7 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
 // maximum or minimum sees a mismatch (every rank returns LH_E_BADARG).
 // MAX over the ranks of buf[0..n), in place (host transport or RCCL); a no-op on one rank
 int rank_max(lh_handle* h, double* buf, int n) {
-    if (h->host_comm) {
+    if (h->host_comm || h->p2p) {
         if (h->opt.allreduce(h->opt.allreduce_user, buf, n, 1) != 0) return LH_E_RCCL;
     } else if (h->comm) {
         DevBuf<double> d;
@@ -1265,6 +1304,53 @@ int rank_max(lh_handle* h, double* buf, int n) {
     return LH_OK;
 }
 
+// P2P: this rank's exchange buffer (2 parities x world slots of the packed reduced system + max|diag H_ll|, then
+// the arrival tags), exported over IPC, and every peer's opened here.  Collective: every rank calls it at the same
+// upload (the buffer size follows from the reduced system's layout, identical on every rank); its handles travel
+// through the caller's all-reduce (a sum of byte values, exact), and a MAX all-reduce of the status ends it, so a
+// rank that cannot map a peer takes every rank's upload down with it.
+int p2p_setup(lh_handle* h) {
+    const int world = h->opt.world_size, rank = h->opt.rank;
+    const long slot = (h->LY.total + 1 + 63) & ~63L;
+    const size_t need = (size_t)2 * world * slot + 2 * (size_t)world;   // (a tag is one 8-byte word)
+    if (h->d_xchg.n >= need && h->xchg_slot == slot) return LH_OK;
+    int st = LH_OK;
+    for (int r = 0; r < world; ++r)
+        if (r != rank && h->peers.p[r]) (void)hipIpcCloseMemHandle(h->peers.p[r]);
+    h->peers = lh_peers{};
+    h->d_xchg.release();
+    hipIpcMemHandle_t mine{};
+    if (h->d_xchg.ensure(need) != hipSuccess ||
+        hipMemsetAsync(h->d_xchg.p, 0, need * sizeof(double), h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess || hipIpcGetMemHandle(&mine, h->d_xchg.p) != hipSuccess)
+        st = LH_E_HIP;
+    static_assert(sizeof(hipIpcMemHandle_t) <= 64, "an IPC handle in 64 byte values");
+    std::vector<double> hb((size_t)world * 64, 0.0);
+    const uint8_t* mb = reinterpret_cast<const uint8_t*>(&mine);
+    for (size_t i = 0; i < sizeof(mine); ++i) hb[(size_t)rank * 64 + i] = (double)mb[i];
+    if (h->opt.allreduce(h->opt.allreduce_user, hb.data(), (int64_t)hb.size(), 0) != 0) return LH_E_RCCL;
+    h->peers.p[rank] = h->d_xchg.p;
+    for (int r = 0; r < world && st == LH_OK; ++r) {
+        if (r == rank) continue;
+        hipIpcMemHandle_t ph{};
+        uint8_t* pb = reinterpret_cast<uint8_t*>(&ph);
+        for (size_t i = 0; i < sizeof(ph); ++i) pb[i] = (uint8_t)hb[(size_t)r * 64 + i];
+        void* p = nullptr;
+        if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !p) {
+            if (getenv("LH_DEBUG_P2P")) fprintf(stderr, "lego_ba: rank %d cannot map rank %d's exchange buffer\n", rank, r);
+            st = LH_E_UNSUPPORTED;
+        } else {
+            h->peers.p[r] = static_cast<double*>(p);
+        }
+    }
+    double fs = (double)st;
+    const int st_r = rank_max(h, &fs, 1);
+    if (st_r != LH_OK) return st_r;
+    if (fs > 0.0) return (int)fs;
+    h->xchg_slot = slot;
+    return LH_OK;
+}
+
 int check_rank_options(lh_handle* h) {
     const lh_options& o = h->opt;
     const int depth = h->host_comm ? 1 : (o.trials_per_sync > 0 ? std::min(o.trials_per_sync, 32) : 2);
@@ -1276,7 +1362,7 @@ int check_rank_options(lh_handle* h) {
     constexpr int n = (int)(sizeof(v) / sizeof(v[0]));
     double buf[2 * n];
     for (int i = 0; i < n; ++i) { buf[i] = v[i]; buf[n + i] = -v[i]; }
-    if (!h->host_comm && !h->comm) return LH_OK;
+    if (!h->host_comm && !h->comm && !h->p2p) return LH_OK;
     const int st = rank_max(h, buf, 2 * n);
     if (st != LH_OK) return st;
     for (int i = 0; i < n; ++i)
@@ -1363,8 +1449,10 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
     if (opt->precision != LH_PREC_FP64 && opt->precision != LH_PREC_FP32_RESID) return LH_E_BADARG;
     if (opt->degenerate_guard != 0 && opt->degenerate_guard != 1) return LH_E_BADARG;
     if (opt->chunk_landmarks < 0 || opt->host_threads < 0) return LH_E_BADARG;
-    if (opt->comm_mode != LH_COMM_RCCL && opt->comm_mode != LH_COMM_HOST) return LH_E_BADARG;
-    if (opt->world_size > 1 && opt->comm_mode == LH_COMM_HOST && !opt->allreduce) return LH_E_BADARG;
+    if (opt->comm_mode != LH_COMM_RCCL && opt->comm_mode != LH_COMM_HOST && opt->comm_mode != LH_COMM_P2P)
+        return LH_E_BADARG;
+    if (opt->world_size > 1 && opt->comm_mode != LH_COMM_RCCL && !opt->allreduce) return LH_E_BADARG;
+    if (opt->comm_mode == LH_COMM_P2P && opt->world_size > LH_P2P_MAX) return LH_E_UNSUPPORTED;
     lh_handle* h = new (std::nothrow) lh_handle();
     if (!h) return LH_E_HIP;
     h->opt = *opt;
@@ -1399,11 +1487,20 @@ int lh_create(lh_handle** hp, const lh_options* opt) {
         return LH_E_HIP;
     }
     h->host_comm = opt->world_size > 1 && opt->comm_mode == LH_COMM_HOST;
+    h->p2p = opt->world_size > 1 && opt->comm_mode == LH_COMM_P2P;
+    if (h->p2p) {
+        if (hipHostMalloc((void**)&h->h_xerr, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&h->d_xerr, h->h_xerr, 0) != hipSuccess) {
+            lh_destroy(h);
+            return LH_E_HIP;
+        }
+        *h->h_xerr = 0;
+    }
     // LH_FORCE_RCCL=1 builds a one-rank communicator on a single GPU, so the data-path
     // collectives (and their stream ordering) run in single-GPU tests too
     const char* force = std::getenv("LH_FORCE_RCCL");
     const bool force_comm = opt->world_size == 1 && force && force[0] == '1';
-    if ((opt->world_size > 1 && !h->host_comm) || force_comm) {
+    if ((opt->world_size > 1 && !h->host_comm && !h->p2p) || force_comm) {
         ncclUniqueId id;
         if (force_comm) {
             if (ncclGetUniqueId(&id) != ncclSuccess) { lh_destroy(h); return LH_E_RCCL; }
@@ -1429,6 +1526,10 @@ void lh_destroy(lh_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm) ncclCommDestroy(h->comm);
+    for (int r = 0; r < LH_P2P_MAX; ++r)
+        if (h->peers.p[r] && h->peers.p[r] != h->d_xchg.p) (void)hipIpcCloseMemHandle(h->peers.p[r]);
+    h->d_xchg.release();
+    if (h->h_xerr) (void)hipHostFree(h->h_xerr);
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     delete h->pool;
     h->f_in.release(); h->f_out.release(); h->f_res.release(); h->s_fin.release(); h->s_fout.release();

@@ -790,15 +790,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
     double pmc[12];
     // the wave that builds the candidate pose tables: 3 or 2 by block parity, so the two chunks sharing a
     // CU build them on different SIMDs (measured 37.7 -> 37.5 us per k_lin against wave 3 in both)
-#ifndef LH_SB_ROT
-#define LH_SB_ROT 0
-#endif
-    // The chunk's sub-batches go round-robin over its waves from wave `rot`: a chunk of 13 gives that wave a
-    // fourth.  Two chunks share a CU (and each SIMD holds one wave of each): rotating one of them by two moves its
-    // heavy wave off the SIMD the other's heavy wave is on (A/B: LH_SB_ROT 1 by block parity, 2 by dispatch
-    // round, blockIdx / 256).  The candidate-table wave is a light one.
-    const int rot = (LH_SB_ROT == 1) ? 2 * (blockIdx.x & 1) : (LH_SB_ROT == 2) ? 2 * ((blockIdx.x >> 8) & 1) : 0;
-    const int cwave = (LH_SB_ROT == 0) ? LH_WAVES - 1 - (blockIdx.x & 1) : (rot + 3 - (blockIdx.x & 1)) & 3;
+    const int cwave = LH_WAVES - 1 - (blockIdx.x & 1);
 
     const double2* __restrict__ rc2 = reinterpret_cast<const double2*>(rec + (size_t)cur * nrec * LH_REC);
     // piece lane & 7 of sub-batch sbx's record (lane >> 3); the initial linearisation reads only X, from the window
@@ -832,7 +824,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
     // prefetch is unconditional (index clamped to the chunk) so the compiler can keep it in
     // flight with counted vmcnt waits across the iteration.
     const int sb_last = (int)sb_end - 1;
-    int sb = (int)sb_begin + ((wave - rot) & (LH_WAVES - 1));
+    int sb = (int)sb_begin + wave;
     // wflag[buffer][slot]: 1 where the linearisation that produced that buffer's state found the edge
     // an inlier (e2 <= delta^2, or no robust kernel), i.e. its robust weight W is exactly I
     const uint8_t* __restrict__ wf_c = wflag + (size_t)cur * nslots;
@@ -4995,6 +4987,75 @@ __global__ __launch_bounds__(256) void k_outlier_flags(const double* __restrict_
         res[1] = (double)cin;
         res[2] = (double)cout;
     }
+}
+
+// ---- the one-shot peer-write exchange (LH_COMM_P2P, lh_common.h) ----
+// Block d writes this rank's partial (the packed reduced system, and max|diag H_ll| at the initial linearisation)
+// into slot `rank` of rank d's buffer, then its arrival tag.  The buffers are plain device memory mapped over IPC,
+// whose caches are not coherent with another agent's: the data goes out as system-scope stores and is read back as
+// system-scope loads (no stale line in either GPU's L2), every thread's stores are fenced at system scope before
+// the block's barrier, and thread 0 stores the tag with a system-scope release.
+__global__ __launch_bounds__(1024) void k_p2p_push(const double* __restrict__ src, const double* __restrict__ maxd,
+                                                   int n, lh_peers peers, int rank, int world, int parity,
+                                                   unsigned long long tag, long slot) {
+    const int d = blockIdx.x;
+    double* dst = peers.p[d] + ((size_t)parity * world + rank) * slot;
+    for (int i = threadIdx.x; i < n; i += 1024) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(dst + n, maxd ? *maxd : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long* tags = reinterpret_cast<unsigned long long*>(peers.p[d] + (size_t)2 * world * slot);
+        __hip_atomic_store(tags + parity * world + rank, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Every block waits for the trial's tags of all ranks in this rank's buffer (system-scope acquire; a bounded
+// wait: past ~4 s the exchange is declared failed in *err, a host-mapped word, and the block exits), then sums
+// its elements over the slots in rank order into the reduced system (max for max|diag H_ll|): every rank gets the
+// same bits.
+__global__ __launch_bounds__(256) void k_p2p_sum(double* __restrict__ dst, double* __restrict__ maxd, int n,
+                                                 const double* __restrict__ buf, int world, int parity,
+                                                 unsigned long long tag, long slot, int mode, volatile int* err) {
+    __shared__ int s_ok;
+    if (threadIdx.x == 0) {
+        const unsigned long long* tags = reinterpret_cast<const unsigned long long*>(buf + (size_t)2 * world * slot) +
+                                         parity * world;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+        int ok = *err ? 0 : 1;   // (an earlier exchange of this handle failed: no second wait)
+        for (int r = 0; r < world && ok; ++r)
+            while (__hip_atomic_load(tags + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) { ok = 0; *err = 1; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const double* src = buf + (size_t)parity * world * slot;
+    auto ld = [](const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        double v = ld(src + i);
+        for (int r = 1; r < world; ++r) v += ld(src + (size_t)r * slot + i);
+        dst[i] = v;
+    }
+    if (mode == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        double m = ld(src + n);
+        for (int r = 1; r < world; ++r) m = fmax(m, ld(src + (size_t)r * slot + n));
+        *maxd = m;
+    }
+}
+
+hipError_t lh_launch_p2p(hipStream_t st, double* rs, double* maxd, int n, lh_peers peers, int rank, int world,
+                         int parity, unsigned long long tag, long slot, int mode, int* err) {
+    if (world < 1 || world > LH_P2P_MAX || (long)n + 1 > slot) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_p2p_push, dim3(world), dim3(1024), 0, st, (const double*)rs, mode == 0 ? (const double*)maxd : nullptr,
+                       n, peers, rank, world, parity, tag, slot);
+    const int nb = std::max(1, std::min(32, (n + 255) / 256));
+    hipLaunchKernelGGL(k_p2p_sum, dim3(nb), dim3(256), 0, st, rs, maxd, n, (const double*)peers.p[rank], world, parity,
+                       tag, slot, mode, (volatile int*)err);
+    return hipGetLastError();
 }
 
 // part: LH_OCB * 5 counters; flags: n_obs bytes, then (16-byte aligned) the threshold and the two counts

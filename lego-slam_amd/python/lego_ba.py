@@ -124,7 +124,7 @@ LH_OK, LH_E_EMPTY, LH_E_BADARG, LH_E_HIP, LH_E_RCCL, LH_E_UNSUPPORTED, LH_E_STAT
 LH_ABI_VERSION = 5
 LH_SOLVER_LDLT, LH_SOLVER_PCG = 0, 1
 LH_PREC_FP64, LH_PREC_FP32_RESID = 0, 1
-LH_COMM_RCCL, LH_COMM_HOST = 0, 1
+LH_COMM_RCCL, LH_COMM_HOST, LH_COMM_P2P = 0, 1, 2
 
 # lh_allreduce_fn: int (*)(void* user, double* buf, int64_t count, int32_t op)   (op 0 sum, 1 max)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32)
@@ -308,7 +308,8 @@ class Solver:
 
     def __init__(self, allreduce=None, **opts):
         """allreduce: optional Python callable f(buf: np.ndarray, op: int) reducing buf in place over
-        the ranks (op 0 sum, 1 max), used with comm_mode=LH_COMM_HOST and world_size > 1."""
+        the ranks (op 0 sum, 1 max), used with comm_mode=LH_COMM_HOST (the exchange) or LH_COMM_P2P (its bootstrap)
+        and world_size > 1."""
         lib = ba_lib()
         self._cb = None
         if allreduce is not None:

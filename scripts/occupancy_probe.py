@@ -1,6 +1,7 @@
 """k_lin's latency hiding, probed: the C3 trial-mode k_lin (lh_debug_time_lin, 50 back-to-back replays) at its
-normal two workgroups per CU (104 landmarks per chunk, ~488 chunks) against one workgroup per CU (extra LDS per
-workgroup, LH_TEST_LIN_LDS_PAD, and 208 landmarks per chunk so the chunks still fit the CUs at once).  The same
+normal two workgroups per CU (104 landmarks per chunk, ~488 chunks) against one workgroup per CU: 208 landmarks per
+chunk (~244 chunks, one per CU), also with 24 KB of extra LDS per workgroup (LH_TEST_LIN_LDS_PAD: two no longer
+fit a CU), and 104 per chunk with the pad (two rounds of chunks).  The same
 work at half the waves per SIMD: how much the second wave hides bounds what a third could."""
 import os
 import subprocess
@@ -19,7 +20,7 @@ s.solve_resident()
 ms = sorted(s.time_lin_ms(50) for _ in range(5))[2]
 print(f"chunk_landmarks {sys.argv[1]} lds_pad {sys.argv[2]}: k_lin {1e3 * ms:.2f} us")
 """ % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "lego-slam_amd", "python"))
-for clm, pad in ((0, 0), (104, 0), (208, 0), (208, 90000), (104, 90000)):
+for clm, pad in ((0, 0), (208, 0), (208, 24000), (104, 24000)):
     env = dict(os.environ)
     if pad:
         env["LH_TEST_LIN_LDS_PAD"] = str(pad)

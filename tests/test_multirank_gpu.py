@@ -304,6 +304,33 @@ def test_sharded_lambda_ladder_is_bitwise_the_serial_chain(case):
     assert lad[0]["trials"] > lad[0]["accepted"]   # the windows reject (so rungs are used)
 
 
+@pytest.mark.parametrize("cfg,seed,family", [("C2", 0, "stable_noout"), ("mini", 2, "default")])
+def test_p2p_exchange_matches_the_host_transport(cfg, seed, family):
+    """LH_COMM_P2P: every rank writes its partial reduced system into every rank's IPC-mapped exchange buffer and
+    sums the slots in rank order on the device (k_p2p_push / k_p2p_sum), the caller's all-reduce carrying only the
+    bootstrap.  Two processes on the one GPU of a test box: the solve must equal the host transport's bit for bit
+    (two ranks: a + b either way), with the same exchange count.  A runtime that refuses to map the other
+    process's buffer on the same device makes lh_upload return LH_E_UNSUPPORTED on both ranks: recorded as a skip,
+    not a pass."""
+    import lego_ba
+    host = run_sharded(cfg, seed, family)
+    p2p = run_sharded(cfg, seed, family, comm_mode=lego_ba.LH_COMM_P2P)
+    if p2p[0]["status"] == lego_ba.LH_E_UNSUPPORTED:
+        assert p2p[1]["status"] == lego_ba.LH_E_UNSUPPORTED
+        pytest.skip("same-device IPC mapping refused by the runtime (LH_COMM_P2P untested here)")
+    for r in (0, 1):
+        a, b = p2p[r], host[r]
+        assert a["status"] == b["status"] == 0
+        for k in ("iterations", "trials", "accepted", "chi2_initial", "chi2_final", "lambda_final", "chains"):
+            assert a[k] == b[k], (r, k)
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda"):
+            assert np.array_equal(a[k], b[k]), (r, k)
+        # the host transport exchanges synchronously (one per chain); the device exchange, like RCCL, keeps two chains
+        # enqueued ahead and tops every rank up to the same count after the stop
+        assert b["exchanges"] == b["chains"] + 1
+        assert a["exchanges"] == 1 + min(a["chains"] + 2, 10 * (10 + 1)), (a["exchanges"], a["chains"])
+
+
 def test_a_rank_failing_after_the_upload_collective_takes_the_others_down():
     """A rank can fail after the envelope collective too (its controller buffers, the image initialisation, the
     copies: here lh_host.cpp's test hook), when its peers have passed it.  The upload's closing status
