@@ -335,6 +335,11 @@ int lh_debug_chains(lh_handle *h, int *chains);
    for them.  Solves that return arrays only (else skipped = -1). */
 int lh_debug_ladder(lh_handle *h, int *rungs, int *skipped);
 
+/* batched evaluation of rejection runs: the most rungs one chain of the uploaded window evaluates
+   (1: off -- sharded solves, LH_NO_BATCH=1), and the batches the last solve decided.  Solves that return arrays
+   only (else batches = -1). */
+int lh_debug_batch(lh_handle *h, int *batch_max, int *batches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -135,6 +135,15 @@ struct lh_ctrl {
     int32_t lskips;            // such decisions in this solve (lh_debug_ladder)
     int32_t dec_tag;           // seq + 1 once workgroup 0 of a controller that decides itself has decided chain seq
                                // (its rung workgroups wait for it; zeroed with the controller at every restart)
+    // Batched evaluation of a rejection run: after a rejection, when the next trials only evaluate
+    // and their steps are built rungs, one chain's k_lin evaluates nbatch consecutive rungs and k_reduce takes their
+    // decisions in order.  An acceptance among them is linearised by the next chain, a full trial at that rung whose
+    // decision is the acceptance already taken (retrial).
+    int32_t nbatch;            // rungs the next chain evaluates (1: an ordinary chain)
+    int32_t retrial;           // the next chain re-runs the accepted rung as a full trial; its decision only commits
+    int32_t rho_sel;           // per-edge rho0 "as last evaluated": rung buffer (0: the ordinary one)
+    int32_t nbatches;          // batches decided in this solve (lh_debug_batch)
+    int32_t nofactor;          // the last decision left nothing to factor (relin | lskip | retrial: ladder_read's one word)
     int32_t lad_its[LH_LAD];   // PCG iterations of each rung's solve (counted when the rung is used)
     double spose_l[LH_LAD];    // pose part of each rung's gain denominator (isGoodStepInLM's scale)
     double trace_chi[LH_TRACE], trace_lambda[LH_TRACE];
@@ -179,6 +188,8 @@ struct lh_params {
                             //    dec_in_reduce; env LH_NO_LADDER=1: 1)
     int32_t ladder_eager;   // 1: every factor builds the ladder; 0: only a factor after a rejection (env LH_LADDER_LAZY)
     int32_t lad_stride;     // doubles of a rung's global scratch (k_ctrl_g: its gA; k_ctrl_p: its row copy of S)
+    int32_t batch;          // rejection runs evaluated in batches of rungs (one rank, k_reduce decides; env LH_NO_BATCH)
+    int32_t n_chunks;       // k_lin chunks of the window (the per-rung chunk scalars' stride)
     double K[4];
 };
 

@@ -332,6 +332,8 @@ struct lh_handle {
     lh_ctrl* h_ctrl = nullptr;   // pinned
     int last_chains = -1;        // lh_debug_chains: the last synchronous solve's stop chain
     int last_lskips = -1;        // lh_debug_ladder: its rejections onto a built ladder rung
+    int last_batches = -1;       // lh_debug_batch: its batches of evaluate-only rungs
+    size_t rho_off = 0;          // the last solve's per-edge rho0 "as last evaluated": its rung buffer in d_rho (a batch)
     int* h_done = nullptr;       // pinned, mapped lh_host_words: [0] k_ctrl raises it when the LM loop stops, [1] progress
                                  // word 2 * (last live trial) + (one iteration from max_iters)
     int* d_done = nullptr;       // device alias of h_done
@@ -635,10 +637,8 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     HIPCHK(h->d_rec.ensure(2 * (size_t)pl.n_rec * LH_REC));
     HIPCHK(h->d_ptab.ensure(2 * PT));
     HIPCHK(h->d_qt.ensure(24 * (size_t)P));
-    HIPCHK(h->d_rho.ensure(pl.n_slots));
     HIPCHK(h->d_wflag.ensure(2 * (size_t)pl.n_slots));
     HIPCHK(h->d_rows.ensure((size_t)pl.n_items * LH_ROW));
-    HIPCHK(h->d_csc.ensure((size_t)pl.n_chunks * 4));
     HIPCHK(h->d_rs_stage.ensure(h->LY.total));
     HIPCHK(h->d_rs_commit.ensure(h->LY.total));
     // the lambda ladder's rungs, one controller workgroup each (LH_NO_LADDER=1: one rung, the A/B
@@ -774,6 +774,13 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         h->band_narrow = narrow;
     }
     if (P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
+    // batches of evaluate-only rungs (one rank, k_reduce's decision; LH_NO_BATCH=1: one rung per
+    // chain, the A/B switch; LH_BATCH_MAX caps the rungs per batch): per rung a per-edge rho0 and the chunk scalars
+    const bool dec1 = (P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm;
+    int batch = (dec1 && ladder > 1 && !getenv("LH_NO_BATCH")) ? ladder : 1;
+    if (const char* bm = getenv("LH_BATCH_MAX")) batch = std::max(1, std::min(batch, atoi(bm)));
+    HIPCHK(h->d_rho.ensure((size_t)batch * pl.n_slots));
+    HIPCHK(h->d_csc.ensure((size_t)batch * pl.n_chunks * 4));
     if (h->band) {   // k_ctrl_b's L rows and ND blocks; L entries outside the envelope are never written: zero
         const size_t NE = (size_t)((6 * P + 15) & ~15);
         const size_t per = NE * 128 + (size_t)(6 * LH_PMAX_ANY / 8) * 64;   // one rung's (k_ctrl_b's layout)
@@ -852,7 +859,9 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
     prm.pcg_max_it = h->opt.pcg_max_iters;
     prm.no_evo = getenv("LH_NO_EVO") != nullptr;
     prm.eval_first = getenv("LH_NO_EVAL_FIRST") == nullptr;
-    prm.dec_in_reduce = ((P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm) ? 1 : 0;
+    prm.dec_in_reduce = dec1 ? 1 : 0;
+    prm.batch = batch;
+    prm.n_chunks = (int32_t)pl.n_chunks;
     prm.commit_in_reduce = h->band ? 1 : 0;
     // every controller builds the ladder: with k_reduce's decision (one rank, k_ctrl and k_ctrl_b) its rungs read it
     // from lh_ctrl; a controller that decides itself (the initial linearisation, sharded solves, k_ctrl_g, k_ctrl_p)
@@ -1045,7 +1054,7 @@ int download(lh_handle* h, lh_result* out, int cur) {
             // handle asks for the flags alike, as it solves alike), and each rank flags its edges at the
             // threshold the totals give
             HIPCHK(h->d_otot.ensure(6));
-            HIPCHK(lh_launch_outlier_counts(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O,
+            HIPCHK(lh_launch_outlier_counts(s, h->d_rho.p + h->rho_off, h->d_obs_perm.p, (long)h->n_slots, (long)h->O,
                                             out->outlier_chi2_th, h->d_ocnt.p, h->d_otot.p));
             if (h->comm) {
                 NCCLCHK(ncclAllReduce(h->d_otot.p, h->d_otot.p, 6, ncclFloat64, ncclSum, h->comm, s));
@@ -1057,10 +1066,10 @@ int download(lh_handle* h, lh_result* out, int cur) {
                 HIPCHK(hipMemcpyAsync(h->d_otot.p, t6, sizeof(t6), hipMemcpyHostToDevice, s));
                 HIPCHK(hipStreamSynchronize(s));   // (t6 is on this stack frame)
             }
-            HIPCHK(lh_launch_outlier_flags(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O,
+            HIPCHK(lh_launch_outlier_flags(s, h->d_rho.p + h->rho_off, h->d_obs_perm.p, (long)h->n_slots, (long)h->O,
                                            out->outlier_chi2_th, h->d_otot.p, h->d_oflag.p));
         } else {
-            HIPCHK(lh_launch_outliers(s, h->d_rho.p, h->d_obs_perm.p, (long)h->n_slots, (long)h->O, out->outlier_chi2_th,
+            HIPCHK(lh_launch_outliers(s, h->d_rho.p + h->rho_off, h->d_obs_perm.p, (long)h->n_slots, (long)h->O, out->outlier_chi2_th,
                                       h->d_ocnt.p, h->d_oflag.p));
         }
         HIPCHK(hipMemcpyAsync(h->s_oflag.p, h->d_oflag.p, o_res + 3 * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -1089,7 +1098,7 @@ int download(lh_handle* h, lh_result* out, int cur) {
     if (nl || ne) {
         // landmarks without an edge are not vertices (backend_lego.cpp:126): they keep their input
         if (nl) HIPCHK(hipMemcpyAsync(h->d_out_xyz.p, h->d_lm_in.p, nl * sizeof(double), hipMemcpyDeviceToDevice, s));
-        HIPCHK(lh_launch_gather(s, h->d_ctrl.p, h->d_rec.p, h->d_lm_perm.p, nl ? h->n_rec : 0, h->d_rho.p,
+        HIPCHK(lh_launch_gather(s, h->d_ctrl.p, h->d_rec.p, h->d_lm_perm.p, nl ? h->n_rec : 0, h->d_rho.p + h->rho_off,
                                 h->d_obs_perm.p, ne ? (long)h->n_slots : 0L, h->d_out_xyz.p, h->d_out_rho.p));
         if (nl) HIPCHK(hipMemcpyAsync(st + np, h->d_out_xyz.p, nl * sizeof(double), hipMemcpyDeviceToHost, s));
     }
@@ -1242,6 +1251,8 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     const int cur = c.cur;
+    h->rho_off = (size_t)c.rho_sel * h->n_slots;
+    h->last_batches = c.nbatches;
     h->last_chains = c.seq_last;
     h->last_lskips = c.lskips;
 
@@ -1934,6 +1945,14 @@ int lh_debug_ladder(lh_handle* h, int* rungs, int* skipped) {
     if (!h->uploaded) return LH_E_STATE;
     *rungs = h->prm.ladder;
     *skipped = h->last_lskips;
+    return LH_OK;
+}
+
+int lh_debug_batch(lh_handle* h, int* batch_max, int* batches) {
+    if (!h || !batch_max || !batches) return LH_E_BADARG;
+    if (!h->uploaded) return LH_E_STATE;
+    *batch_max = h->prm.batch;
+    *batches = h->last_batches;
     return LH_OK;
 }
 

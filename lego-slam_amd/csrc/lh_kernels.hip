@@ -642,6 +642,29 @@ __device__ __forceinline__ void group_sum(double (&v)[N], int lg) {
     }
 }
 
+// the whole-wave butterfly in the other order, v + v[lane ^ 32], then ^16, ^8, ^4, ^2, ^1: the bits of the
+// `v += __shfl_xor(v, off)` loop over off = 32 .. 1 (k_reduce's scalar sums) in plain VALU (ds_bpermute takes LDS
+// bandwidth, which a batch's 32 sums per wave exhausted)
+template <int N>
+__device__ __forceinline__ void wave_sum_desc(double (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = xor32_sum(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = xor16_sum(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_d<0x128>(v[i]);
+    const bool up = (__lane_id() & 4) != 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double a = dpp_d<0x12C>(v[i]), b = dpp_d<0x124>(v[i]);
+        v[i] += up ? b : a;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_d<0x4E>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_d<0xB1>(v[i]);
+}
+
 // max over the wave, every lane gets it: DPP within 16-lane rows, then the permlane swaps
 __device__ __forceinline__ double wave_max(double v) {
     v = fmax(v, dpp_d<0xB1>(v));                                            // ^1
@@ -697,6 +720,101 @@ __device__ __forceinline__ void st_rec2(double2* p, double2 v, __amdgpu_buffer_r
 
 static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
 
+// A batch rung's candidate pose tables (k_lin's batch path, one wave): the window's candidate poses from the committed
+// ones pm (slot lane's pose cpose[lane]) and the rung's step (LDS wdx), then their tables per (slot, camera) into
+// LDS wt_n, as k_lin's own candidate build does; LDS operands as offsets into the dynamic LDS.  Then the release of
+// the flag the other waves wait on.
+__device__ __attribute__((noinline)) void lin_cand_tables(const double* __restrict__ pm, const uint16_t* __restrict__ cpose,
+                                                          int pmax1, int U, int ncam, int o_wdx, int o_wext, int o_wtn,
+                                                          int o_scr, int o_flag) {
+    extern __shared__ __attribute__((aligned(16))) double dsm[];
+    const int lane = threadIdx.x & 63;
+    const uint32_t pp = min((uint32_t)cpose[min(lane, max(U - 1, 0))], (uint32_t)pmax1);
+    double pmc[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) pmc[i] = pm[pp * 12 + i];
+    double* scr = dsm + o_scr;
+    if (lane < U) {
+        double To[12];
+        d_pose_candidate(pmc, dsm + o_wdx + 6 * lane, To);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) scr[lane * 12 + i] = To[i];
+    }
+    wave_sync();
+    if (lane < U * ncam) {
+        const int sl = lane / ncam, c = lane - sl * ncam;
+        double To[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) To[i] = scr[sl * 12 + i];
+        d_pose_table(To, dsm + o_wext + c * LH_EXT, dsm + o_wtn + (sl * ncam + c) * LH_PT_LDS);
+    }
+    __hip_atomic_store(reinterpret_cast<int*>(dsm + o_flag), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ---- back-substitution of the pending pose step (problem.cpp:426-429) for one sub-batch: the lane's edge term
+//      J_l^T W J_p dx (at the committed linearisation: pt the committed pose table, d the slot's step), summed over
+//      the landmark's lane group, then the landmark's update from its cached factor cl (VertexXYZ::add) and the
+//      lead lane's gain-scale term (isGoodStepInLM's scale) ----
+template <bool F32>
+__device__ __forceinline__ void lin_backsub(const double* __restrict__ pt, const double* __restrict__ e,
+                                            const double* __restrict__ d, bool live, bool ext_id, bool ext_rot, double u,
+                                            double v, int wfl, int lg, bool lmok, bool lead, const double (&cl)[12],
+                                            double lambda, const lh_params& prm, double (&X)[3], double& scale_acc) {
+    double v3[3] = {0.0, 0.0, 0.0};
+    if (live) {
+        EdgeEval E;
+        if constexpr (F32) {   // fp64 residual and weight (as below), fp32 Jacobians
+            if (wfl) {
+                E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+            } else {
+                double Pc[3];
+                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                edge_robust(E, prm);
+            }
+            edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+        } else {
+            double Pc[3];
+            if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
+                E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+                edge_pc(pt, e, ext_id, ext_rot, X, Pc);
+            } else {
+                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                edge_robust(E, prm);
+            }
+            edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
+        }
+        double jd0 = 0.0, jd1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            if (!jz(0, a)) jd0 += E.Jp[a] * d[a];
+            if (!jz(1, a)) jd1 += E.Jp[6 + a] * d[a];
+        }
+        const double y0 = E.W00 * jd0 + E.W01 * jd1, y1 = E.W10 * jd0 + E.W11 * jd1;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v3[c] = E.Jl[c] * y0 + E.Jl[3 + c] * y1;
+    }
+    group_sum(v3, lg);
+    const double s0 = v3[0], s1 = v3[1], s2 = v3[2];
+    if (lmok) {
+        // the cached factor holds 1/L_ii on the diagonal
+        const double i00 = cl[0], l10 = cl[1], i11 = cl[2], l20 = cl[3], l21 = cl[4], i22 = cl[5];
+        const double b0 = cl[6], b1 = cl[7], b2 = cl[8];
+        const double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
+        const double y0 = t0 * i00, y1 = (t1 - l10 * y0) * i11, y2 = (t2 - l20 * y0 - l21 * y1) * i22;
+        double d2 = y2 * i22, d1 = (y1 - l21 * d2) * i11, d0 = (y0 - l10 * d1 - l20 * d2) * i00;
+        if (prm.guard && !(i00 == i00)) { d0 = d1 = d2 = 0.0; }   // skipped degenerate landmark
+        double x0 = X[0], x1 = X[1], x2 = X[2];
+        if (isfinite(d0) && isfinite(d1) && isfinite(d2)) { x0 += d0; x1 += d1; x2 += d2; }   // VertexXYZ::add
+        if (lead) {
+            double sc;
+            if (prm.strategy == 0) sc = d0 * (lambda * d0 + b0) + d1 * (lambda * d1 + b1) + d2 * (lambda * d2 + b2);
+            else sc = d0 * (lambda * cl[9] * d0 + b0) + d1 * (lambda * cl[10] * d1 + b1) + d2 * (lambda * cl[11] * d2 + b2);
+            scale_acc += sc;
+        }
+        X[0] = x0; X[1] = x1; X[2] = x2;
+    }
+}
+
 #ifndef LH_LIN_OCC
 #define LH_LIN_OCC 2   // k_lin<T <= 3> workgroups per CU the registers are budgeted for
 #endif
@@ -724,6 +842,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
     // no candidate; the committed landmarks and pose tables are linearised into the candidate side, which the
     // chain's decision commits (the writer copies the committed poses and tables across first)
     const bool relin = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->relin) != 0;
+    // the evo word: a trial of the final LM iteration or after a rejection (ctrl_lm_step) only evaluates, and above
+    // its low byte the rung count of a batch of such trials (k_reduce's decision; the batch path after the tables)
+    const int evw = TRIAL ? __builtin_amdgcn_readfirstlane(ctrl->evo) : 0;
+    const int nbatch = max(evw >> 8, 1);
     // the pending step: lambda-ladder rung ctrl->lad's (the rung the last decision moved to; 0 after a factor)
     if (TRIAL) dxp += (size_t)__builtin_amdgcn_readfirstlane(ctrl->lad) * prm.n;
     // The candidate poses of a trial (VertexPose::add of the step k_ctrl solved) are built here, not in
@@ -741,7 +863,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
         return;
     }
     if (TRIAL && writer && blockIdx.x == 0) {
-        if (done) return;
+        if (done || nbatch > 1) return;   // (a batch writes no candidate: its accepted rung is re-run in full)
         const int P = prm.P, nc = prm.ncam, cnd = 1 - cur;
         if (relin) {
             for (int i = threadIdx.x; i < P * 12; i += 256) pose_mat[(size_t)cnd * P * 12 + i] = pose_mat[(size_t)cur * P * 12 + i];
@@ -764,7 +886,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
     const int chunk = chunk_base + blockIdx.x - (writer ? 1 : 0);
     // a trial of the final LM iteration (ctrl->evo, ctrl_lm_step): back substitution and the
     // candidate's evaluation only (landmark positions, rho0 per edge, chi2 and the gain scale)
-    const bool evo = TRIAL && __builtin_amdgcn_readfirstlane(ctrl->evo) != 0;
+    const bool evo = evw != 0;
     const double lambda = TRIAL ? ctrl->lambda : 0.0;
     const uint32_t* __restrict__ chw = reinterpret_cast<const uint32_t*>(chunks + chunk);
     const uint32_t sb_begin = __builtin_amdgcn_readfirstlane(chw[0]), sb_end = __builtin_amdgcn_readfirstlane(chw[1]);
@@ -900,6 +1022,107 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
         if (tid == 0) *cflag = 0;
     }
     lds_barrier();   // window tables
+    if (TRIAL && nbatch > 1) {
+        // ---- a batch: the evaluate-only trials of rungs lad .. lad + nbatch - 1 after a rejection,
+        //      each evaluated as the evaluate-only path below evaluates one trial: the back substitution of the
+        //      rung's step at the rung's lambda, the rung's candidate pose tables, rho0 per edge (edge_rho + r nslots)
+        //      and the chunk's chi2 and gain scale (csc + (r n_chunks + chunk) 4).  Nothing else is written: k_reduce
+        //      decides the rungs in order, and the next chain re-runs an accepted rung as a full trial. ----
+        double lam_r = lambda, ni_r = ctrl->ni;
+        const int umax1 = max(U - 1, 0);
+        const size_t dofs = 6 * (size_t)min((uint32_t)cpose[min(tid / 6, umax1)], (uint32_t)(prm.P - 1)) + (tid - 6 * (tid / 6));
+        double dv_n = dxp[(size_t)prm.n + dofs];   // rung lad + 1's step, in flight while rung lad is evaluated
+        for (int r = 0; r < nbatch; ++r) {
+            if (r > 0) {
+                // the rung's lambda: one more rejection's update (ctrl_lm_step, ladder_read's order)
+                if (prm.strategy == 0) { lam_r *= ni_r; ni_r *= 2.0; }
+                else lam_r = fmin(lam_r * 11.0, 1e7);
+                lds_barrier();   // every wave is done with the previous rung's step, tables and combine
+                if (tid < 6 * U) wdx[tid] = dv_n;
+                if (tid == 0) *cflag = 0;
+                dv_n = dxp[(size_t)min(r + 1, nbatch - 1) * prm.n + dofs];
+                lds_barrier();
+            }
+            // the rung's candidate pose tables (k_lin's build below, out of line)
+            if (wave == cwave) lin_cand_tables(pose_mat + (size_t)cur * prm.P * 12, cpose, prm.P - 1, U, ncam,
+                                               (int)(wdx - dsm), (int)(wext - dsm), (int)(wt_n - dsm), (int)(scr - dsm),
+                                               (int)(reinterpret_cast<double*>(cflag) - dsm));
+            bool ready = false;
+            double chi_b = 0.0, scale_b = 0.0;
+            for (int sbi = (int)sb_begin + wave; sbi < (int)sb_end; sbi += LH_WAVES) {
+                const lh_subbatch S = S_n;
+                const int lg = S.lg, nlm = S.n_lm;
+                const int ls = lane >> lg, gj = lane & ((1 << lg) - 1);
+                const bool lmok = ls < nlm;
+                const bool lead = gj == 0 && lmok;
+                const uint32_t meta = meta_n;
+                const double u = u_n, v = v_n;
+                const double2 rr = r_n;
+                const int wfl = wfl_n;
+                const int o = sbi * 64 + lane;
+                {   // the next sub-batch's words: after the wave's last one, its first again (the next rung's)
+                    const int sbw = sbi + LH_WAVES < (int)sb_end ? sbi + LH_WAVES : (int)sb_begin + wave;
+                    const int sbn = min(sbw, sb_last);
+                    const int on = sbn * 64 + lane;
+                    S_n = sbs[sbn];
+                    meta_n = obs_meta[on];
+                    wfl_n = wf_c[on];
+                    const float2 z = reinterpret_cast<const float2*>(obs_uv)[on];
+                    u_n = (double)z.x;
+                    v_n = (double)z.y;
+                    r_n = rec_piece(sbn);
+                }
+                reinterpret_cast<double2*>(scr)[(lane >> 3) * (LH_REC_LDS / 2) + (lane & 7)] = rr;
+                wave_sync();
+                const double* myrec = scr + (ls & 7) * LH_REC_LDS;
+                double X[3] = {myrec[LH_REC_X], myrec[LH_REC_X + 1], myrec[LH_REC_X + 2]};
+                double cl[12];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) cl[i] = myrec[LH_REC_L + i];
+                wave_sync();
+                const bool has = (meta & LH_META_VALID) != 0u;
+                const int p = LH_META_POSE(meta), cam = LH_META_CAM(meta), slot = LH_META_SLOT(meta);
+                const bool pfixed = (fixed_bits[p >> 6] >> (p & 63)) & 1ull;
+                const bool live = has && !pfixed;
+                const double* e = wext + cam * LH_EXT;
+                const bool ext_id = (prm.ext_identity >> cam) & 1;
+                const bool ext_rot = (prm.ext_rot_identity >> cam) & 1;
+                lin_backsub<F32>(wt_c + (slot * ncam + cam) * LH_PT_LDS, e, wdx + 6 * slot, live, ext_id, ext_rot, u, v,
+                                 wfl, lg, lmok, lead, cl, lam_r, prm, X, scale_b);
+                if (!ready) {
+                    while (__hip_atomic_load(cflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+                    ready = true;
+                }
+                if (has) {
+                    const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
+                    EdgeEval E;
+                    double Pc[3];
+                    edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+                    edge_robust(E, prm);
+                    st_out(edge_rho + (size_t)r * nslots + o, E.rho0);
+                    chi_b += E.rho0;
+                }
+            }
+            {   // the wave's totals and the 4-wave combine, as the evaluate-only epilogue below
+                double t3[3] = {chi_b, scale_b, 0.0};
+                group_sum(t3, 6);
+                chi_b = t3[0]; scale_b = t3[1];
+            }
+            lds_barrier();
+            for (int phase = 0; phase < 2; ++phase) {
+                if ((wave >> 1) == phase && lane == 0) {
+                    double* sc = dsm + (wave & 1) * 2;
+                    if (phase == 0) { sc[0] = chi_b; sc[1] = scale_b; }
+                    else { sc[0] += chi_b; sc[1] += scale_b; }
+                }
+                lds_barrier();
+            }
+            double* gs = csc + ((size_t)r * prm.n_chunks + chunk) * 4;
+            if (tid < 2) gs[tid] = dsm[tid] + dsm[2 + tid];
+            if (tid == 2 || tid == 3) gs[tid] = 0.0;
+        }
+        return;
+    }
     // A trial's candidate pose tables (wt_n): wave cwave composes the window's candidate poses (lane = slot)
     // and their tables (lane = (slot, camera)) while the other waves start their first back
     // substitution, which needs only the committed tables; they wait on cflag before their first
@@ -977,63 +1200,9 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
         const bool ext_rot = (prm.ext_rot_identity >> cam) & 1;
 
         // ---- back-substitution of the pending pose step (problem.cpp:426-429) ----
-        if (TRIAL && !relin) {
-            double v3[3] = {0.0, 0.0, 0.0};
-            if (live) {
-                const double* pt = wt_c + (slot * ncam + cam) * LH_PT_LDS;
-                EdgeEval E;
-                if constexpr (F32) {   // fp64 residual and weight (as below), fp32 Jacobians
-                    if (wfl) {
-                        E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
-                    } else {
-                        double Pc[3];
-                        edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                        edge_robust(E, prm);
-                    }
-                    edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
-                } else {
-                    double Pc[3];
-                    if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
-                        E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
-                        edge_pc(pt, e, ext_id, ext_rot, X, Pc);
-                    } else {
-                        edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                        edge_robust(E, prm);
-                    }
-                    edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
-                }
-                const double* d = wdx + 6 * slot;
-                double jd0 = 0.0, jd1 = 0.0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    if (!jz(0, a)) jd0 += E.Jp[a] * d[a];
-                    if (!jz(1, a)) jd1 += E.Jp[6 + a] * d[a];
-                }
-                const double y0 = E.W00 * jd0 + E.W01 * jd1, y1 = E.W10 * jd0 + E.W11 * jd1;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) v3[c] = E.Jl[c] * y0 + E.Jl[3 + c] * y1;
-            }
-            group_sum(v3, lg);
-            const double s0 = v3[0], s1 = v3[1], s2 = v3[2];
-            if (lmok) {
-                // the cached factor holds 1/L_ii on the diagonal
-                const double i00 = cl[0], l10 = cl[1], i11 = cl[2], l20 = cl[3], l21 = cl[4], i22 = cl[5];
-                const double b0 = cl[6], b1 = cl[7], b2 = cl[8];
-                const double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
-                const double y0 = t0 * i00, y1 = (t1 - l10 * y0) * i11, y2 = (t2 - l20 * y0 - l21 * y1) * i22;
-                double d2 = y2 * i22, d1 = (y1 - l21 * d2) * i11, d0 = (y0 - l10 * d1 - l20 * d2) * i00;
-                if (prm.guard && !(i00 == i00)) { d0 = d1 = d2 = 0.0; }   // skipped degenerate landmark
-                double x0 = X[0], x1 = X[1], x2 = X[2];
-                if (isfinite(d0) && isfinite(d1) && isfinite(d2)) { x0 += d0; x1 += d1; x2 += d2; }   // VertexXYZ::add
-                if (lead) {
-                    double sc;
-                    if (prm.strategy == 0) sc = d0 * (lambda * d0 + b0) + d1 * (lambda * d1 + b1) + d2 * (lambda * d2 + b2);
-                    else sc = d0 * (lambda * cl[9] * d0 + b0) + d1 * (lambda * cl[10] * d1 + b1) + d2 * (lambda * cl[11] * d2 + b2);
-                    scale_acc += sc;
-                }
-                X[0] = x0; X[1] = x1; X[2] = x2;
-            }
-        }
+        if (TRIAL && !relin)
+            lin_backsub<F32>(wt_c + (slot * ncam + cam) * LH_PT_LDS, e, wdx + 6 * slot, live, ext_id, ext_rot, u, v, wfl,
+                             lg, lmok, lead, cl, lambda, prm, X, scale_acc);
         STAMP(0);
         if (!tabs_ready) {   // wave-uniform: once per wave
             while (__hip_atomic_load(cflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
@@ -1293,6 +1462,7 @@ struct CtrlWords {
     double chi, lam, ni, last, spose, chi0;
     int iter, fc, trials, nacc, done, cur, tl;
     int evo, relin;   // this trial only evaluated; this chain re-linearises (the previous trial was such an acceptance)
+    int retrial;      // this chain re-runs a batch's accepted rung (lh_ctrl.retrial: 2 when that acceptance stopped the loop)
     int lad, lad_n;   // the rung this trial's step came from; the rungs built (lh_ctrl.lad)
 };
 __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl) {
@@ -1301,7 +1471,7 @@ __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl)
     w.chi0 = ctrl->chi2_initial;
     w.iter = ctrl->iter; w.fc = ctrl->false_cnt; w.trials = ctrl->trials; w.nacc = ctrl->accepted;
     w.done = ctrl->done; w.cur = ctrl->cur; w.tl = ctrl->trace_len;
-    w.evo = ctrl->evo; w.relin = ctrl->relin;
+    w.evo = ctrl->evo; w.relin = ctrl->relin; w.retrial = ctrl->retrial;
     w.lad = ctrl->lad; w.lad_n = ctrl->lad_n;
     // every rung's gain part is loaded and the trial's selected (no load that waits on lad)
     double sp[LH_LAD];
@@ -1312,6 +1482,50 @@ __device__ __forceinline__ CtrlWords ctrl_load(const lh_ctrl* __restrict__ ctrl)
     for (int i = 1; i < LH_LAD; ++i) w.spose = (w.lad == i) ? sp[i] : w.spose;
     return w;
 }
+// A batch's decisions (k_reduce) run back to back on one thread: the controller words and the
+// counters they update stay in registers between the rungs, the rungs' gain parts and PCG counts in LDS (reloading
+// them from lh_ctrl after each decision cost two dependent round trips per rung); each decision still stores its
+// words.
+struct BatchWords {
+    CtrlWords w;              // the words the next rung's decision starts from
+    const double* sp;         // lh_ctrl.spose_l (an LDS copy)
+    const int* lad_its;       // lh_ctrl.lad_its (an LDS copy)
+    int* cnt;                 // (LDS) lh_ctrl's counters lskips, pcg_iters; the last decision's lskip and nbatch
+};
+enum { BW_LSKIPS, BW_PCG, BW_LSKIP, BW_NBATCH };
+__device__ __forceinline__ void batch_load(const lh_ctrl* __restrict__ ctrl, BatchWords& b, double* sp, int* its, int* cnt) {
+    b.w = ctrl_load(ctrl);
+#pragma unroll
+    for (int i = 0; i < LH_LAD; ++i) { sp[i] = ctrl->spose_l[i]; its[i] = ctrl->lad_its[i]; }
+    b.sp = sp;
+    b.lad_its = its;
+    b.cnt = cnt;
+    cnt[BW_LSKIPS] = ctrl->lskips;
+    cnt[BW_PCG] = ctrl->pcg_iters;
+    cnt[BW_LSKIP] = 0;
+    cnt[BW_NBATCH] = 1;
+}
+
+// a batch's words after its last decision (what ctrl_lm_step stores after a decision, from the batch's registers)
+__device__ __forceinline__ void batch_store(lh_ctrl* __restrict__ ctrl, const BatchWords& b, int seq) {
+    const CtrlWords& o = b.w;
+    ctrl->chi = o.chi; ctrl->lambda = o.lam; ctrl->ni = o.ni; ctrl->last_chi = o.last; ctrl->chi2_initial = o.chi0;
+    ctrl->iter = o.iter; ctrl->false_cnt = o.fc; ctrl->trials = o.trials; ctrl->accepted = o.nacc;
+    ctrl->done = o.done; ctrl->cur = o.cur; ctrl->trace_len = o.tl;
+    ctrl->retrial = o.retrial;
+    ctrl->lad = o.lad;
+    ctrl->lskip = b.cnt[BW_LSKIP];
+    ctrl->lskips = b.cnt[BW_LSKIPS];
+    ctrl->pcg_iters = b.cnt[BW_PCG];
+    ctrl->acc_hist[seq & 1] = 0;   // a batch commits nothing (a retrial does)
+    ctrl->seq_last = seq;
+    ctrl->relin = o.relin;
+    ctrl->nofactor = o.relin | b.cnt[BW_LSKIP] | (o.retrial != 0 ? 1 : 0);
+    ctrl->evo = o.evo;
+    ctrl->nbatch = b.cnt[BW_NBATCH];
+    ctrl->evo_seq[(seq + 1) & 1] = o.evo;
+}
+
 // The stop trial's summary and trace to the host words, then done, by ONE thread behind its own
 // system-scope fence.  A kernel boundary releases at agent scope only, and the trace entries were
 // decided by earlier kernels on other CUs, so every word the host reads after done is stored here,
@@ -1330,26 +1544,42 @@ __device__ __noinline__ void publish_stop(const lh_ctrl* __restrict__ ctrl, vola
     host_done[0] = 1;
 }
 
+// The host's progress word after chain seq's decision (ctrl_lm_step; a batch's after its last rung, k_reduce):
+// 2 seq + near, near = 1 when the next chain may be the last (one more completed iteration reaches max_iters, a
+// stalled iteration's last rejection, or a pending retrial that stops the loop).
+__device__ __forceinline__ void ctrl_progress(const lh_params& prm, volatile int* __restrict__ host_done, int seq, int iter,
+                                              int fc, double last, double chi, int hold) {
+    const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
+    const int last_try = (fc + 1 >= prm.max_trials && last - chi < prm.stop_dchi2) ? 1 : 0;
+    host_done[1] = 2 * seq + (near | last_try | hold);
+}
+
 // Returns 1 when the controller has nothing to factor: this trial was an evaluate-only one accepted outside the
 // final iteration (the next chain re-linearises the accepted state, relin; that chain's decision commits the new
-// linearisation like the initial one and leaves the LM state alone), or a rejection whose step a lambda-ladder
-// rung already holds (lskip).
+// linearisation like the initial one and leaves the LM state alone), a rejection whose step a lambda-ladder
+// rung already holds (lskip), or a batch's acceptance (retrial).
+// batch: the decision of one rung of a batch (k_reduce's loop over the rungs a chain evaluated):
+// an acceptance commits nothing (the next chain re-runs the rung as a full trial, lh_ctrl.retrial, and its
+// decision commits it; a stop it causes is raised by that chain), and the host word is the loop's to write.
 __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
                                              volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
-                                             int& cur_o, double& lam_o, bool raise_done = true) {
+                                             int& cur_o, double& lam_o, bool raise_done = true, BatchWords* bw = nullptr) {
+    const bool batch = bw != nullptr;
     double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
     int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
     int done = w.done, cur = w.cur;
-    int accept = 0, trace = 0, relin = 0;
+    int accept = 0, trace = 0, relin = 0, retrial = 0;
     int lad = 0, lskip = 0;   // the next step's rung: 0 after any factor; a rejection moves up the ladder
     if (!done) {
-        if (mode != 0 && w.relin) {
+        if (mode != 0 && (w.relin || w.retrial)) {
             // the re-linearisation of an evaluate-only acceptance: its records and pose tables were written
             // to the candidate side (k_lin), which becomes the committed one; lambda, chi2 and the counts
-            // were updated by the acceptance
+            // were updated by the acceptance.  A retrial (a batch's accepted rung as a full trial) likewise,
+            // and it raises the stop that acceptance took.
             cur = 1 - cur;
             accept = 1;
+            if (w.retrial == 2) done = 1;
         } else if (mode == 0) {
             // computeLambdaInitLM (problem.cpp:470-504)
             ni = 2.0;
@@ -1398,8 +1628,13 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
             bool inner_end;
             if (ok) {
                 nacc += 1;
-                cur = 1 - cur;       // commit candidate landmarks, caches and poses
-                accept = 1;
+                if (!batch) {
+                    cur = 1 - cur;   // commit candidate landmarks, caches and poses
+                    accept = 1;
+                } else {
+                    retrial = 1;     // the next chain linearises this rung's candidate (its step: rung w.lad)
+                    lad = w.lad;
+                }
                 fc = 0;
                 inner_end = true;
             } else {
@@ -1412,7 +1647,7 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
                     lskip = 1;
                 }
             }
-            relin = (ok && w.evo) ? 1 : 0;   // (cleared below when the loop stops)
+            relin = (ok && w.evo && !batch) ? 1 : 0;   // (cleared below when the loop stops)
             if (inner_end) {
                 iter += 1;
                 if (last - chi < prm.stop_dchi2) done = 1;
@@ -1425,18 +1660,28 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
             if (tl < LH_TRACE) { ctrl->trace_chi[tl] = chi; ctrl->trace_lambda[tl] = lam; }
             tl += 1;
         }
-        ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
-        ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
-        ctrl->done = done; ctrl->cur = cur; ctrl->trace_len = tl;
+        if (retrial && done) retrial = 2;   // the stop is the retrial's to raise
         if (done) lskip = 0;
-        ctrl->lad = lad;
-        ctrl->lskip = lskip;
-        if (lskip) ctrl->lskips += 1;
-        if (lskip && prm.solver == 1) ctrl->pcg_iters += ctrl->lad_its[lad];   // the rung's solve counts now
-        ctrl->acc_hist[seq & 1] = accept;
-        ctrl->seq_last = seq;
         if (done) relin = 0;
-        ctrl->relin = relin;
+        // (a batch's rung stores its words once, after the batch's last decision: batch_store)
+        if (!batch) {
+            ctrl->chi = chi; ctrl->lambda = lam; ctrl->ni = ni; ctrl->last_chi = last; ctrl->chi2_initial = chi0;
+            ctrl->iter = iter; ctrl->false_cnt = fc; ctrl->trials = trials; ctrl->accepted = nacc;
+            ctrl->done = retrial ? 0 : done; ctrl->cur = cur; ctrl->trace_len = tl;
+            ctrl->retrial = retrial;
+            ctrl->rho_sel = 0;
+            ctrl->lad = lad;
+            ctrl->lskip = lskip;
+            if (lskip) ctrl->lskips += 1;
+            if (lskip && prm.solver == 1) ctrl->pcg_iters += ctrl->lad_its[lad];   // the rung's solve counts now
+            ctrl->acc_hist[seq & 1] = accept;
+            ctrl->seq_last = seq;
+            ctrl->relin = relin;
+            ctrl->nofactor = relin | lskip | (retrial != 0 ? 1 : 0);
+        } else {   // (the same counts from the batch's registers)
+            bw->cnt[BW_LSKIPS] += lskip;
+            if (lskip && prm.solver == 1) bw->cnt[BW_PCG] += bw->lad_its[lad];
+        }
         // The next trial is in the final iteration when one more completed iteration reaches max_iters.
         // Its decision then either stops the loop (accept, or the last rejection) or leads to another
         // such trial, so its candidate linearisation is never used: k_lin only evaluates (evo).  With
@@ -1444,16 +1689,28 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
         // rejections (every solve that stops on a stalled chi2 ends with max_trials of them) then pays
         // evaluations only, and an acceptance among them one re-linearisation chain (relin).
         const int near = (prm.max_iters > 0 && iter + 1 >= prm.max_iters) ? 1 : 0;
-        const int evo_n = (done || relin || prm.no_evo) ? 0 : (near | ((prm.eval_first && fc > 0) ? 1 : 0));
-        ctrl->evo = evo_n;
-        ctrl->evo_seq[(seq + 1) & 1] = evo_n;
+        // A retrial is a full trial (it linearises the accepted rung's candidate, as a re-linearisation does), or an
+        // evaluate-only one when that acceptance stopped the loop (it then only writes the candidate, as the serial
+        // evaluate-only trial that stopped the loop did)
+        const int evo_n = retrial == 2 ? 1
+                        : (done || relin || retrial || prm.no_evo) ? 0 : (near | ((prm.eval_first && fc > 0) ? 1 : 0));
+        // the next chain evaluates a batch of rungs when it is an evaluate-only trial after a rejection onto a built
+        // rung: the rungs from there up to the last built one, within the trials left in the iteration
+        const int nbatch_n = (prm.batch > 1 && evo_n && fc > 0 && lskip) ? min(min(w.lad_n - lad, prm.max_trials - fc), prm.batch) : 1;
+        // (the evo words: evo in the low byte, a batch's rung count above it)
+        const int evw = evo_n | (nbatch_n > 1 ? nbatch_n << 8 : 0);
+        if (!batch) {
+            ctrl->evo = evw;
+            ctrl->nbatch = nbatch_n;
+            ctrl->evo_seq[(seq + 1) & 1] = evw;
+        }
         // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
         // trial's controller has decided (its k_lin and k_reduce are done), and near = 1 when one
         // more completed iteration reaches max_iters.  The host keeps the queue filled from it (one
         // trial ahead when near, so a stop by max_iters leaves nothing enqueued past it); it never
         // advances past the stop trial, which bounds how many trials (and all-reduces) any rank
         // can have enqueued.  One 32-bit store: the host never sees a torn pair.
-        if (host_done) {
+        if (host_done && !batch) {
             if (done) {
                 ctrl->done_seq = seq;
                 if (raise_done) publish_stop(ctrl, host_done);   // reads back this thread's stores above
@@ -1461,17 +1718,29 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
                 // (publish_stop): only stores of the thread that fences are ordered before done
             } else {
                 // near also when the next trial's rejection would end its iteration at an unchanged chi2 (a
-                // stalled solve's last trial: the stop rule then ends the loop), so no chain is left past it
-                const int last_try = (fc + 1 >= prm.max_trials && last - chi < prm.stop_dchi2) ? 1 : 0;
-                host_done[1] = 2 * seq + (near | last_try);
+                // stalled solve's last trial: the stop rule then ends the loop), so no chain is left past it; and
+                // likewise when the next chain is a batch whose last rung is such a trial
+                const int hold = (nbatch_n > 1 && fc + nbatch_n >= prm.max_trials && last - chi < prm.stop_dchi2) ? 1 : 0;
+                ctrl_progress(prm, host_done, seq, iter, fc, last, chi, hold);
             }
+        }
+        if (retrial == 2) done = 0;
+        if (batch) {   // the words the next rung's decision starts from (as ctrl_load would read them back)
+            CtrlWords& o = bw->w;
+            o.chi = chi; o.lam = lam; o.ni = ni; o.last = last; o.chi0 = chi0;
+            o.iter = iter; o.fc = fc; o.trials = trials; o.nacc = nacc; o.done = done; o.cur = cur; o.tl = tl;
+            o.evo = evw; o.relin = relin; o.retrial = retrial; o.lad = lad;
+            o.spose = bw->sp[lad];
+            bw->cnt[BW_LSKIP] = lskip;
+            bw->cnt[BW_NBATCH] = nbatch_n;
         }
     }
     done_o = done;
     accept_o = accept;
     cur_o = cur;
     lam_o = lam;
-    return relin | lskip;   // nothing to factor: an evaluate-only acceptance, or a rejection onto a built rung
+    // nothing to factor: an evaluate-only acceptance, a rejection onto a built rung, or a batch's acceptance
+    return relin | lskip | (retrial != 0 ? 1 : 0);
 }
 
 // ---- the lambda ladder's rung workgroups (lh_ctrl.lad) ----
@@ -1500,7 +1769,7 @@ __device__ __forceinline__ LadderDec ladder_read(const lh_ctrl* __restrict__ ctr
     d.done = __builtin_amdgcn_readfirstlane(ctrl->done);
     d.accept = __builtin_amdgcn_readfirstlane(ctrl->acc_hist[seq & 1]);
     // an evaluate-only acceptance (nothing to factor), or a rejection onto a built rung (its step is solved)
-    d.skip = __builtin_amdgcn_readfirstlane(ctrl->relin) | __builtin_amdgcn_readfirstlane(ctrl->lskip);
+    d.skip = __builtin_amdgcn_readfirstlane(ctrl->nofactor);
     double lambda = ctrl->lambda, ni = ctrl->ni;
     for (int i = 0; i < rung; ++i) {
         if (prm.strategy == 0) { lambda *= ni; ni *= 2; }
@@ -1549,7 +1818,10 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
     const int p = (int)(rt.w & 0xffffu), q = (int)(rt.w >> 16);
     const int done = __builtin_amdgcn_readfirstlane(ctrl->done);
     // k_lin wrote the chunk scalars only (this trial's word: the scalar block's decision writes the next one's)
+    // this chain's evo word (evo, and above it a batch's rung count: k_lin evaluated rungs lad .. lad + nb - 1, their
+    // chunk scalars at csc + r n_chunks 4)
     const int evo = mode != 0 ? __builtin_amdgcn_readfirstlane(ctrl->evo_seq[seq & 1]) : 0;
+    const int nb = max(evo >> 8, 1);
     const bool copy_prev = (prm.commit_in_reduce | prm.img) && mode != 0 && b < LY.npairs && done == 0 && wave == 0;
     const int prev_acc = copy_prev ? __builtin_amdgcn_readfirstlane(ctrl->acc_hist[(seq - 1) & 1]) : 0;
     if (copy_prev) {
@@ -1607,7 +1879,74 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
         // the LM decision's controller words go out with the chunk scalars (one round trip, not a third
         // after the sums; only this block's thread 0 writes them in this kernel)
         CtrlWords cw0{};
-        if (prm.dec_in_reduce && mode != 0 && tid == 0) cw0 = ctrl_load(ctrl);
+        BatchWords bw0;
+        __shared__ double b_sp[LH_LAD];
+        __shared__ int b_its[LH_LAD], b_cnt[4];
+        if (prm.dec_in_reduce && mode != 0 && tid == 0) {
+            if (nb > 1) batch_load(ctrl, bw0, b_sp, b_its, b_cnt);
+            else cw0 = ctrl_load(ctrl);
+        }
+        if (nb > 1) {
+            // each rung's chi2 and gain-scale sums in the order below (thread, lane butterfly, waves in order):
+            // eight rungs per round of loads, the butterflies in VALU (wave_sum_desc)
+            for (int g = 0; g < nb; g += 8) {
+                double b[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) b[j] = 0.0;
+                for (int c = tid; c < n_chunks; c += RT) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (g + j < nb) {
+                            const double* sc = csc + ((size_t)(g + j) * n_chunks + c) * 4;
+                            b[2 * j] += sc[0]; b[2 * j + 1] += sc[1];
+                        }
+                }
+                wave_sum_desc(b);
+                if (lane == 0)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j)
+                        if (2 * g + j < 2 * nb) part[0][wave][2 * g + j] = b[j];
+            }
+            lds_barrier();
+            // each rung's totals over the waves, in wave order, by one thread per rung
+            __shared__ double b_a[2 * LH_LAD];
+            if (tid < nb) {
+                double a0 = 0.0, a1 = 0.0;
+                for (int wv = 0; wv < RW; ++wv) { a0 += part[0][wv][2 * tid]; a1 += part[0][wv][2 * tid + 1]; }
+                b_a[2 * tid] = a0;
+                b_a[2 * tid + 1] = a1;
+            }
+            lds_barrier();
+            if (tid == 0) {
+                // the rungs' decisions in order, each the one the serial chain of that trial takes; the batch ends
+                // at an acceptance (retrial), the stop, or a next trial that is not the batch's next rung
+                double a0 = 0.0, a1 = 0.0;
+                int r = 0;
+                for (;; ++r) {
+                    a0 = b_a[2 * r];
+                    a1 = b_a[2 * r + 1];
+                    int d_o, a_o, c_o;
+                    double l_o;
+                    ctrl_lm_step(ctrl, bw0.w, prm, 1, 0.0, 0.5 * a0, a1, 0.0, host_done, seq, d_o, a_o, c_o, l_o, false, &bw0);
+                    const CtrlWords& w = bw0.w;
+                    if (r + 1 >= nb || w.done || w.retrial || !w.evo || !b_cnt[BW_LSKIP]) break;
+                }
+                const CtrlWords& w = bw0.w;
+                batch_store(ctrl, bw0, seq);
+                ctrl->rho_sel = r;   // the per-edge rho0 of the last rung decided
+                ctrl->nbatches += 1;
+                rs[LY.off_sc + LH_SC_CHI2] = a0;
+                rs[LY.off_sc + LH_SC_SCALE] = a1;
+                rs[LY.off_sc + LH_SC_NDEG] = 0.0;
+                rs[LY.off_sc + LH_SC_MAXD] = 0.0;
+                *maxd_out = 0.0;
+                if (host_done) {
+                    if (w.done) ctrl->done_seq = seq;   // this chain's controller publishes the stop
+                    else ctrl_progress(prm, host_done, seq, w.iter, w.fc, w.last, w.chi, w.retrial == 2 ? 1 : 0);
+                }
+            }
+            return;
+        }
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, mx = 0.0;
         for (int c = tid; c < n_chunks; c += RT) {
             const double* sc = csc + (size_t)c * 4;

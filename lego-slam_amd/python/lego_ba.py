@@ -208,6 +208,7 @@ ABI_SYMBOLS = [
     "lh_estimate_pose", "lh_lk_track",
     "lh_debug_mfma_probe", "lh_debug_ldlt_probe", "lh_debug_pcg_probe", "lh_debug_event_floor", "lh_debug_stamps",
     "lh_debug_time_lin", "lh_debug_comm_count", "lh_debug_controller", "lh_debug_chains", "lh_debug_ladder",
+    "lh_debug_batch",
 ]
 
 _balib = None
@@ -245,6 +246,8 @@ def ba_lib():
         lib.lh_debug_controller.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         lib.lh_debug_chains.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         lib.lh_debug_ladder.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        if hasattr(lib, "lh_debug_batch"):   # (an older library of an A/B run lacks it)
+            lib.lh_debug_batch.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _balib = lib
     return _balib
 
@@ -526,6 +529,13 @@ class Solver:
         r, k = C.c_int(0), C.c_int(0)
         _check(ba_lib().lh_debug_ladder(self.h, C.byref(r), C.byref(k)), "lh_debug_ladder")
         return r.value, k.value
+
+    def batch(self):
+        """(most rungs one chain of the uploaded window evaluates -- 1: batching off --, batches of evaluate-only
+        rungs the last solve decided) (lh_debug_batch)."""
+        m, k = C.c_int(0), C.c_int(0)
+        _check(ba_lib().lh_debug_batch(self.h, C.byref(m), C.byref(k)), "lh_debug_batch")
+        return m.value, k.value
 
     def comm_count(self):
         """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""

@@ -758,6 +758,7 @@ def _eval_first_run(wargs, kw, env_off, monkeypatch):
 
 
 def test_trials_after_a_rejection_evaluate_first(monkeypatch):
+    monkeypatch.setenv("LH_NO_BATCH", "1")   # one trial per chain: the chain counts below (batches: the test after)
     for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
         full = _eval_first_run(wargs, kw, True, monkeypatch)
         ef = _eval_first_run(wargs, kw, False, monkeypatch)
@@ -790,6 +791,7 @@ def _relin_run(gen, opt, env, monkeypatch):
 def test_rejection_then_acceptance_relinearises(case, monkeypatch):
     from windows import RELIN_WINDOWS, relin_window
     kind, gen, opt, dec, ctrl = RELIN_WINDOWS[case]
+    monkeypatch.setenv("LH_NO_BATCH", "1")   # one trial per chain: the chain counts below (batches: test below)
     o = ob.solve(relin_window(gen), max_iters=3, **opt)
     assert (o["iterations"], o["trials"], o["accepted"]) == (3, len(dec), dec.count("A")), kind
     ef = _relin_run(gen, opt, {}, monkeypatch)
@@ -866,6 +868,74 @@ def test_lambda_ladder_is_bitwise_the_serial_chain(monkeypatch, eager):
             used.append((name, ctrl))
         assert skipped <= lad["trials"] - lad["accepted"], name
     assert len(used) >= 4, used
+
+
+# Batched rejection runs: after a rejection onto a built rung, one chain evaluates the rungs up
+# to the last built one (or the iteration's last trial) and k_reduce decides them in order; an acceptance among them
+# is re-run by the next chain as a full trial at that rung (lh_ctrl.retrial), whose decision commits it.  Every
+# rung is evaluated at its own step and lambda with the serial evaluate-only path's arithmetic and summation order,
+# so the solve must equal the one-rung-per-chain run (LH_NO_BATCH=1) bit for bit: the LM counts and trace, the
+# states, the per-edge rho0 "as last evaluated" (a rung buffer when the solve stops inside a batch) and the device
+# outlier pass on it; and the windows with rejection runs must have run batches (fewer chains).
+def _batch_run(w, kw, env, monkeypatch, th):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = lego_ba.Solver(**kw)
+    r = s.solve(w)
+    r["chains"], r["batch"] = s.chains(), s.batch()
+    o = s.solve(w, outlier_chi2_th=th)
+    r["is_outlier"], r["n_outlier"] = o["is_outlier"].copy(), o["n_outlier"]
+    s.close()
+    for k in env:
+        monkeypatch.delenv(k)
+    return r
+
+
+def _batch_windows():
+    from windows import RELIN_WINDOWS, relin_window, multi_camera
+    out = []
+    for name, wargs, kw, ctrl in EVAL_FIRST_CASES:
+        wa = dict(wargs)
+        cams = wa.pop("cams", 0)
+        w = window(wa.pop("cfg"), seed=wa.pop("seed")) if "cfg" in wa else lego_ba.generate_window(k=8, **wa)
+        if cams:
+            w = multi_camera(w, cams, seed=1)
+        out.append((name, w, kw, ctrl))
+    for kind, gen, opt, dec, ctrl in RELIN_WINDOWS:
+        out.append(("relin " + kind, relin_window(gen), dict(max_iters=3, **opt), ctrl))
+    # the bench's live configuration (a stalled solve ends every run of it with max_trials rejections)
+    out.append(("C3 live", window("C3", seed=0, family="default"), {}, "k_ctrl"))
+    return out
+
+
+@pytest.mark.parametrize("env", [{}, {"LH_BATCH_MAX": "3"}, {"LH_LADDER_LAZY": "1"}])
+def test_batched_rejection_runs_are_bitwise_the_serial_chain(monkeypatch, env):
+    batched = []
+    for name, w, kw, ctrl in _batch_windows():
+        th = 5.991
+        serial = _batch_run(w, kw, dict(env, LH_NO_BATCH="1"), monkeypatch, th)
+        bat = _batch_run(w, kw, env, monkeypatch, th)
+        assert serial["batch"][0] == 1, name
+        for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final", "chi2_initial", "pcg_iterations",
+                  "n_outlier"):
+            assert serial[k] == bat[k], (name, k)
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2", "trace_lambda", "is_outlier"):
+            assert np.array_equal(serial[k], bat[k]), (name, k)
+        bmax, nb = bat["batch"]
+        if ctrl in ("k_ctrl", "k_ctrl_b"):   # one rank, k_reduce decides
+            assert bmax == min(kw.get("max_trials", 10), int(env.get("LH_BATCH_MAX", 16))), name
+        else:
+            assert bmax == 1 and nb == 0, name
+        # a batch replaces its rungs' chains by one, plus the retrial of an acceptance that stopped the loop (where
+        # the serial run's accepted evaluate-only trial was its last chain)
+        if nb > 0:
+            batched.append(name)
+            assert bat["chains"] <= serial["chains"] + nb, (name, bat["chains"], serial["chains"], nb)
+        else:
+            assert bat["chains"] == serial["chains"], name
+        if name == "C3 live":
+            assert bat["chains"] < serial["chains"], (bat["chains"], serial["chains"])
+    assert "C3 live" in batched and len(batched) >= 8, batched
 
 
 # ---------------------------------------------------------------------------------------------
