@@ -755,43 +755,52 @@ __device__ __attribute__((noinline)) void lin_cand_tables(const double* __restri
 //      J_l^T W J_p dx (at the committed linearisation: pt the committed pose table, d the slot's step), summed over
 //      the landmark's lane group, then the landmark's update from its cached factor cl (VertexXYZ::add) and the
 //      lead lane's gain-scale term (isGoodStepInLM's scale) ----
+// (1) the edge's weight and Jacobians at the committed linearisation: pt the committed pose table, X the
+//     committed landmark (a live edge only)
 template <bool F32>
-__device__ __forceinline__ void lin_backsub(const double* __restrict__ pt, const double* __restrict__ e,
-                                            const double* __restrict__ d, bool live, bool ext_id, bool ext_rot, double u,
-                                            double v, int wfl, int lg, bool lmok, bool lead, const double (&cl)[12],
-                                            double lambda, const lh_params& prm, double (&X)[3], double& scale_acc) {
-    double v3[3] = {0.0, 0.0, 0.0};
-    if (live) {
-        EdgeEval E;
-        if constexpr (F32) {   // fp64 residual and weight (as below), fp32 Jacobians
-            if (wfl) {
-                E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
-            } else {
-                double Pc[3];
-                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                edge_robust(E, prm);
-            }
-            edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+__device__ __forceinline__ void backsub_jac(const double* __restrict__ pt, const double* __restrict__ e, bool ext_id,
+                                            bool ext_rot, double u, double v, int wfl, const double (&X)[3],
+                                            const lh_params& prm, EdgeEval& E) {
+    if constexpr (F32) {   // fp64 residual and weight (as below), fp32 Jacobians
+        if (wfl) {
+            E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
         } else {
             double Pc[3];
-            if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
-                E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
-                edge_pc(pt, e, ext_id, ext_rot, X, Pc);
-            } else {
-                edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                edge_robust(E, prm);
-            }
-            edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
+            edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+            edge_robust(E, prm);
         }
+        edge_eval_f<false, true>(pt, e, ext_id, ext_rot, X, u, v, prm, E);
+    } else {
+        double Pc[3];
+        if (wfl) {   // an inlier at the committed linearisation: W = I, no residual needed
+            E.W00 = 1.0; E.W01 = 0.0; E.W10 = 0.0; E.W11 = 1.0;
+            edge_pc(pt, e, ext_id, ext_rot, X, Pc);
+        } else {
+            edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
+            edge_robust(E, prm);
+        }
+        edge_jac_pc(Pc, pt + LH_PT_RT, e, ext_rot, prm, E.Jp, E.Jl);
+    }
+}
+// (2) the step d's term J_l^T W J_p d over the landmark's lane group, the landmark's update from its cached factor
+//     cl, and the lead lane's gain-scale term at lambda.  The multiply-adds are explicit fused ones: where the
+//     compiler contracts a * b + c * d it picks the product to fuse by the products' use counts, which depend on the
+//     code around the call, and the batch path (one Jacobian, several steps) and the trial path must round alike.
+//     The forms below are the ones the trial path was compiled to (the pre-split build's bits, scripts/lib_bitwise.py).
+__device__ __forceinline__ void backsub_apply(const EdgeEval& E, bool live, const double* __restrict__ d, int lg,
+                                              bool lmok, bool lead, const double (&cl)[12], double lambda,
+                                              const lh_params& prm, double (&X)[3], double& scale_acc) {
+    double v3[3] = {0.0, 0.0, 0.0};
+    if (live) {
         double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            if (!jz(0, a)) jd0 += E.Jp[a] * d[a];
-            if (!jz(1, a)) jd1 += E.Jp[6 + a] * d[a];
+            if (!jz(0, a)) jd0 = __builtin_fma(E.Jp[a], d[a], jd0);
+            if (!jz(1, a)) jd1 = __builtin_fma(E.Jp[6 + a], d[a], jd1);
         }
-        const double y0 = E.W00 * jd0 + E.W01 * jd1, y1 = E.W10 * jd0 + E.W11 * jd1;
+        const double y0 = __builtin_fma(E.W01, jd1, E.W00 * jd0), y1 = __builtin_fma(E.W11, jd1, E.W10 * jd0);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) v3[c] = E.Jl[c] * y0 + E.Jl[3 + c] * y1;
+        for (int c = 0; c < 3; ++c) v3[c] = __builtin_fma(E.Jl[c], y0, E.Jl[3 + c] * y1);
     }
     group_sum(v3, lg);
     const double s0 = v3[0], s1 = v3[1], s2 = v3[2];
@@ -800,18 +809,64 @@ __device__ __forceinline__ void lin_backsub(const double* __restrict__ pt, const
         const double i00 = cl[0], l10 = cl[1], i11 = cl[2], l20 = cl[3], l21 = cl[4], i22 = cl[5];
         const double b0 = cl[6], b1 = cl[7], b2 = cl[8];
         const double t0 = b0 - s0, t1 = b1 - s1, t2 = b2 - s2;
-        const double y0 = t0 * i00, y1 = (t1 - l10 * y0) * i11, y2 = (t2 - l20 * y0 - l21 * y1) * i22;
-        double d2 = y2 * i22, d1 = (y1 - l21 * d2) * i11, d0 = (y0 - l10 * d1 - l20 * d2) * i00;
+        const double y0 = t0 * i00, y1 = __builtin_fma(-l10, y0, t1) * i11;
+        const double y2 = __builtin_fma(-l21, y1, __builtin_fma(-l20, y0, t2)) * i22;
+        double d2 = y2 * i22, d1 = __builtin_fma(-l21, d2, y1) * i11;
+        double d0 = __builtin_fma(-l20, d2, __builtin_fma(-l10, d1, y0)) * i00;
         if (prm.guard && !(i00 == i00)) { d0 = d1 = d2 = 0.0; }   // skipped degenerate landmark
         double x0 = X[0], x1 = X[1], x2 = X[2];
         if (isfinite(d0) && isfinite(d1) && isfinite(d2)) { x0 += d0; x1 += d1; x2 += d2; }   // VertexXYZ::add
         if (lead) {
-            double sc;
-            if (prm.strategy == 0) sc = d0 * (lambda * d0 + b0) + d1 * (lambda * d1 + b1) + d2 * (lambda * d2 + b2);
-            else sc = d0 * (lambda * cl[9] * d0 + b0) + d1 * (lambda * cl[10] * d1 + b1) + d2 * (lambda * cl[11] * d2 + b2);
+            double q0, q1, q2;
+            if (prm.strategy == 0) {
+                q0 = __builtin_fma(lambda, d0, b0); q1 = __builtin_fma(lambda, d1, b1); q2 = __builtin_fma(lambda, d2, b2);
+            } else {
+                q0 = __builtin_fma(lambda * cl[9], d0, b0); q1 = __builtin_fma(lambda * cl[10], d1, b1);
+                q2 = __builtin_fma(lambda * cl[11], d2, b2);
+            }
+            const double sc = __builtin_fma(d2, q2, __builtin_fma(d0, q0, d1 * q1));
             scale_acc += sc;
         }
         X[0] = x0; X[1] = x1; X[2] = x2;
+    }
+}
+template <bool F32>
+__device__ __forceinline__ void lin_backsub(const double* __restrict__ pt, const double* __restrict__ e,
+                                            const double* __restrict__ d, bool live, bool ext_id, bool ext_rot, double u,
+                                            double v, int wfl, int lg, bool lmok, bool lead, const double (&cl)[12],
+                                            double lambda, const lh_params& prm, double (&X)[3], double& scale_acc) {
+    EdgeEval E;
+    if (live) backsub_jac<F32>(pt, e, ext_id, ext_rot, u, v, wfl, X, prm, E);
+    backsub_apply(E, live, d, lg, lmok, lead, cl, lambda, prm, X, scale_acc);
+}
+
+// A batch group's candidate pose tables (k_lin's batch path, all threads): item i < gn U is rung i / U's candidate
+// pose of slot i % U, from the committed pose pm (slot's pose cpose[slot]) and the rung's step (LDS wd + 6 U r),
+// staged in LDS cand; then item j < gn U ncam builds the table of (rung, slot, camera) into LDS tabs + per_tab r,
+// as k_lin's own candidate build does.  LDS operands as offsets into the dynamic LDS; out of line, so that its
+// registers are not the trial path's.
+__device__ __attribute__((noinline)) void lin_cand_batch(const double* __restrict__ pm, const uint16_t* __restrict__ cpose,
+                                                         int pmax1, int U, int ncam, int gn, int o_wd, int o_cand,
+                                                         int o_tabs, int per_tab, int o_wext) {
+    extern __shared__ __attribute__((aligned(16))) double dsm[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < gn * U; i += 256) {
+        const int r = i / U, sl = i - r * U;
+        const uint32_t pp = min((uint32_t)cpose[sl], (uint32_t)pmax1);
+        double pmc[12], To[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) pmc[k] = pm[pp * 12 + k];
+        d_pose_candidate(pmc, dsm + o_wd + 6 * U * r + 6 * sl, To);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) dsm[o_cand + 12 * i + k] = To[k];
+    }
+    lds_barrier();
+    for (int i = tid; i < gn * U * ncam; i += 256) {
+        const int r = i / (U * ncam), j = i - r * U * ncam, sl = j / ncam, c = j - sl * ncam;
+        double To[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) To[k] = dsm[o_cand + 12 * (r * U + sl) + k];
+        d_pose_table(To, dsm + o_wext + c * LH_EXT, dsm + o_tabs + per_tab * r + (sl * ncam + c) * LH_PT_LDS);
     }
 }
 
@@ -1026,29 +1081,51 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
         // ---- a batch: the evaluate-only trials of rungs lad .. lad + nbatch - 1 after a rejection,
         //      each evaluated as the evaluate-only path below evaluates one trial: the back substitution of the
         //      rung's step at the rung's lambda, the rung's candidate pose tables, rho0 per edge (edge_rho + r nslots)
-        //      and the chunk's chi2 and gain scale (csc + (r n_chunks + chunk) 4).  Nothing else is written: k_reduce
-        //      decides the rungs in order, and the next chain re-runs an accepted rung as a full trial. ----
-        double lam_r = lambda, ni_r = ctrl->ni;
-        const int umax1 = max(U - 1, 0);
-        const size_t dofs = 6 * (size_t)min((uint32_t)cpose[min(tid / 6, umax1)], (uint32_t)(prm.P - 1)) + (tid - 6 * (tid / 6));
-        double dv_n = dxp[(size_t)prm.n + dofs];   // rung lad + 1's step, in flight while rung lad is evaluated
-        for (int r = 0; r < nbatch; ++r) {
-            if (r > 0) {
-                // the rung's lambda: one more rejection's update (ctrl_lm_step, ladder_read's order)
-                if (prm.strategy == 0) { lam_r *= ni_r; ni_r *= 2.0; }
-                else lam_r = fmin(lam_r * 11.0, 1e7);
-                lds_barrier();   // every wave is done with the previous rung's step, tables and combine
-                if (tid < 6 * U) wdx[tid] = dv_n;
-                if (tid == 0) *cflag = 0;
-                dv_n = dxp[(size_t)min(r + 1, nbatch - 1) * prm.n + dofs];
-                lds_barrier();
+        //      and the chunk's chi2 and gain scale (csc + (r n_chunks + chunk) 4).  The rungs of a group share one
+        //      pass over the chunk's sub-batches: an edge's weight and Jacobians at the committed state are computed
+        //      once, then each rung's step is applied and its candidate evaluated.  Each lane's chi2 and scale sums
+        //      per rung stay in LDS (the same per-lane order as the single-trial path).  Nothing else is written:
+        //      k_reduce decides the rungs in order, and the next chain re-runs an accepted rung as a full trial.
+        //      LDS: the trial path's wave scratch [0, 4 SCR), free here: record stages, rung lambdas, the combine's
+        //      wave totals, then per rung of a group: the lanes' sums, candidate tables, step, candidate poses. ----
+        double* stg = dsm + wave * (8 * LH_REC_LDS);               // this wave's landmark-record stage
+        double* lam_l = dsm + LH_WAVES * 8 * LH_REC_LDS;           // [LH_LAD] the rungs' lambdas
+        double* wtot = lam_l + LH_LAD;                             // [LH_LAD][LH_WAVES][2] wave totals
+        double* gbase = wtot + LH_LAD * LH_WAVES * 2;
+        const int per_tab = U * ncam * LH_PT_LDS;
+        const int per_rung = 2 * LH_WAVES * 64 + per_tab + 6 * U + 12 * U;
+        const int avail = LH_WAVES * Cfg::SCR - (int)(gbase - dsm);
+        static_assert(LH_WAVES * Cfg::SCR - (LH_WAVES * 8 * LH_REC_LDS + LH_LAD + LH_LAD * LH_WAVES * 2) >=
+                          2 * LH_WAVES * 64 + Cfg::UMAX * 4 * LH_PT_LDS + 18 * Cfg::UMAX,
+                      "a batch group of one rung (4 cameras) fits the wave scratch");
+        const int G = max(1, min(nbatch, avail / per_rung));      // rungs per group
+        double* acc_c = gbase;                                     // [G][LH_WAVES][64] chi2 per lane
+        double* acc_s = acc_c + G * LH_WAVES * 64;                 // [G][LH_WAVES][64] gain scale per lane
+        double* tabs = acc_s + G * LH_WAVES * 64;                  // [G][per_tab] candidate tables
+        double* wd = tabs + G * per_tab;                           // [G][6 U] steps
+        double* cand = wd + G * 6 * U;                             // [G][U][12] candidate poses
+        if (tid == 0) {   // rung r's lambda: r more rejections' updates (ctrl_lm_step, ladder_read's order)
+            double lam = lambda, ni = ctrl->ni;
+            for (int r = 0; r < nbatch; ++r) {
+                if (r > 0) {
+                    if (prm.strategy == 0) { lam *= ni; ni *= 2.0; }
+                    else lam = fmin(lam * 11.0, 1e7);
+                }
+                lam_l[r] = lam;
             }
-            // the rung's candidate pose tables (k_lin's build below, out of line)
-            if (wave == cwave) lin_cand_tables(pose_mat + (size_t)cur * prm.P * 12, cpose, prm.P - 1, U, ncam,
-                                               (int)(wdx - dsm), (int)(wext - dsm), (int)(wt_n - dsm), (int)(scr - dsm),
-                                               (int)(reinterpret_cast<double*>(cflag) - dsm));
-            bool ready = false;
-            double chi_b = 0.0, scale_b = 0.0;
+        }
+        for (int g0 = 0; g0 < nbatch; g0 += G) {
+            const int gn = min(G, nbatch - g0);
+            lds_barrier();   // (the previous group's combine is done with the LDS)
+            for (int i = tid; i < gn * 6 * U; i += 256) {
+                const int r = i / (6 * U), k = i - r * 6 * U;
+                wd[i] = dxp[(size_t)(g0 + r) * prm.n + 6 * (size_t)min((uint32_t)cpose[k / 6], (uint32_t)(prm.P - 1)) + k % 6];
+            }
+            for (int i = tid; i < gn * LH_WAVES * 64; i += 256) { acc_c[i] = 0.0; acc_s[i] = 0.0; }
+            lds_barrier();
+            lin_cand_batch(pose_mat + (size_t)cur * prm.P * 12, cpose, prm.P - 1, U, ncam, gn, (int)(wd - dsm),
+                           (int)(cand - dsm), (int)(tabs - dsm), per_tab, (int)(wext - dsm));
+            lds_barrier();
             for (int sbi = (int)sb_begin + wave; sbi < (int)sb_end; sbi += LH_WAVES) {
                 const lh_subbatch S = S_n;
                 const int lg = S.lg, nlm = S.n_lm;
@@ -1060,7 +1137,7 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
                 const double2 rr = r_n;
                 const int wfl = wfl_n;
                 const int o = sbi * 64 + lane;
-                {   // the next sub-batch's words: after the wave's last one, its first again (the next rung's)
+                {   // the next sub-batch's words: after the wave's last one, its first again (the next group's)
                     const int sbw = sbi + LH_WAVES < (int)sb_end ? sbi + LH_WAVES : (int)sb_begin + wave;
                     const int sbn = min(sbw, sb_last);
                     const int on = sbn * 64 + lane;
@@ -1072,10 +1149,10 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
                     v_n = (double)z.y;
                     r_n = rec_piece(sbn);
                 }
-                reinterpret_cast<double2*>(scr)[(lane >> 3) * (LH_REC_LDS / 2) + (lane & 7)] = rr;
+                reinterpret_cast<double2*>(stg)[(lane >> 3) * (LH_REC_LDS / 2) + (lane & 7)] = rr;
                 wave_sync();
-                const double* myrec = scr + (ls & 7) * LH_REC_LDS;
-                double X[3] = {myrec[LH_REC_X], myrec[LH_REC_X + 1], myrec[LH_REC_X + 2]};
+                const double* myrec = stg + (ls & 7) * LH_REC_LDS;
+                const double X[3] = {myrec[LH_REC_X], myrec[LH_REC_X + 1], myrec[LH_REC_X + 2]};
                 double cl[12];
 #pragma unroll
                 for (int i = 0; i < 12; ++i) cl[i] = myrec[LH_REC_L + i];
@@ -1087,39 +1164,40 @@ __global__ __launch_bounds__(256, (T <= 3) ? LH_LIN_OCC : 1) void k_lin(
                 const double* e = wext + cam * LH_EXT;
                 const bool ext_id = (prm.ext_identity >> cam) & 1;
                 const bool ext_rot = (prm.ext_rot_identity >> cam) & 1;
-                lin_backsub<F32>(wt_c + (slot * ncam + cam) * LH_PT_LDS, e, wdx + 6 * slot, live, ext_id, ext_rot, u, v,
-                                 wfl, lg, lmok, lead, cl, lam_r, prm, X, scale_b);
-                if (!ready) {
-                    while (__hip_atomic_load(cflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
-                    ready = true;
-                }
-                if (has) {
-                    const double* pt = wt_n + (slot * ncam + cam) * LH_PT_LDS;
-                    EdgeEval E;
-                    double Pc[3];
-                    edge_residual(pt, e, ext_id, ext_rot, X, u, v, prm, E.r0, E.r1, Pc);
-                    edge_robust(E, prm);
-                    st_out(edge_rho + (size_t)r * nslots + o, E.rho0);
-                    chi_b += E.rho0;
+                EdgeEval E;
+                if (live) backsub_jac<F32>(wt_c + (slot * ncam + cam) * LH_PT_LDS, e, ext_id, ext_rot, u, v, wfl, X, prm, E);
+                for (int r = 0; r < gn; ++r) {
+                    double Xr[3] = {X[0], X[1], X[2]};
+                    const int ai = (r * LH_WAVES + wave) * 64 + lane;
+                    double sa = acc_s[ai];
+                    backsub_apply(E, live, wd + r * 6 * U + 6 * slot, lg, lmok, lead, cl, lam_l[g0 + r], prm, Xr, sa);
+                    acc_s[ai] = sa;
+                    if (has) {
+                        const double* pt = tabs + r * per_tab + (slot * ncam + cam) * LH_PT_LDS;
+                        EdgeEval Ec;
+                        double Pc[3];
+                        edge_residual(pt, e, ext_id, ext_rot, Xr, u, v, prm, Ec.r0, Ec.r1, Pc);
+                        edge_robust(Ec, prm);
+                        st_out(edge_rho + (size_t)(g0 + r) * nslots + o, Ec.rho0);
+                        acc_c[ai] = acc_c[ai] + Ec.rho0;
+                    }
                 }
             }
-            {   // the wave's totals and the 4-wave combine, as the evaluate-only epilogue below
-                double t3[3] = {chi_b, scale_b, 0.0};
+            // each rung's wave totals (the single-trial path's butterflies), then its chunk scalars in that path's
+            // combine order, (w0 + w2) + (w1 + w3)
+            for (int r = 0; r < gn; ++r) {
+                const int ai = (r * LH_WAVES + wave) * 64 + lane;
+                double t3[3] = {acc_c[ai], acc_s[ai], 0.0};
                 group_sum(t3, 6);
-                chi_b = t3[0]; scale_b = t3[1];
+                if (lane == 0) { wtot[(r * LH_WAVES + wave) * 2] = t3[0]; wtot[(r * LH_WAVES + wave) * 2 + 1] = t3[1]; }
             }
             lds_barrier();
-            for (int phase = 0; phase < 2; ++phase) {
-                if ((wave >> 1) == phase && lane == 0) {
-                    double* sc = dsm + (wave & 1) * 2;
-                    if (phase == 0) { sc[0] = chi_b; sc[1] = scale_b; }
-                    else { sc[0] += chi_b; sc[1] += scale_b; }
-                }
-                lds_barrier();
+            for (int i = tid; i < gn * 4; i += 256) {
+                const int r = i >> 2, k = i & 3;
+                const double* wt = wtot + r * LH_WAVES * 2;
+                csc[((size_t)(g0 + r) * prm.n_chunks + chunk) * 4 + k] =
+                    k < 2 ? (wt[0 * 2 + k] + wt[2 * 2 + k]) + (wt[1 * 2 + k] + wt[3 * 2 + k]) : 0.0;
             }
-            double* gs = csc + ((size_t)r * prm.n_chunks + chunk) * 4;
-            if (tid < 2) gs[tid] = dsm[tid] + dsm[2 + tid];
-            if (tid == 2 || tid == 3) gs[tid] = 0.0;
         }
         return;
     }
