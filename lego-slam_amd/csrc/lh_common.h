@@ -94,7 +94,7 @@ struct lh_subbatch {
 
 // reduced-system buffer layout (one per state buffer)
 struct lh_rs_layout {
-    int npairs, off_S, off_bs, off_bp, off_hd, off_sc, total;
+    int npairs, off_S, off_bs, off_bp, off_hd, off_sc, off_bsc, total;
 };
 
 // npairs: the blocks of S (every pose pair up to LH_PMAX_WIN poses, P (P + 1) / 2; past it the pairs
@@ -107,7 +107,10 @@ LH_HD static inline lh_rs_layout lh_rs_make(int P, int npairs) {
     L.off_bp = L.off_bs + 6 * P;
     L.off_hd = L.off_bp + 6 * P;
     L.off_sc = L.off_hd + 6 * P;
-    L.total = L.off_sc + 8;
+    // a batch's per-rung chi2 and gain scale, last: in the same chunk of a ring all-reduce as the
+    // single-trial scalars, so they are summed over the ranks in the same order
+    L.off_bsc = L.off_sc + 8;
+    L.total = L.off_bsc + 2 * LH_LAD;
     return L;
 }
 

@@ -774,10 +774,10 @@ int upload_body(lh_handle* h, const lh_window* w, bool sync) {
         h->band_narrow = narrow;
     }
     if (P > LH_PMAX_WIN && h->opt.linear_solver == LH_SOLVER_LDLT && !h->band) return LH_E_UNSUPPORTED;
-    // batches of evaluate-only rungs (one rank, k_reduce's decision; LH_NO_BATCH=1: one rung per
-    // chain, the A/B switch; LH_BATCH_MAX caps the rungs per batch): per rung a per-edge rho0 and the chunk scalars
+    // batches of evaluate-only rungs (every controller, one rank or sharded; LH_NO_BATCH=1: one rung
+    // per chain, the A/B switch; LH_BATCH_MAX caps the rungs per batch): per rung a per-edge rho0 and the chunk scalars
     const bool dec1 = (P <= LH_PMAX || h->band) && h->opt.world_size == 1 && !h->comm;
-    int batch = (dec1 && ladder > 1 && !getenv("LH_NO_BATCH")) ? ladder : 1;
+    int batch = (ladder > 1 && !getenv("LH_NO_BATCH")) ? ladder : 1;
     if (const char* bm = getenv("LH_BATCH_MAX")) batch = std::max(1, std::min(batch, atoi(bm)));
     HIPCHK(h->d_rho.ensure((size_t)batch * pl.n_slots));
     HIPCHK(h->d_csc.ensure((size_t)batch * pl.n_chunks * 4));

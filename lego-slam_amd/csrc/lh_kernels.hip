@@ -1821,6 +1821,65 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
     return relin | lskip | (retrial != 0 ? 1 : 0);
 }
 
+// A batch's decisions, thread 0 of the deciding kernel (k_reduce with one rank, else the
+// controller after the exchange): rung r's chi2 (not halved) and gain scale at sc[2 r], sc[2 r + 1] (summed over
+// the chunks, and over the ranks when sharded, as a single trial's are), decided in order until an acceptance
+// (retrial), the stop, or a next trial that is not the batch's next rung.  bw holds the words batch_load read.
+// Stores the words once, the rung whose rho0 is "as last evaluated", and the host word (raise_done: publish the
+// stop here, else the chain's controller does).  Returns nothing-to-factor, with ctrl_lm_step's outputs.
+__device__ __forceinline__ int ctrl_batch_decide(lh_ctrl* __restrict__ ctrl, BatchWords& bw, const lh_params& prm,
+                                                 const double* sc, int nb, volatile int* __restrict__ host_done, int seq,
+                                                 bool raise_done, int& done_o, int& accept_o, int& cur_o, double& lam_o) {
+    int r = 0;
+    for (;; ++r) {
+        int d_o, a_o, c_o;
+        double l_o;
+        ctrl_lm_step(ctrl, bw.w, prm, 1, 0.0, 0.5 * sc[2 * r], sc[2 * r + 1], 0.0, host_done, seq, d_o, a_o, c_o, l_o,
+                     false, &bw);
+        const CtrlWords& w = bw.w;
+        if (r + 1 >= nb || w.done || w.retrial || !w.evo || !bw.cnt[BW_LSKIP]) break;
+    }
+    const CtrlWords& w = bw.w;
+    batch_store(ctrl, bw, seq);
+    ctrl->rho_sel = r;   // the per-edge rho0 of the last rung decided
+    ctrl->nbatches += 1;
+    if (host_done) {
+        if (w.done) {
+            ctrl->done_seq = seq;
+            if (raise_done) publish_stop(ctrl, host_done);   // else this chain's controller publishes it
+        } else {
+            ctrl_progress(prm, host_done, seq, w.iter, w.fc, w.last, w.chi, w.retrial == 2 ? 1 : 0);
+        }
+    }
+    done_o = w.done;
+    accept_o = 0;
+    cur_o = w.cur;
+    lam_o = w.lam;
+    return w.relin | bw.cnt[BW_LSKIP] | (w.retrial != 0 ? 1 : 0);
+}
+// a self-deciding controller's decision (thread 0): a batch's (this chain's evo word above its low byte, the
+// rungs' scalars behind the exchanged system, lh_rs_layout.off_bsc) or one trial's
+__device__ __forceinline__ int ctrl_decide(lh_ctrl* __restrict__ ctrl, const CtrlWords& cw, const lh_params& prm, int mode,
+                                           double mdiag, double tchi, double sl, double ndg, const double* rs_stage,
+                                           const lh_rs_layout& LY, volatile int* __restrict__ host_done, int seq,
+                                           int& done_o, int& accept_o, int& cur_o, double& lam_o, int* cnt) {
+    const int nb = cw.evo >> 8;   // (cw.evo: this chain's evo word, read before its decision)
+    if (mode != 0 && nb > 1) {
+        BatchWords bw;
+        bw.w = cw;
+        bw.sp = ctrl->spose_l;   // (global: one load per rung)
+        bw.lad_its = ctrl->lad_its;
+        bw.cnt = cnt;
+        cnt[BW_LSKIPS] = ctrl->lskips;
+        cnt[BW_PCG] = ctrl->pcg_iters;
+        cnt[BW_LSKIP] = 0;
+        cnt[BW_NBATCH] = 1;
+        return ctrl_batch_decide(ctrl, bw, prm, rs_stage + LY.off_bsc, nb, host_done, seq, true, done_o, accept_o, cur_o,
+                                 lam_o);
+    }
+    return ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done_o, accept_o, cur_o, lam_o);
+}
+
 // ---- the lambda ladder's rung workgroups (lh_ctrl.lad) ----
 // Workgroup 0 of a controller that takes the LM decision itself (the initial linearisation, sharded solves,
 // k_ctrl_g, k_ctrl_p) publishes it: ctrl_lm_step's words, then dec_tag = seq + 1 (release).  Its rung workgroups
@@ -1986,42 +2045,27 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                         if (2 * g + j < 2 * nb) part[0][wave][2 * g + j] = b[j];
             }
             lds_barrier();
-            // each rung's totals over the waves, in wave order, by one thread per rung
+            // each rung's totals over the waves, in wave order, by one thread per rung: into LDS for the decisions
+            // here (one rank), and behind the system (off_bsc) for the exchange and a controller that decides
             __shared__ double b_a[2 * LH_LAD];
             if (tid < nb) {
                 double a0 = 0.0, a1 = 0.0;
                 for (int wv = 0; wv < RW; ++wv) { a0 += part[0][wv][2 * tid]; a1 += part[0][wv][2 * tid + 1]; }
                 b_a[2 * tid] = a0;
                 b_a[2 * tid + 1] = a1;
+                rs[LY.off_bsc + 2 * tid] = a0;
+                rs[LY.off_bsc + 2 * tid + 1] = a1;
+            }
+            if (tid == 0) {
+                rs[LY.off_sc + LH_SC_CHI2] = 0.0; rs[LY.off_sc + LH_SC_SCALE] = 0.0;
+                rs[LY.off_sc + LH_SC_NDEG] = 0.0; rs[LY.off_sc + LH_SC_MAXD] = 0.0;
+                *maxd_out = 0.0;
             }
             lds_barrier();
-            if (tid == 0) {
-                // the rungs' decisions in order, each the one the serial chain of that trial takes; the batch ends
-                // at an acceptance (retrial), the stop, or a next trial that is not the batch's next rung
-                double a0 = 0.0, a1 = 0.0;
-                int r = 0;
-                for (;; ++r) {
-                    a0 = b_a[2 * r];
-                    a1 = b_a[2 * r + 1];
-                    int d_o, a_o, c_o;
-                    double l_o;
-                    ctrl_lm_step(ctrl, bw0.w, prm, 1, 0.0, 0.5 * a0, a1, 0.0, host_done, seq, d_o, a_o, c_o, l_o, false, &bw0);
-                    const CtrlWords& w = bw0.w;
-                    if (r + 1 >= nb || w.done || w.retrial || !w.evo || !b_cnt[BW_LSKIP]) break;
-                }
-                const CtrlWords& w = bw0.w;
-                batch_store(ctrl, bw0, seq);
-                ctrl->rho_sel = r;   // the per-edge rho0 of the last rung decided
-                ctrl->nbatches += 1;
-                rs[LY.off_sc + LH_SC_CHI2] = a0;
-                rs[LY.off_sc + LH_SC_SCALE] = a1;
-                rs[LY.off_sc + LH_SC_NDEG] = 0.0;
-                rs[LY.off_sc + LH_SC_MAXD] = 0.0;
-                *maxd_out = 0.0;
-                if (host_done) {
-                    if (w.done) ctrl->done_seq = seq;   // this chain's controller publishes the stop
-                    else ctrl_progress(prm, host_done, seq, w.iter, w.fc, w.last, w.chi, w.retrial == 2 ? 1 : 0);
-                }
+            if (prm.dec_in_reduce && tid == 0) {
+                int d_o, a_o, c_o;
+                double l_o;
+                ctrl_batch_decide(ctrl, bw0, prm, b_a, nb, host_done, seq, false, d_o, a_o, c_o, l_o);
             }
             return;
         }
@@ -3179,7 +3223,9 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             }
             int d_o, a_o, c_o;
             double lam_n;
-            s_flags[2] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            __shared__ int b_cnt[4];
+            s_flags[2] = ctrl_decide(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, rs_stage, LY, host_done, seq, d_o, a_o, c_o,
+                                     lam_n, b_cnt);
             if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
             s_flags[0] = d_o;
             s_flags[1] = a_o;
@@ -3661,7 +3707,9 @@ __global__ __launch_bounds__(GT) void k_ctrl_g(lh_ctrl* __restrict__ ctrl, doubl
         }
         int done, accept, cur;
         double lam_n;
-        s_flags[3] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        __shared__ int b_cnt[4];
+        s_flags[3] = ctrl_decide(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, rs_stage, LY, host_done, seq, done, accept, cur,
+                                 lam_n, b_cnt);
         if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
         s_flags[0] = done;
         s_flags[1] = accept;
@@ -3887,7 +3935,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_b(lh_ctrl* __restrict__ ctrl, const
             }
             int d_o, a_o, c_o;
             double lam_n;
-            s_flags[2] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
+            __shared__ int b_cnt[4];
+            s_flags[2] = ctrl_decide(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, rs_stage, LY, host_done, seq, d_o, a_o, c_o,
+                                     lam_n, b_cnt);
             if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
             s_flags[0] = d_o;
             s_flags[1] = a_o;
@@ -4414,7 +4464,9 @@ __global__ __launch_bounds__(CT) void k_ctrl_p(lh_ctrl* __restrict__ ctrl, doubl
         }
         int done, accept, cur;
         double lam_n;
-        s_flags[3] = ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done, accept, cur, lam_n);
+        __shared__ int b_cnt[4];
+        s_flags[3] = ctrl_decide(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, rs_stage, LY, host_done, seq, done, accept, cur,
+                                 lam_n, b_cnt);
         if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
         s_flags[0] = done;
         s_flags[1] = accept;

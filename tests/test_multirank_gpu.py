@@ -63,6 +63,7 @@ def _rank_main(rank, world, rdzv, cfg, seed, family, opts, q):
             return
         r["exchanges"] = s.comm_count()
         r["chains"] = s.chains()
+        r["batch"] = s.batch()
         r["controller"] = s.controller()
         r["status"] = 0
         s.close()
@@ -127,7 +128,7 @@ def test_two_rank_sharded_solve_matches_one_rank(cfg, seed, family):
     # identical controller on both ranks: same trajectory, bit-identical poses
     assert (a["iterations"], a["trials"]) == (b["iterations"], b["trials"])
     assert a["chi2_final"] == b["chi2_final"] and np.array_equal(a["pose_Tcw"], b["pose_Tcw"])
-    assert a["exchanges"] == b["exchanges"] == a["chains"] + 1 and a["chains"] >= a["trials"]
+    assert a["exchanges"] == b["exchanges"] == a["chains"] + 1 and a["chains"] + 15 * a["batch"][1] >= a["trials"]
     # = the one-rank solve of the whole window, to summation order
     assert a["iterations"] == one["iterations"] and a["trials"] == one["trials"]
     assert rel(a["chi2_initial"], one["chi2_initial"]) < 1e-12
@@ -183,7 +184,7 @@ def test_c4_sharded_solve_matches_oracle_and_one_rank(c4_gate1, world):
         assert (a["iterations"], a["trials"], a["chi2_final"]) == (b["iterations"], b["trials"], b["chi2_final"])
         assert np.array_equal(a["pose_Tcw"], b["pose_Tcw"])
         assert np.array_equal(a["trace_chi2"], b["trace_chi2"]) and np.array_equal(a["trace_lambda"], b["trace_lambda"])
-        assert b["exchanges"] == a["exchanges"] == a["chains"] + 1 and a["chains"] >= a["trials"]
+        assert b["exchanges"] == a["exchanges"] == a["chains"] + 1 and a["chains"] + 15 * a["batch"][1] >= a["trials"]
     lm = np.vstack([out[r]["lm_xyz"] for r in range(world)])
     rho = np.concatenate([out[r]["edge_robust_chi2"] for r in range(world)])
     assert lm.shape == w["lm_xyz"].shape
@@ -293,7 +294,7 @@ def test_sharded_lambda_ladder_is_bitwise_the_serial_chain(case):
     _, gen, opt, _, _ = RELIN_WINDOWS[case]
     gen = dict(gen)
     seed = gen.pop("seed")
-    lad = run_sharded(gen, seed, None, max_iters=3, **opt)
+    lad = run_sharded(gen, seed, None, max_iters=3, env={"LH_NO_BATCH": "1"}, **opt)
     one = run_sharded(gen, seed, None, max_iters=3, env={"LH_NO_LADDER": "1"}, **opt)
     for r in (0, 1):
         a, b = lad[r], one[r]
@@ -302,6 +303,17 @@ def test_sharded_lambda_ladder_is_bitwise_the_serial_chain(case):
         for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2"):
             assert np.array_equal(a[k], b[k]), (r, k)
     assert lad[0]["trials"] > lad[0]["accepted"]   # the windows reject (so rungs are used)
+    # and batched (the default): the rungs' scalars ride behind the exchanged system and the
+    # controller decides the batch after the exchange: the same solve bit for bit, in fewer chains (exchanges)
+    bat = run_sharded(gen, seed, None, max_iters=3, **opt)
+    for r in (0, 1):
+        a, b = bat[r], one[r]
+        for k in ("iterations", "trials", "accepted", "chi2_final", "lambda_final"):
+            assert a[k] == b[k], (r, k)
+        for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2"):
+            assert np.array_equal(a[k], b[k]), (r, k)
+        assert a["batch"][0] == 10 and a["batch"][1] > 0, (r, a["batch"])
+        assert a["exchanges"] == a["chains"] + 1 and a["chains"] < b["chains"], (r, a["chains"], b["chains"])
 
 
 @pytest.mark.parametrize("cfg,seed,family", [("C2", 0, "stable_noout"), ("mini", 2, "default")])
@@ -366,7 +378,7 @@ def test_two_rank_sharded_banded_ldlt(P, L, seed):
     assert a["controller"] == b["controller"] == "k_ctrl_b"
     assert (a["iterations"], a["trials"]) == (b["iterations"], b["trials"])
     assert a["chi2_final"] == b["chi2_final"] and np.array_equal(a["pose_Tcw"], b["pose_Tcw"])
-    assert a["exchanges"] == b["exchanges"] == a["chains"] + 1 and a["chains"] >= a["trials"]
+    assert a["exchanges"] == b["exchanges"] == a["chains"] + 1 and a["chains"] + 15 * a["batch"][1] >= a["trials"]
     assert (a["iterations"], a["trials"]) == (one["iterations"], one["trials"])
     assert rel(a["chi2_final"], one["chi2_final"]) < 1e-9
     assert np.allclose(a["pose_Tcw"], one["pose_Tcw"], atol=1e-9)
