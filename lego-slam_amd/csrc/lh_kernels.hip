@@ -1830,7 +1830,35 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
 __device__ __forceinline__ int ctrl_batch_decide(lh_ctrl* __restrict__ ctrl, BatchWords& bw, const lh_params& prm,
                                                  const double* sc, int nb, volatile int* __restrict__ host_done, int seq,
                                                  bool raise_done, int& done_o, int& accept_o, int& cur_o, double& lam_o) {
+    // The rungs before the first that will be accepted (or the last) are plain rejections: each only advances
+    // lambda and nu, the counts and the rung (ctrl_lm_step's rejection, which moves onto a built rung and, before
+    // the batch's last rung, never ends the iteration: nbatch <= max_trials - false_cnt).  Their gain ratios are
+    // independent (chi2 does not change across rejections), so they are found first and skipped forward with
+    // that arithmetic; ctrl_lm_step takes the decisive rung.
     int r = 0;
+    {
+        CtrlWords& w = bw.w;
+        const double chi = w.chi;
+        int j = nb - 1;
+        for (int q = 0; q < nb - 1; ++q) {
+            double scale = 0.5 * (bw.sp[w.lad + q] + sc[2 * q + 1]);
+            scale += 1e-10;
+            const double tchi = 0.5 * sc[2 * q];
+            const double rho = (chi - tchi) / scale;
+            if (rho > 0 && isfinite(tchi)) { j = q; break; }
+        }
+        for (; r < j; ++r) {   // rung r rejected: the decision ctrl_lm_step takes for it, in its order
+            if (prm.strategy == 0) { w.lam *= w.ni; w.ni *= 2; }
+            else w.lam = fmin(w.lam * 11.0, 1e7);
+            w.trials += 1;
+            w.fc += 1;
+            w.lad += 1;
+            bw.cnt[BW_LSKIPS] += 1;
+            if (prm.solver == 1) bw.cnt[BW_PCG] += bw.lad_its[w.lad];
+        }
+        w.spose = bw.sp[w.lad];
+        bw.cnt[BW_LSKIP] = r > 0 ? 1 : bw.cnt[BW_LSKIP];
+    }
     for (;; ++r) {
         int d_o, a_o, c_o;
         double l_o;
@@ -2025,14 +2053,15 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
         }
         if (nb > 1) {
             // each rung's chi2 and gain-scale sums in the order below (thread, lane butterfly, waves in order):
-            // eight rungs per round of loads, the butterflies in VALU (wave_sum_desc)
-            for (int g = 0; g < nb; g += 8) {
-                double b[16];
+            // ten rungs (a default ladder's batch) per round of loads, the butterflies in VALU (wave_sum_desc)
+            constexpr int BG = 10;
+            for (int g = 0; g < nb; g += BG) {
+                double b[2 * BG];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) b[j] = 0.0;
+                for (int j = 0; j < 2 * BG; ++j) b[j] = 0.0;
                 for (int c = tid; c < n_chunks; c += RT) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j)
+                    for (int j = 0; j < BG; ++j)
                         if (g + j < nb) {
                             const double* sc = csc + ((size_t)(g + j) * n_chunks + c) * 4;
                             b[2 * j] += sc[0]; b[2 * j + 1] += sc[1];
@@ -2041,7 +2070,7 @@ __global__ __launch_bounds__(RT) void k_reduce(const double* __restrict__ rows, 
                 wave_sum_desc(b);
                 if (lane == 0)
 #pragma unroll
-                    for (int j = 0; j < 16; ++j)
+                    for (int j = 0; j < 2 * BG; ++j)
                         if (2 * g + j < 2 * nb) part[0][wave][2 * g + j] = b[j];
             }
             lds_barrier();
