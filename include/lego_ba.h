@@ -336,9 +336,10 @@ int lh_debug_chains(lh_handle *h, int *chains);
 int lh_debug_ladder(lh_handle *h, int *rungs, int *skipped);
 
 /* batched evaluation of rejection runs: the most rungs one chain of the uploaded window evaluates
-   (1: off -- sharded solves, LH_NO_BATCH=1), and the batches the last solve decided.  Solves that return arrays
-   only (else batches = -1). */
-int lh_debug_batch(lh_handle *h, int *batch_max, int *batches);
+   (1: off -- LH_NO_BATCH=1, or a ladder of one rung), the batches the last solve decided, and (retrials, two ints,
+   may be NULL) the acceptances among them: [0] re-run by the next chain as a full trial, [1] re-run and stopping
+   the loop.  Solves that return arrays only (else -1). */
+int lh_debug_batch(lh_handle *h, int *batch_max, int *batches, int *retrials);
 
 #ifdef __cplusplus
 }

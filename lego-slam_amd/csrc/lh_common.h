@@ -146,6 +146,7 @@ struct lh_ctrl {
     int32_t retrial;           // the next chain re-runs the accepted rung as a full trial; its decision only commits
     int32_t rho_sel;           // per-edge rho0 "as last evaluated": rung buffer (0: the ordinary one)
     int32_t nbatches;          // batches decided in this solve (lh_debug_batch)
+    int32_t nretrials[2];      // their acceptances: [0] re-run as a full trial, [1] that also stopped the loop
     int32_t nofactor;          // the last decision left nothing to factor (relin | lskip | retrial: ladder_read's one word)
     int32_t lad_its[LH_LAD];   // PCG iterations of each rung's solve (counted when the rung is used)
     double spose_l[LH_LAD];    // pose part of each rung's gain denominator (isGoodStepInLM's scale)

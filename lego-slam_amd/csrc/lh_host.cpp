@@ -333,6 +333,7 @@ struct lh_handle {
     int last_chains = -1;        // lh_debug_chains: the last synchronous solve's stop chain
     int last_lskips = -1;        // lh_debug_ladder: its rejections onto a built ladder rung
     int last_batches = -1;       // lh_debug_batch: its batches of evaluate-only rungs
+    int last_retrials[2] = {-1, -1};   // lh_debug_batch: their acceptances (re-run; re-run and stopping)
     size_t rho_off = 0;          // the last solve's per-edge rho0 "as last evaluated": its rung buffer in d_rho (a batch)
     int* h_done = nullptr;       // pinned, mapped lh_host_words: [0] k_ctrl raises it when the LM loop stops, [1] progress
                                  // word 2 * (last live trial) + (one iteration from max_iters)
@@ -1253,6 +1254,8 @@ int solve_resident_impl(lh_handle* h, lh_result* out) {
     const int cur = c.cur;
     h->rho_off = (size_t)c.rho_sel * h->n_slots;
     h->last_batches = c.nbatches;
+    h->last_retrials[0] = c.nretrials[0];
+    h->last_retrials[1] = c.nretrials[1];
     h->last_chains = c.seq_last;
     h->last_lskips = c.lskips;
 
@@ -1948,11 +1951,12 @@ int lh_debug_ladder(lh_handle* h, int* rungs, int* skipped) {
     return LH_OK;
 }
 
-int lh_debug_batch(lh_handle* h, int* batch_max, int* batches) {
+int lh_debug_batch(lh_handle* h, int* batch_max, int* batches, int* retrials) {
     if (!h || !batch_max || !batches) return LH_E_BADARG;
     if (!h->uploaded) return LH_E_STATE;
     *batch_max = h->prm.batch;
     *batches = h->last_batches;
+    if (retrials) { retrials[0] = h->last_retrials[0]; retrials[1] = h->last_retrials[1]; }
     return LH_OK;
 }
 

@@ -1871,6 +1871,7 @@ __device__ __forceinline__ int ctrl_batch_decide(lh_ctrl* __restrict__ ctrl, Bat
     batch_store(ctrl, bw, seq);
     ctrl->rho_sel = r;   // the per-edge rho0 of the last rung decided
     ctrl->nbatches += 1;
+    if (w.retrial) ctrl->nretrials[w.retrial - 1] += 1;
     if (host_done) {
         if (w.done) {
             ctrl->done_seq = seq;

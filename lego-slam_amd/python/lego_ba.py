@@ -247,7 +247,7 @@ def ba_lib():
         lib.lh_debug_chains.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         lib.lh_debug_ladder.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         if hasattr(lib, "lh_debug_batch"):   # (an older library of an A/B run lacks it)
-            lib.lh_debug_batch.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+            lib.lh_debug_batch.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _balib = lib
     return _balib
 
@@ -533,9 +533,13 @@ class Solver:
     def batch(self):
         """(most rungs one chain of the uploaded window evaluates -- 1: batching off --, batches of evaluate-only
         rungs the last solve decided) (lh_debug_batch)."""
-        m, k = C.c_int(0), C.c_int(0)
-        _check(ba_lib().lh_debug_batch(self.h, C.byref(m), C.byref(k)), "lh_debug_batch")
-        return m.value, k.value
+        return self.batch_detail()[:2]
+
+    def batch_detail(self):
+        """batch() and the acceptances inside the batches: (re-run as a full trial, re-run and stopping the loop)."""
+        m, k, rt = C.c_int(0), C.c_int(0), (C.c_int * 2)()
+        _check(ba_lib().lh_debug_batch(self.h, C.byref(m), C.byref(k), rt), "lh_debug_batch")
+        return m.value, k.value, (rt[0], rt[1])
 
     def comm_count(self):
         """Reduced-system all-reduces the last solve issued (lh_debug_comm_count)."""

@@ -887,7 +887,7 @@ def _batch_run(w, kw, env, monkeypatch, th):
         monkeypatch.setenv(k, v)
     s = lego_ba.Solver(**kw)
     r = s.solve(w)
-    r["chains"], r["batch"] = s.chains(), s.batch()
+    r["chains"], r["batch"], r["retrials"] = s.chains(), s.batch(), s.batch_detail()[2]
     o = s.solve(w, outlier_chi2_th=th)
     r["is_outlier"], r["n_outlier"] = o["is_outlier"].copy(), o["n_outlier"]
     s.close()
@@ -915,7 +915,7 @@ def _batch_windows():
 
 @pytest.mark.parametrize("env", [{}, {"LH_BATCH_MAX": "3"}, {"LH_LADDER_LAZY": "1"}])
 def test_batched_rejection_runs_are_bitwise_the_serial_chain(monkeypatch, env):
-    batched = []
+    batched, retrials = [], [0, 0]
     for name, w, kw, ctrl in _batch_windows():
         th = 5.991
         serial = _batch_run(w, kw, dict(env, LH_NO_BATCH="1"), monkeypatch, th)
@@ -932,12 +932,17 @@ def test_batched_rejection_runs_are_bitwise_the_serial_chain(monkeypatch, env):
         # the serial run's accepted evaluate-only trial was its last chain)
         if nb > 0:
             batched.append(name)
+            retrials[0] += bat["retrials"][0]
+            retrials[1] += bat["retrials"][1]
             assert bat["chains"] <= serial["chains"] + nb, (name, bat["chains"], serial["chains"], nb)
         else:
             assert bat["chains"] == serial["chains"], name
         if name == "C3 live":
             assert bat["chains"] < serial["chains"], (bat["chains"], serial["chains"])
     assert "C3 live" in batched and len(batched) >= 10, batched
+    # both kinds of acceptance inside a batch ran: re-run as a full trial, and re-run as the stopping trial
+    if not env:
+        assert retrials[0] > 0 and retrials[1] > 0, retrials
 
 
 # ---------------------------------------------------------------------------------------------
