@@ -139,10 +139,10 @@ struct lh_ctrl {
     int32_t dec_tag;           // seq + 1 once workgroup 0 of a controller that decides itself has decided chain seq
                                // (its rung workgroups wait for it; zeroed with the controller at every restart)
     // Batched evaluation of a rejection run: after a rejection, when the next trials only evaluate
-    // and their steps are built rungs, one chain's k_lin evaluates nbatch consecutive rungs and k_reduce takes their
+    // and their steps are built rungs, one chain's k_lin evaluates consecutive rungs (their count rides above the low
+    // byte of the evo words, evo and evo_seq) and k_reduce (or the controller after an exchange) takes their
     // decisions in order.  An acceptance among them is linearised by the next chain, a full trial at that rung whose
     // decision is the acceptance already taken (retrial).
-    int32_t nbatch;            // rungs the next chain evaluates (1: an ordinary chain)
     int32_t retrial;           // the next chain re-runs the accepted rung as a full trial; its decision only commits
     int32_t rho_sel;           // per-edge rho0 "as last evaluated": rung buffer (0: the ordinary one)
     int32_t nbatches;          // batches decided in this solve (lh_debug_batch)

@@ -720,37 +720,6 @@ __device__ __forceinline__ void st_rec2(double2* p, double2 v, __amdgpu_buffer_r
 
 static_assert(offsetof(lh_chunk, sb_end) == 4 && offsetof(lh_chunk, U) == 8, "k_lin reads the chunk header as dwords");
 
-// A batch rung's candidate pose tables (k_lin's batch path, one wave): the window's candidate poses from the committed
-// ones pm (slot lane's pose cpose[lane]) and the rung's step (LDS wdx), then their tables per (slot, camera) into
-// LDS wt_n, as k_lin's own candidate build does; LDS operands as offsets into the dynamic LDS.  Then the release of
-// the flag the other waves wait on.
-__device__ __attribute__((noinline)) void lin_cand_tables(const double* __restrict__ pm, const uint16_t* __restrict__ cpose,
-                                                          int pmax1, int U, int ncam, int o_wdx, int o_wext, int o_wtn,
-                                                          int o_scr, int o_flag) {
-    extern __shared__ __attribute__((aligned(16))) double dsm[];
-    const int lane = threadIdx.x & 63;
-    const uint32_t pp = min((uint32_t)cpose[min(lane, max(U - 1, 0))], (uint32_t)pmax1);
-    double pmc[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) pmc[i] = pm[pp * 12 + i];
-    double* scr = dsm + o_scr;
-    if (lane < U) {
-        double To[12];
-        d_pose_candidate(pmc, dsm + o_wdx + 6 * lane, To);
-#pragma unroll
-        for (int i = 0; i < 12; ++i) scr[lane * 12 + i] = To[i];
-    }
-    wave_sync();
-    if (lane < U * ncam) {
-        const int sl = lane / ncam, c = lane - sl * ncam;
-        double To[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) To[i] = scr[sl * 12 + i];
-        d_pose_table(To, dsm + o_wext + c * LH_EXT, dsm + o_wtn + (sl * ncam + c) * LH_PT_LDS);
-    }
-    __hip_atomic_store(reinterpret_cast<int*>(dsm + o_flag), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 // ---- back-substitution of the pending pose step (problem.cpp:426-429) for one sub-batch: the lane's edge term
 //      J_l^T W J_p dx (at the committed linearisation: pt the committed pose table, d the slot's step), summed over
 //      the landmark's lane group, then the landmark's update from its cached factor cl (VertexXYZ::add) and the
@@ -1568,9 +1537,9 @@ struct BatchWords {
     CtrlWords w;              // the words the next rung's decision starts from
     const double* sp;         // lh_ctrl.spose_l (an LDS copy)
     const int* lad_its;       // lh_ctrl.lad_its (an LDS copy)
-    int* cnt;                 // (LDS) lh_ctrl's counters lskips, pcg_iters; the last decision's lskip and nbatch
+    int* cnt;                 // (LDS) lh_ctrl's counters lskips, pcg_iters; the last decision's lskip
 };
-enum { BW_LSKIPS, BW_PCG, BW_LSKIP, BW_NBATCH };
+enum { BW_LSKIPS, BW_PCG, BW_LSKIP };
 __device__ __forceinline__ void batch_load(const lh_ctrl* __restrict__ ctrl, BatchWords& b, double* sp, int* its, int* cnt) {
     b.w = ctrl_load(ctrl);
 #pragma unroll
@@ -1581,7 +1550,6 @@ __device__ __forceinline__ void batch_load(const lh_ctrl* __restrict__ ctrl, Bat
     cnt[BW_LSKIPS] = ctrl->lskips;
     cnt[BW_PCG] = ctrl->pcg_iters;
     cnt[BW_LSKIP] = 0;
-    cnt[BW_NBATCH] = 1;
 }
 
 // a batch's words after its last decision (what ctrl_lm_step stores after a decision, from the batch's registers)
@@ -1600,7 +1568,6 @@ __device__ __forceinline__ void batch_store(lh_ctrl* __restrict__ ctrl, const Ba
     ctrl->relin = o.relin;
     ctrl->nofactor = o.relin | b.cnt[BW_LSKIP] | (o.retrial != 0 ? 1 : 0);
     ctrl->evo = o.evo;
-    ctrl->nbatch = b.cnt[BW_NBATCH];
     ctrl->evo_seq[(seq + 1) & 1] = o.evo;
 }
 
@@ -1794,7 +1761,6 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
         const int evw = evo_n | (nbatch_n > 1 ? nbatch_n << 8 : 0);
         if (!batch) {
             ctrl->evo = evw;
-            ctrl->nbatch = nbatch_n;
             ctrl->evo_seq[(seq + 1) & 1] = evw;
         }
         // host words: [0] the loop stopped; else [1] = 2 seq + near, the progress word: this live
@@ -1825,7 +1791,6 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
             o.evo = evw; o.relin = relin; o.retrial = retrial; o.lad = lad;
             o.spose = bw->sp[lad];
             bw->cnt[BW_LSKIP] = lskip;
-            bw->cnt[BW_NBATCH] = nbatch_n;
         }
     }
     done_o = done;
@@ -1917,7 +1882,6 @@ __device__ __forceinline__ int ctrl_decide(lh_ctrl* __restrict__ ctrl, const Ctr
         cnt[BW_LSKIPS] = ctrl->lskips;
         cnt[BW_PCG] = ctrl->pcg_iters;
         cnt[BW_LSKIP] = 0;
-        cnt[BW_NBATCH] = 1;
         return ctrl_batch_decide(ctrl, bw, prm, rs_stage + LY.off_bsc, nb, host_done, seq, true, done_o, accept_o, cur_o,
                                  lam_o);
     }
