@@ -1583,10 +1583,12 @@ __device__ __noinline__ void publish_stop(const lh_ctrl* __restrict__ ctrl, vola
     hw->iter = ctrl->iter; hw->trials = ctrl->trials; hw->accepted = ctrl->accepted; hw->trace_len = tl;
     hw->nonpd = ctrl->nonpd; hw->pcg_iters = ctrl->pcg_iters;
     hw->chi2_initial = ctrl->chi2_initial; hw->chi = ctrl->chi; hw->lambda = ctrl->lambda;
-    for (int i0 = 0; i0 < nt; i0 += 16) {   // sixteen entries' loads in flight (unconditional, in the array), then stores
-        double c[16], l[16];
+    // four entries' loads in flight (unconditional, in the array), then their stores: few registers, so that a
+    // caller's live values need no saving around this call (sixteen at a time spilled k_ctrl<0, false>)
+    for (int i0 = 0; i0 < nt; i0 += 4) {
+        double c[4], l[4];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < 4; ++j) {
             const int i = min(i0 + j, LH_TRACE - 1);
             c[j] = ctrl->trace_chi[i];
             l[j] = ctrl->trace_lambda[i];
@@ -1594,7 +1596,7 @@ __device__ __noinline__ void publish_stop(const lh_ctrl* __restrict__ ctrl, vola
         // (unconditional too: an entry past trace_len is never read by the host, and a store behind a branch
         // waited for the stores before it)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < 4; ++j) {
             const int i = min(i0 + j, LH_TRACE - 1);
             hw->trace_chi[i] = c[j];
             hw->trace_lambda[i] = l[j];
@@ -1624,8 +1626,11 @@ __device__ __forceinline__ void ctrl_progress(const lh_params& prm, volatile int
 __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const CtrlWords& w, const lh_params& prm,
                                              int mode, double mdiag, double tchi, double sl, double ndg,
                                              volatile int* __restrict__ host_done, int seq, int& done_o, int& accept_o,
-                                             int& cur_o, double& lam_o, bool raise_done = true, BatchWords* bw = nullptr) {
-    const bool batch = bw != nullptr;
+                                             int& cur_o, double& lam_o, bool raise_done = true, BatchWords* bw = nullptr,
+                                             bool in_batch = true) {
+    // (bw is always a valid pointer where the decision may be a batch's, and in_batch says whether it is one: a
+    // pointer chosen at run time would keep the caller's words out of registers)
+    const bool batch = bw != nullptr && in_batch;
     double chi = w.chi, lam = w.lam, ni = w.ni, last = w.last, spose = w.spose, chi0 = w.chi0;
     int iter = w.iter, fc = w.fc, trials = w.trials, nacc = w.nacc, tl = w.tl;
     int done = w.done, cur = w.cur;
@@ -1805,48 +1810,42 @@ __device__ __forceinline__ int ctrl_lm_step(lh_ctrl* __restrict__ ctrl, const Ct
 // controller after the exchange): rung r's chi2 (not halved) and gain scale at sc[2 r], sc[2 r + 1] (summed over
 // the chunks, and over the ranks when sharded, as a single trial's are), decided in order until an acceptance
 // (retrial), the stop, or a next trial that is not the batch's next rung.  bw holds the words batch_load read.
-// Stores the words once, the rung whose rho0 is "as last evaluated", and the host word (raise_done: publish the
-// stop here, else the chain's controller does).  Returns nothing-to-factor, with ctrl_lm_step's outputs.
-__device__ __forceinline__ int ctrl_batch_decide(lh_ctrl* __restrict__ ctrl, BatchWords& bw, const lh_params& prm,
-                                                 const double* sc, int nb, volatile int* __restrict__ host_done, int seq,
-                                                 bool raise_done, int& done_o, int& accept_o, int& cur_o, double& lam_o) {
-    // The rungs before the first that will be accepted (or the last) are plain rejections: each only advances
-    // lambda and nu, the counts and the rung (ctrl_lm_step's rejection, which moves onto a built rung and, before
-    // the batch's last rung, never ends the iteration: nbatch <= max_trials - false_cnt).  Their gain ratios are
-    // independent (chi2 does not change across rejections), so they are found first and skipped forward with
-    // that arithmetic; ctrl_lm_step takes the decisive rung.
-    int r = 0;
-    {
-        CtrlWords& w = bw.w;
-        const double chi = w.chi;
-        int j = nb - 1;
-        for (int q = 0; q < nb - 1; ++q) {
-            double scale = 0.5 * (bw.sp[w.lad + q] + sc[2 * q + 1]);
-            scale += 1e-10;
-            const double tchi = 0.5 * sc[2 * q];
-            const double rho = (chi - tchi) / scale;
-            if (rho > 0 && isfinite(tchi)) { j = q; break; }
-        }
-        for (; r < j; ++r) {   // rung r rejected: the decision ctrl_lm_step takes for it, in its order
-            if (prm.strategy == 0) { w.lam *= w.ni; w.ni *= 2; }
-            else w.lam = fmin(w.lam * 11.0, 1e7);
-            w.trials += 1;
-            w.fc += 1;
-            w.lad += 1;
-            bw.cnt[BW_LSKIPS] += 1;
-            if (prm.solver == 1) bw.cnt[BW_PCG] += bw.lad_its[w.lad];
-        }
-        w.spose = bw.sp[w.lad];
-        bw.cnt[BW_LSKIP] = r > 0 ? 1 : bw.cnt[BW_LSKIP];
+//
+// (1) The rungs before the first that will be accepted (or the last) are plain rejections: each only advances
+// lambda and nu, the counts and the rung (ctrl_lm_step's rejection, which moves onto a built rung and, before the
+// batch's last rung, never ends the iteration: nbatch <= max_trials - false_cnt).  Their gain ratios are
+// independent (chi2 does not change across rejections), so they are found first and skipped forward with that
+// arithmetic; ctrl_lm_step takes the decisive rung.  Returns that rung.
+__device__ __forceinline__ int batch_skip_forward(BatchWords& bw, const lh_params& prm, const double* sc, int nb) {
+    CtrlWords& w = bw.w;
+    const double chi = w.chi;
+    int j = nb - 1;
+    for (int q = 0; q < nb - 1; ++q) {
+        double scale = 0.5 * (bw.sp[w.lad + q] + sc[2 * q + 1]);
+        scale += 1e-10;
+        const double tchi = 0.5 * sc[2 * q];
+        const double rho = (chi - tchi) / scale;
+        if (rho > 0 && isfinite(tchi)) { j = q; break; }
     }
-    for (;; ++r) {
-        int d_o, a_o, c_o;
-        double l_o;
-        ctrl_lm_step(ctrl, bw.w, prm, 1, 0.0, 0.5 * sc[2 * r], sc[2 * r + 1], 0.0, host_done, seq, d_o, a_o, c_o, l_o,
-                     false, &bw);
-        const CtrlWords& w = bw.w;
-        if (r + 1 >= nb || w.done || w.retrial || !w.evo || !bw.cnt[BW_LSKIP]) break;
+    for (int r = 0; r < j; ++r) {   // rung r rejected: the decision ctrl_lm_step takes for it, in its order
+        if (prm.strategy == 0) { w.lam *= w.ni; w.ni *= 2; }
+        else w.lam = fmin(w.lam * 11.0, 1e7);
+        w.trials += 1;
+        w.fc += 1;
+        w.lad += 1;
+        bw.cnt[BW_LSKIPS] += 1;
+        if (prm.solver == 1) bw.cnt[BW_PCG] += bw.lad_its[w.lad];
     }
+    w.spose = bw.sp[w.lad];
+    if (j > 0) bw.cnt[BW_LSKIP] = 1;
+    return j;
+}
+// (2) after the decisive rung r: the words stored once, the rung whose rho0 is "as last evaluated", and the host word
+// (raise_done: publish the stop here, else the chain's controller does).  Returns nothing-to-factor, with
+// ctrl_lm_step's outputs.
+__device__ __forceinline__ int batch_finish(lh_ctrl* __restrict__ ctrl, BatchWords& bw, const lh_params& prm, int r,
+                                            volatile int* __restrict__ host_done, int seq, bool raise_done, int& done_o,
+                                            int& accept_o, int& cur_o, double& lam_o) {
     const CtrlWords& w = bw.w;
     batch_store(ctrl, bw, seq);
     ctrl->rho_sel = r;   // the per-edge rho0 of the last rung decided
@@ -1866,28 +1865,49 @@ __device__ __forceinline__ int ctrl_batch_decide(lh_ctrl* __restrict__ ctrl, Bat
     lam_o = w.lam;
     return w.relin | bw.cnt[BW_LSKIP] | (w.retrial != 0 ? 1 : 0);
 }
+__device__ __forceinline__ bool batch_more(const BatchWords& bw, int r, int nb) {
+    const CtrlWords& w = bw.w;
+    return !(r + 1 >= nb || w.done || w.retrial || !w.evo || !bw.cnt[BW_LSKIP]);
+}
+// k_reduce's (one rank)
+__device__ __forceinline__ int ctrl_batch_decide(lh_ctrl* __restrict__ ctrl, BatchWords& bw, const lh_params& prm,
+                                                 const double* sc, int nb, volatile int* __restrict__ host_done, int seq,
+                                                 bool raise_done, int& done_o, int& accept_o, int& cur_o, double& lam_o) {
+    int r = batch_skip_forward(bw, prm, sc, nb);
+    for (;; ++r) {
+        int d_o, a_o, c_o;
+        double l_o;
+        ctrl_lm_step(ctrl, bw.w, prm, 1, 0.0, 0.5 * sc[2 * r], sc[2 * r + 1], 0.0, host_done, seq, d_o, a_o, c_o, l_o,
+                     false, &bw);
+        if (!batch_more(bw, r, nb)) break;
+    }
+    return batch_finish(ctrl, bw, prm, r, host_done, seq, raise_done, done_o, accept_o, cur_o, lam_o);
+}
 // a self-deciding controller's decision (thread 0): a batch's (this chain's evo word above its low byte, the
-// rungs' scalars behind the exchanged system, lh_rs_layout.off_bsc) or one trial's
+// rungs' scalars behind the exchanged system, lh_rs_layout.off_bsc) or one trial's.  BATCH false: the caller's
+// batches are decided elsewhere (k_ctrl: its decider workgroup, ctrl_batch_decider)
+template <bool BATCH = true>
 __device__ __forceinline__ int ctrl_decide(lh_ctrl* __restrict__ ctrl, const CtrlWords& cw, const lh_params& prm, int mode,
                                            double mdiag, double tchi, double sl, double ndg, const double* rs_stage,
                                            const lh_rs_layout& LY, volatile int* __restrict__ host_done, int seq,
                                            int& done_o, int& accept_o, int& cur_o, double& lam_o, int* cnt) {
-    const int nb = cw.evo >> 8;   // (cw.evo: this chain's evo word, read before its decision)
-    if (mode != 0 && nb > 1) {
-        BatchWords bw;
-        bw.w = cw;
-        bw.sp = ctrl->spose_l;   // (global: one load per rung)
-        bw.lad_its = ctrl->lad_its;
-        bw.cnt = cnt;
-        cnt[BW_LSKIPS] = ctrl->lskips;
-        cnt[BW_PCG] = ctrl->pcg_iters;
-        cnt[BW_LSKIP] = 0;
-        return ctrl_batch_decide(ctrl, bw, prm, rs_stage + LY.off_bsc, nb, host_done, seq, true, done_o, accept_o, cur_o,
-                                 lam_o);
+    if constexpr (BATCH) {
+        const int nb = cw.evo >> 8;   // (cw.evo: this chain's evo word, read before its decision)
+        if (mode != 0 && nb > 1) {
+            BatchWords bw;
+            bw.w = cw;
+            bw.sp = ctrl->spose_l;   // (global: one load per rung)
+            bw.lad_its = ctrl->lad_its;
+            bw.cnt = cnt;
+            cnt[BW_LSKIPS] = ctrl->lskips;
+            cnt[BW_PCG] = ctrl->pcg_iters;
+            cnt[BW_LSKIP] = 0;
+            return ctrl_batch_decide(ctrl, bw, prm, rs_stage + LY.off_bsc, nb, host_done, seq, true, done_o, accept_o,
+                                     cur_o, lam_o);
+        }
     }
     return ctrl_lm_step(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, host_done, seq, done_o, accept_o, cur_o, lam_o);
 }
-
 // ---- the lambda ladder's rung workgroups (lh_ctrl.lad) ----
 // Workgroup 0 of a controller that takes the LM decision itself (the initial linearisation, sharded solves,
 // k_ctrl_g, k_ctrl_p) publishes it: ctrl_lm_step's words, then dec_tag = seq + 1 (release).  Its rung workgroups
@@ -1923,6 +1943,34 @@ __device__ __forceinline__ LadderDec ladder_read(const lh_ctrl* __restrict__ ctr
     d.lambda = lambda;
     return d;
 }
+// k_ctrl's decider workgroup (the launch's last, when the controller decides itself: sharded solves): thread 0
+// takes the chain's LM decision -- one trial's, or a batch's -- then publishes the tag the factoring workgroup and
+// the rungs wait for (ladder_publish).  It holds no prefetched system: workgroup 0, deciding with that system in
+// registers, spilled (k_ctrl<0, false>, once the decision learnt batches).
+__device__ __forceinline__ void ctrl_decider(lh_ctrl* __restrict__ ctrl, const lh_params& prm, const double* rs_stage,
+                                             const lh_rs_layout& LY, int nb, volatile int* __restrict__ host_done,
+                                             int seq) {
+    __shared__ int cnt[4];
+    int d_o, a_o, c_o;
+    double l_o;
+    if (nb > 1) {
+        BatchWords bw;
+        bw.w = ctrl_load(ctrl);
+        bw.sp = ctrl->spose_l;
+        bw.lad_its = ctrl->lad_its;
+        bw.cnt = cnt;
+        cnt[BW_LSKIPS] = ctrl->lskips;
+        cnt[BW_PCG] = ctrl->pcg_iters;
+        cnt[BW_LSKIP] = 0;
+        ctrl_batch_decide(ctrl, bw, prm, rs_stage + LY.off_bsc, nb, host_done, seq, true, d_o, a_o, c_o, l_o);
+    } else {
+        const CtrlWords cw = ctrl_load(ctrl);
+        ctrl_lm_step(ctrl, cw, prm, 1, 0.0, 0.5 * rs_stage[LY.off_sc + LH_SC_CHI2], rs_stage[LY.off_sc + LH_SC_SCALE],
+                     rs_stage[LY.off_sc + LH_SC_NDEG], host_done, seq, d_o, a_o, c_o, l_o);
+    }
+    ladder_publish(ctrl, seq);
+}
+
 // a factoring controller's rung count: prm.ladder rungs at every factor (ladder_eager) or a factor after a rejection
 __device__ __forceinline__ bool ladder_build(const lh_params& prm, int accept) {
     return prm.ladder > 1 && (prm.ladder_eager || !accept);
@@ -3056,7 +3104,17 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // k_reduce took this trial's LM decision; a rung workgroup > 0 reads it (or workgroup 0's) from lh_ctrl
     const int rung = (int)blockIdx.x;
     const bool dec_src = mode != 0 && prm.dec_in_reduce;
-    const bool decided = dec_src || rung > 0;
+    // A batch chain of a controller that decides itself (sharded: after the exchange) is decided by the launch's
+    // last workgroup (lh_launch_ctrl adds it), and every other workgroup, 0 included, waits for that decision
+    // (this chain's evo word: no decision has rewritten it yet)
+    const int nwg = prm.ladder > 1 ? prm.ladder : 1;
+    const bool dwg = !dec_src && mode != 0;   // the decider workgroup decides this chain
+    if (!prm.dec_in_reduce && rung == nwg) {
+        if (dwg && threadIdx.x == 0)
+            ctrl_decider(ctrl, prm, rs_stage, LY, __builtin_amdgcn_readfirstlane(ctrl->evo) >> 8, host_done, seq);
+        return;
+    }
+    const bool decided = dec_src || rung > 0 || dwg;
     const bool nd = SOLVER == 0 && prm.nd_steps > 0;        // the two-chain LDL^T schedule
     // k_reduce wrote S and b_s in this kernel's LDS layout (img[0] staged, img[1] committed): the system
     // arrives by a straight copy, no index math per entry (the scatter below was 2.2 us of wave 0's time)
@@ -3094,7 +3152,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
     // (the initial linearisation's controller builds no ladder: its release on workgroup 0's path cost ~5 us per
     // solve, and a rejection right after it refactors and builds one)
     if (rung && mode == 0) return;
-    if (rung && !dec_src) ladder_wait(ctrl, seq);   // workgroup 0 decides (thread 0 below) and publishes
+    // the decider workgroup decides and publishes (workgroup 0's thread 0 below decides the initial linearisation)
+    if (dwg) ladder_wait(ctrl, seq);
     if (decided) {
         const LadderDec d = ladder_read(ctrl, prm, seq, rung);   // (the rung's lambda: block 0's early factor uses it)
         done = d.done;
@@ -3232,10 +3291,8 @@ __global__ __launch_bounds__(CT) void k_ctrl(lh_ctrl* __restrict__ ctrl, double*
             }
             int d_o, a_o, c_o;
             double lam_n;
-            __shared__ int b_cnt[4];
-            s_flags[2] = ctrl_decide(ctrl, cw, prm, mode, mdiag, tchi, sl, ndg, rs_stage, LY, host_done, seq, d_o, a_o, c_o,
-                                     lam_n, b_cnt);
-            if (prm.ladder > 1 && mode != 0) ladder_publish(ctrl, seq);   // the rung workgroups wait for it
+            // (only the initial linearisation's: a later chain's is the decider workgroup's)
+            s_flags[2] = ctrl_lm_step(ctrl, cw, prm, 0, mdiag, tchi, sl, ndg, host_done, seq, d_o, a_o, c_o, lam_n);
             s_flags[0] = d_o;
             s_flags[1] = a_o;
             s_lam = lam_n;
@@ -5330,15 +5387,19 @@ hipError_t lh_launch_ctrl(hipStream_t st, lh_ctrl* ctrl, double* rs_commit, cons
     else if (prm.P > LH_PMAX)
         hipLaunchKernelGGL(k_ctrl_g, gl, dim3(GT), 0, st, ctrl, rs_commit, rs_stage, maxd, rsmap,
                            dxp, prm, mode, (volatile int*)host_done, seq, gA, gS);
-    else if (prm.solver == 1)
-        hipLaunchKernelGGL((k_ctrl<1, false>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
-                           dxp, prm, mode, (volatile int*)host_done, seq, img);
-    else if (prm.img)
-        hipLaunchKernelGGL((k_ctrl<0, true>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
-                           dxp, prm, mode, (volatile int*)host_done, seq, img);
-    else
-        hipLaunchKernelGGL((k_ctrl<0, false>), gl, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq,
-                           units, dxp, prm, mode, (volatile int*)host_done, seq, img);
+    else {
+        // k_ctrl deciding itself: one more workgroup, the decider of batch chains (ctrl_batch_decider)
+        const dim3 gk(gl.x + (prm.dec_in_reduce ? 0 : 1));
+        if (prm.solver == 1)
+            hipLaunchKernelGGL((k_ctrl<1, false>), gk, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
+                               dxp, prm, mode, (volatile int*)host_done, seq, img);
+        else if (prm.img)
+            hipLaunchKernelGGL((k_ctrl<0, true>), gk, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq, units,
+                               dxp, prm, mode, (volatile int*)host_done, seq, img);
+        else
+            hipLaunchKernelGGL((k_ctrl<0, false>), gk, dim3(CT), 0, st, ctrl, rs_commit, rs_stage, maxd, pair_pq,
+                               units, dxp, prm, mode, (volatile int*)host_done, seq, img);
+    }
     return hipGetLastError();
 }
 
