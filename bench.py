@@ -49,7 +49,7 @@ FP64_PEAK_TFS = 78.6       # MI355X FP64 spec (vector = matrix);
 # the committed rocprofv3 evidence of this tree's k_lin (LH_PMC_JSON / LH_ROCPROF_JSON: the same files written
 # earlier in the same GPU call, before they are committed)
 PMC_TRAFFIC = os.environ.get("LH_PMC_JSON", os.path.join(ROOT, "profiles", "r06ak_pmc_k_lin.json"))
-ROCPROF_K_LIN = os.environ.get("LH_ROCPROF_JSON", os.path.join(ROOT, "profiles", "r06ak_rocprof_k_lin.json"))
+ROCPROF_K_LIN = os.environ.get("LH_ROCPROF_JSON", os.path.join(ROOT, "profiles", "r06av_rocprof_k_lin.json"))
 # L: landmarks of the window; per_rank: L per rank (the window has L N landmarks; weak scaling)
 WORKLOADS = {"C3": dict(P=20, L=50_000, k=8), "C3w": dict(P=20, L=50_000, k=8, per_rank=True),
              "C4": dict(P=20, L=500_000, k=8)}
