@@ -284,12 +284,13 @@ def test_sharded_outlier_pass_equals_the_whole_window(cfg, seed, family, th):
     assert a["exchanges"] == b["exchanges"] == a["chains"] + 1   # the pass's exchange is not a solve collective
 
 
-@pytest.mark.parametrize("case", [0, 4, 8])
+@pytest.mark.parametrize("case", [0, 3, 4, 8])
 def test_sharded_lambda_ladder_is_bitwise_the_serial_chain(case):
     """A sharded solve's controller takes the LM decision itself (after the exchange): its workgroup 0 publishes the
     decision to the lambda ladder's rung workgroups (ladder_publish / ladder_wait).  Every rank's solve must equal
     the one-rung run (LH_NO_LADDER=1) bit for bit, the exchanges included, on windows that reject (tests/windows.py
-    RELIN_WINDOWS: k_ctrl, k_ctrl_b and k_ctrl_p sharded two ways)."""
+    RELIN_WINDOWS: k_ctrl LDL^T and PCG -- decided on k_ctrl's decider workgroup --, k_ctrl_b and k_ctrl_p sharded
+    two ways)."""
     from windows import RELIN_WINDOWS
     _, gen, opt, _, _ = RELIN_WINDOWS[case]
     gen = dict(gen)
@@ -313,7 +314,9 @@ def test_sharded_lambda_ladder_is_bitwise_the_serial_chain(case):
         for k in ("pose_Tcw", "lm_xyz", "edge_robust_chi2", "trace_chi2"):
             assert np.array_equal(a[k], b[k]), (r, k)
         assert a["batch"][0] == 10 and a["batch"][1] > 0, (r, a["batch"])
-        assert a["exchanges"] == a["chains"] + 1 and a["chains"] < b["chains"], (r, a["chains"], b["chains"])
+        # (a batch replaces its rungs' chains by one; an acceptance at its first rung costs the same chains as the
+        # serial run's evaluate-only acceptance and re-linearisation, and one stopping the loop one chain more)
+        assert a["exchanges"] == a["chains"] + 1 and a["chains"] <= b["chains"] + a["batch"][1], (r, a["chains"], b["chains"])
 
 
 @pytest.mark.parametrize("cfg,seed,family", [("C2", 0, "stable_noout"), ("mini", 2, "default")])
