@@ -910,6 +910,8 @@ def _batch_windows():
         out.append(("relin " + kind, relin_window(gen), dict(max_iters=3, **opt), ctrl))
     # the bench's live configuration (a stalled solve ends every run of it with max_trials rejections)
     out.append(("C3 live", window("C3", seed=0, family="default"), {}, "k_ctrl"))
+    # sixteen rungs (the most, LH_LAD): batches past k_reduce's ten rungs per round of loads
+    out.append(("C3 live 16 trials", window("C3", seed=0, family="default"), dict(max_trials=16), "k_ctrl"))
     return out
 
 
